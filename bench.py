@@ -1,0 +1,237 @@
+"""Benchmark: the per-channel INT8 DFQ weight sweep on MI355X.
+
+One STEP = one pass of the fused DFQ sweep (per-channel symmetric INT8
+quantize-dequantize + integer codes + clip_weight + bias-correction error sums
+E[o,i]) over a batch of ``--copies`` independent MobileNetV2 weight sets
+(BASELINE.json configs[1]; synthetic random-init weights of the reference's
+shapes, already resident in HBM).  The batch defeats the 256 MB Infinity Cache
+(SURVEY.md 8d), so the number is an HBM number.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N     (one process per GPU; weak scaling)
+
+Rank 0 prints ONE JSON line (contract in the task statement); ``roofline``
+times the sweep kernel with HIP events on the stream it is launched on;
+``cpu_baseline`` times the CPU port (oracle/, 1 thread) on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "weight-GB/s quantized (per-ch INT8 DFQ sweep) + top-1 delta, MobileNetV2"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--model", default="mobilenetv2", choices=["mobilenetv2", "resnet50", "deeplab"])
+    p.add_argument("--copies", type=int, default=0, help="weight sets per GPU (0: enough for >= 2 GiB)")
+    p.add_argument("--bits", type=int, default=8)
+    p.add_argument("--granularity", default="channel", choices=["channel", "tensor"])
+    p.add_argument("--asym", action="store_true", help="asymmetric (reference default) instead of symmetric")
+    p.add_argument("--no-esum", action="store_true", help="skip the bias-correction error sums")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
+    p.add_argument("--no-pipeline", action="store_true", help="skip the one-off full-DFQ pipeline timing")
+    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r01.json"))
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, torch.device(f"cuda:{local if world > 1 else 0}")
+
+
+def build_batch(args, dev):
+    """Synthetic weight sets of the model's target-layer shapes, generated on the
+    GPU (conv ~ N(0, sqrt(2/(k*k*O))), linear ~ N(0, 0.01), as SURVEY.md 8d)."""
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd.sweep import allocate, khw_of
+    model = zoo.MODELS[args.model]()
+    shapes = [tuple(m.weight.shape) for m in zoo.target_layers(model)]
+    per_copy = sum(int(torch.Size(s).numel()) for s in shapes)
+    copies = args.copies or max(1, -(-(2 << 30) // (4 * per_copy)))   # >= 2 GiB of fp32 weights
+    gen = torch.Generator(device=dev).manual_seed(1234 + int(os.environ.get("RANK", "0")))
+    items = []
+    for c in range(copies):
+        for s in shapes:
+            if len(s) == 4:
+                std = (2.0 / (s[2] * s[3] * s[0])) ** 0.5
+            else:
+                std = 0.01
+            w = torch.randn(s, device=dev, generator=gen) * std
+            items.append(allocate(w, bits=args.bits, per_channel=args.granularity == "channel",
+                                  symmetric=not args.asym, khw=khw_of(w), want_esum=not args.no_esum,
+                                  clip=(-15.0, 15.0)))
+    return items, shapes, per_copy, copies
+
+
+def cpu_baseline(args, shapes, seconds):
+    """The CPU port (oracle/dfq_oracle.c, scalar, 1 thread) on a bounded sample of
+    the same workload: whole MobileNetV2 weight sets, same mode/flags."""
+    import numpy as np
+    from oracle import oracle as O
+    rng = np.random.default_rng(0)
+    ws = []
+    for s in shapes:
+        std = (2.0 / (s[2] * s[3] * s[0])) ** 0.5 if len(s) == 4 else 0.01
+        ws.append(rng.normal(0, std, s).astype(np.float32))
+    mode = (O.CHANNEL_ASYM if args.asym else O.CHANNEL_SYM) if args.granularity == "channel" else \
+        (O.TENSOR_ASYM if args.asym else O.TENSOR_SYM)
+    elems = sum(w.size for w in ws)
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        for w in ws:
+            rows = w.shape[0] if mode >= 2 else 1
+            khw = w.shape[2] * w.shape[3] if w.ndim == 4 else 1
+            O.quantize(w, args.bits, mode, rows=rows, khw=khw, flags=O.F_CLIP, clip=(-15.0, 15.0),
+                       want_esum=not args.no_esum)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(4.0 * elems * passes / el / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{args.model} x1 weight set ({len(ws)} layers, {elems} weights) x {passes} passes, "
+                      f"{el:.1f} s, scalar C port (oracle/dfq_oracle.c), 1 thread"}
+
+
+def pipeline_timing(dev):
+    """One-off: the full main_dfq stage order on one MobileNetV2 (per-channel
+    sym INT8, fused BC) on the GPU; seconds per stage (after a warm-up run)."""
+    import torch.nn as nn
+    from data_free_quantization_amd import zoo, Cross_layer_equal as cle
+    from data_free_quantization_amd.pipeline import run_dfq
+    from data_free_quantization_amd.utils.tracer import build_graph
+    out = {}
+    for rep in range(2):
+        m = zoo.build("mobilenetv2", seed=0, relu=True).to(dev)
+        g = build_graph(m, "positional")
+        t = {}
+        t0 = time.perf_counter()
+        run_dfq(m, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel", symmetric=True,
+                bc_mode="fused", timings=t)
+        torch.cuda.synchronize(dev)
+        total = time.perf_counter() - t0
+        out = {k: round(v * 1e3, 3) for k, v in t.items()}
+        out["total"] = round(total * 1e3, 3)
+        out["cle_iterations"] = cle.LAST_RUN.get("iterations")
+    return out
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist(args)
+    from data_free_quantization_amd.sweep import SweepPlan
+    items, shapes, per_copy, copies = build_batch(args, dev)
+    plan = SweepPlan(items)
+    st = plan.stats
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup):
+        plan.execute(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        plan.execute(stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1)          # device time of the K launches on this stream
+    t_step = wall / args.steps
+    if world > 1:
+        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_step = float(tt.item()) / args.steps
+    weight_bytes = 4 * per_copy * copies * world
+    value = weight_bytes / t_step / 1e9
+    launch_ms = dev_ms / (args.steps * st["launches"])
+    achieved = st["algo_bytes"] / (launch_ms / 1e3) / 1e9
+    traffic = None
+    tj = Path(args.traffic_json)
+    if tj.exists():
+        try:
+            traffic = json.loads(tj.read_text()).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    res = None
+    if rank == 0:
+        cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
+        pipe = None if args.no_pipeline else pipeline_timing(dev)
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_step * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (int8 codes)",
+            "data": "synthetic random-init weights of the reference shapes (no checkpoints offline)",
+            "config": {
+                "workload": f"{args.model} x{copies} weight sets per GPU: {args.granularity} "
+                            f"{'asym' if args.asym else 'sym'} INT{args.bits} quantize-dequantize + codes + "
+                            f"clip[-15,15]" + ("" if args.no_esum else " + bias-correction error sums"),
+                "model": args.model,
+                "copies_per_gpu": copies,
+                "layers_per_copy": len(shapes),
+                "weights_per_copy": per_copy,
+                "parallelism": f"layer-list sharding, {world} rank(s), no data-path collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algo_bytes_per_launch": st["algo_bytes"],
+                "launch_ms": round(launch_ms, 4),
+                "kernel": "sweep_main_kernel",
+            },
+            "cpu_baseline": cpu,
+            "pipeline_ms": pipe,
+            "top1_delta": None,
+            "notes": "top-1 needs ImageNet-val + the pretrained checkpoint (absent offline); weight outputs are "
+                     "bit-exact with the reference CPU path (tests/test_gpu_pipeline.py)",
+        }
+        print(json.dumps(res), flush=True)
+    plan.destroy()
+    if world > 1:
+        dist.destroy_process_group()
+    return res
+
+
+if __name__ == "__main__":
+    main()

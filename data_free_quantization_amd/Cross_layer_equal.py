@@ -1,0 +1,133 @@
+"""Drop-in for the reference's ``Cross_layer_equal.py`` (Cross_layer_equal.py:1-116).
+
+``_layer_equalization`` runs one relation as HIP kernels (channel-parallel
+ranges + rescale, bit-exact with the reference's sequential channel loop);
+``cross_layer_equalization`` keeps the reference's host loop and stop rule, with
+the per-iteration convergence metric reduced on the GPU (``dfq_diff_plan``)
+instead of a deep copy of the graph.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import warnings
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+#: statistics of the last cross_layer_equalization call (extension, for tests/bench)
+LAST_RUN = {}
+
+
+def _layer_equalization(W1, W2, B1, Batnorm_weight=None, Batnorm_bias=None, s_min_max=(1e-8, 1e8), signed=False,
+                        eps=0, S_acc=None):
+    """Equalize the output channels of W1 with the input channels of W2, in place.
+    Returns (W1, W2, B1, S).  ``S_acc`` (extension): a [C] device tensor the scales
+    are multiplied into (``None``: not accumulated)."""
+    _lib.require_device(W1, W2, B1, Batnorm_weight, Batnorm_bias)
+    c1 = W1.shape[0]
+    o2, i2 = W2.shape[0], W2.shape[1]
+    S = torch.empty(c1, dtype=torch.float32, device=W1.device)
+    L = _lib.load()
+    ws_bytes = L.dfq_cle_ws_bytes(c1)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=W1.device)
+    rc = L.dfq_cle_relation(
+        _lib.ptr(W1), _lib.ptr(W2), _lib.ptr(B1), _lib.ptr(Batnorm_weight), _lib.ptr(Batnorm_bias), c1,
+        W1.numel() // c1, o2, i2, W2.numel() // (o2 * i2), float(s_min_max[0]), float(s_min_max[1]),
+        int(bool(signed)), float(eps), _lib.ptr(S), _lib.ptr(S_acc), 0, C.c_void_p(ws.data_ptr()), ws_bytes,
+        _lib.stream_of(W1))
+    _lib.check(rc, "dfq_cle_relation")
+    return W1, W2, B1, S
+
+
+class _DiffPlan:
+    """mean|W - W_old| per target layer, snapshot kept on the device."""
+
+    def __init__(self, weights):
+        self.weights = weights
+        self.snaps = [torch.empty_like(w) for w in weights]
+        n = len(weights)
+        L = _lib.load()
+        wp = (C.c_void_p * max(n, 1))(*[w.data_ptr() for w in weights])
+        sp = (C.c_void_p * max(n, 1))(*[s.data_ptr() for s in self.snaps])
+        ns = (C.c_int64 * max(n, 1))(*[w.numel() for w in weights])
+        self._plan = C.c_void_p()
+        _lib.check(L.dfq_diff_plan_create(wp, sp, ns, n, C.byref(self._plan)), "dfq_diff_plan_create")
+        self._out = (C.c_double * max(n, 1))()
+        self._dev = weights[0].device if weights else None
+
+    def snapshot(self):
+        _lib.check(_lib.load().dfq_diff_plan_snapshot(self._plan, _lib.stream_of(self.weights[0])),
+                   "dfq_diff_plan_snapshot")
+
+    def diffs(self):
+        _lib.check(_lib.load().dfq_diff_plan_execute(self._plan, self._out, _lib.stream_of(self.weights[0])),
+                   "dfq_diff_plan_execute")
+        return [float(self._out[i]) for i in range(len(self.weights))]
+
+    def close(self):
+        if self._plan is not None:
+            _lib.load().dfq_diff_plan_destroy(self._plan)
+            self._plan = None
+
+
+def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8], Treshhold=2e-7, Count=20,
+                             signed=False, eps=0, Save_state=True):
+    """Iterate the relations until the summed mean weight change is <= Treshhold
+    or it stayed within 1e-9 for ``Count`` iterations (Cross_layer_equal.py:81-115)."""
+    print("Cross layer equalization")
+    if Save_state:
+        warnings.warn("Save_state plots (ourplots.save_layer) are visualization, not part of the weight path; "
+                      "skipped")
+    with torch.no_grad():
+        targets = [graph[k] for k in graph if type(graph[k]) in Target_list]
+        plan = _DiffPlan([t.weight.data for t in targets]) if targets else None
+        diff = 1e8
+        iter_count = 0
+        history = []
+        iters = 0
+        try:
+            if plan is not None:
+                plan.snapshot()
+            while diff > Treshhold and iter_count < Count:
+                for rel in relations:
+                    first, second, bn_idx = rel.get_idxs()
+                    l1, l2 = graph[first], graph[second]
+                    if l1.bias is None:   # :93-94
+                        l1.bias = nn.Parameter(torch.zeros(l1.weight.size(0), dtype=torch.float32,
+                                                           device=l1.weight.device), requires_grad=False)
+                    bn = graph[bn_idx]
+                    first_time = rel.S is None
+                    if first_time:
+                        rel.S = torch.empty(l1.weight.size(0), dtype=torch.float32, device=l1.weight.device)
+                    _cle_into(l1.weight.data, l2.weight.data, l1.bias.data, bn.fake_weight, bn.fake_bias,
+                              s_min_max, signed, eps, rel.S, first_time)
+                diff_list = plan.diffs() if plan is not None else []
+                diff_tmp = np.sum(diff_list)
+                history.append(float(diff_tmp))
+                iters += 1
+                if abs(diff - diff_tmp) > 1e-9:
+                    iter_count = 0
+                    diff = diff_tmp
+                else:
+                    iter_count += 1
+        finally:
+            if plan is not None:
+                plan.close()
+        LAST_RUN.clear()
+        LAST_RUN.update(iterations=iters, diffs=history)
+
+
+def _cle_into(W1, W2, B1, bnw, bnb, s_min_max, signed, eps, S_acc, first_time):
+    c1 = W1.shape[0]
+    o2, i2 = W2.shape[0], W2.shape[1]
+    L = _lib.load()
+    ws_bytes = L.dfq_cle_ws_bytes(c1)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=W1.device)
+    rc = L.dfq_cle_relation(
+        _lib.ptr(W1), _lib.ptr(W2), _lib.ptr(B1), _lib.ptr(bnw), _lib.ptr(bnb), c1, W1.numel() // c1, o2, i2,
+        W2.numel() // (o2 * i2), float(s_min_max[0]), float(s_min_max[1]), int(bool(signed)), float(eps), None,
+        _lib.ptr(S_acc), 1 if first_time else 0, C.c_void_p(ws.data_ptr()), ws_bytes, _lib.stream_of(W1))
+    _lib.check(rc, "dfq_cle_relation")

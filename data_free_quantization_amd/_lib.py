@@ -1,0 +1,141 @@
+"""ctypes binding of libdfq_hip.so (include/dfq_hip.h).
+
+This is the only door from the Python host layer into the HIP kernels.  There is
+no CPU fallback: if the library is missing, or a tensor is not on a ROCm device,
+the call raises.  (The CPU restatement under oracle/ is test infrastructure and
+is never imported here.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libdfq_hip.so"
+
+DFQ_TENSOR_ASYM, DFQ_TENSOR_SYM, DFQ_CHANNEL_ASYM, DFQ_CHANNEL_SYM = 0, 1, 2, 3
+DFQ_CLIP, DFQ_GIVEN_RANGE, DFQ_SCALE_F32 = 0x1, 0x2, 0x4
+DFQ_OK, DFQ_ERR_INVALID, DFQ_ERR_HIP, DFQ_ERR_UNSUPPORTED = 0, -1, -2, -3
+DFQ_ERR_NOMEM, DFQ_ERR_SHAPE, DFQ_ERR_WORKSPACE = -4, -5, -6
+
+EXPORTS = [
+    "dfq_abi_version", "dfq_error_string", "dfq_last_hip_error",
+    "dfq_quantize_ws_bytes", "dfq_quantize_tensor",
+    "dfq_sweep_plan_create", "dfq_sweep_plan_execute", "dfq_sweep_plan_stats", "dfq_sweep_plan_destroy",
+    "dfq_bn_fold", "dfq_clamp",
+    "dfq_cle_ws_bytes", "dfq_cle_relation",
+    "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
+    "dfq_bias_absorb", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate",
+]
+
+
+class TensorDesc(C.Structure):
+    _fields_ = [
+        ("src", C.c_void_p), ("dst", C.c_void_p), ("codes", C.c_void_p), ("scale", C.c_void_p),
+        ("zero", C.c_void_p), ("esum", C.c_void_p), ("rows", C.c_int64), ("row_len", C.c_int64),
+        ("khw", C.c_int32), ("bits", C.c_int32), ("mode", C.c_int32), ("flags", C.c_int32),
+        ("clip_lo", C.c_float), ("clip_hi", C.c_float), ("given_min", C.c_double), ("given_max", C.c_double),
+    ]
+
+
+class SweepStats(C.Structure):
+    _fields_ = [
+        ("n_tensors", C.c_int64), ("n_elems", C.c_int64), ("n_tasks_reduce", C.c_int64),
+        ("n_tasks_main", C.c_int64), ("algo_bytes", C.c_int64), ("launches", C.c_int32),
+        ("grid_blocks", C.c_int32),
+    ]
+
+
+_LIB: Optional[C.CDLL] = None
+
+
+class DFQLibraryError(RuntimeError):
+    pass
+
+
+def load(path: Optional[os.PathLike] = None) -> C.CDLL:
+    """Load (once) and type the library.  Raises if it is not built."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise DFQLibraryError(
+            f"{p} is missing: build it with `python -m data_free_quantization_amd.build` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(str(p))
+    P, I32, I64, F32, F64, SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double, C.c_size_t
+    sig = {
+        "dfq_abi_version": ([], C.c_int),
+        "dfq_error_string": ([C.c_int], C.c_char_p),
+        "dfq_last_hip_error": ([], C.c_char_p),
+        "dfq_quantize_ws_bytes": ([C.POINTER(TensorDesc), C.POINTER(SZ)], C.c_int),
+        "dfq_quantize_tensor": ([C.POINTER(TensorDesc), P, SZ, P], C.c_int),
+        "dfq_sweep_plan_create": ([C.POINTER(TensorDesc), I32, C.POINTER(P)], C.c_int),
+        "dfq_sweep_plan_execute": ([P, P], C.c_int),
+        "dfq_sweep_plan_stats": ([P, C.POINTER(SweepStats)], C.c_int),
+        "dfq_sweep_plan_destroy": ([P], C.c_int),
+        "dfq_bn_fold": ([P, P, P, P, P, P, P, P, F32, I64, I64, P], C.c_int),
+        "dfq_clamp": ([P, I64, F32, F32, P], C.c_int),
+        "dfq_cle_ws_bytes": ([I64], SZ),
+        "dfq_cle_relation": ([P, P, P, P, P, I64, I64, I64, I64, I64, F64, F64, I32, F32, P, P, I32, P, SZ, P],
+                             C.c_int),
+        "dfq_diff_plan_create": ([C.POINTER(P), C.POINTER(P), C.POINTER(I64), I32, C.POINTER(P)], C.c_int),
+        "dfq_diff_plan_snapshot": ([P, P], C.c_int),
+        "dfq_diff_plan_execute": ([P, C.POINTER(F64), P], C.c_int),
+        "dfq_diff_plan_destroy": ([P], C.c_int),
+        "dfq_bias_absorb": ([P, P, P, P, P, I64, I64, I64, I64, F32, P], C.c_int),
+        "dfq_bc_expect": ([P, P, I64, I32, I32, P, P], C.c_int),
+        "dfq_bc_apply": ([P, I64, I64, P, I64, P, P, C.POINTER(I64), P], C.c_int),
+        "dfq_bc_propagate": ([P, I64, P, I64, P], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    if L.dfq_abi_version() != 1:
+        raise DFQLibraryError("libdfq_hip.so ABI version mismatch")
+    if path is None:
+        _LIB = L
+    return L
+
+
+def check(rc: int, what: str, shape_error=RuntimeError):
+    """Map a DFQ_ERR_* code to the exception the reference would raise."""
+    if rc == DFQ_OK:
+        return
+    L = load()
+    msg = f"{what}: {L.dfq_error_string(rc).decode()}"
+    if rc == DFQ_ERR_HIP:
+        msg += f" ({L.dfq_last_hip_error().decode()})"
+    if rc == DFQ_ERR_SHAPE:
+        raise shape_error(msg)
+    if rc == DFQ_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise DFQLibraryError(msg)
+
+
+def require_device(*tensors: Optional[torch.Tensor]):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                "data_free_quantization_amd runs the DFQ weight path on a ROCm GPU only; "
+                f"got a tensor on {t.device} (move the model with .cuda() first)")
+        if t.dtype != torch.float32:
+            raise TypeError(f"expected float32 tensors, got {t.dtype}")
+        if not t.is_contiguous():
+            raise ValueError("expected contiguous tensors")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_of(t: torch.Tensor):
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)

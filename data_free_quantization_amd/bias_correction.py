@@ -1,0 +1,182 @@
+"""Drop-in for the reference's ``bias_correction.py`` (bias_correction.py:1-258).
+
+The host walk is the reference's, quirks included:
+it iterates ``enumerate(graph.values())`` and looks the *index* up in
+``bottoms`` (:185-190), so with opaque graph keys every layer is skipped (the
+reference's effective no-op), and with positional keys the coded arithmetic runs.
+The arithmetic is HIP:
+  * E[o,i] = sum_k (Q(W) - W)[o,i,k]   -- the quantize sweep's error sums
+    (``_quantize_error`` + spatial sum, :128-131,231)
+  * expect from BN fake stats            -- ``dfq_bc_expect`` (:33-53,170-172)
+  * bias += mean_j (E + expect)[o, j]     -- ``dfq_bc_apply`` (:61-106)
+  * next BN fake_bias += mean over rows   -- ``dfq_bc_propagate`` (:206-213)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import logging
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .utils.layer_transform import find_prev_bn
+from .utils.quantize import fake_quant
+
+logging.basicConfig(level=logging.INFO)
+logger = logging.getLogger(__name__)
+
+
+def _bc_expect(bn_weight, bn_bias, relu, out=None):
+    """calculate_mean (γφ(-β/γ) + β(1-Φ(-β/γ)), clamped at 0) when a ReLU follows the
+    BN, else β; ``out`` given: accumulate into it (the 'add' branch sum)."""
+    _lib.require_device(bn_weight, bn_bias, out)
+    acc = out is not None
+    if out is None:
+        out = torch.empty_like(bn_bias)
+    rc = _lib.load().dfq_bc_expect(_lib.ptr(bn_weight), _lib.ptr(bn_bias), bn_bias.numel(), int(bool(relu)),
+                                   int(acc), _lib.ptr(out), _lib.stream_of(bn_bias))
+    _lib.check(rc, "dfq_bc_expect")
+    return out
+
+
+def _calculate_bias_correction_for_branches(bn_branch, calculate_mean=None):
+    """bias_correction.py:15-58 (``calculate_mean`` is the HIP expectation)."""
+    res = {}
+    for key, branch in bn_branch.items():
+        cum = None
+        connect_type = None
+        for layer, relu_attached, connect_type in branch:
+            if connect_type == "cat":
+                e = _bc_expect(layer.fake_weight, layer.fake_bias, relu_attached)
+                cum = e if cum is None else torch.cat([cum, e])
+            elif cum is None:
+                cum = _bc_expect(layer.fake_weight, layer.fake_bias, relu_attached)
+            else:
+                _bc_expect(layer.fake_weight, layer.fake_bias, relu_attached, out=cum)
+        res[key] = (connect_type, cum)
+    return res
+
+
+def _broadcast_cols(i2: int, f: int) -> int:
+    if i2 == f or f == 1:
+        return i2
+    if i2 == 1:
+        return f
+    raise RuntimeError(f"The size of tensor a ({i2}) must match the size of tensor b ({f}) at non-singleton "
+                       "dimension 1")
+
+
+def _apply_bias_correction_E(layer, E, o, i2, connect_type, expect):
+    """_compute_final_bias_correction + _apply_bias_correction (:61-106) on the
+    device; returns the [o*bcols] bias_vec (kept for the next BN)."""
+    if connect_type == "cat":
+        # torch.cat([eps (2-D), expect (1-D)]) raises in the reference (:74-75)
+        raise RuntimeError("Tensors must have same number of dimensions: got 2 and 1")
+    if layer.bias is None:   # :89-90 references an undefined `nn`
+        raise NameError("name 'nn' is not defined")
+    f = expect.numel()
+    bcols = _broadcast_cols(i2, f)
+    if o * bcols <= o:
+        logger.error("Error in applying bias correction: Bias correction shape mismatch that cannot be handled "
+                     "automatically.")
+        raise ValueError("Bias correction shape mismatch that cannot be handled automatically.")
+    vec = torch.empty(o * bcols, dtype=torch.float32, device=E.device)
+    out_cols = C.c_int64(0)
+    rc = _lib.load().dfq_bc_apply(_lib.ptr(E), o, i2, _lib.ptr(expect), f, _lib.ptr(layer.bias.data),
+                                  _lib.ptr(vec), C.byref(out_cols), _lib.stream_of(E))
+    _lib.check(rc, "dfq_bc_apply", ValueError)
+    return vec
+
+
+def _quantize_error(param, num_bits=8, reduction="none", signed=False):
+    """bias_correction.py:111-144: Q(param) - param (per-tensor range), reduced."""
+    x = param.detach().contiguous()
+    r = fake_quant(x, num_bits, symmetric=signed, want_codes=False, khw=1, want_esum=True)
+    err = r.esum.view_as(x)
+    if reduction == "sum":
+        return torch.sum(torch.abs(err))
+    if reduction == "mean":
+        return torch.mean(torch.abs(err))
+    if reduction == "channel":
+        return torch.sum(torch.abs(err.view(err.size(0), -1)), dim=-1)
+    if reduction == "spatial":
+        return torch.sum(torch.abs(err.view(err.size(0), err.size(1), -1)), dim=-1)
+    if reduction == "none" or reduction is None:
+        return err
+    raise ValueError(f"Unknown reduction method: {reduction}")
+
+
+def _error_sums(weight, bits, signed, precomputed=None):
+    """E [O, I] = sum over KH*KW of the per-tensor quantization error."""
+    o, i2 = weight.size(0), weight.size(1)
+    khw = weight.numel() // (o * i2)
+    if precomputed is not None:
+        return precomputed.view(o, i2), o, i2
+    r = fake_quant(weight.detach().contiguous(), bits, symmetric=signed, want_codes=False, khw=khw,
+                   want_esum=True)
+    return r.esum.view(o, i2), o, i2
+
+
+def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.BatchNorm2d, signed=False, *,
+                    error_sums=None):
+    """Returns (bias_before_correction, bias_after_correction) keyed "layer_<idx>".
+
+    ``error_sums`` (extension, ``--bc_mode fused``): {graph key: E} from the fused
+    quantize sweep, used instead of re-quantizing the (already quantized) weight."""
+    assert isinstance(graph, dict), "Expected 'graph' to be a dictionary."
+    assert isinstance(bottoms, dict), "Expected 'bottoms' to be a dictionary."
+    assert isinstance(targ_type, (type, tuple)), "Expected 'targ_type' to be a type or tuple of types."
+    logger.info("Starting bias correction...")
+    bn_module, relu_attached = {}, {}
+    bias_prev = None        # device bias_vec of the last corrected layer (negated when used)
+    bias = None             # persists across layers like the reference's local
+    before, after = {}, {}
+    keys = list(graph.keys())
+    with torch.no_grad():
+        for idx_layer, layer in enumerate(graph.values()):
+            layer_name = f"layer_{idx_layer}"
+            if idx_layer not in bottoms:
+                logger.warning(f"Layer index {idx_layer} not found in bottoms")
+                continue
+            bot = bottoms[idx_layer]
+            if isinstance(layer, targ_type) and getattr(layer, "bias", None) is not None:
+                before[layer_name] = layer.bias.data.clone()
+            if bot is None or bot[0] == "Data":
+                continue
+            node = graph[idx_layer]
+            if isinstance(node, bn_type):
+                bn_module[idx_layer] = node
+                relu_attached[idx_layer] = False
+                if bias_prev is not None:
+                    f = node.fake_bias.size(0)
+                    if bias_prev.numel() == f:
+                        # fake_bias.add_(bias_prev) with a 2-D bias_prev cannot broadcast in place
+                        raise RuntimeError("output with shape [{}] doesn't match the broadcast shape".format(f))
+                    rc = _lib.load().dfq_bc_propagate(_lib.ptr(bias_prev), bias_prev.numel(),
+                                                      _lib.ptr(node.fake_bias), f, _lib.stream_of(bias_prev))
+                    _lib.check(rc, "dfq_bc_propagate", RuntimeError)
+                    bias_prev = None
+                continue
+            if isinstance(node, torch.nn.ReLU) and bot[0] in bn_module:
+                relu_attached[bot[0]] = True
+            if isinstance(node, targ_type):
+                bn_list, relu_list, type_list, _ = find_prev_bn(bn_module, relu_attached, graph, bottoms, bot[:])
+                pre = None if error_sums is None else error_sums.get(keys[idx_layer])
+                E, o, i2 = _error_sums(node.weight.data, bits_weight, signed, pre)
+                branches = {}
+                for j, (bn_layer, bid) in enumerate(bn_list):
+                    branches.setdefault(bid[0], []).append((bn_layer, relu_list[j], type_list[j]))
+                for connect_type, expect in _calculate_bias_correction_for_branches(branches).values():
+                    try:
+                        bias = _apply_bias_correction_E(node, E, o, i2, connect_type, expect)
+                    except ValueError as e:
+                        logger.error(f"Error in applying bias correction: {e}")
+                        raise
+                if bias is None:
+                    raise UnboundLocalError("local variable 'bias' referenced before assignment")
+                bias_prev = bias
+                if getattr(layer, "bias", None) is not None:
+                    after[layer_name] = layer.bias.data.clone()
+    logger.info("Bias correction completed.")
+    return before, after

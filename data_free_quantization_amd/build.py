@@ -1,0 +1,66 @@
+"""Build libdfq_hip.so (gfx950) in-tree with hipcc.
+
+The library is the product: plain C ABI (include/dfq_hip.h), loaded by
+``data_free_quantization_amd._lib`` through ctypes.  Built artefacts stay in the
+package directory so they travel to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "libdfq_hip.so"
+SOURCES = ["dfq_lib.hip", "dfq_sweep.hip", "dfq_transform.hip"]
+ARCH = os.environ.get("DFQ_OFFLOAD_ARCH", "gfx950")
+
+# -ffp-contract=off: no FMA contraction (bit parity with torch CPU eager ops).
+# Correctly-rounded fp32 divide/sqrt is hipcc's default; keep it explicit.
+FLAGS = [
+    "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+    "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+    "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or Path(c).exists()):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    deps = [CSRC / s for s in SOURCES] + [CSRC / "dfq_common.h", ROOT / "include" / "dfq_hip.h", Path(__file__)]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objs = []
+    for s in SOURCES:
+        obj = CSRC / (Path(s).stem + ".o")
+        cmd = [hipcc(), *FLAGS, "-I", str(ROOT / "include"), "-I", str(CSRC), "-c", str(CSRC / s), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        objs.append(str(obj))
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *objs]
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,615 @@
+// Grouped quantize-dequantize sweep over many fp32 weight tensors (gfx950).
+//
+// Replaces, for every target layer at once:
+//   * quantize()/UniformQuantize.forward          utils/quantize.py:16-89
+//   * quantize_targ_layer's per-layer loop         utils/layer_transform.py:288-305
+//   * clip_weight's clamp                          clip_weight.py:29
+//   * the bias-correction error reduction          bias_correction.py:128-131,231
+//
+// Work decomposition: every tensor is cut on the host into WAVE TASKS of at most
+// kChunk (2048) contiguous fp32 elements.  A task is either
+//   - "whole rows": up to kMaxRows complete rows; the wave reduces each row's
+//     min/max itself (CHANNEL modes, row_len <= kChunk), or
+//   - a "piece": its (min, max) come from a workspace slot filled by the
+//     reduce launch (TENSOR modes; CHANNEL rows longer than kChunk).
+// One wave owns one task at a time (no workgroup barriers): it streams the chunk
+// HBM -> VGPRs with 16-B loads, stages it in a wave-private LDS region for the
+// per-row reductions and the KHW error sums, and writes dq (16 B/lane), codes
+// (4 B/lane) and E.  Waves walk the task table grid-stride (persistent grid).
+#include "dfq_common.h"
+
+#include <algorithm>
+#include <new>
+#include <numeric>
+#include <vector>
+
+namespace dfq {
+
+constexpr int kChunk = 2048;                   // elements per wave task
+constexpr int kMaxRows = 256;                  // rows per whole-row task
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlockThreads = kWave * kWavesPerBlock;
+constexpr int kNV = kChunk / kWave;            // 32 scalar slots per lane
+constexpr int kNV4 = kChunk / (4 * kWave);     // 8 float4 slots per lane
+
+struct alignas(16) DevTensor {
+    const float* src;
+    float* dst;
+    void* codes;
+    float* scale;
+    float* zero;
+    float* esum;
+    int64_t rows;
+    int64_t row_len;
+    int32_t khw;
+    int32_t bits;
+    int32_t mode;
+    int32_t flags;
+    float clip_lo;
+    float clip_hi;
+    double given_min;
+    double given_max;
+    float inv_len;     // 1/row_len, for the element -> row map inside a task
+    int32_t vec4;      // 16-B loads / stores legal
+    int32_t code_bytes;
+    int32_t pad;
+};
+
+struct alignas(16) DevTask {
+    int64_t elem_start;  // first element (tensor-relative)
+    int32_t tensor;
+    int32_t n;           // elements in the task
+    int32_t row0;        // first row of a whole-row task / the row of a long-row piece
+    int32_t nrows;       // > 0: whole rows; 0: piece
+    int32_t slot;        // workspace (min,max) slot for pieces, -1 = given range
+    int32_t first;       // this piece writes scale/zero for its slot
+};
+
+struct WaveLds {
+    float data[kChunk];
+    float s[kMaxRows];
+    float mn[kMaxRows];
+};
+
+__device__ __forceinline__ bool is_sym(int mode) { return mode == DFQ_TENSOR_SYM || mode == DFQ_CHANNEL_SYM; }
+
+__device__ __forceinline__ void store_code(void* codes, int cb, int64_t idx, float q) {
+    if (cb == 1) {
+        static_cast<int8_t*>(codes)[idx] = (int8_t)(int)q;  // same bits as uint8 for 0..255
+    } else {
+        static_cast<int16_t*>(codes)[idx] = (int16_t)(int)q;
+    }
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+// HBM -> LDS without a VGPR landing (global_load_lds_dwordx4 / _dword): lane l's
+// bytes land at lds_base + l*size, so one wave-instruction fills a contiguous
+// 1 KiB (16 B/lane) or 256 B (4 B/lane) block of the task's LDS image.
+__device__ __forceinline__ void glds16(const float* g, float* lds_base) {
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const float* g, float* lds_base) {
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 4, 0, 0);
+}
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ---------------------------------------------------------------------------
+// Reduce launch: per-slot (min,max) of pieces via ordered-uint atomics.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlockThreads)
+sweep_reduce_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restrict__ tasks,
+                    int64_t ntasks, uint32_t* __restrict__ slot_min, uint32_t* __restrict__ slot_max) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + wave_uniform(threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t t = wave0; t < ntasks; t += nwaves) {
+        const DevTask task = tasks[t];
+        const DevTensor& T = tensors[task.tensor];
+        const float* src = T.src + task.elem_start;
+        float vmin = INFINITY, vmax = -INFINITY;
+        if (T.vec4) {
+            const int nj = task.n >> 2;
+#pragma unroll 8
+            for (int j = lane; j < nj; j += kWave) {
+                const float4 v = reinterpret_cast<const float4*>(src)[j];
+                vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+                vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+            }
+        } else {
+#pragma unroll 8
+            for (int e = lane; e < task.n; e += kWave) {
+                const float x = src[e];
+                vmin = fminf(vmin, x);
+                vmax = fmaxf(vmax, x);
+            }
+        }
+        vmin = wave_min(vmin);
+        vmax = wave_max(vmax);
+        if (lane == 0) {
+            atomicMin(&slot_min[task.slot], enc_ord(vmin));
+            atomicMax(&slot_max[task.slot], enc_ord(vmax));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Main launch: one wave task.
+// ---------------------------------------------------------------------------
+template <bool VEC>
+__device__ __forceinline__ void process_task(const DevTensor& T, const DevTask& task, WaveLds& L,
+                                             const uint32_t* __restrict__ slot_min,
+                                             const uint32_t* __restrict__ slot_max, int lane) {
+    const float* src = T.src + task.elem_start;
+    const int n = task.n;
+    const bool sym = is_sym(T.mode);
+    const int len = (int)T.row_len;
+
+    // 1. chunk HBM -> LDS by DMA; every load is in flight before the first wait
+    if constexpr (VEC) {
+        const int nj = n >> 2;
+        for (int m = 0; m * kWave < nj; ++m) {
+            const int j = lane + m * kWave;
+            if (j < nj) glds16(src + 4 * j, &L.data[4 * kWave * m]);
+        }
+    } else {
+        for (int m = 0; m * kWave < n; ++m) {
+            const int e = lane + m * kWave;
+            if (e < n) glds4(src + e, &L.data[kWave * m]);
+        }
+    }
+    vm_wait_all();
+    wave_lds_sync();
+
+    // 2. per-row parameters (whole-row tasks) or the slot's parameters (pieces)
+    QParams pc{};
+    const bool whole = task.nrows > 0;
+    if (whole) {
+        const int nrows = task.nrows;
+        if (len >= kWave) {
+            for (int r = 0; r < nrows; ++r) {
+                float vmin = INFINITY, vmax = -INFINITY;
+                const float* row = &L.data[r * len];
+                if (VEC) {
+                    for (int i = lane; 4 * i < len; i += kWave) {
+                        const float4 v = reinterpret_cast<const float4*>(row)[i];
+                        vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+                        vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+                    }
+                } else {
+                    for (int i = lane; i < len; i += kWave) {
+                        const float v = row[i];
+                        vmin = fminf(vmin, v);
+                        vmax = fmaxf(vmax, v);
+                    }
+                }
+                vmin = wave_min(vmin);
+                vmax = wave_max(vmax);
+                if (lane == 0) {
+                    const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
+                    L.s[r] = p.s;
+                    L.mn[r] = p.mn;
+                    const int64_t row_g = task.row0 + r;
+                    if (T.scale) T.scale[row_g] = p.s;
+                    if (T.zero) T.zero[row_g] = p.mn;
+                }
+            }
+        } else {
+            int seg = 1;
+            while (seg < len) seg <<= 1;
+            const int per_pass = kWave / seg;
+            const int sub = lane / seg, idx = lane % seg;
+            for (int r0 = 0; r0 < nrows; r0 += per_pass) {
+                const int r = r0 + sub;
+                const bool ok = (r < nrows) && (idx < len);
+                const float v = ok ? L.data[r * len + idx] : 0.f;
+                float vmin = ok ? v : INFINITY;
+                float vmax = ok ? v : -INFINITY;
+                for (int off = seg >> 1; off >= 1; off >>= 1) {
+                    vmin = fminf(vmin, __shfl_xor(vmin, off, kWave));
+                    vmax = fmaxf(vmax, __shfl_xor(vmax, off, kWave));
+                }
+                if (idx == 0 && r < nrows) {
+                    const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
+                    L.s[r] = p.s;
+                    L.mn[r] = p.mn;
+                    const int64_t row_g = task.row0 + r;
+                    if (T.scale) T.scale[row_g] = p.s;
+                    if (T.zero) T.zero[row_g] = p.mn;
+                }
+            }
+        }
+        wave_lds_sync();
+    } else {
+        float mn = 0.f, mx = 0.f;
+        if (task.slot >= 0) {
+            mn = dec_ord(slot_min[task.slot]);
+            mx = dec_ord(slot_max[task.slot]);
+        }
+        pc = make_qparams(mn, mx, T.bits, sym, T.flags, T.given_min, T.given_max);
+        if (task.first && lane == 0) {
+            const int64_t row_g = (T.mode == DFQ_CHANNEL_ASYM || T.mode == DFQ_CHANNEL_SYM) ? task.row0 : 0;
+            if (T.scale) T.scale[row_g] = pc.s;
+            if (T.zero) T.zero[row_g] = pc.mn;
+        }
+    }
+
+    // 3. quantize / dequantize / clip from LDS; write dq + codes; eps for bias correction.
+    //    eps overwrites the x it came from (same lane, same slot), so no hazard.
+    const bool clip = (T.flags & DFQ_CLIP) != 0;
+    const bool want_e = T.esum != nullptr;
+    const int khw = T.khw;
+    const float qmin = sym ? -(float)(1 << (T.bits - 1)) : 0.f;
+    const float qmax = sym ? (float)((1 << (T.bits - 1)) - 1) : (float)((1 << T.bits) - 1);
+    const int64_t base = task.elem_start;
+
+    auto params_for = [&](int e) -> QParams {
+        if (!whole) return pc;
+        // row = floor(e / len): (e + 0.5)/len is >= 0.5/len from an integer and
+        // e < 2048, so this fp32 estimate is exact.
+        int r = (int)(((float)e + 0.5f) * T.inv_len);
+        r = min(r, kMaxRows - 1);
+        QParams p;
+        p.s = L.s[r];
+        p.mn = L.mn[r];
+        p.negmn = -p.mn;
+        p.qmin = qmin;
+        p.qmax = qmax;
+        return p;
+    };
+    auto one = [&](float xv, const QParams& p, float& qv) -> float {
+        float yv = qdq(xv, p, qv);
+        if (clip) yv = fminf(fmaxf(yv, T.clip_lo), T.clip_hi);
+        return yv;
+    };
+
+    if constexpr (VEC) {
+        const int nj = n >> 2;
+#pragma unroll 2
+        for (int j = lane; j < nj; j += kWave) {
+            const float4 xv = reinterpret_cast<const float4*>(L.data)[j];
+            const QParams p = params_for(4 * j);   // 4 | len: one row per float4
+            float q0, q1, q2, q3;
+            const float y0 = one(xv.x, p, q0);
+            const float y1 = one(xv.y, p, q1);
+            const float y2 = one(xv.z, p, q2);
+            const float y3 = one(xv.w, p, q3);
+            if (T.dst) reinterpret_cast<float4*>(T.dst + base)[j] = make_float4(y0, y1, y2, y3);
+            if (T.codes) {
+                if (T.code_bytes == 1) {
+                    const uint32_t c = ((uint32_t)(uint8_t)(int)q0) | ((uint32_t)(uint8_t)(int)q1 << 8) |
+                                       ((uint32_t)(uint8_t)(int)q2 << 16) | ((uint32_t)(uint8_t)(int)q3 << 24);
+                    reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base)[j] = c;
+                } else {
+                    const uint2 c = make_uint2(((uint32_t)(uint16_t)(int)q0) | ((uint32_t)(uint16_t)(int)q1 << 16),
+                                               ((uint32_t)(uint16_t)(int)q2) | ((uint32_t)(uint16_t)(int)q3 << 16));
+                    reinterpret_cast<uint2*>(static_cast<uint16_t*>(T.codes) + base)[j] = c;
+                }
+            }
+            if (want_e) {
+                const float4 ev = make_float4(y0 - xv.x, y1 - xv.y, y2 - xv.z, y3 - xv.w);
+                if (khw == 1) reinterpret_cast<float4*>(T.esum + base)[j] = ev;
+                else reinterpret_cast<float4*>(L.data)[j] = ev;
+            }
+        }
+    } else {
+#pragma unroll 4
+        for (int e = lane; e < n; e += kWave) {
+            const float xv = L.data[e];
+            float qv;
+            const float yv = one(xv, params_for(e), qv);
+            if (T.dst) T.dst[base + e] = yv;
+            if (T.codes) store_code(T.codes, T.code_bytes, base + e, qv);
+            if (want_e) {
+                if (khw == 1) T.esum[base + e] = yv - xv;
+                else L.data[e] = yv - xv;
+            }
+        }
+    }
+
+    // 4. KHW error sums: E[p] = sum_k eps[p*khw + k], k ascending
+    if (want_e && khw > 1) {
+        wave_lds_sync();
+        const int np = n / khw;
+        const int64_t pbase = base / khw;
+        for (int pi = lane; pi < np; pi += kWave) {
+            float acc = 0.f;
+            for (int k = 0; k < khw; ++k) acc += L.data[pi * khw + k];
+            T.esum[pbase + pi] = acc;
+        }
+    }
+    wave_lds_sync();  // LDS is reused by this wave's next task
+}
+
+__global__ void __launch_bounds__(kBlockThreads)
+sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restrict__ tasks, int64_t ntasks,
+                  const uint32_t* __restrict__ slot_min, const uint32_t* __restrict__ slot_max) {
+    __shared__ WaveLds lds[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = wave_uniform(threadIdx.x >> 6);
+    const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + w;
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t t = wave0; t < ntasks; t += nwaves) {
+        const DevTask task = tasks[t];
+        const DevTensor T = tensors[task.tensor];
+        if (T.vec4) process_task<true>(T, task, lds[w], slot_min, slot_max, lane);
+        else process_task<false>(T, task, lds[w], slot_min, slot_max, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host: validation, task building, plans.
+// ---------------------------------------------------------------------------
+static bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+static int validate(const dfq_tensor_desc& d) {
+    if (d.rows < 0 || d.row_len < 0) return DFQ_ERR_INVALID;
+    if (!d.src && d.rows * d.row_len > 0) return DFQ_ERR_INVALID;
+    if (d.bits < 2 || d.bits > 16) return DFQ_ERR_INVALID;
+    if (d.mode < DFQ_TENSOR_ASYM || d.mode > DFQ_CHANNEL_SYM) return DFQ_ERR_INVALID;
+    if (d.khw < 1) return DFQ_ERR_INVALID;
+    if (d.esum && (d.row_len % d.khw) != 0) return DFQ_ERR_SHAPE;
+    if (d.rows > INT32_MAX) return DFQ_ERR_UNSUPPORTED;
+    const bool channel = d.mode >= DFQ_CHANNEL_ASYM;
+    if (channel && (d.flags & DFQ_GIVEN_RANGE)) return DFQ_ERR_INVALID;
+    return DFQ_OK;
+}
+
+struct Built {
+    std::vector<DevTensor> tensors;
+    std::vector<DevTask> reduce;
+    std::vector<DevTask> main;
+    int64_t slots = 0;
+    int64_t elems = 0;
+    int64_t algo_bytes = 0;
+};
+
+static DevTensor to_dev(const dfq_tensor_desc& d) {
+    DevTensor t{};
+    t.src = d.src; t.dst = d.dst; t.codes = d.codes; t.scale = d.scale; t.zero = d.zero; t.esum = d.esum;
+    t.rows = d.rows; t.row_len = d.row_len; t.khw = d.khw; t.bits = d.bits; t.mode = d.mode;
+    t.flags = d.flags; t.clip_lo = d.clip_lo; t.clip_hi = d.clip_hi;
+    t.given_min = d.given_min; t.given_max = d.given_max;
+    t.inv_len = d.row_len > 0 ? 1.0f / (float)d.row_len : 0.f;
+    t.code_bytes = d.bits <= 8 ? 1 : 2;
+    const int64_t n = d.rows * d.row_len;
+    const bool channel = d.mode >= DFQ_CHANNEL_ASYM;
+    bool v = (n % 4 == 0) && aligned(d.src, 16) && (!d.dst || aligned(d.dst, 16)) &&
+             (!d.codes || aligned(d.codes, 4 * t.code_bytes)) &&
+             (!d.esum || d.khw > 1 || aligned(d.esum, 16));
+    if (channel) v = v && (d.row_len % 4 == 0);
+    t.vec4 = v ? 1 : 0;
+    return t;
+}
+
+// Piece length: a multiple of khw (E sums never straddle a piece) and of 4 (vec4).
+static int piece_len(int khw, bool vec4) {
+    const int unit = vec4 ? std::lcm(4, khw) : khw;
+    int p = (kChunk / unit) * unit;
+    return p > 0 ? p : -1;
+}
+
+static int build(const dfq_tensor_desc* descs, int32_t n, Built& B) {
+    for (int32_t ti = 0; ti < n; ++ti) {
+        const dfq_tensor_desc& d = descs[ti];
+        int rc = validate(d);
+        if (rc) return rc;
+        DevTensor T = to_dev(d);
+        const int64_t total = d.rows * d.row_len;
+        B.elems += total;
+        // algorithmic bytes: read x, write dq / codes / E / per-row params once
+        int64_t bytes = 4 * total;
+        if (d.dst) bytes += 4 * total;
+        if (d.codes) bytes += (int64_t)T.code_bytes * total;
+        if (d.esum) bytes += 4 * (total / d.khw);
+        const bool channel = d.mode >= DFQ_CHANNEL_ASYM;
+        const int64_t nparams = channel ? d.rows : 1;
+        if (d.scale) bytes += 4 * nparams;
+        if (d.zero) bytes += 4 * nparams;
+        B.algo_bytes += bytes;
+        B.tensors.push_back(T);
+        if (total == 0) continue;
+        const int plen = piece_len(d.khw, T.vec4);
+        if (plen <= 0) return DFQ_ERR_UNSUPPORTED;   // khw > kChunk
+        if (channel && d.row_len <= kChunk) {
+            const int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(kMaxRows, kChunk / d.row_len));
+            for (int64_t r = 0; r < d.rows; r += rpt) {
+                const int64_t nr = std::min<int64_t>(rpt, d.rows - r);
+                DevTask k{};
+                k.elem_start = r * d.row_len; k.tensor = ti; k.n = (int32_t)(nr * d.row_len);
+                k.row0 = (int32_t)r; k.nrows = (int32_t)nr; k.slot = -1; k.first = 0;
+                B.main.push_back(k);
+            }
+        } else if (channel) {   // long rows: one slot per row
+            for (int64_t r = 0; r < d.rows; ++r) {
+                const int64_t slot = B.slots++;
+                for (int64_t off = 0; off < d.row_len; off += plen) {
+                    DevTask k{};
+                    k.elem_start = r * d.row_len + off; k.tensor = ti;
+                    k.n = (int32_t)std::min<int64_t>(plen, d.row_len - off);
+                    k.row0 = (int32_t)r; k.nrows = 0; k.slot = (int32_t)slot; k.first = (off == 0);
+                    B.reduce.push_back(k);
+                    B.main.push_back(k);
+                }
+            }
+        } else {                // tensor modes: one slot per tensor (none for a given range)
+            const bool given = (d.flags & DFQ_GIVEN_RANGE) != 0;
+            const int64_t slot = given ? -1 : B.slots++;
+            for (int64_t off = 0; off < total; off += plen) {
+                DevTask k{};
+                k.elem_start = off; k.tensor = ti; k.n = (int32_t)std::min<int64_t>(plen, total - off);
+                k.row0 = 0; k.nrows = 0; k.slot = (int32_t)slot; k.first = (off == 0);
+                if (!given) B.reduce.push_back(k);
+                B.main.push_back(k);
+            }
+        }
+    }
+    return DFQ_OK;
+}
+
+static int grid_for(int64_t ntasks) {
+    // persistent grid: 4 blocks (16 waves) per CU on 256 CUs, fewer if there is little work
+    const int64_t want = ceil_div(ntasks, kWavesPerBlock);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(want, 256 * 4));
+}
+
+}  // namespace dfq
+
+using namespace dfq;
+
+struct dfq_sweep_plan {
+    DevTensor* d_tensors = nullptr;
+    DevTask* d_reduce = nullptr;
+    DevTask* d_main = nullptr;
+    uint32_t* d_slots = nullptr;   // [slots] mins then [slots] maxs
+    int64_t n_reduce = 0, n_main = 0, n_slots = 0, n_tensors = 0, n_elems = 0, algo_bytes = 0;
+};
+
+extern "C" int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, dfq_sweep_plan** out) {
+    if (!out || (n > 0 && !descs) || n < 0) return DFQ_ERR_INVALID;
+    *out = nullptr;
+    Built B;
+    int rc = build(descs, n, B);
+    if (rc) return rc;
+    dfq_sweep_plan* p = new (std::nothrow) dfq_sweep_plan();
+    if (!p) return DFQ_ERR_NOMEM;
+    p->n_reduce = (int64_t)B.reduce.size();
+    p->n_main = (int64_t)B.main.size();
+    p->n_slots = B.slots;
+    p->n_tensors = n;
+    p->n_elems = B.elems;
+    p->algo_bytes = B.algo_bytes;
+    auto fail = [&](hipError_t e) {
+        set_last_hip_error(e);
+        (void)hipFree(p->d_tensors); (void)hipFree(p->d_reduce); (void)hipFree(p->d_main); (void)hipFree(p->d_slots);
+        delete p;
+        return DFQ_ERR_HIP;
+    };
+    hipError_t e;
+    if (n > 0) {
+        if ((e = hipMalloc(&p->d_tensors, sizeof(DevTensor) * n)) != hipSuccess) return fail(e);
+        if ((e = hipMemcpy(p->d_tensors, B.tensors.data(), sizeof(DevTensor) * n, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    }
+    if (p->n_reduce > 0) {
+        if ((e = hipMalloc(&p->d_reduce, sizeof(DevTask) * p->n_reduce)) != hipSuccess) return fail(e);
+        if ((e = hipMemcpy(p->d_reduce, B.reduce.data(), sizeof(DevTask) * p->n_reduce, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    }
+    if (p->n_main > 0) {
+        if ((e = hipMalloc(&p->d_main, sizeof(DevTask) * p->n_main)) != hipSuccess) return fail(e);
+        if ((e = hipMemcpy(p->d_main, B.main.data(), sizeof(DevTask) * p->n_main, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    }
+    if (p->n_slots > 0) {
+        if ((e = hipMalloc(&p->d_slots, sizeof(uint32_t) * 2 * p->n_slots)) != hipSuccess) return fail(e);
+    }
+    *out = p;
+    return DFQ_OK;
+}
+
+extern "C" int dfq_sweep_plan_execute(dfq_sweep_plan* p, void* stream) {
+    if (!p) return DFQ_ERR_INVALID;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (p->n_reduce > 0) {
+        DFQ_HIP_CHECK(hipMemsetAsync(p->d_slots, 0xFF, sizeof(uint32_t) * p->n_slots, s));
+        DFQ_HIP_CHECK(hipMemsetAsync(p->d_slots + p->n_slots, 0x00, sizeof(uint32_t) * p->n_slots, s));
+        hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for(p->n_reduce)), dim3(kBlockThreads), 0, s,
+                           p->d_tensors, p->d_reduce, p->n_reduce, p->d_slots, p->d_slots + p->n_slots);
+        DFQ_LAUNCH_CHECK();
+    }
+    if (p->n_main > 0) {
+        hipLaunchKernelGGL(sweep_main_kernel, dim3(grid_for(p->n_main)), dim3(kBlockThreads), 0, s,
+                           p->d_tensors, p->d_main, p->n_main, p->d_slots, p->d_slots + p->n_slots);
+        DFQ_LAUNCH_CHECK();
+    }
+    return DFQ_OK;
+}
+
+extern "C" int dfq_sweep_plan_stats(const dfq_sweep_plan* p, dfq_sweep_stats* st) {
+    if (!p || !st) return DFQ_ERR_INVALID;
+    st->n_tensors = p->n_tensors;
+    st->n_elems = p->n_elems;
+    st->n_tasks_reduce = p->n_reduce;
+    st->n_tasks_main = p->n_main;
+    st->algo_bytes = p->algo_bytes;
+    st->launches = (p->n_reduce > 0 ? 1 : 0) + (p->n_main > 0 ? 1 : 0);
+    st->grid_blocks = p->n_main > 0 ? grid_for(p->n_main) : 0;
+    return DFQ_OK;
+}
+
+extern "C" int dfq_sweep_plan_destroy(dfq_sweep_plan* p) {
+    if (!p) return DFQ_OK;
+    (void)hipFree(p->d_tensors); (void)hipFree(p->d_reduce); (void)hipFree(p->d_main); (void)hipFree(p->d_slots);
+    delete p;
+    return DFQ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Single-tensor path: tasks are uploaded into the caller's workspace with
+// hipMemcpyAsync from a per-call host staging vector kept alive by a stream
+// callback-free scheme: the workspace carries [slots | tensor | tasks] and the
+// host copy is made from pinned-agnostic memory, so we synchronise the copy
+// only (hipMemcpyAsync on pageable memory stages synchronously).
+// ---------------------------------------------------------------------------
+namespace dfq {
+static size_t single_ws_layout(const Built& B, size_t* off_tensor, size_t* off_reduce, size_t* off_main) {
+    size_t o = 0;
+    o += sizeof(uint32_t) * 2 * (size_t)B.slots;
+    o = (o + 63) & ~size_t(63);
+    *off_tensor = o; o += sizeof(DevTensor) * B.tensors.size();
+    o = (o + 63) & ~size_t(63);
+    *off_reduce = o; o += sizeof(DevTask) * B.reduce.size();
+    o = (o + 63) & ~size_t(63);
+    *off_main = o; o += sizeof(DevTask) * B.main.size();
+    return o;
+}
+}  // namespace dfq
+
+extern "C" int dfq_quantize_ws_bytes(const dfq_tensor_desc* d, size_t* bytes) {
+    if (!d || !bytes) return DFQ_ERR_INVALID;
+    Built B;
+    int rc = build(d, 1, B);
+    if (rc) return rc;
+    size_t a, b, c;
+    *bytes = single_ws_layout(B, &a, &b, &c);
+    return DFQ_OK;
+}
+
+extern "C" int dfq_quantize_tensor(const dfq_tensor_desc* d, void* ws, size_t ws_bytes, void* stream) {
+    if (!d) return DFQ_ERR_INVALID;
+    Built B;
+    int rc = build(d, 1, B);
+    if (rc) return rc;
+    size_t ot, orr, om;
+    const size_t need = single_ws_layout(B, &ot, &orr, &om);
+    if (!ws || ws_bytes < need) return DFQ_ERR_WORKSPACE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    char* base = static_cast<char*>(ws);
+    uint32_t* slots = reinterpret_cast<uint32_t*>(base);
+    DevTensor* dt = reinterpret_cast<DevTensor*>(base + ot);
+    DevTask* dr = reinterpret_cast<DevTask*>(base + orr);
+    DevTask* dm = reinterpret_cast<DevTask*>(base + om);
+    // Pageable host->device async copies are staged before hipMemcpyAsync returns,
+    // so the local vectors may be released afterwards.
+    DFQ_HIP_CHECK(hipMemcpyAsync(dt, B.tensors.data(), sizeof(DevTensor), hipMemcpyHostToDevice, s));
+    if (!B.reduce.empty())
+        DFQ_HIP_CHECK(hipMemcpyAsync(dr, B.reduce.data(), sizeof(DevTask) * B.reduce.size(), hipMemcpyHostToDevice, s));
+    if (!B.main.empty())
+        DFQ_HIP_CHECK(hipMemcpyAsync(dm, B.main.data(), sizeof(DevTask) * B.main.size(), hipMemcpyHostToDevice, s));
+    if (!B.reduce.empty()) {
+        DFQ_HIP_CHECK(hipMemsetAsync(slots, 0xFF, sizeof(uint32_t) * B.slots, s));
+        DFQ_HIP_CHECK(hipMemsetAsync(slots + B.slots, 0x00, sizeof(uint32_t) * B.slots, s));
+        hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for((int64_t)B.reduce.size())), dim3(kBlockThreads), 0, s,
+                           dt, dr, (int64_t)B.reduce.size(), slots, slots + B.slots);
+        DFQ_LAUNCH_CHECK();
+    }
+    if (!B.main.empty()) {
+        hipLaunchKernelGGL(sweep_main_kernel, dim3(grid_for((int64_t)B.main.size())), dim3(kBlockThreads), 0, s,
+                           dt, dm, (int64_t)B.main.size(), slots, slots + B.slots);
+        DFQ_LAUNCH_CHECK();
+    }
+    // The staging copies above read host vectors that die at return: make sure the
+    // runtime has consumed them (pageable memcpy is host-synchronous on ROCm, but
+    // do not rely on it for correctness).
+    DFQ_HIP_CHECK(hipStreamSynchronize(s));
+    return DFQ_OK;
+}

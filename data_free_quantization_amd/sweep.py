@@ -1,0 +1,119 @@
+"""Grouped weight sweep: many tensors, one (or two) kernel launches.
+
+Host wrapper of ``dfq_sweep_plan_*`` (include/dfq_hip.h).  A ``SweepPlan`` keeps
+every tensor it references alive; ``execute()`` is asynchronous on the current
+stream and replays with no host work beyond one C call.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib
+
+
+@dataclass
+class SweepItem:
+    """One fp32 tensor viewed as [rows, row_len] and what to write for it."""
+    src: torch.Tensor
+    bits: int = 8
+    per_channel: bool = True
+    symmetric: bool = True
+    dst: Optional[torch.Tensor] = None       # dequantized output (may be src)
+    codes: Optional[torch.Tensor] = None
+    scale: Optional[torch.Tensor] = None
+    zero: Optional[torch.Tensor] = None
+    esum: Optional[torch.Tensor] = None
+    khw: int = 1
+    clip: Optional[Sequence[float]] = None
+    rows: Optional[int] = None
+
+    def mode(self) -> int:
+        if self.per_channel:
+            return _lib.DFQ_CHANNEL_SYM if self.symmetric else _lib.DFQ_CHANNEL_ASYM
+        return _lib.DFQ_TENSOR_SYM if self.symmetric else _lib.DFQ_TENSOR_ASYM
+
+
+def code_dtype(bits: int, symmetric: bool) -> torch.dtype:
+    if bits <= 8:
+        return torch.int8 if symmetric else torch.uint8
+    return torch.int16
+
+
+def allocate(src: torch.Tensor, bits=8, per_channel=True, symmetric=True, khw=1, in_place=False,
+             want_codes=True, want_esum=False, clip=None) -> SweepItem:
+    """A SweepItem with freshly allocated outputs on src's device."""
+    rows = src.shape[0] if (per_channel and src.dim() > 0) else 1
+    npar = rows if per_channel else 1
+    dev = src.device
+    return SweepItem(
+        src=src, bits=bits, per_channel=per_channel, symmetric=symmetric,
+        dst=src if in_place else torch.empty_like(src),
+        codes=torch.empty(src.shape, dtype=code_dtype(bits, symmetric), device=dev) if want_codes else None,
+        scale=torch.empty(npar, dtype=torch.float32, device=dev),
+        zero=torch.empty(npar, dtype=torch.float32, device=dev),
+        esum=torch.empty(src.numel() // khw, dtype=torch.float32, device=dev) if want_esum else None,
+        khw=khw, clip=clip, rows=rows)
+
+
+class SweepPlan:
+    def __init__(self, items: List[SweepItem]):
+        self.items = list(items)
+        L = _lib.load()
+        descs = (_lib.TensorDesc * max(len(self.items), 1))()
+        for i, it in enumerate(self.items):
+            _lib.require_device(it.src, it.dst, it.scale, it.zero, it.esum)
+            if it.codes is not None and not it.codes.is_cuda:
+                raise RuntimeError("codes must live on the GPU")
+            rows = it.rows if it.rows is not None else (it.src.shape[0] if (it.per_channel and it.src.dim()) else 1)
+            d = descs[i]
+            d.src = it.src.data_ptr()
+            d.dst = it.dst.data_ptr() if it.dst is not None else None
+            d.codes = it.codes.data_ptr() if it.codes is not None else None
+            d.scale = it.scale.data_ptr() if it.scale is not None else None
+            d.zero = it.zero.data_ptr() if it.zero is not None else None
+            d.esum = it.esum.data_ptr() if it.esum is not None else None
+            d.rows = rows
+            d.row_len = it.src.numel() // rows if rows else 0
+            d.khw = it.khw
+            d.bits = it.bits
+            d.mode = it.mode()
+            d.flags = _lib.DFQ_CLIP if it.clip is not None else 0
+            if it.clip is not None:
+                d.clip_lo, d.clip_hi = float(it.clip[0]), float(it.clip[1])
+        self._plan = C.c_void_p()
+        _lib.check(L.dfq_sweep_plan_create(descs, len(self.items), C.byref(self._plan)), "dfq_sweep_plan_create",
+                   ValueError)
+        st = _lib.SweepStats()
+        _lib.check(L.dfq_sweep_plan_stats(self._plan, C.byref(st)), "dfq_sweep_plan_stats")
+        self.stats = {f: getattr(st, f) for f, _ in _lib.SweepStats._fields_}
+        self._device = self.items[0].src.device if self.items else None
+
+    def execute(self, stream: Optional[torch.cuda.Stream] = None):
+        if self._plan is None:
+            raise RuntimeError("plan destroyed")
+        if not self.items:
+            return
+        s = stream if stream is not None else torch.cuda.current_stream(self._device)
+        _lib.check(_lib.load().dfq_sweep_plan_execute(self._plan, C.c_void_p(s.cuda_stream)),
+                   "dfq_sweep_plan_execute")
+
+    def destroy(self):
+        if self._plan is not None and self._plan.value:
+            torch.cuda.synchronize(self._device)
+            _lib.load().dfq_sweep_plan_destroy(self._plan)
+        self._plan = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def khw_of(weight: torch.Tensor) -> int:
+    """Spatial size KH*KW of a KCRS conv weight (1 for Linear)."""
+    return int(weight[0, 0].numel()) if weight.dim() >= 3 else 1

@@ -1,0 +1,345 @@
+"""Drop-in for the reference's ``utils/quantize.py`` (utils/quantize.py:1-379).
+
+Same names, signatures and semantics; the fake-quant arithmetic runs in the HIP
+kernel ``dfq_quantize_tensor`` (libdfq_hip.so), bit-exact with the reference's
+CPU path.  Extensions are additive keyword arguments or
+new functions (``quantize_per_channel``, ``fake_quant``).
+
+Tensors must live on a ROCm device; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.autograd.function import InplaceFunction
+
+from .. import _lib
+
+
+@dataclass
+class QuantResult:
+    """Outputs of one fake-quant call (extension API)."""
+    dq: torch.Tensor                 # dequantized fp32, same shape as the input
+    codes: Optional[torch.Tensor]    # integer grid indices (uint8/int8/int16)
+    scale: torch.Tensor              # [rows] or [1]
+    zero: torch.Tensor               # [rows] or [1] (the range min for asym, 0 for sym)
+    esum: Optional[torch.Tensor] = None
+
+
+def _code_dtype(bits: int, symmetric: bool):
+    if bits <= 8:
+        return torch.int8 if symmetric else torch.uint8
+    return torch.int16
+
+
+def _is_tensor_value(v) -> bool:
+    return isinstance(v, torch.Tensor)
+
+
+def fake_quant(x: torch.Tensor, num_bits: int = 8, *, per_channel: bool = False, symmetric: bool = False,
+               min_value=None, max_value=None, out: Optional[torch.Tensor] = None, want_codes: bool = True,
+               khw: int = 1, want_esum: bool = False, clip=None, scale_f32: bool = False) -> QuantResult:
+    """Quantize-dequantize ``x`` (viewed as [x.shape[0], -1] in per-channel mode)
+    on the GPU.  ``min_value``/``max_value`` (Python floats) fix the per-tensor
+    range like quantize(x, b, min, max); otherwise the data range is used."""
+    _lib.require_device(x, out)
+    L = _lib.load()
+    rows = x.shape[0] if (per_channel and x.dim() > 0) else 1
+    n = x.numel()
+    row_len = n // rows if rows else 0
+    d = _lib.TensorDesc()
+    d.src = x.data_ptr()
+    dq = torch.empty_like(x) if out is None else out
+    d.dst = dq.data_ptr()
+    codes = torch.empty(x.shape, dtype=_code_dtype(num_bits, symmetric), device=x.device) if want_codes else None
+    d.codes = codes.data_ptr() if codes is not None else None
+    npar = rows if per_channel else 1
+    scale = torch.empty(npar, dtype=torch.float32, device=x.device)
+    zero = torch.empty(npar, dtype=torch.float32, device=x.device)
+    d.scale, d.zero = scale.data_ptr(), zero.data_ptr()
+    esum = None
+    if want_esum:
+        esum = torch.empty(n // khw, dtype=torch.float32, device=x.device)
+        d.esum = esum.data_ptr()
+    d.rows, d.row_len, d.khw, d.bits = rows, row_len, khw, num_bits
+    d.mode = (_lib.DFQ_CHANNEL_SYM if symmetric else _lib.DFQ_CHANNEL_ASYM) if per_channel else \
+        (_lib.DFQ_TENSOR_SYM if symmetric else _lib.DFQ_TENSOR_ASYM)
+    flags = 0
+    if clip is not None:
+        flags |= _lib.DFQ_CLIP
+        d.clip_lo, d.clip_hi = float(clip[0]), float(clip[1])
+    if min_value is not None or max_value is not None:
+        if per_channel:
+            raise ValueError("a fixed range is per-tensor only")
+        flags |= _lib.DFQ_GIVEN_RANGE
+        d.given_min, d.given_max = float(min_value), float(max_value)
+    if scale_f32:
+        flags |= _lib.DFQ_SCALE_F32
+    d.flags = flags
+    if n == 0:
+        return QuantResult(dq, codes, scale, zero, esum)
+    ws_bytes = C.c_size_t(0)
+    _lib.check(L.dfq_quantize_ws_bytes(C.byref(d), C.byref(ws_bytes)), "dfq_quantize_ws_bytes", ValueError)
+    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=x.device)
+    _lib.check(L.dfq_quantize_tensor(C.byref(d), C.c_void_p(ws.data_ptr()), ws_bytes, _lib.stream_of(x)),
+               "dfq_quantize_tensor", ValueError)
+    return QuantResult(dq, codes, scale, zero, esum)
+
+
+class UniformQuantize(InplaceFunction):
+    """Uniform quantize -> dequantize with a straight-through backward
+    (utils/quantize.py:16-85)."""
+
+    @staticmethod
+    def forward(ctx, input, num_bits=8, min_value=None, max_value=None, inplace=False, symmetric=False,
+                num_chunks=None):
+        scale_f32 = False
+        if min_value is None or max_value is None:
+            # utils/quantize.py:26-37: range from the data as 0-d fp32 tensors
+            num_chunks = input.shape[0] if num_chunks is None else num_chunks
+            if input.shape[0] // num_chunks != 1:
+                raise NotImplementedError(
+                    "chunked range statistics (num_chunks < batch) belong to the activation path")
+            scale_f32 = True
+        if _is_tensor_value(min_value) or _is_tensor_value(max_value):
+            scale_f32 = True
+        ctx.inplace = inplace
+        ctx.num_bits = num_bits
+        ctx.min_value = min_value
+        ctx.max_value = max_value
+        if inplace:
+            ctx.mark_dirty(input)
+            out = input
+        else:
+            out = torch.empty_like(input)
+        given_min = given_max = None
+        if min_value is not None or max_value is not None:
+            # one given, one from data: compute the missing one on the device range path
+            if min_value is None or max_value is None:
+                mn, mx = _data_range(input)
+                given_min = float(mn) if min_value is None else float(min_value)
+                given_max = float(mx) if max_value is None else float(max_value)
+            else:
+                given_min, given_max = float(min_value), float(max_value)
+        fake_quant(input.detach(), num_bits, symmetric=symmetric, min_value=given_min, max_value=given_max,
+                   out=out, want_codes=False, scale_f32=scale_f32)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return grad_output, None, None, None, None, None, None
+
+
+def _data_range(x: torch.Tensor):
+    """fp32 (min, max) of x via the device sweep (asym zero == min; max from the
+    negated tensor's min)."""
+    r1 = fake_quant(x.detach().contiguous(), 8, want_codes=False)
+    r2 = fake_quant((-x.detach()).contiguous(), 8, want_codes=False)
+    return r1.zero[0].item(), -r2.zero[0].item()
+
+
+def quantize(x, num_bits=8, min_value=None, max_value=None, inplace=False, symmetric=False, num_chunks=None):
+    """utils/quantize.py:88-89."""
+    return UniformQuantize.apply(x, num_bits, min_value, max_value, inplace, symmetric, num_chunks)
+
+
+def quantize_per_channel(x, num_bits=8, symmetric=False, inplace=False):
+    """Extension: the reference ``quantize()`` applied to every output-channel
+    slice ``x[o]`` with that slice's own float(min)/float(max) -- one kernel."""
+    out = x if inplace else torch.empty_like(x)
+    fake_quant(x.detach(), num_bits, per_channel=True, symmetric=symmetric, out=out, want_codes=False)
+    return out
+
+
+class QuantMeasure(nn.Module):
+    """Activation range observer + fake quant (utils/quantize.py:94-126)."""
+
+    def __init__(self, update_stat=False, num_bits=8, momentum=0.1):
+        super().__init__()
+        self.register_buffer("running_min", torch.zeros(1))
+        self.register_buffer("running_max", torch.zeros(1))
+        self.momentum = momentum
+        self.num_bits = num_bits
+        self.update_stat = update_stat
+
+    def forward(self, input):
+        flat = input.detach().view(input.size(0), -1)
+        if self.update_stat:
+            self.running_max = max(self.running_max, flat.max(-1)[0].mean())
+            self.running_min = min(self.running_min, flat.min(-1)[0].mean())
+        if self.training:
+            mn = flat.min(-1)[0].mean()
+            mx = flat.max(-1)[0].mean()
+            self.running_min.mul_(1 - self.momentum).add_(mn * self.momentum)
+            self.running_max.mul_(1 - self.momentum).add_(mx * self.momentum)
+        else:
+            mn, mx = self.running_min, self.running_max
+        return quantize(input, self.num_bits, min_value=float(mn), max_value=float(mx), num_chunks=16)
+
+    def set_update_stat(self, update_stat):
+        self.update_stat = update_stat
+
+
+class _QuantWeightMixin:
+    """Forward of the Quant* layers: activation fake-quant, per-tensor weight
+    fake-quant with float(min)/float(max), bias fake-quant with the data range."""
+
+    def _qparams(self, weight, bias):
+        qweight = quantize(weight, num_bits=self.num_bits, min_value=float(weight.min()),
+                           max_value=float(weight.max()))
+        qbias = quantize(bias, num_bits=self.num_bits_bias) if bias is not None else None
+        return qweight, qbias
+
+
+class QuantConv2d(_QuantWeightMixin, nn.Conv2d):
+    """utils/quantize.py:213-238."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1, groups=1,
+                 bias=True, num_bits=8, num_bits_act=8, num_bits_bias=16, momentum=0.1):
+        super().__init__(in_channels, out_channels, kernel_size, stride, padding, dilation, groups, bias)
+        self.num_bits = num_bits
+        self.num_bits_bias = num_bits_bias
+        self.quant = QuantMeasure(num_bits=num_bits_act, momentum=momentum)
+
+    def forward(self, input):
+        input = self.quant(input)
+        qweight, qbias = self._qparams(self.weight, self.bias)
+        return F.conv2d(input, qweight, qbias, self.stride, self.padding, self.dilation, self.groups)
+
+
+class QuantNConv2d(nn.Conv2d):
+    """Conv2d with activation fake-quant only (utils/quantize.py:240-256)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1, groups=1,
+                 bias=True, num_bits=8, num_bits_act=8, momentum=0.1):
+        super().__init__(in_channels, out_channels, kernel_size, stride, padding, dilation, groups, bias)
+        self.quant = QuantMeasure(num_bits=num_bits_act, momentum=momentum)
+
+    def forward(self, input):
+        return F.conv2d(self.quant(input), self.weight, self.bias, self.stride, self.padding, self.dilation,
+                        self.groups)
+
+
+class QuantLinear(_QuantWeightMixin, nn.Linear):
+    """utils/quantize.py:326-348."""
+
+    def __init__(self, in_features, out_features, bias=True, num_bits=8, num_bits_act=8, num_bits_bias=16,
+                 momentum=0.1):
+        super().__init__(in_features, out_features, bias)
+        self.num_bits = num_bits
+        self.num_bits_bias = num_bits_bias
+        self.quant = QuantMeasure(num_bits=num_bits_act, momentum=momentum)
+
+    def forward(self, input):
+        input = self.quant(input)
+        qweight, qbias = self._qparams(self.weight, self.bias)
+        return F.linear(input, qweight, qbias)
+
+
+class QuantNLinear(nn.Linear):
+    """utils/quantize.py:350-363."""
+
+    def __init__(self, in_features, out_features, bias=True, num_bits=8, num_bits_act=8, momentum=0.1):
+        super().__init__(in_features, out_features, bias)
+        self.quant = QuantMeasure(num_bits=num_bits_act, momentum=momentum)
+
+    def forward(self, input):
+        return F.linear(self.quant(input), self.weight, self.bias)
+
+
+class QConv2d(QuantConv2d):
+    """QConv2d with the (unused by main_dfq) scale/scale_prev hooks
+    (utils/quantize.py:129-210)."""
+
+    def set_scale(self, scale=None, scale_prev=None):
+        if scale is not None:
+            self.register_parameter("scale", nn.Parameter(scale.view(-1, 1, 1, 1)))
+        if scale_prev is not None:
+            self.scale_prev = scale_prev
+
+    def _scaled(self):
+        w, b = self.weight, self.bias
+        sp = getattr(self, "scale_prev", None)
+        if sp is not None:
+            step, step_s = w.shape[0] // self.groups, w.shape[1]
+            sp = sp[:, 0, 0, 0].view(1, -1, 1, 1)
+            w = torch.cat([w[g * step:(g + 1) * step] / sp[:, g * step_s:(g + 1) * step_s]
+                           for g in range(self.groups)])
+        sc = getattr(self, "scale", None)
+        if sc is not None:
+            w = w * sc
+            b = b * sc.view(-1) if b is not None else None
+        return w, b
+
+    def merge_scale_to_weight(self):
+        with torch.no_grad():
+            w, b = self._scaled()
+            self.weight.data.copy_(w)
+            if b is not None:
+                self.bias.data.copy_(b)
+        self.scale_prev = None
+        self.scale = None
+
+    def forward(self, input):
+        input = self.quant(input)
+        w, b = self._scaled()
+        qweight, qbias = self._qparams(w, b)
+        return F.conv2d(input, qweight, qbias, self.stride, self.padding, self.dilation, self.groups)
+
+
+class QLinear(QuantLinear):
+    """utils/quantize.py:260-324."""
+
+    def set_scale(self, scale=None, scale_prev=None):
+        if scale is not None:
+            self.register_parameter("scale", nn.Parameter(scale.view(-1, 1)))
+        if scale_prev is not None:
+            self.scale_prev = scale_prev
+
+    def _scaled(self):
+        w, b = self.weight, self.bias
+        sp = getattr(self, "scale_prev", None)
+        if sp is not None:
+            w = w * sp.view(1, -1)
+        sc = getattr(self, "scale", None)
+        if sc is not None:
+            w = w * sc
+            b = b * sc.view(-1) if b is not None else None
+        return w, b
+
+    def merge_scale_to_weight(self):
+        with torch.no_grad():
+            w, b = self._scaled()
+            self.weight.data.copy_(w)
+            if b is not None:
+                self.bias.data.copy_(b)
+        self.scale_prev = None
+        self.scale = None
+
+    def forward(self, input):
+        input = self.quant(input)
+        w, b = self._scaled()
+        qweight, qbias = self._qparams(w, b)
+        return F.linear(input, qweight, qbias)
+
+
+def set_layer_bits(graph, bits_weight=8, bits_activation=8, bits_bias=16, targ_type=None):
+    """utils/quantize.py:366-379, including its quirk: ``QuantMeasure(bits_activation)``
+    passes the bit width positionally into ``update_stat`` so activations stay
+    8-bit."""
+    print("Setting num_bits for targ layers...")
+    assert targ_type is not None, "targ_type cannot be None"
+    for idx in graph:
+        if type(graph[idx]) in targ_type:
+            if hasattr(graph[idx], "quant"):
+                dev = next(graph[idx].parameters()).device
+                graph[idx].quant = QuantMeasure(bits_activation).to(dev)
+            if hasattr(graph[idx], "num_bits"):
+                graph[idx].num_bits = bits_weight
+            if hasattr(graph[idx], "num_bits_bias"):
+                graph[idx].num_bits_bias = bits_bias

@@ -1,0 +1,182 @@
+/*
+ * dfq_hip.h -- C ABI of libdfq_hip.so, the MI355X (gfx950) data-free-quantization
+ * weight-transform path.
+ *
+ * Every entry point is plain C: raw device pointers, integer sizes, an opaque
+ * hipStream_t passed as `void*` (NULL = the legacy default stream).  All compute
+ * calls are asynchronous on that stream unless the comment says "blocking".
+ * Nothing here allocates device memory on the hot path: the one-shot calls take
+ * a caller-provided workspace, and the plan objects allocate once at create().
+ *
+ * Return value: 0 on success, a negative DFQ_ERR_* code otherwise
+ * (dfq_error_string() gives the text).  The Python host layer maps
+ * DFQ_ERR_SHAPE to ValueError/RuntimeError exactly where the reference raises.
+ *
+ * Each function cites the reference interface (KadAMRN/Data_Free_Quantization)
+ * whose arithmetic it replaces.  The binding a maintainer adds on the reference
+ * side (ctypes) is in INTEGRATION.md.
+ */
+#ifndef DFQ_HIP_H_
+#define DFQ_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFQ_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------- */
+#define DFQ_OK              0
+#define DFQ_ERR_INVALID    -1   /* bad argument (null pointer, bits out of range, ...) */
+#define DFQ_ERR_HIP        -2   /* a HIP runtime call failed */
+#define DFQ_ERR_UNSUPPORTED -3  /* valid request this build does not implement */
+#define DFQ_ERR_NOMEM      -4   /* device / host allocation failed (plan create only) */
+#define DFQ_ERR_SHAPE      -5   /* shape mismatch the reference would raise on */
+#define DFQ_ERR_WORKSPACE  -6   /* caller workspace too small */
+
+/* ---- quantizer modes ---------------------------------------------------- */
+/* TENSOR_* use one (min, max) for the whole tensor (reference default,
+ * utils/quantize.py:62-66 via utils/layer_transform.py:298).  CHANNEL_* use one
+ * (min, max) per row = per output channel (extension: the reference quantize()
+ * applied to each W[o] slice).  *_SYM is utils/quantize.py:51-60.              */
+#define DFQ_TENSOR_ASYM   0
+#define DFQ_TENSOR_SYM    1
+#define DFQ_CHANNEL_ASYM  2
+#define DFQ_CHANNEL_SYM   3
+
+/* ---- descriptor flags --------------------------------------------------- */
+#define DFQ_CLIP          0x1  /* clamp the dequantized output to [clip_lo, clip_hi] (clip_weight.py:29) */
+#define DFQ_GIVEN_RANGE   0x2  /* use given_min/given_max (Python doubles) instead of the data range */
+#define DFQ_SCALE_F32     0x4  /* scale arithmetic in fp32 (quantize() called with min/max=None,
+                                  utils/quantize.py:26-37: 0-d fp32 tensors) instead of fp64;
+                                  with DFQ_GIVEN_RANGE the given values are fp32 tensor values */
+
+/* One fp32 tensor viewed as [rows, row_len], row_len = I*KH*KW (KCRS) or I (Linear).
+ * Outputs are written only where the pointer is non-NULL:
+ *   dst    fp32 dequantized values (may alias src: in-place, like weight.data.copy_)
+ *   codes  integer grid indices: uint8 (asym, bits<=8), int8 (sym, bits<=8),
+ *          uint16/int16 for 8<bits<=16
+ *   scale  fp32 step, [rows] in CHANNEL modes, [1] in TENSOR modes
+ *   zero   fp32 value added back after scaling (the range min for asym, +0 for sym)
+ *   esum   fp32 bias-correction error sums E[o,i] = sum_k (y - x)[o, i*khw + k],
+ *          [rows * row_len/khw]  (bias_correction.py:128-131,231 on the fused output y)
+ */
+typedef struct dfq_tensor_desc {
+    const float* src;
+    float*       dst;
+    void*        codes;
+    float*       scale;
+    float*       zero;
+    float*       esum;
+    int64_t      rows;
+    int64_t      row_len;
+    int32_t      khw;       /* spatial size for esum (1 for Linear / 1x1) */
+    int32_t      bits;      /* 2..16 */
+    int32_t      mode;      /* DFQ_TENSOR_ASYM ... DFQ_CHANNEL_SYM */
+    int32_t      flags;     /* DFQ_CLIP | DFQ_GIVEN_RANGE | DFQ_SCALE_F32 */
+    float        clip_lo;
+    float        clip_hi;
+    double       given_min;
+    double       given_max;
+} dfq_tensor_desc;
+
+/* ---- library ------------------------------------------------------------ */
+int         dfq_abi_version(void);
+const char* dfq_error_string(int code);
+/* Last HIP error text seen by the library on this thread ("" if none). */
+const char* dfq_last_hip_error(void);
+
+/* ---- single-tensor quantize (replaces quantize()/UniformQuantize.forward,
+ *      utils/quantize.py:16-89) ------------------------------------------- */
+/* Workspace bytes dfq_quantize_tensor needs for this descriptor (0 is possible). */
+int dfq_quantize_ws_bytes(const dfq_tensor_desc* desc, size_t* bytes);
+/* Blocking (returns after the stream drains: the reference quantize() is
+ * synchronous too).  ws: device memory of >= dfq_quantize_ws_bytes bytes. */
+int dfq_quantize_tensor(const dfq_tensor_desc* desc, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- grouped sweep over many tensors (replaces quantize_targ_layer,
+ *      utils/layer_transform.py:288-305, fused with clip_weight.py:4-33 and the
+ *      bias-correction error reduction bias_correction.py:111-144,231) ------- */
+typedef struct dfq_sweep_plan dfq_sweep_plan;
+typedef struct dfq_sweep_stats {
+    int64_t n_tensors;
+    int64_t n_elems;          /* sum of rows*row_len */
+    int64_t n_tasks_reduce;   /* wave tasks of the range-reduction launch (0 = launch skipped) */
+    int64_t n_tasks_main;     /* wave tasks of the quantize launch */
+    int64_t algo_bytes;       /* algorithmic HBM bytes of one execute */
+    int32_t launches;         /* kernel launches per execute (1 or 2) */
+    int32_t grid_blocks;      /* blocks of the quantize launch */
+} dfq_sweep_stats;
+/* Blocking (uploads the descriptor/task tables once).  descs is copied. */
+int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, dfq_sweep_plan** plan);
+int dfq_sweep_plan_execute(dfq_sweep_plan* plan, void* stream);
+int dfq_sweep_plan_stats(const dfq_sweep_plan* plan, dfq_sweep_stats* stats);
+int dfq_sweep_plan_destroy(dfq_sweep_plan* plan);
+
+/* ---- BatchNorm folding (merge_batchnorm, utils/layer_transform.py:255-281) ---
+ * w[o,:] *= g[o]/sqrt(v[o]+eps);  bias[o] = bias[o]*f[o] + (b[o] - g[o]*m[o]/sqrt(v[o]+eps));
+ * fake_w = |g|, fake_b = b (either may be NULL); then the BN becomes identity:
+ * g=1, v=1, b=0, m=0 (the caller sets module.eps = 0).  rows = O, row_len = numel/O. */
+int dfq_bn_fold(float* w, float* bias, float* bn_w, float* bn_b, float* bn_mean, float* bn_var,
+                float* fake_w, float* fake_b, float eps, int64_t rows, int64_t row_len,
+                void* stream);
+
+/* ---- weight clipping (clip_weight.py:18-29): w = min(max(w, lo), hi), in place */
+int dfq_clamp(float* w, int64_t n, float lo, float hi, void* stream);
+
+/* ---- cross-layer equalization (Cross_layer_equal.py) -------------------- */
+/* Workspace bytes for one relation with c1 = W1.shape[0] channels. */
+size_t dfq_cle_ws_bytes(int64_t c1);
+/* One relation (_layer_equalization, Cross_layer_equal.py:11-59), in place:
+ *   W1 [c1, len1] rows, W2 [o2, i2, khw2], B1/bn_w/bn_b [c1] (each may be NULL),
+ *   groups G = (c1 == i2) ? 1 : c1 / i2.
+ * S (may be NULL) receives the per-channel scale; S_acc (may be NULL) is
+ * multiplied by it (Relation.set_scale_vec, utils/relation.py:26-30; pass
+ * s_acc_init=1 on the first call to store instead of multiply). */
+int dfq_cle_relation(float* w1, float* w2, float* b1, float* bn_w, float* bn_b,
+                     int64_t c1, int64_t len1, int64_t o2, int64_t i2, int64_t khw2,
+                     double s_min, double s_max, int32_t is_signed, float eps,
+                     float* S, float* S_acc, int32_t s_acc_init,
+                     void* ws, size_t ws_bytes, void* stream);
+/* Convergence metric of Cross_layer_equal.py:83,107-108 for a set of layers:
+ * out_mean[l] = (double)(float)( sum|W_l - snap_l| / n_l ), then snap_l := W_l.
+ * Blocking: waits for the stream and copies the n means to host memory. */
+typedef struct dfq_diff_plan dfq_diff_plan;
+int dfq_diff_plan_create(float* const* w, float* const* snap, const int64_t* n, int32_t count,
+                         dfq_diff_plan** plan);
+int dfq_diff_plan_snapshot(dfq_diff_plan* plan, void* stream);  /* snap := W, async */
+int dfq_diff_plan_execute(dfq_diff_plan* plan, double* out_mean, void* stream);
+int dfq_diff_plan_destroy(dfq_diff_plan* plan);
+
+/* ---- high-bias absorption (bias_absorption.py:147-197) ------------------
+ * c = max(bn_b - N*bn_w, 0) (bn_* = the BN's fake_weight / fake_bias);
+ * b2[o] += sum_i (sum_k W2[o,i,k]) * c[g*i2 + i];  b1 -= c;  bn_b -= c.
+ * W2 is [o2, i2, khw2], c1 = W1.shape[0], groups = c1 / i2. */
+int dfq_bias_absorb(const float* w2, float* b1, float* b2, float* bn_w, float* bn_b,
+                    int64_t c1, int64_t o2, int64_t i2, int64_t khw2, float n_sigma,
+                    void* stream);
+
+/* ---- bias correction (bias_correction.py) -------------------------------
+ * dfq_bc_expect: out[j] (+)= relu ? max(0, w*phi(-b/w) + b*(1-Phi(-b/w))) : b
+ *                (calculate_mean + branch sum, bias_correction.py:33-53,170-172). */
+int dfq_bc_expect(const float* fake_w, const float* fake_b, int64_t n, int32_t relu,
+                  int32_t accumulate, float* out, void* stream);
+/* dfq_bc_apply: bias_vec[o,j] = E[o, i2>1 ? j : 0] + expect[f>1 ? j : 0] over the
+ * broadcast shape [o, bcols]; bias[o] += mean_j bias_vec[o,j]
+ * (_compute_final_bias_correction + _apply_bias_correction, :61-106).
+ * bias_vec (may be NULL) keeps the [o*bcols] vector for dfq_bc_propagate.
+ * Returns DFQ_ERR_SHAPE where torch would raise (non-broadcastable, or numel == o). */
+int dfq_bc_apply(const float* E, int64_t o, int64_t i2, const float* expect, int64_t f,
+                 float* bias, float* bias_vec, int64_t* bcols_out, void* stream);
+/* dfq_bc_propagate: fake_b[c] += mean_r ( -bias_vec[r*f + c] ), r < numel/f
+ * (bias_prev.view(-1, F).mean(0), bias_correction.py:206-213,251). */
+int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_t f,
+                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFQ_HIP_H_ */

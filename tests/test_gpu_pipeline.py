@@ -1,0 +1,84 @@
+"""The whole DFQ pipeline (main_dfq stage order) on the GPU vs the reference run
+on identical synthetic models (tests/golden/pipeline_<model>.npz).
+
+Bit-exact per stage (sha256 of every target weight and bias): BN fold, CLE
+(weights, biases, accumulated scales, iteration count), 2nd BN fold, quantize,
+clip.  Tolerance (rtol 1e-5, atol 1e-6): biases after absorption (GEMV order)
+and after bias correction (mean order).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from tests.helpers import hb, pipeline
+
+pytestmark = pytest.mark.gpu
+TARG = (nn.Conv2d, nn.Linear)
+
+
+@pytest.mark.parametrize("name", ["mobilenetv2", "resnet50", "deeplab"])
+def test_pipeline_matches_reference(name):
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    from data_free_quantization_amd.pipeline import run_dfq
+    from data_free_quantization_amd.utils.tracer import build_graph
+    P = pipeline(name)
+    model = zoo.build(name, seed=0, relu=True).cuda()
+    g = build_graph(model, "positional")
+    graph, bottoms = g.getGraph(), g.getBottoms()
+    tkeys = [k for k in graph if type(graph[k]) in TARG]
+    assert tkeys == list(P["targets"])
+    failures = []
+
+    def check(stage):
+        ws = np.stack([np.frombuffer(hb(graph[k].weight.detach().cpu().numpy()), np.uint8) for k in tkeys])
+        if not np.array_equal(ws, P[f"{stage}_wh"]):
+            bad = [i for i in range(len(tkeys)) if not np.array_equal(ws[i], P[f"{stage}_wh"][i])]
+            failures.append((stage, "weights", bad[:5]))
+        biases = [graph[k].bias.detach().cpu().numpy() if graph[k].bias is not None else np.zeros(0, np.float32)
+                  for k in tkeys]
+        if f"{stage}_bias" in P.files:
+            got = np.concatenate(biases)
+            np.testing.assert_allclose(got, P[f"{stage}_bias"], rtol=1e-5, atol=1e-6, err_msg=stage)
+        else:
+            bh = np.stack([np.frombuffer(hb(b), np.uint8) for b in biases])
+            if not np.array_equal(bh, P[f"{stage}_bh"]):
+                failures.append((stage, "bias"))
+
+    def hook(stage):
+        if stage in ("bn1", "cle", "absorb", "bn2", "quant", "clip", "bc"):
+            check(stage)
+        if stage == "cle":
+            assert cle.LAST_RUN["iterations"] == len(P["cle_diffs"])
+            np.testing.assert_allclose(cle.LAST_RUN["diffs"], P["cle_diffs"], rtol=1e-5)
+
+    bc_error = str(P["bc_error"])
+    if bc_error:
+        with pytest.raises(RuntimeError):
+            run_dfq(model, graph, bottoms, TARG, bc_mode="reference", stage_hook=hook)
+    else:
+        rels = run_dfq(model, graph, bottoms, TARG, bc_mode="reference", stage_hook=hook)
+        assert [[r.layer_first, r.layer_second, r.bn_idx] for r in rels] == P["relations"].tolist()
+        Sh = np.stack([np.frombuffer(hb(r.S.cpu().numpy()), np.uint8) for r in rels])
+        assert np.array_equal(Sh, P["cle_Sh"])
+    assert not failures, failures
+
+
+def test_per_channel_extension_matches_reference_slices():
+    """Per-channel INT8 (sym and asym) of the post-absorption MobileNetV2 weights
+    == the reference quantize() applied to every W[o] slice."""
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd.pipeline import run_dfq
+    from data_free_quantization_amd.utils.quantize import fake_quant
+    from data_free_quantization_amd.utils.tracer import build_graph
+    P = pipeline("mobilenetv2")
+    model = zoo.build("mobilenetv2", seed=0, relu=True).cuda()
+    g = build_graph(model, "positional")
+    graph, bottoms = g.getGraph(), g.getBottoms()
+    run_dfq(model, graph, bottoms, TARG, quantize=False, clip=False, correction=False)
+    tkeys = [k for k in graph if type(graph[k]) in TARG]
+    for tag, sym in (("chsym8", True), ("chasym8", False)):
+        for i, k in enumerate(tkeys):
+            r = fake_quant(graph[k].weight.detach(), 8, per_channel=True, symmetric=sym)
+            assert hb(r.dq.cpu().numpy()) == bytes(P[f"{tag}_wh"][i]), (tag, k)

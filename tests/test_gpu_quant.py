@@ -1,0 +1,178 @@
+"""HIP quantize path vs the reference's golden vectors and the pinned oracle.
+
+Bit-exact: dequantized fp32 values (signed zeros folded), integer codes, scales.
+Tolerance (written here): BC error sums E, rtol 1e-5 / atol 1e-6 -- torch's
+spatial sum order differs from the kernel's k-ascending sum.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.helpers import case_flags, h, quant_cases
+
+pytestmark = pytest.mark.gpu
+CASES = quant_cases()
+DEV = "cuda:0"
+
+
+def _run_hip(case):
+    from data_free_quantization_amd.utils.quantize import fake_quant
+    mode, rows, flags, given = case_flags(case)
+    x = torch.from_numpy(case["x"]).to(DEV)
+    kw = dict(per_channel=mode >= 2, symmetric=mode in (1, 3), khw=case["khw"], want_esum=case["esum"])
+    if case["given"] is not None:
+        kw.update(min_value=given[0], max_value=given[1])
+    if case["default_range"]:
+        kw.update(scale_f32=True)
+    if case["clip"] is not None:
+        kw.update(clip=tuple(case["clip"]))
+    return fake_quant(x, case["bits"], **kw)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c['idx']}-{c['name']}-{c['mode']}-b{c['bits']}" for c in CASES])
+def test_hip_quantize_matches_reference(case):
+    r = _run_hip(case)
+    torch.cuda.synchronize()
+    dq = r.dq.cpu().numpy()
+    assert h(dq) == case["dqh"], "dequantized values differ from the reference"
+    if case["dq"] is not None:
+        assert np.array_equal(dq, case["dq"])
+    if case["esum"]:
+        np.testing.assert_allclose(r.esum.cpu().numpy(), case["esum_ref"], rtol=1e-5, atol=1e-6)
+    mode, rows, flags, given = case_flags(case)
+    o = O.quantize(case["x"], case["bits"], mode, rows=rows, khw=case["khw"], flags=flags,
+                   clip=tuple(case["clip"]) if case["clip"] else (0.0, 0.0), given=given)
+    assert np.array_equal(r.codes.cpu().numpy(), o["codes"]), "codes differ from the oracle"
+    assert np.array_equal(r.scale.cpu().numpy(), o["scale"])
+    assert np.array_equal(r.zero.cpu().numpy() + np.float32(0), o["zero"] + np.float32(0))
+
+
+def test_grouped_sweep_matches_single_calls():
+    """All golden cases in ONE grouped plan (mixed modes, bits, rows, khw)."""
+    from data_free_quantization_amd.sweep import SweepItem, SweepPlan
+    items, cases = [], []
+    for c in CASES:
+        if c["given"] is not None or c["default_range"]:
+            continue
+        mode, rows, flags, _ = case_flags(c)
+        x = torch.from_numpy(c["x"]).to(DEV).contiguous()
+        sym = mode in (1, 3)
+        npar = rows if mode >= 2 else 1
+        cdt = (torch.int8 if sym else torch.uint8) if c["bits"] <= 8 else torch.int16
+        it = SweepItem(src=x, bits=c["bits"], per_channel=mode >= 2, symmetric=sym, dst=torch.empty_like(x),
+                       codes=torch.empty(x.shape, dtype=cdt, device=DEV),
+                       scale=torch.empty(npar, device=DEV), zero=torch.empty(npar, device=DEV),
+                       esum=torch.empty(x.numel() // c["khw"], device=DEV) if c["esum"] else None,
+                       khw=c["khw"], clip=tuple(c["clip"]) if c["clip"] else None, rows=rows)
+        items.append(it)
+        cases.append(c)
+    plan = SweepPlan(items)
+    for _ in range(2):   # replay: identical results
+        plan.execute()
+        torch.cuda.synchronize()
+        for it, c in zip(items, cases):
+            assert h(it.dst.cpu().numpy()) == c["dqh"], c["name"]
+            if c["esum"]:
+                np.testing.assert_allclose(it.esum.cpu().numpy(), c["esum_ref"], rtol=1e-5, atol=1e-6)
+    plan.destroy()
+
+
+@pytest.mark.parametrize("model", ["mobilenetv2", "resnet50", "deeplab"])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_full_model_sweep_vs_oracle(model, mode):
+    """Every target weight of the model in one plan, vs the oracle layer by layer."""
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd.sweep import allocate, SweepPlan, khw_of
+    m = zoo.build(model, seed=3)
+    layers = [l.weight.detach() for l in zoo.target_layers(m)]
+    bits = 8 if mode != 1 else 4
+    items = []
+    for w in layers:
+        wd = w.to(DEV).contiguous()
+        items.append(allocate(wd, bits=bits, per_channel=mode >= 2, symmetric=mode in (1, 3), khw=khw_of(wd),
+                              want_esum=True, clip=(-0.5, 0.5) if mode == 3 else None))
+    plan = SweepPlan(items)
+    plan.execute()
+    torch.cuda.synchronize()
+    for w, it in zip(layers, items):
+        x = w.numpy()
+        rows = x.shape[0] if mode >= 2 else 1
+        o = O.quantize(x, bits, mode, rows=rows, khw=it.khw, flags=1 if mode == 3 else 0, clip=(-0.5, 0.5),
+                       want_esum=True)
+        assert np.array_equal(it.dst.cpu().numpy(), o["dq"])
+        assert np.array_equal(it.codes.cpu().numpy(), o["codes"])
+        assert np.array_equal(it.scale.cpu().numpy(), o["scale"])
+        np.testing.assert_allclose(it.esum.cpu().numpy(), o["esum"], rtol=1e-5, atol=1e-6)
+    plan.destroy()
+
+
+def test_long_rows_and_odd_sizes_vs_oracle():
+    """rows longer than one wave task (two-launch path), odd row lengths
+    (scalar path), empty tensors, a single element."""
+    from data_free_quantization_amd.sweep import allocate, SweepPlan
+    rng = np.random.default_rng(7)
+    shapes = [(3, 4608), (2, 20000), (7, 27), (5, 9), (1, 1), (33, 13), (0, 9), (513, 4100)]
+    items, xs = [], []
+    for shp in shapes:
+        x = rng.normal(0, 1, shp).astype(np.float32)
+        xs.append(x)
+        for mode in range(4):
+            items.append(allocate(torch.from_numpy(x).to(DEV), bits=8, per_channel=mode >= 2,
+                                  symmetric=mode in (1, 3), want_esum=True))
+    plan = SweepPlan(items)
+    plan.execute()
+    torch.cuda.synchronize()
+    k = 0
+    for x in xs:
+        for mode in range(4):
+            it = items[k]
+            k += 1
+            if x.size == 0:
+                continue
+            o = O.quantize(x, 8, mode, rows=x.shape[0] if mode >= 2 else 1, want_esum=True)
+            assert np.array_equal(it.dst.cpu().numpy(), o["dq"]), (x.shape, mode)
+            assert np.array_equal(it.codes.cpu().numpy(), o["codes"]), (x.shape, mode)
+            np.testing.assert_allclose(it.esum.cpu().numpy(), o["esum"], rtol=1e-5, atol=1e-6)
+    plan.destroy()
+
+
+def test_large_sweep_properties():
+    """Full-size (1 GiB) sweep: properties that need no oracle -- codes in range,
+    the dequant identity dq == code*s + zero (bit-exact), the rounding bound
+    |dq - x| <= s/2, and E == dq - x for 1x1 layers."""
+    from data_free_quantization_amd.sweep import allocate, SweepPlan
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(65536, 4096, device=DEV, generator=g)
+    it = allocate(x, bits=8, per_channel=True, symmetric=True, want_esum=True)
+    plan = SweepPlan([it])
+    plan.execute()
+    torch.cuda.synchronize()
+    assert int(it.codes.min()) >= -128 and int(it.codes.max()) <= 127
+    regen = it.codes.float() * it.scale.view(-1, 1) + it.zero.view(-1, 1)
+    assert torch.equal(regen, it.dst)
+    err = (it.dst - x).abs()
+    assert bool((err <= it.scale.view(-1, 1) * 0.5000001).all())
+    assert torch.equal(it.esum.view_as(x), it.dst - x)
+    plan.destroy()
+
+
+def test_reference_quantize_api_on_gpu():
+    from data_free_quantization_amd.utils.quantize import quantize
+    for c in CASES[:40]:
+        if c["mode"].startswith("channel") or c["clip"] is not None:
+            continue
+        x = torch.from_numpy(c["x"]).to(DEV)
+        sym = c["mode"] == "tensor_sym"
+        if c["given"] is not None:
+            y = quantize(x, c["bits"], c["given"][0], c["given"][1], symmetric=sym)
+        elif c["default_range"]:
+            y = quantize(x, c["bits"], symmetric=sym)
+        else:
+            y = quantize(x, c["bits"], float(x.min()), float(x.max()), symmetric=sym)
+        assert h(y.cpu().numpy()) == c["dqh"]
+    # in-place + STE backward
+    x = torch.randn(64, 32, device=DEV, requires_grad=True)
+    y = quantize(x, 8, float(x.min()), float(x.max()))
+    y.sum().backward()
+    assert torch.equal(x.grad, torch.ones_like(x))

@@ -1,0 +1,115 @@
+"""HIP graph transforms (BN fold, CLE relation, absorption, BC helpers) vs the
+reference's golden outputs.  Bit-exact except where the reference reduces in
+an unspecified order (absorption GEMV, BC means): rtol 1e-5 / atol 1e-6."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+from collections import OrderedDict
+
+from tests.helpers import transform_cases
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def test_bn_fold():
+    from data_free_quantization_amd.utils.layer_transform import merge_batchnorm
+    z, meta = transform_cases()
+    for tag in ("bnfold_a", "bnfold_b"):
+        w = z[f"{tag}_w"]
+        conv = nn.Conv2d(w.shape[1], w.shape[0], w.shape[2], bias=True).to(DEV)
+        bn = nn.BatchNorm2d(w.shape[0]).to(DEV)
+        with torch.no_grad():
+            conv.weight.copy_(T(w)); conv.bias.copy_(T(z[f"{tag}_b"]))
+            bn.weight.copy_(T(z[f"{tag}_g"])); bn.bias.copy_(T(z[f"{tag}_beta"]))
+            bn.running_mean.copy_(T(z[f"{tag}_m"])); bn.running_var.copy_(T(z[f"{tag}_v"]))
+        graph = OrderedDict([("Data", "Data"), (1, conv), (2, bn)])
+        bottoms = OrderedDict([("Data", None), (1, ["Data"]), (2, [1])])
+        merge_batchnorm(None, graph, bottoms, (nn.Conv2d, nn.Linear))
+        assert np.array_equal(conv.weight.detach().cpu().numpy(), z[f"{tag}_w_out"])
+        assert np.array_equal(conv.bias.detach().cpu().numpy(), z[f"{tag}_b_out"])
+        assert np.array_equal(bn.fake_weight.cpu().numpy(), z[f"{tag}_fw"])
+        assert np.array_equal(bn.fake_bias.cpu().numpy(), z[f"{tag}_fb"])
+        after = np.stack([t.detach().cpu().numpy() for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)])
+        assert np.array_equal(after, z[f"{tag}_bn_after"])
+        assert bn.eps == 0
+
+
+@pytest.mark.parametrize("tag", ["cle_dense", "cle_pw_dw", "cle_dw_pw", "cle_signed", "cle_dead", "cle_linear",
+                                 "cle_grouped2"])
+def test_cle_relation(tag):
+    from data_free_quantization_amd.Cross_layer_equal import _layer_equalization
+    z, meta = transform_cases()
+    w1, w2, b1 = T(z[f"{tag}_w1"]), T(z[f"{tag}_w2"]), T(z[f"{tag}_b1"])
+    bnw, bnb = T(z[f"{tag}_bnw"]), T(z[f"{tag}_bnb"])
+    W1, W2, B1, S = _layer_equalization(w1, w2, b1, bnw, bnb, s_min_max=[1e-8, 1e8], signed=meta[tag]["signed"])
+    for got, key in ((W1, "w1_out"), (W2, "w2_out"), (B1, "b1_out"), (bnw, "bnw_out"), (bnb, "bnb_out"),
+                     (S, "S")):
+        assert np.array_equal(got.cpu().numpy(), z[f"{tag}_{key}"]), key
+
+
+@pytest.mark.parametrize("tag", ["absorb_dense", "absorb_dw"])
+def test_absorption(tag):
+    from data_free_quantization_amd.bias_absorption import bias_absorption
+    from data_free_quantization_amd.utils.relation import Relation
+    z, meta = transform_cases()
+    c1 = meta[tag]["c1"]
+    w2 = z[f"{tag}_w2"]
+    conv1 = nn.Conv2d(8, c1, 1, bias=True).to(DEV)
+    groups = c1 // w2.shape[1]
+    conv2 = nn.Conv2d(c1, w2.shape[0], 3, padding=1, groups=groups, bias=True).to(DEV)
+    bn = nn.BatchNorm2d(c1).to(DEV)
+    with torch.no_grad():
+        conv1.bias.copy_(T(z[f"{tag}_b1"])); conv2.weight.copy_(T(w2)); conv2.bias.copy_(T(z[f"{tag}_b2"]))
+    bn.register_buffer("fake_weight", T(z[f"{tag}_fw"]).clone())
+    bn.register_buffer("fake_bias", T(z[f"{tag}_fb"]).clone())
+    graph = OrderedDict([("Data", "Data"), (1, conv1), (2, bn), (3, nn.ReLU()), (4, conv2)])
+    bottoms = OrderedDict([("Data", None), (1, ["Data"]), (2, [1]), (3, [2]), (4, [3])])
+    bias_absorption(graph, [Relation(1, 4, 2)], bottoms, N=3)
+    assert np.array_equal(conv1.bias.detach().cpu().numpy(), z[f"{tag}_b1_out"])
+    assert np.array_equal(bn.fake_bias.cpu().numpy(), z[f"{tag}_fb_out"])
+    np.testing.assert_allclose(conv2.bias.detach().cpu().numpy(), z[f"{tag}_b2_out"], rtol=1e-5, atol=1e-6)
+
+
+def test_bias_correction_helpers():
+    from data_free_quantization_amd import bias_correction as bc
+    z, _ = transform_cases()
+    w, b = T(z["bc_w"]), T(z["bc_b"])
+    ex = bc._bc_expect(w, b, True)
+    np.testing.assert_allclose(ex.cpu().numpy(), z["bc_expect_relu"], rtol=1e-6, atol=1e-7)
+    ex2 = bc._bc_expect(w, b, True)
+    bc._bc_expect(w.flip(0).contiguous(), b.flip(0).contiguous(), False, out=ex2)
+    np.testing.assert_allclose(ex2.cpu().numpy(), z["bc_expect_add"], rtol=1e-6, atol=1e-7)
+    layer = nn.Conv2d(64, 32, 1, bias=True).to(DEV)
+    with torch.no_grad():
+        layer.bias.copy_(T(z["bc_bias"]))
+    E = T(z["bc_E"])
+    vec = bc._apply_bias_correction_E(layer, E, 32, 64, "one", T(z["bc_expect_relu"]))
+    np.testing.assert_allclose(layer.bias.detach().cpu().numpy(), z["bc_bias_out"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(vec.cpu().numpy(), z["bc_vec"], rtol=1e-6, atol=1e-7)
+    fb = T(z["bc_fb"]).clone()
+    from data_free_quantization_amd import _lib
+    _lib.check(_lib.load().dfq_bc_propagate(_lib.ptr(vec), vec.numel(), _lib.ptr(fb), 32, _lib.stream_of(fb)), "p")
+    np.testing.assert_allclose(fb.cpu().numpy(), z["bc_fb_out"], rtol=1e-5, atol=1e-6)
+    dw = nn.Conv2d(64, 64, 3, groups=64, bias=True).to(DEV)
+    with torch.no_grad():
+        dw.bias.zero_()
+    bc._apply_bias_correction_E(dw, T(z["bc_Ed"]), 64, 1, "one", T(z["bc_expect_relu"]))
+    np.testing.assert_allclose(dw.bias.detach().cpu().numpy(), z["bc_dw_bias_out"], rtol=1e-5, atol=1e-6)
+    with pytest.raises(RuntimeError):   # 'cat' branch: the reference's torch.cat of 2-D with 1-D
+        bc._apply_bias_correction_E(layer, E, 32, 64, "cat", T(z["bc_expect_relu"]))
+
+
+def test_clip_weight():
+    from data_free_quantization_amd.clip_weight import clip_weight
+    conv = nn.Conv2d(16, 32, 3).to(DEV)
+    with torch.no_grad():
+        conv.weight.normal_(0, 20)
+    ref = conv.weight.detach().clamp(-15, 15)
+    clip_weight({1: conv}, [-15, 15], [nn.Conv2d, nn.Linear])
+    assert torch.equal(conv.weight.detach(), ref)
