@@ -123,14 +123,19 @@ def pipeline_timing(dev):
     from data_free_quantization_amd import zoo, Cross_layer_equal as cle
     from data_free_quantization_amd.pipeline import run_dfq
     from data_free_quantization_amd.utils.tracer import build_graph
+    import contextlib
+    import io
+    import logging
+    logging.getLogger("data_free_quantization_amd.bias_correction").setLevel(logging.ERROR)
     out = {}
     for rep in range(2):
         m = zoo.build("mobilenetv2", seed=0, relu=True).to(dev)
         g = build_graph(m, "positional")
         t = {}
         t0 = time.perf_counter()
-        run_dfq(m, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel", symmetric=True,
-                bc_mode="fused", timings=t)
+        with contextlib.redirect_stdout(io.StringIO()):   # the reference's progress prints
+            run_dfq(m, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel",
+                    symmetric=True, bc_mode="fused", timings=t)
         torch.cuda.synchronize(dev)
         total = time.perf_counter() - t0
         out = {k: round(v * 1e3, 3) for k, v in t.items()}
@@ -219,6 +224,8 @@ def main():
                 "algo_bytes_per_launch": st["algo_bytes"],
                 "launch_ms": round(launch_ms, 4),
                 "kernel": "sweep_main_kernel",
+                "tasks": st["n_tasks_main"],
+                "grid_blocks": st["grid_blocks"],
             },
             "cpu_baseline": cpu,
             "pipeline_ms": pipe,

@@ -46,7 +46,7 @@ class SweepStats(C.Structure):
     _fields_ = [
         ("n_tensors", C.c_int64), ("n_elems", C.c_int64), ("n_tasks_reduce", C.c_int64),
         ("n_tasks_main", C.c_int64), ("algo_bytes", C.c_int64), ("launches", C.c_int32),
-        ("grid_blocks", C.c_int32),
+        ("grid_blocks", C.c_int32), ("variant", C.c_int32), ("reserved", C.c_int32),
     ]
 
 
@@ -91,7 +91,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_bias_absorb": ([P, P, P, P, P, I64, I64, I64, I64, F32, P], C.c_int),
         "dfq_bc_expect": ([P, P, I64, I32, I32, P, P], C.c_int),
         "dfq_bc_apply": ([P, I64, I64, P, I64, P, P, C.POINTER(I64), P], C.c_int),
-        "dfq_bc_propagate": ([P, I64, P, I64, P], C.c_int),
+        "dfq_bc_propagate": ([P, I64, P, I64, I32, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -135,6 +135,11 @@ def require_device(*tensors: Optional[torch.Tensor]):
 
 def ptr(t: Optional[torch.Tensor]):
     return None if t is None else C.c_void_p(t.data_ptr())
+
+
+#: intra-op thread count of the reference run the BC reductions reproduce
+#: (torch.get_num_threads() when tests/golden was generated)
+REF_THREADS = int(os.environ.get("DFQ_REF_THREADS", "8"))
 
 
 def stream_of(t: torch.Tensor):

@@ -154,7 +154,8 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                         # fake_bias.add_(bias_prev) with a 2-D bias_prev cannot broadcast in place
                         raise RuntimeError("output with shape [{}] doesn't match the broadcast shape".format(f))
                     rc = _lib.load().dfq_bc_propagate(_lib.ptr(bias_prev), bias_prev.numel(),
-                                                      _lib.ptr(node.fake_bias), f, _lib.stream_of(bias_prev))
+                                                      _lib.ptr(node.fake_bias), f, _lib.REF_THREADS,
+                                                      _lib.stream_of(bias_prev))
                     _lib.check(rc, "dfq_bc_propagate", RuntimeError)
                     bias_prev = None
                 continue

@@ -135,6 +135,96 @@ __device__ __forceinline__ float qdq(float x, const QParams& p, float& q) {
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// ---------------------------------------------------------------------------
+// ATen's CPU fp32 summation order (at::native cascade_sum, SumKernel.cpp), which
+// the reference's torch.sum / torch.mean follow.  Characterised against torch
+// 2.10 in the dev container: vector width 8, ILP 4, a 4-level
+// cascade with level step 2^max(4, CeilLog2(n)/4), and, for reductions over a
+// strided dim of >= 32768 elements, an intra-op split over columns in chunks of
+// ceil(F/threads) rounded down to multiples of 32.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline int aten_ceil_log2(int64_t x) {
+    if (x <= 2) return 1;
+    int r = 0;
+    for (uint64_t v = (uint64_t)(x - 1); v; v >>= 1) ++r;
+    return r;
+}
+
+// multi_row_sum for one stream: sequential adds, flushed up a 4-level cascade.
+template <typename Get>
+__host__ __device__ inline float aten_cascade(Get get, int64_t size) {
+    const int lp = aten_ceil_log2(size) / 4 > 4 ? aten_ceil_log2(size) / 4 : 4;
+    const int64_t step = (int64_t)1 << lp, mask = step - 1;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int64_t i = 0;
+    while (i + step <= size) {
+        for (int64_t j = 0; j < step; ++j, ++i) a0 += get(i);
+        a1 += a0; a0 = 0.f;
+        if (i & (mask << lp)) continue;
+        a2 += a1; a1 = 0.f;
+        if (i & (mask << (2 * lp))) continue;
+        a3 += a2; a2 = 0.f;
+    }
+    for (; i < size; ++i) a0 += get(i);
+    a0 += a1;
+    a0 += a2;
+    a0 += a3;
+    return a0;
+}
+
+// row_sum: 4 interleaved cascades (ILP 4), tail into the first, then combined.
+template <typename Get>
+__host__ __device__ inline float aten_row_sum(Get get, int64_t size) {
+    const int64_t sz = size / 4;
+    float p0 = aten_cascade([&](int64_t i) { return get(4 * i + 0); }, sz);
+    const float p1 = aten_cascade([&](int64_t i) { return get(4 * i + 1); }, sz);
+    const float p2 = aten_cascade([&](int64_t i) { return get(4 * i + 2); }, sz);
+    const float p3 = aten_cascade([&](int64_t i) { return get(4 * i + 3); }, sz);
+    for (int64_t i = 4 * sz; i < size; ++i) p0 += get(i);
+    p0 += p1;
+    p0 += p2;
+    p0 += p3;
+    return p0;
+}
+
+// Sum over a contiguous dim of n elements (vectorized_inner_sum / scalar_inner_sum).
+template <typename Get>
+__host__ __device__ inline float aten_inner_sum(Get get, int64_t n) {
+    if (n < 8) return aten_row_sum(get, n);
+    const int64_t vs = n / 8;
+    float fa = 0.f;
+    for (int64_t k = 8 * vs; k < n; ++k) fa += get(k);
+    for (int l = 0; l < 8; ++l) fa += aten_row_sum([&](int64_t i) { return get(8 * i + l); }, vs);
+    return fa;
+}
+
+// Column c of a row-major [R, F] summed over R (vectorized_outer_sum /
+// scalar_outer_sum inside TensorIterator::parallel_reduce with `threads`).
+__host__ __device__ inline float aten_outer_col_sum(const float* a, int64_t R, int64_t F, int64_t c, int threads) {
+    int64_t c0 = 0, c1 = F;
+    if (R * F >= 32768 && threads > 1) {
+        const int64_t nt = F < threads ? F : threads;
+        const int64_t chunk = ceil_div(F, nt);
+        c0 = c1 = -1;
+        for (int64_t t = 0; t < nt; ++t) {
+            int64_t b = t * chunk, e = b + chunk < F ? b + chunk : F;
+            if (b >= F) break;
+            b = b >= F ? b : b - b % 32;
+            e = e >= F ? e : e - e % 32;
+            if (b <= c && c < e) { c0 = b; c1 = e; break; }
+        }
+        if (c0 < 0) { c0 = 0; c1 = F; }   // unreachable for 0 <= c < F
+    }
+    // Column groups of the chunk: vectorized (>= 8 columns) takes 4x8-column
+    // multi_row_sum groups, then 8-column row_sum groups, then scalar row_sums;
+    // scalar_outer_sum (< 8 columns) takes 4-column multi_row_sum groups first.
+    const int64_t w = c1 - c0;
+    const int64_t g = w >= 8 ? 32 : 4;
+    const bool cascade = (c - c0) < g * (w / g);
+    auto get = [&](int64_t r) { return a[r * F + c]; };
+    return cascade ? aten_cascade(get, R) : aten_row_sum(get, R);
+}
+
 }  // namespace dfq
 
 // Host-side error plumbing shared by the translation units.

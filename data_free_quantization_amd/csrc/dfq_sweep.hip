@@ -19,18 +19,31 @@
 #include "dfq_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <new>
 #include <numeric>
 #include <vector>
 
 namespace dfq {
 
-constexpr int kChunk = 2048;                   // elements per wave task
-constexpr int kMaxRows = 256;                  // rows per whole-row task
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlockThreads = kWave * kWavesPerBlock;
-constexpr int kNV = kChunk / kWave;            // 32 scalar slots per lane
-constexpr int kNV4 = kChunk / (4 * kWave);     // 8 float4 slots per lane
+
+// Kernel variants (chunk elements per wave task, rows per whole-row task, LDS-DMA
+// prefetch of the next task).  The task table is built for the plan's variant.
+struct Variant {
+    int chunk;
+    int max_rows;
+    bool prefetch;
+};
+constexpr Variant kVariants[] = {
+    {2048, 256, false},   // 0: 10 KB LDS / wave, 16 waves / CU
+    {1024, 128, true},    // 1: 2 x 4 KB + 1 KB, next task's DMA in flight during compute
+    {2048, 256, true},    // 2: 2 x 8 KB + 2 KB
+    {1024, 128, false},   // 3: 5 KB / wave, 32 waves / CU
+};
+constexpr int kNumVariants = 4;
+constexpr int kDefaultVariant = 0;
 
 struct alignas(16) DevTensor {
     const float* src;
@@ -65,10 +78,13 @@ struct alignas(16) DevTask {
     int32_t first;       // this piece writes scale/zero for its slot
 };
 
-struct WaveLds {
-    float data[kChunk];
-    float s[kMaxRows];
-    float mn[kMaxRows];
+// Per-wave LDS image: [NB buffers of CHUNK floats][MAXROWS scales][MAXROWS mins],
+// carved out of ONE __shared__ array (a second __shared__ object next to an
+// LDS-DMA target can make hipcc drain vmcnt before every ds_read).
+template <int CHUNK, int MAXROWS, int NB>
+struct LdsLayout {
+    static constexpr int kPerWave = NB * CHUNK + 2 * MAXROWS;
+    static constexpr int kTotal = kWavesPerBlock * kPerWave;
 };
 
 __device__ __forceinline__ bool is_sym(int mode) { return mode == DFQ_TENSOR_SYM || mode == DFQ_CHANNEL_SYM; }
@@ -137,30 +153,32 @@ sweep_reduce_kernel(const DevTensor* __restrict__ tensors, const DevTask* __rest
 // ---------------------------------------------------------------------------
 // Main launch: one wave task.
 // ---------------------------------------------------------------------------
-template <bool VEC>
-__device__ __forceinline__ void process_task(const DevTensor& T, const DevTask& task, WaveLds& L,
-                                             const uint32_t* __restrict__ slot_min,
-                                             const uint32_t* __restrict__ slot_max, int lane) {
+// Issue the task's HBM -> LDS DMA (all loads in flight; no wait).
+__device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTask& task, float* data, int lane) {
     const float* src = T.src + task.elem_start;
     const int n = task.n;
-    const bool sym = is_sym(T.mode);
-    const int len = (int)T.row_len;
-
-    // 1. chunk HBM -> LDS by DMA; every load is in flight before the first wait
-    if constexpr (VEC) {
+    if (T.vec4) {
         const int nj = n >> 2;
         for (int m = 0; m * kWave < nj; ++m) {
             const int j = lane + m * kWave;
-            if (j < nj) glds16(src + 4 * j, &L.data[4 * kWave * m]);
+            if (j < nj) glds16(src + 4 * j, data + 4 * kWave * m);
         }
     } else {
         for (int m = 0; m * kWave < n; ++m) {
             const int e = lane + m * kWave;
-            if (e < n) glds4(src + e, &L.data[kWave * m]);
+            if (e < n) glds4(src + e, data + kWave * m);
         }
     }
-    vm_wait_all();
-    wave_lds_sync();
+}
+
+// Steps 2-4 on a chunk that has landed in ``data``.
+template <int MAXROWS, bool VEC>
+__device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& task, float* data, float* ls,
+                                             float* lmn, const uint32_t* __restrict__ slot_min,
+                                             const uint32_t* __restrict__ slot_max, int lane) {
+    const int n = task.n;
+    const bool sym = is_sym(T.mode);
+    const int len = (int)T.row_len;
 
     // 2. per-row parameters (whole-row tasks) or the slot's parameters (pieces)
     QParams pc{};
@@ -170,7 +188,7 @@ __device__ __forceinline__ void process_task(const DevTensor& T, const DevTask& 
         if (len >= kWave) {
             for (int r = 0; r < nrows; ++r) {
                 float vmin = INFINITY, vmax = -INFINITY;
-                const float* row = &L.data[r * len];
+                const float* row = data + r * len;
                 if (VEC) {
                     for (int i = lane; 4 * i < len; i += kWave) {
                         const float4 v = reinterpret_cast<const float4*>(row)[i];
@@ -188,8 +206,8 @@ __device__ __forceinline__ void process_task(const DevTensor& T, const DevTask& 
                 vmax = wave_max(vmax);
                 if (lane == 0) {
                     const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
-                    L.s[r] = p.s;
-                    L.mn[r] = p.mn;
+                    ls[r] = p.s;
+                    lmn[r] = p.mn;
                     const int64_t row_g = task.row0 + r;
                     if (T.scale) T.scale[row_g] = p.s;
                     if (T.zero) T.zero[row_g] = p.mn;
@@ -203,7 +221,7 @@ __device__ __forceinline__ void process_task(const DevTensor& T, const DevTask& 
             for (int r0 = 0; r0 < nrows; r0 += per_pass) {
                 const int r = r0 + sub;
                 const bool ok = (r < nrows) && (idx < len);
-                const float v = ok ? L.data[r * len + idx] : 0.f;
+                const float v = ok ? data[r * len + idx] : 0.f;
                 float vmin = ok ? v : INFINITY;
                 float vmax = ok ? v : -INFINITY;
                 for (int off = seg >> 1; off >= 1; off >>= 1) {
@@ -212,8 +230,8 @@ __device__ __forceinline__ void process_task(const DevTensor& T, const DevTask& 
                 }
                 if (idx == 0 && r < nrows) {
                     const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
-                    L.s[r] = p.s;
-                    L.mn[r] = p.mn;
+                    ls[r] = p.s;
+                    lmn[r] = p.mn;
                     const int64_t row_g = task.row0 + r;
                     if (T.scale) T.scale[row_g] = p.s;
                     if (T.zero) T.zero[row_g] = p.mn;
@@ -249,10 +267,10 @@ __device__ __forceinline__ void process_task(const DevTensor& T, const DevTask& 
         // row = floor(e / len): (e + 0.5)/len is >= 0.5/len from an integer and
         // e < 2048, so this fp32 estimate is exact.
         int r = (int)(((float)e + 0.5f) * T.inv_len);
-        r = min(r, kMaxRows - 1);
+        r = min(r, MAXROWS - 1);
         QParams p;
-        p.s = L.s[r];
-        p.mn = L.mn[r];
+        p.s = ls[r];
+        p.mn = lmn[r];
         p.negmn = -p.mn;
         p.qmin = qmin;
         p.qmax = qmax;
@@ -268,7 +286,7 @@ __device__ __forceinline__ void process_task(const DevTensor& T, const DevTask& 
         const int nj = n >> 2;
 #pragma unroll 2
         for (int j = lane; j < nj; j += kWave) {
-            const float4 xv = reinterpret_cast<const float4*>(L.data)[j];
+            const float4 xv = reinterpret_cast<const float4*>(data)[j];
             const QParams p = params_for(4 * j);   // 4 | len: one row per float4
             float q0, q1, q2, q3;
             const float y0 = one(xv.x, p, q0);
@@ -290,51 +308,84 @@ __device__ __forceinline__ void process_task(const DevTensor& T, const DevTask& 
             if (want_e) {
                 const float4 ev = make_float4(y0 - xv.x, y1 - xv.y, y2 - xv.z, y3 - xv.w);
                 if (khw == 1) reinterpret_cast<float4*>(T.esum + base)[j] = ev;
-                else reinterpret_cast<float4*>(L.data)[j] = ev;
+                else reinterpret_cast<float4*>(data)[j] = ev;
             }
         }
     } else {
 #pragma unroll 4
         for (int e = lane; e < n; e += kWave) {
-            const float xv = L.data[e];
+            const float xv = data[e];
             float qv;
             const float yv = one(xv, params_for(e), qv);
             if (T.dst) T.dst[base + e] = yv;
             if (T.codes) store_code(T.codes, T.code_bytes, base + e, qv);
             if (want_e) {
                 if (khw == 1) T.esum[base + e] = yv - xv;
-                else L.data[e] = yv - xv;
+                else data[e] = yv - xv;
             }
         }
     }
 
-    // 4. KHW error sums: E[p] = sum_k eps[p*khw + k], k ascending
+    // 4. KHW error sums: E[p] = sum_k eps[p*khw + k] in ATen's order
     if (want_e && khw > 1) {
         wave_lds_sync();
         const int np = n / khw;
         const int64_t pbase = base / khw;
         for (int pi = lane; pi < np; pi += kWave) {
-            float acc = 0.f;
-            for (int k = 0; k < khw; ++k) acc += L.data[pi * khw + k];
-            T.esum[pbase + pi] = acc;
+            const float* e = data + pi * khw;   // torch.sum(eps.view(O, I, -1), -1) order
+            T.esum[pbase + pi] = aten_inner_sum([&](int64_t k) { return e[k]; }, khw);
         }
     }
     wave_lds_sync();  // LDS is reused by this wave's next task
 }
 
+template <int CHUNK, int MAXROWS, bool PREFETCH>
 __global__ void __launch_bounds__(kBlockThreads)
 sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restrict__ tasks, int64_t ntasks,
                   const uint32_t* __restrict__ slot_min, const uint32_t* __restrict__ slot_max) {
-    __shared__ WaveLds lds[kWavesPerBlock];
+    constexpr int NB = PREFETCH ? 2 : 1;
+    using Lay = LdsLayout<CHUNK, MAXROWS, NB>;
+    __shared__ __attribute__((aligned(16))) float lds[Lay::kTotal];
     const int lane = threadIdx.x & (kWave - 1);
     const int w = wave_uniform(threadIdx.x >> 6);
+    float* wl = lds + w * Lay::kPerWave;
+    float* ls = wl + NB * CHUNK;
+    float* lmn = ls + MAXROWS;
     const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + w;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
-    for (int64_t t = wave0; t < ntasks; t += nwaves) {
-        const DevTask task = tasks[t];
-        const DevTensor T = tensors[task.tensor];
-        if (T.vec4) process_task<true>(T, task, lds[w], slot_min, slot_max, lane);
-        else process_task<false>(T, task, lds[w], slot_min, slot_max, lane);
+    if constexpr (!PREFETCH) {
+        for (int64_t t = wave0; t < ntasks; t += nwaves) {
+            const DevTask task = tasks[t];
+            const DevTensor T = tensors[task.tensor];
+            issue_task_load(T, task, wl, lane);
+            vm_wait_all();
+            wave_lds_sync();
+            if (T.vec4) compute_task<MAXROWS, true>(T, task, wl, ls, lmn, slot_min, slot_max, lane);
+            else compute_task<MAXROWS, false>(T, task, wl, ls, lmn, slot_min, slot_max, lane);
+        }
+    } else {
+        // Double-buffered: the next task's DMA is issued before this task computes.
+        int cur = 0;
+        int64_t t = wave0;
+        if (t < ntasks) {
+            const DevTask task = tasks[t];
+            issue_task_load(tensors[task.tensor], task, wl, lane);
+        }
+        for (; t < ntasks; t += nwaves) {
+            const DevTask task = tasks[t];
+            const DevTensor T = tensors[task.tensor];
+            vm_wait_all();          // this task's chunk (and the previous task's stores)
+            wave_lds_sync();
+            const int64_t tn = t + nwaves;
+            if (tn < ntasks) {
+                const DevTask nt = tasks[tn];
+                issue_task_load(tensors[nt.tensor], nt, wl + (cur ^ 1) * CHUNK, lane);
+            }
+            float* data = wl + cur * CHUNK;
+            if (T.vec4) compute_task<MAXROWS, true>(T, task, data, ls, lmn, slot_min, slot_max, lane);
+            else compute_task<MAXROWS, false>(T, task, data, ls, lmn, slot_min, slot_max, lane);
+            cur ^= 1;
+        }
     }
 }
 
@@ -384,13 +435,14 @@ static DevTensor to_dev(const dfq_tensor_desc& d) {
 }
 
 // Piece length: a multiple of khw (E sums never straddle a piece) and of 4 (vec4).
-static int piece_len(int khw, bool vec4) {
+static int piece_len(int khw, bool vec4, int chunk) {
     const int unit = vec4 ? std::lcm(4, khw) : khw;
-    int p = (kChunk / unit) * unit;
+    int p = (chunk / unit) * unit;
     return p > 0 ? p : -1;
 }
 
-static int build(const dfq_tensor_desc* descs, int32_t n, Built& B) {
+static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Variant& V) {
+    const int kChunk = V.chunk, kMaxRows = V.max_rows;
     for (int32_t ti = 0; ti < n; ++ti) {
         const dfq_tensor_desc& d = descs[ti];
         int rc = validate(d);
@@ -410,7 +462,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B) {
         B.algo_bytes += bytes;
         B.tensors.push_back(T);
         if (total == 0) continue;
-        const int plen = piece_len(d.khw, T.vec4);
+        const int plen = piece_len(d.khw, T.vec4, kChunk);
         if (plen <= 0) return DFQ_ERR_UNSUPPORTED;   // khw > kChunk
         if (channel && d.row_len <= kChunk) {
             const int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(kMaxRows, kChunk / d.row_len));
@@ -448,10 +500,46 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B) {
     return DFQ_OK;
 }
 
-static int grid_for(int64_t ntasks) {
-    // persistent grid: 4 blocks (16 waves) per CU on 256 CUs, fewer if there is little work
+static int lds_bytes(const Variant& V) {
+    return 4 * kWavesPerBlock * ((V.prefetch ? 2 : 1) * V.chunk + 2 * V.max_rows);
+}
+
+// Persistent grid: as many blocks per CU as LDS admits (<= 8), on 256 CUs; fewer
+// if there is little work.
+static int grid_for(int64_t ntasks, const Variant& V) {
+    const int per_cu = std::max(1, std::min(8, (160 * 1024) / lds_bytes(V)));
     const int64_t want = ceil_div(ntasks, kWavesPerBlock);
-    return (int)std::max<int64_t>(1, std::min<int64_t>(want, 256 * 4));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(want, 256 * per_cu));
+}
+static int grid_for(int64_t ntasks) { return grid_for(ntasks, kVariants[kDefaultVariant]); }
+
+static int variant_from_env() {
+    const char* e = getenv("DFQ_SWEEP_VARIANT");
+    if (!e || !*e) return kDefaultVariant;
+    const int v = atoi(e);
+    return (v >= 0 && v < kNumVariants) ? v : kDefaultVariant;
+}
+
+static void launch_main(int variant, int grid, hipStream_t s, const DevTensor* t, const DevTask* k, int64_t n,
+                        const uint32_t* smin, const uint32_t* smax) {
+    switch (variant) {
+        case 1:
+            hipLaunchKernelGGL((sweep_main_kernel<1024, 128, true>), dim3(grid), dim3(kBlockThreads), 0, s, t, k, n,
+                               smin, smax);
+            break;
+        case 2:
+            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, true>), dim3(grid), dim3(kBlockThreads), 0, s, t, k, n,
+                               smin, smax);
+            break;
+        case 3:
+            hipLaunchKernelGGL((sweep_main_kernel<1024, 128, false>), dim3(grid), dim3(kBlockThreads), 0, s, t, k,
+                               n, smin, smax);
+            break;
+        default:
+            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false>), dim3(grid), dim3(kBlockThreads), 0, s, t, k,
+                               n, smin, smax);
+            break;
+    }
 }
 
 }  // namespace dfq
@@ -459,6 +547,7 @@ static int grid_for(int64_t ntasks) {
 using namespace dfq;
 
 struct dfq_sweep_plan {
+    int variant = kDefaultVariant;
     DevTensor* d_tensors = nullptr;
     DevTask* d_reduce = nullptr;
     DevTask* d_main = nullptr;
@@ -469,11 +558,13 @@ struct dfq_sweep_plan {
 extern "C" int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, dfq_sweep_plan** out) {
     if (!out || (n > 0 && !descs) || n < 0) return DFQ_ERR_INVALID;
     *out = nullptr;
+    const int variant = variant_from_env();
     Built B;
-    int rc = build(descs, n, B);
+    int rc = build(descs, n, B, kVariants[variant]);
     if (rc) return rc;
     dfq_sweep_plan* p = new (std::nothrow) dfq_sweep_plan();
     if (!p) return DFQ_ERR_NOMEM;
+    p->variant = variant;
     p->n_reduce = (int64_t)B.reduce.size();
     p->n_main = (int64_t)B.main.size();
     p->n_slots = B.slots;
@@ -517,8 +608,8 @@ extern "C" int dfq_sweep_plan_execute(dfq_sweep_plan* p, void* stream) {
         DFQ_LAUNCH_CHECK();
     }
     if (p->n_main > 0) {
-        hipLaunchKernelGGL(sweep_main_kernel, dim3(grid_for(p->n_main)), dim3(kBlockThreads), 0, s,
-                           p->d_tensors, p->d_main, p->n_main, p->d_slots, p->d_slots + p->n_slots);
+        launch_main(p->variant, grid_for(p->n_main, kVariants[p->variant]), s, p->d_tensors, p->d_main, p->n_main,
+                    p->d_slots, p->d_slots + p->n_slots);
         DFQ_LAUNCH_CHECK();
     }
     return DFQ_OK;
@@ -532,7 +623,8 @@ extern "C" int dfq_sweep_plan_stats(const dfq_sweep_plan* p, dfq_sweep_stats* st
     st->n_tasks_main = p->n_main;
     st->algo_bytes = p->algo_bytes;
     st->launches = (p->n_reduce > 0 ? 1 : 0) + (p->n_main > 0 ? 1 : 0);
-    st->grid_blocks = p->n_main > 0 ? grid_for(p->n_main) : 0;
+    st->grid_blocks = p->n_main > 0 ? grid_for(p->n_main, kVariants[p->variant]) : 0;
+    st->variant = p->variant;
     return DFQ_OK;
 }
 
@@ -567,7 +659,7 @@ static size_t single_ws_layout(const Built& B, size_t* off_tensor, size_t* off_r
 extern "C" int dfq_quantize_ws_bytes(const dfq_tensor_desc* d, size_t* bytes) {
     if (!d || !bytes) return DFQ_ERR_INVALID;
     Built B;
-    int rc = build(d, 1, B);
+    int rc = build(d, 1, B, kVariants[kDefaultVariant]);
     if (rc) return rc;
     size_t a, b, c;
     *bytes = single_ws_layout(B, &a, &b, &c);
@@ -577,7 +669,7 @@ extern "C" int dfq_quantize_ws_bytes(const dfq_tensor_desc* d, size_t* bytes) {
 extern "C" int dfq_quantize_tensor(const dfq_tensor_desc* d, void* ws, size_t ws_bytes, void* stream) {
     if (!d) return DFQ_ERR_INVALID;
     Built B;
-    int rc = build(d, 1, B);
+    int rc = build(d, 1, B, kVariants[kDefaultVariant]);
     if (rc) return rc;
     size_t ot, orr, om;
     const size_t need = single_ws_layout(B, &ot, &orr, &om);
@@ -603,8 +695,8 @@ extern "C" int dfq_quantize_tensor(const dfq_tensor_desc* d, void* ws, size_t ws
         DFQ_LAUNCH_CHECK();
     }
     if (!B.main.empty()) {
-        hipLaunchKernelGGL(sweep_main_kernel, dim3(grid_for((int64_t)B.main.size())), dim3(kBlockThreads), 0, s,
-                           dt, dm, (int64_t)B.main.size(), slots, slots + B.slots);
+        launch_main(kDefaultVariant, grid_for((int64_t)B.main.size()), s, dt, dm, (int64_t)B.main.size(), slots,
+                    slots + B.slots);
         DFQ_LAUNCH_CHECK();
     }
     // The staging copies above read host vectors that die at return: make sure the

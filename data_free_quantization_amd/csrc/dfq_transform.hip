@@ -334,6 +334,16 @@ __global__ void absorb_channel_kernel(float* __restrict__ b1, float* __restrict_
 // ---------------------------------------------------------------------------
 // Bias correction: bias_correction.py:15-106,170-172,206-213
 // ---------------------------------------------------------------------------
+// scipy.stats.norm: pdf = exp(-x^2/2)/sqrt(2 pi); cdf = cephes ndtr (erf below
+// |x|/sqrt2 < 1/sqrt2, erfc above), both in float64 on the fp32 argument.
+__device__ __forceinline__ double ndtr_d(double a) {
+    const double x = a * 0.70710678118654752440;
+    const double z = fabs(x);
+    if (z < 0.70710678118654752440) return 0.5 + 0.5 * erf(x);
+    const double y = 0.5 * erfc(z);
+    return x > 0.0 ? 1.0 - y : y;
+}
+
 __global__ void bc_expect_kernel(const float* __restrict__ w, const float* __restrict__ b, int64_t n, int relu,
                                  int accumulate, float* __restrict__ out) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
@@ -341,10 +351,10 @@ __global__ void bc_expect_kernel(const float* __restrict__ w, const float* __res
         float ex;
         if (relu) {
             const float x = (-bj) / wj;               // -bias/weight (fp32)
-            const double xd = (double)x;               // scipy evaluates in float64 ...
-            const float pdf = (float)(exp(-xd * xd / 2.0) / 2.5066282746310002);  // norm.pdf, sqrt(2*pi)
-            const float cdf = (float)(0.5 * erfc(-xd / 1.4142135623730951));     // norm.cdf
-            ex = wj * pdf + bj * (1.0f - cdf);        // ... and torch finishes in fp32
+            const double xd = (double)x;
+            const float pdf = (float)(exp(-(xd * xd) / 2.0) / 2.5066282746310002);
+            const float cdf = (float)ndtr_d(xd);
+            ex = wj * pdf + bj * (1.0f - cdf);        // torch finishes in fp32
             if (ex < 0.0f) ex = 0.0f;                  // expect[expect < 0] = 0
         } else {
             ex = bj;
@@ -353,32 +363,26 @@ __global__ void bc_expect_kernel(const float* __restrict__ w, const float* __res
     }
 }
 
+// One thread per output row: bias_vec[r, :] = E (+) expect, bias[r] += mean in
+// ATen's order (bias.view(O, -1).mean(dim=1)).
 __global__ void bc_apply_kernel(const float* __restrict__ E, int64_t o, int64_t i2, const float* __restrict__ ex,
-                                int64_t f, int64_t bcols, float* __restrict__ bias, float* __restrict__ bias_vec,
-                                int do_mean) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
-    for (int64_t r = wave; r < o; r += nwaves) {
-        float acc = 0.f;
-        for (int64_t j = lane; j < bcols; j += 64) {
-            const float v = E[r * i2 + (i2 > 1 ? j : 0)] + ex[f > 1 ? j : 0];
-            if (bias_vec) bias_vec[r * bcols + j] = v;
-            acc += v;
-        }
-        if (do_mean) {
-            acc = wave_sum_f(acc);
-            if (lane == 0) bias[r] = bias[r] + acc / (float)bcols;
-        }
+                                int64_t f, int64_t bcols, float* __restrict__ bias, float* __restrict__ bias_vec) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < o; r += (int64_t)gridDim.x * blockDim.x) {
+        auto get = [&](int64_t j) { return E[r * i2 + (i2 > 1 ? j : 0)] + ex[f > 1 ? j : 0]; };
+        if (bias_vec)
+            for (int64_t j = 0; j < bcols; ++j) bias_vec[r * bcols + j] = get(j);
+        const float sum = aten_inner_sum(get, bcols);
+        bias[r] = bias[r] + sum / (float)bcols;
     }
 }
 
-__global__ void bc_propagate_kernel(const float* __restrict__ bias_vec, int64_t nrows, int64_t f,
+// One thread per BN channel: fake_b[c] += mean_r(-bias_vec[r*f + c]) in ATen's
+// order for bias_prev.view(-1, F).mean(0) with `threads` intra-op threads.
+__global__ void bc_propagate_kernel(const float* __restrict__ bias_vec, int64_t nrows, int64_t f, int threads,
                                     float* __restrict__ fake_b) {
     for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < f; c += (int64_t)gridDim.x * blockDim.x) {
-        float acc = 0.f;
-        for (int64_t r = 0; r < nrows; ++r) acc += -bias_vec[r * f + c];
-        fake_b[c] = fake_b[c] + acc / (float)nrows;
+        const float s = -aten_outer_col_sum(bias_vec, nrows, f, c, threads);   // sum(-v) == -sum(v) exactly
+        fake_b[c] = fake_b[c] + s / (float)nrows;
     }
 }
 
@@ -574,18 +578,18 @@ extern "C" int dfq_bc_apply(const float* E, int64_t o, int64_t i2, const float* 
     if (bcols_out) *bcols_out = bcols;
     // _apply_bias_correction: sizes never equal (2-D vs 1-D); numel must exceed o
     if (o * bcols <= o) return DFQ_ERR_SHAPE;
-    const int wave_blocks = (int)std::min<int64_t>(ceil_div(o, kThreads / 64), 2048);
-    hipLaunchKernelGGL(bc_apply_kernel, dim3(wave_blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream), E, o,
-                       i2, expect, f, bcols, bias, bias_vec, 1);
+    hipLaunchKernelGGL(bc_apply_kernel, dim3(blocks_for(o)), dim3(kThreads), 0, static_cast<hipStream_t>(stream), E,
+                       o, i2, expect, f, bcols, bias, bias_vec);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }
 
-extern "C" int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_t f, void* stream) {
-    if (!bias_vec || !fake_b || numel <= 0 || f <= 0) return DFQ_ERR_INVALID;
+extern "C" int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_t f, int32_t ref_threads,
+                                void* stream) {
+    if (!bias_vec || !fake_b || numel <= 0 || f <= 0 || ref_threads < 1) return DFQ_ERR_INVALID;
     if (numel % f != 0) return DFQ_ERR_SHAPE;   // .view(-1, F) fails
     hipLaunchKernelGGL(bc_propagate_kernel, dim3(blocks_for(f)), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
-                       bias_vec, numel / f, f, fake_b);
+                       bias_vec, numel / f, f, (int)ref_threads, fake_b);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }

@@ -109,6 +109,8 @@ typedef struct dfq_sweep_stats {
     int64_t algo_bytes;       /* algorithmic HBM bytes of one execute */
     int32_t launches;         /* kernel launches per execute (1 or 2) */
     int32_t grid_blocks;      /* blocks of the quantize launch */
+    int32_t variant;          /* kernel variant (env DFQ_SWEEP_VARIANT at create) */
+    int32_t reserved;
 } dfq_sweep_stats;
 /* Blocking (uploads the descriptor/task tables once).  descs is copied. */
 int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, dfq_sweep_plan** plan);
@@ -165,16 +167,18 @@ int dfq_bias_absorb(const float* w2, float* b1, float* b2, float* bn_w, float* b
 int dfq_bc_expect(const float* fake_w, const float* fake_b, int64_t n, int32_t relu,
                   int32_t accumulate, float* out, void* stream);
 /* dfq_bc_apply: bias_vec[o,j] = E[o, i2>1 ? j : 0] + expect[f>1 ? j : 0] over the
- * broadcast shape [o, bcols]; bias[o] += mean_j bias_vec[o,j]
+ * broadcast shape [o, bcols]; bias[o] += mean_j bias_vec[o,j] (ATen's sum order)
  * (_compute_final_bias_correction + _apply_bias_correction, :61-106).
  * bias_vec (may be NULL) keeps the [o*bcols] vector for dfq_bc_propagate.
  * Returns DFQ_ERR_SHAPE where torch would raise (non-broadcastable, or numel == o). */
 int dfq_bc_apply(const float* E, int64_t o, int64_t i2, const float* expect, int64_t f,
                  float* bias, float* bias_vec, int64_t* bcols_out, void* stream);
 /* dfq_bc_propagate: fake_b[c] += mean_r ( -bias_vec[r*f + c] ), r < numel/f
- * (bias_prev.view(-1, F).mean(0), bias_correction.py:206-213,251). */
+ * (bias_prev.view(-1, F).mean(0), bias_correction.py:206-213,251).  The fp32 sums
+ * follow ATen's CPU reduction order for `ref_threads` intra-op threads (the
+ * reference's torch.get_num_threads()). */
 int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_t f,
-                     void* stream);
+                     int32_t ref_threads, void* stream);
 
 #ifdef __cplusplus
 }

@@ -40,7 +40,7 @@ def lib():
         L.oracle_bias_absorb.argtypes = [P, P, P, P, P, I64, I64, I64, I64, F32]
         L.oracle_bc_expect.argtypes = [P, P, I64, I32, I32, P]
         L.oracle_bc_apply.argtypes = [P, I64, I64, P, I64, P, P, C.POINTER(I64)]
-        L.oracle_bc_propagate.argtypes = [P, I64, P, I64]
+        L.oracle_bc_propagate.argtypes = [P, I64, P, I64, I32]
         _lib = L
     return _lib
 
@@ -137,10 +137,10 @@ def bc_apply(E, expect, bias):
     return bias, vec[: o * bcols.value]
 
 
-def bc_propagate(vec, fake_b):
+def bc_propagate(vec, fake_b, threads=8):
     vec = _f32(vec)
     fake_b = _f32(fake_b).copy()
-    rc = lib().oracle_bc_propagate(_p(vec), vec.size, _p(fake_b), fake_b.size)
+    rc = lib().oracle_bc_propagate(_p(vec), vec.size, _p(fake_b), fake_b.size, threads)
     if rc:
         raise RuntimeError(f"oracle_bc_propagate rc={rc}")
     return fake_b

@@ -1,0 +1,62 @@
+"""A/B the sweep kernel variants in ONE process on the same data (interleaved
+rounds, median and min per variant; cdna_hip_programming.md 5.4 rule 24)."""
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    import argparse
+    p = argparse.ArgumentParser()
+    p.add_argument("--variants", default="0,1,2,3")
+    p.add_argument("--rounds", type=int, default=7)
+    p.add_argument("--reps", type=int, default=10)
+    p.add_argument("--model", default="mobilenetv2")
+    p.add_argument("--no-esum", action="store_true")
+    p.add_argument("--asym", action="store_true")
+    a = p.parse_args()
+    import bench
+    from data_free_quantization_amd.sweep import SweepPlan
+    dev = torch.device("cuda:0")
+    args = bench.parse.__wrapped__() if hasattr(bench.parse, "__wrapped__") else None
+    ns = type("A", (), dict(model=a.model, copies=0, bits=8, granularity="channel", asym=a.asym,
+                            no_esum=a.no_esum))()
+    items, shapes, per_copy, copies = bench.build_batch(ns, dev)
+    plans = {}
+    for v in [int(x) for x in a.variants.split(",")]:
+        os.environ["DFQ_SWEEP_VARIANT"] = str(v)
+        plans[v] = SweepPlan(items)
+    stream = torch.cuda.current_stream(dev)
+    times = {v: [] for v in plans}
+    for v, pl in plans.items():
+        for _ in range(3):
+            pl.execute(stream)
+    torch.cuda.synchronize()
+    for r in range(a.rounds):
+        for v, pl in plans.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(a.reps):
+                pl.execute(stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / a.reps)
+    out = {}
+    for v, pl in plans.items():
+        med = statistics.median(times[v])
+        gbs = pl.stats["algo_bytes"] / (med / 1e3) / 1e9
+        out[v] = dict(median_ms=round(med, 4), min_ms=round(min(times[v]), 4), algo_GBs=round(gbs, 1),
+                      frac=round(gbs / 8000, 4), tasks=pl.stats["n_tasks_main"], grid=pl.stats["grid_blocks"])
+    print(json.dumps(dict(model=a.model, copies=copies, no_esum=a.no_esum, variants=out)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,26 @@
+"""main_dfq flag surface on the GPU (reference README.md:137 command)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("extra", [[], ["--granularity", "channel", "--symmetric", "--bc_mode", "fused"],
+                                   ["--bc_mode", "reference"]])
+def test_main_dfq_full_flags(extra, tmp_path, monkeypatch):
+    from data_free_quantization_amd import main_dfq
+    from data_free_quantization_amd.utils.quantize import QuantConv2d, QuantLinear
+    monkeypatch.chdir(tmp_path)
+    argv = ["--task", "cls", "--relu", "--equalize", "--absorption", "--quantize", "--correction", "--clip_weight",
+            "--bits_weight", "8", "--bits_activation", "8", "--bits_bias", "8", "--log"] + extra
+    model, graph, acc = main_dfq.main(argv)
+    targets = [m for m in graph.values() if type(m) in (QuantConv2d, QuantLinear)]
+    assert len(targets) == 53
+    for m in targets:
+        w = m.weight.detach()
+        assert w.is_cuda and torch.isfinite(w).all()
+        if "--granularity" not in extra:   # per-tensor 8-bit grid: at most 256 distinct values
+            assert torch.unique(w).numel() <= 256
+    assert (tmp_path / "dfq_result.txt").read_text().startswith("task: cls")

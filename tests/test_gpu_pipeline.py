@@ -30,6 +30,7 @@ def test_pipeline_matches_reference(name):
     tkeys = [k for k in graph if type(graph[k]) in TARG]
     assert tkeys == list(P["targets"])
     failures = []
+    exact_bias = []
 
     def check(stage):
         ws = np.stack([np.frombuffer(hb(graph[k].weight.detach().cpu().numpy()), np.uint8) for k in tkeys])
@@ -40,7 +41,17 @@ def test_pipeline_matches_reference(name):
                   for k in tkeys]
         if f"{stage}_bias" in P.files:
             got = np.concatenate(biases)
-            np.testing.assert_allclose(got, P[f"{stage}_bias"], rtol=1e-5, atol=1e-6, err_msg=stage)
+            if stage == "bc" or name != "resnet50":
+                # bit-exact (ATen's reduction order reproduced in the BC kernels)
+                if not np.array_equal(got, P[f"{stage}_bias"]):
+                    failures.append((stage, "bias", int((got != P[f"{stage}_bias"]).sum())))
+            else:
+                # ResNet-50 absorption: the reference's b2 += W2.sum(-1) @ c is an MKL
+                # sgemv of unspecified order -> north_star's 1e-5 until the next quantization
+                np.testing.assert_allclose(got, P[f"{stage}_bias"], rtol=1e-5, atol=1e-5, err_msg=stage)
+            bh = np.stack([np.frombuffer(hb(b), np.uint8) for b in biases])
+            if stage in ("absorb", "bn2") and np.array_equal(bh, P[f"{stage}_bh"]):
+                exact_bias.append(stage)
         else:
             bh = np.stack([np.frombuffer(hb(b), np.uint8) for b in biases])
             if not np.array_equal(bh, P[f"{stage}_bh"]):
@@ -50,7 +61,9 @@ def test_pipeline_matches_reference(name):
         if stage in ("bn1", "cle", "absorb", "bn2", "quant", "clip", "bc"):
             check(stage)
         if stage == "cle":
+            assert not failures, failures
             assert cle.LAST_RUN["iterations"] == len(P["cle_diffs"])
+            # per-layer means: fp64 on the GPU vs torch's fp32 cascade sum on the CPU
             np.testing.assert_allclose(cle.LAST_RUN["diffs"], P["cle_diffs"], rtol=1e-5)
 
     bc_error = str(P["bc_error"])
