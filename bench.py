@@ -144,6 +144,33 @@ def pipeline_timing(dev):
     return out
 
 
+def same_mix_probe(n, dev, stream, reps=10):
+    """Achievable-ceiling probe: a grid-stride stream with the sweep's 1x1-layer
+    traffic mix (read 4 B, write 4 + 1 + 4 B per element) and no arithmetic."""
+    import ctypes as C
+    from data_free_quantization_amd import _lib
+    n = n // 16 * 16
+    x = torch.randn(n, device=dev)
+    y = torch.empty_like(x)
+    cds = torch.empty(n, dtype=torch.uint8, device=dev)
+    e = torch.empty_like(x)
+    L = _lib.load()
+    best = None
+    for blocks in (2048, 8192, -4096):
+        for _ in range(2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                _lib.check(L.dfq_probe_stream(_lib.ptr(x), _lib.ptr(y), C.c_void_p(cds.data_ptr()), _lib.ptr(e), n,
+                                              blocks, C.c_void_p(stream.cuda_stream)), "dfq_probe_stream")
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1) / reps
+            best = ms if best is None else min(best, ms)
+    del x, y, cds, e
+    return round(13 * n / (best / 1e3) / 1e9, 1)
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist(args)
@@ -188,6 +215,7 @@ def main():
         except Exception:
             traffic = None
     res = None
+    probe = same_mix_probe(per_copy * copies, dev, stream) if rank == 0 else None
     if rank == 0:
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
         pipe = None if args.no_pipeline else pipeline_timing(dev)
@@ -226,6 +254,8 @@ def main():
                 "kernel": "sweep_main_kernel",
                 "tasks": st["n_tasks_main"],
                 "grid_blocks": st["grid_blocks"],
+                "variant": st["variant"],
+                "same_mix_probe_GBs": probe,
             },
             "cpu_baseline": cpu,
             "pipeline_ms": pipe,

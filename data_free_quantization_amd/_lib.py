@@ -30,6 +30,7 @@ EXPORTS = [
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
     "dfq_bias_absorb", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate",
+    "dfq_probe_stream",
 ]
 
 
@@ -92,6 +93,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_bc_expect": ([P, P, I64, I32, I32, P, P], C.c_int),
         "dfq_bc_apply": ([P, I64, I64, P, I64, P, P, C.POINTER(I64), P], C.c_int),
         "dfq_bc_propagate": ([P, I64, P, I64, I32, P], C.c_int),
+        "dfq_probe_stream": ([P, P, P, P, I64, I32, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

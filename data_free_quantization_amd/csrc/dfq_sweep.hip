@@ -40,10 +40,12 @@ constexpr Variant kVariants[] = {
     {2048, 256, false},   // 0: 10 KB LDS / wave, 16 waves / CU
     {1024, 128, true},    // 1: 2 x 4 KB + 1 KB, next task's DMA in flight during compute
     {2048, 256, true},    // 2: 2 x 8 KB + 2 KB
-    {1024, 128, false},   // 3: 5 KB / wave, 32 waves / CU
+    {1024, 128, false},   // 3: 5 KB / wave, 28 waves / CU
+    {4096, 256, false},   // 4: 18 KB / wave, 8 waves / CU
+    {2048, 256, false},   // 5: variant 0 with non-temporal loads and stores
 };
-constexpr int kNumVariants = 4;
-constexpr int kDefaultVariant = 0;
+constexpr int kNumVariants = 6;
+constexpr int kDefaultVariant = 5;   // fastest in the A/B (profiles/r01/ab_*.json)
 
 struct alignas(16) DevTensor {
     const float* src;
@@ -89,11 +91,14 @@ struct LdsLayout {
 
 __device__ __forceinline__ bool is_sym(int mode) { return mode == DFQ_TENSOR_SYM || mode == DFQ_CHANNEL_SYM; }
 
+template <bool NT, typename V>
+__device__ __forceinline__ void st(V* p, const V& v);
+
 __device__ __forceinline__ void store_code(void* codes, int cb, int64_t idx, float q) {
     if (cb == 1) {
-        static_cast<int8_t*>(codes)[idx] = (int8_t)(int)q;  // same bits as uint8 for 0..255
+        st<false>(static_cast<int8_t*>(codes) + idx, (int8_t)(int)q);  // same bits as uint8 for 0..255
     } else {
-        static_cast<int16_t*>(codes)[idx] = (int16_t)(int)q;
+        st<false>(static_cast<int16_t*>(codes) + idx, (int16_t)(int)q);
     }
 }
 
@@ -103,11 +108,37 @@ typedef __attribute__((address_space(1))) void gbl_void_t;
 // HBM -> LDS without a VGPR landing (global_load_lds_dwordx4 / _dword): lane l's
 // bytes land at lds_base + l*size, so one wave-instruction fills a contiguous
 // 1 KiB (16 B/lane) or 256 B (4 B/lane) block of the task's LDS image.
+template <bool NT = false>
 __device__ __forceinline__ void glds16(const float* g, float* lds_base) {
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 16, 0, NT ? 2 : 0);
 }
+template <bool NT = false>
 __device__ __forceinline__ void glds4(const float* g, float* lds_base) {
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 4, 0, NT ? 2 : 0);
+}
+// Output stores; NT: non-temporal (streamed out, never re-read by this launch).
+// Stores through address_space(1) pointers: the descriptor fields are generic
+// pointers, and a flat_store also counts on lgkmcnt, so every LDS wait would
+// drain the wave's outstanding stores.  global_store_* does not.
+#define DFQ_GLOBAL __attribute__((address_space(1)))
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <bool NT, typename V>
+__device__ __forceinline__ void st(V* p, const V& v) {
+    if constexpr (sizeof(V) == 16) {
+        const f32x4 w = {v.x, v.y, v.z, v.w};
+        DFQ_GLOBAL f32x4* g = (DFQ_GLOBAL f32x4*)p;
+        if constexpr (NT) __builtin_nontemporal_store(w, g);
+        else *g = w;
+    } else {
+        DFQ_GLOBAL V* g = (DFQ_GLOBAL V*)p;
+        if constexpr (NT) __builtin_nontemporal_store(v, g);
+        else *g = v;
+    }
+}
+__device__ __forceinline__ float ld(const float* p) { return *(const DFQ_GLOBAL float*)p; }
+__device__ __forceinline__ float4 ld(const float4* p) {
+    const f32x4 v = *(const DFQ_GLOBAL f32x4*)p;
+    return make_float4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -129,14 +160,14 @@ sweep_reduce_kernel(const DevTensor* __restrict__ tensors, const DevTask* __rest
             const int nj = task.n >> 2;
 #pragma unroll 8
             for (int j = lane; j < nj; j += kWave) {
-                const float4 v = reinterpret_cast<const float4*>(src)[j];
+                const float4 v = ld(reinterpret_cast<const float4*>(src) + j);
                 vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
                 vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
             }
         } else {
 #pragma unroll 8
             for (int e = lane; e < task.n; e += kWave) {
-                const float x = src[e];
+                const float x = ld(src + e);
                 vmin = fminf(vmin, x);
                 vmax = fmaxf(vmax, x);
             }
@@ -154,6 +185,7 @@ sweep_reduce_kernel(const DevTensor* __restrict__ tensors, const DevTask* __rest
 // Main launch: one wave task.
 // ---------------------------------------------------------------------------
 // Issue the task's HBM -> LDS DMA (all loads in flight; no wait).
+template <bool NT = false>
 __device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTask& task, float* data, int lane) {
     const float* src = T.src + task.elem_start;
     const int n = task.n;
@@ -161,18 +193,18 @@ __device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTas
         const int nj = n >> 2;
         for (int m = 0; m * kWave < nj; ++m) {
             const int j = lane + m * kWave;
-            if (j < nj) glds16(src + 4 * j, data + 4 * kWave * m);
+            if (j < nj) glds16<NT>(src + 4 * j, data + 4 * kWave * m);
         }
     } else {
         for (int m = 0; m * kWave < n; ++m) {
             const int e = lane + m * kWave;
-            if (e < n) glds4(src + e, data + kWave * m);
+            if (e < n) glds4<NT>(src + e, data + kWave * m);
         }
     }
 }
 
 // Steps 2-4 on a chunk that has landed in ``data``.
-template <int MAXROWS, bool VEC>
+template <int MAXROWS, bool VEC, bool NT = false>
 __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& task, float* data, float* ls,
                                              float* lmn, const uint32_t* __restrict__ slot_min,
                                              const uint32_t* __restrict__ slot_max, int lane) {
@@ -184,58 +216,45 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
     QParams pc{};
     const bool whole = task.nrows > 0;
     if (whole) {
+        // G lanes per row (G * next_pow2(nrows) = 64): every row of the task is
+        // reduced at once; shuffles stay inside a G-lane group and every group
+        // leader builds its row's parameters concurrently.
         const int nrows = task.nrows;
-        if (len >= kWave) {
-            for (int r = 0; r < nrows; ++r) {
-                float vmin = INFINITY, vmax = -INFINITY;
+        int p2 = 1;
+        while (p2 < nrows && p2 < kWave) p2 <<= 1;
+        const int G = kWave / p2;
+        const int sub = lane / G, sl = lane % G;
+        for (int r0 = 0; r0 < nrows; r0 += p2) {
+            const int r = r0 + sub;
+            float vmin = INFINITY, vmax = -INFINITY;
+            if (r < nrows) {
                 const float* row = data + r * len;
                 if (VEC) {
-                    for (int i = lane; 4 * i < len; i += kWave) {
+                    const int q4 = len >> 2;
+                    for (int i = sl; i < q4; i += G) {
                         const float4 v = reinterpret_cast<const float4*>(row)[i];
                         vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
                         vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
                     }
                 } else {
-                    for (int i = lane; i < len; i += kWave) {
+                    for (int i = sl; i < len; i += G) {
                         const float v = row[i];
                         vmin = fminf(vmin, v);
                         vmax = fmaxf(vmax, v);
                     }
                 }
-                vmin = wave_min(vmin);
-                vmax = wave_max(vmax);
-                if (lane == 0) {
-                    const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
-                    ls[r] = p.s;
-                    lmn[r] = p.mn;
-                    const int64_t row_g = task.row0 + r;
-                    if (T.scale) T.scale[row_g] = p.s;
-                    if (T.zero) T.zero[row_g] = p.mn;
-                }
             }
-        } else {
-            int seg = 1;
-            while (seg < len) seg <<= 1;
-            const int per_pass = kWave / seg;
-            const int sub = lane / seg, idx = lane % seg;
-            for (int r0 = 0; r0 < nrows; r0 += per_pass) {
-                const int r = r0 + sub;
-                const bool ok = (r < nrows) && (idx < len);
-                const float v = ok ? data[r * len + idx] : 0.f;
-                float vmin = ok ? v : INFINITY;
-                float vmax = ok ? v : -INFINITY;
-                for (int off = seg >> 1; off >= 1; off >>= 1) {
-                    vmin = fminf(vmin, __shfl_xor(vmin, off, kWave));
-                    vmax = fmaxf(vmax, __shfl_xor(vmax, off, kWave));
-                }
-                if (idx == 0 && r < nrows) {
-                    const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
-                    ls[r] = p.s;
-                    lmn[r] = p.mn;
-                    const int64_t row_g = task.row0 + r;
-                    if (T.scale) T.scale[row_g] = p.s;
-                    if (T.zero) T.zero[row_g] = p.mn;
-                }
+            for (int off = G >> 1; off >= 1; off >>= 1) {
+                vmin = fminf(vmin, __shfl_xor(vmin, off, kWave));
+                vmax = fmaxf(vmax, __shfl_xor(vmax, off, kWave));
+            }
+            if (sl == 0 && r < nrows) {
+                const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
+                ls[r] = p.s;
+                lmn[r] = p.mn;
+                const int64_t row_g = task.row0 + r;
+                if (T.scale) st<false>(T.scale + row_g, p.s);
+                if (T.zero) st<false>(T.zero + row_g, p.mn);
             }
         }
         wave_lds_sync();
@@ -248,8 +267,8 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         pc = make_qparams(mn, mx, T.bits, sym, T.flags, T.given_min, T.given_max);
         if (task.first && lane == 0) {
             const int64_t row_g = (T.mode == DFQ_CHANNEL_ASYM || T.mode == DFQ_CHANNEL_SYM) ? task.row0 : 0;
-            if (T.scale) T.scale[row_g] = pc.s;
-            if (T.zero) T.zero[row_g] = pc.mn;
+            if (T.scale) st<false>(T.scale + row_g, pc.s);
+            if (T.zero) st<false>(T.zero + row_g, pc.mn);
         }
     }
 
@@ -293,21 +312,21 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
             const float y1 = one(xv.y, p, q1);
             const float y2 = one(xv.z, p, q2);
             const float y3 = one(xv.w, p, q3);
-            if (T.dst) reinterpret_cast<float4*>(T.dst + base)[j] = make_float4(y0, y1, y2, y3);
+            if (T.dst) st<NT>(reinterpret_cast<float4*>(T.dst + base) + j, make_float4(y0, y1, y2, y3));
             if (T.codes) {
                 if (T.code_bytes == 1) {
                     const uint32_t c = ((uint32_t)(uint8_t)(int)q0) | ((uint32_t)(uint8_t)(int)q1 << 8) |
                                        ((uint32_t)(uint8_t)(int)q2 << 16) | ((uint32_t)(uint8_t)(int)q3 << 24);
-                    reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base)[j] = c;
+                    st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, c);
                 } else {
-                    const uint2 c = make_uint2(((uint32_t)(uint16_t)(int)q0) | ((uint32_t)(uint16_t)(int)q1 << 16),
-                                               ((uint32_t)(uint16_t)(int)q2) | ((uint32_t)(uint16_t)(int)q3 << 16));
-                    reinterpret_cast<uint2*>(static_cast<uint16_t*>(T.codes) + base)[j] = c;
+                    const uint64_t c = ((uint64_t)(uint16_t)(int)q0) | ((uint64_t)(uint16_t)(int)q1 << 16) |
+                                       ((uint64_t)(uint16_t)(int)q2 << 32) | ((uint64_t)(uint16_t)(int)q3 << 48);
+                    st<NT>(reinterpret_cast<uint64_t*>(static_cast<uint16_t*>(T.codes) + base) + j, c);
                 }
             }
             if (want_e) {
                 const float4 ev = make_float4(y0 - xv.x, y1 - xv.y, y2 - xv.z, y3 - xv.w);
-                if (khw == 1) reinterpret_cast<float4*>(T.esum + base)[j] = ev;
+                if (khw == 1) st<NT>(reinterpret_cast<float4*>(T.esum + base) + j, ev);
                 else reinterpret_cast<float4*>(data)[j] = ev;
             }
         }
@@ -317,10 +336,10 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
             const float xv = data[e];
             float qv;
             const float yv = one(xv, params_for(e), qv);
-            if (T.dst) T.dst[base + e] = yv;
+            if (T.dst) st<false>(T.dst + base + e, yv);
             if (T.codes) store_code(T.codes, T.code_bytes, base + e, qv);
             if (want_e) {
-                if (khw == 1) T.esum[base + e] = yv - xv;
+                if (khw == 1) st<false>(T.esum + base + e, yv - xv);
                 else data[e] = yv - xv;
             }
         }
@@ -333,13 +352,13 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         const int64_t pbase = base / khw;
         for (int pi = lane; pi < np; pi += kWave) {
             const float* e = data + pi * khw;   // torch.sum(eps.view(O, I, -1), -1) order
-            T.esum[pbase + pi] = aten_inner_sum([&](int64_t k) { return e[k]; }, khw);
+            st<false>(T.esum + pbase + pi, aten_inner_sum([&](int64_t k) { return e[k]; }, khw));
         }
     }
     wave_lds_sync();  // LDS is reused by this wave's next task
 }
 
-template <int CHUNK, int MAXROWS, bool PREFETCH>
+template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false>
 __global__ void __launch_bounds__(kBlockThreads)
 sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restrict__ tasks, int64_t ntasks,
                   const uint32_t* __restrict__ slot_min, const uint32_t* __restrict__ slot_max) {
@@ -354,14 +373,18 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
     const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + w;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     if constexpr (!PREFETCH) {
+        DevTask task;
+        if (wave0 < ntasks) task = tasks[wave0];
         for (int64_t t = wave0; t < ntasks; t += nwaves) {
-            const DevTask task = tasks[t];
             const DevTensor T = tensors[task.tensor];
-            issue_task_load(T, task, wl, lane);
+            issue_task_load<NT>(T, task, wl, lane);
+            DevTask next = task;   // next record's scalar load overlaps this task
+            if (t + nwaves < ntasks) next = tasks[t + nwaves];
             vm_wait_all();
             wave_lds_sync();
-            if (T.vec4) compute_task<MAXROWS, true>(T, task, wl, ls, lmn, slot_min, slot_max, lane);
-            else compute_task<MAXROWS, false>(T, task, wl, ls, lmn, slot_min, slot_max, lane);
+            if (T.vec4) compute_task<MAXROWS, true, NT>(T, task, wl, ls, lmn, slot_min, slot_max, lane);
+            else compute_task<MAXROWS, false, NT>(T, task, wl, ls, lmn, slot_min, slot_max, lane);
+            task = next;
         }
     } else {
         // Double-buffered: the next task's DMA is issued before this task computes.
@@ -534,6 +557,14 @@ static void launch_main(int variant, int grid, hipStream_t s, const DevTensor* t
         case 3:
             hipLaunchKernelGGL((sweep_main_kernel<1024, 128, false>), dim3(grid), dim3(kBlockThreads), 0, s, t, k,
                                n, smin, smax);
+            break;
+        case 4:
+            hipLaunchKernelGGL((sweep_main_kernel<4096, 256, false>), dim3(grid), dim3(kBlockThreads), 0, s, t, k,
+                               n, smin, smax);
+            break;
+        case 5:
+            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false, true>), dim3(grid), dim3(kBlockThreads), 0, s,
+                               t, k, n, smin, smax);
             break;
         default:
             hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false>), dim3(grid), dim3(kBlockThreads), 0, s, t, k,

@@ -180,6 +180,14 @@ int dfq_bc_apply(const float* E, int64_t o, int64_t i2, const float* expect, int
 int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_t f,
                      int32_t ref_threads, void* stream);
 
+/* ---- measurement --------------------------------------------------------
+ * Same-mix streaming probe (no arithmetic): y = x, codes = bits of x, esum = x,
+ * n elements (multiple of 4); blocks < 0 selects a 4-deep variant with -blocks
+ * blocks (n multiple of 16).  Used by bench.py as the achievable ceiling for
+ * the sweep's traffic mix; not part of the reference interface. */
+int dfq_probe_stream(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t blocks,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

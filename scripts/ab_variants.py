@@ -16,7 +16,7 @@ sys.path.insert(0, str(ROOT))
 def main():
     import argparse
     p = argparse.ArgumentParser()
-    p.add_argument("--variants", default="0,1,2,3")
+    p.add_argument("--variants", default="0,2,4,5")
     p.add_argument("--rounds", type=int, default=7)
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--model", default="mobilenetv2")
@@ -49,13 +49,36 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / a.reps)
+    # same-mix streaming probe (13 B / element: read 4, write 4 + 1 + 4)
+    import ctypes as C
+    from data_free_quantization_amd import _lib
+    n = per_copy * copies // 16 * 16
+    x = torch.randn(n, device=dev)
+    y = torch.empty_like(x)
+    cds = torch.empty(n, dtype=torch.uint8, device=dev)
+    e = torch.empty_like(x)
+    L = _lib.load()
+    pt = []
+    for blocks in (2048, 8192, -2048, -4096, -8192):
+        for r in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(a.reps):
+                _lib.check(L.dfq_probe_stream(_lib.ptr(x), _lib.ptr(y), None if a.no_esum else C.c_void_p(cds.data_ptr()),
+                                              None if a.no_esum else _lib.ptr(e), n, blocks, _lib.stream_of(x)), "probe")
+            e1.record(stream)
+            torch.cuda.synchronize()
+            pt.append((e0.elapsed_time(e1) / a.reps, blocks))
+    best = min(pt)
+    probe_bytes = (4 + 4 + (0 if a.no_esum else 5)) * n
+    probe = dict(ms=round(best[0], 4), blocks=best[1], GBs=round(probe_bytes / (best[0] / 1e3) / 1e9, 1))
     out = {}
     for v, pl in plans.items():
         med = statistics.median(times[v])
         gbs = pl.stats["algo_bytes"] / (med / 1e3) / 1e9
         out[v] = dict(median_ms=round(med, 4), min_ms=round(min(times[v]), 4), algo_GBs=round(gbs, 1),
                       frac=round(gbs / 8000, 4), tasks=pl.stats["n_tasks_main"], grid=pl.stats["grid_blocks"])
-    print(json.dumps(dict(model=a.model, copies=copies, no_esum=a.no_esum, variants=out)))
+    print(json.dumps(dict(model=a.model, copies=copies, no_esum=a.no_esum, probe=probe, variants=out)))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,39 @@
+"""Copy a rocprofv3 run (scripts/profile.sh output under gpurun_out/<tag>) into
+profiles/<round>/ and write profiles/traffic_<round>.json: HBM bytes per launch of
+the sweep kernel from FETCH_SIZE / WRITE_SIZE, corrected per MI355X_MICROARCH.md
+(FETCH_SIZE reports 1/2 of wide streaming reads on gfx950)."""
+import csv
+import json
+import shutil
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def main(tag, rnd, algo_bytes, workload):
+    src = ROOT / "gpurun_out" / tag
+    dst = ROOT / "profiles" / rnd
+    dst.mkdir(parents=True, exist_ok=True)
+    shutil.copy(src / "kt" / "kt_kernel_stats.csv", dst / "kernel_stats.csv")
+    vals = {}
+    for name in ("fetch", "write"):
+        f = src / name / f"{name}_counter_collection.csv"
+        shutil.copy(f, dst / f"pmc_{name}.csv")
+        rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("sweep_main")]
+        vals[name] = sum(float(r["Counter_Value"]) for r in rows) / len(rows)
+    stats = {r["Name"]: r for r in csv.DictReader(open(src / "kt" / "kt_kernel_stats.csv"))}
+    avg_ns = float(stats["sweep_main_kernel"]["AverageNs"])
+    rd, wr = vals["fetch"] * 1024 * 2, vals["write"] * 1024
+    res = {"kernel": "sweep_main_kernel", "workload": workload, "FETCH_SIZE_KB": vals["fetch"],
+           "WRITE_SIZE_KB": vals["write"],
+           "correction": "FETCH_SIZE x2 (gfx950 reports 1/2 of 16B/lane streaming reads), WRITE_SIZE as is",
+           "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
+           "algo_bytes_per_launch": algo_bytes, "rocprof_avg_ns": avg_ns,
+           "algo_GBs_at_rocprof_avg": algo_bytes / avg_ns}
+    (ROOT / "profiles" / f"traffic_{rnd}.json").write_text(json.dumps(res, indent=1))
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4])
