@@ -55,11 +55,19 @@ def setup_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+        # DFQ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
+        # cards round-robin); the default is RCCL, one rank per GPU.
+        backend = os.environ.get("DFQ_DIST_BACKEND", "nccl")
+        local = local % torch.cuda.device_count() if backend == "gloo" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     else:
+        local = 0
         torch.cuda.set_device(0)
-    return world, rank, torch.device(f"cuda:{local if world > 1 else 0}")
+    return world, rank, torch.device(f"cuda:{local}")
 
 
 def build_batch(args, dev):
@@ -198,11 +206,8 @@ def main():
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)          # device time of the K launches on this stream
-    t_step = wall / args.steps
-    if world > 1:
-        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_step = float(tt.item()) / args.steps
+    from data_free_quantization_amd.distributed import max_over_ranks
+    t_step = max_over_ranks(wall, dev) / args.steps
     weight_bytes = 4 * per_copy * copies * world
     value = weight_bytes / t_step / 1e9
     launch_ms = dev_ms / (args.steps * st["launches"])
@@ -240,7 +245,8 @@ def main():
                 "copies_per_gpu": copies,
                 "layers_per_copy": len(shapes),
                 "weights_per_copy": per_copy,
-                "parallelism": f"layer-list sharding, {world} rank(s), no data-path collective",
+                "parallelism": f"{world} rank(s), one process per GPU, independent weight sets per rank "
+                               "(no data-path collective)",
             },
             "roofline": {
                 "bound": "hbm",
