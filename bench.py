@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--no-esum", action="store_true", help="skip the bias-correction error sums")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     p.add_argument("--no-pipeline", action="store_true", help="skip the one-off full-DFQ pipeline timing")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the other BASELINE configs (ResNet-50, DeepLab, INT4, per-tensor; sharded single model)")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r01.json"))
     return p.parse_args()
 
@@ -70,28 +72,108 @@ def setup_dist(args):
     return world, rank, torch.device(f"cuda:{local}")
 
 
-def build_batch(args, dev):
-    """Synthetic weight sets of the model's target-layer shapes, generated on the
-    GPU (conv ~ N(0, sqrt(2/(k*k*O))), linear ~ N(0, 0.01), as SURVEY.md 8d)."""
+def model_shapes(name):
     from data_free_quantization_amd import zoo
+    return [tuple(m.weight.shape) for m in zoo.target_layers(zoo.MODELS[name]())]
+
+
+def synth_weight(s, dev, gen):
+    """conv ~ N(0, sqrt(2/(k*k*O))), linear ~ N(0, 0.01)."""
+    std = (2.0 / (s[2] * s[3] * s[0])) ** 0.5 if len(s) == 4 else 0.01
+    return torch.randn(s, device=dev, generator=gen) * std
+
+
+def build_batch(model, dev, copies=0, bits=8, channel=True, sym=True, esum=True, seed=1234):
+    """Synthetic weight sets of the model's target-layer shapes, generated on the
+    GPU; ``copies`` = 0 picks enough for >= 2 GiB of fp32 weights (past the
+    256 MB Infinity Cache)."""
     from data_free_quantization_amd.sweep import allocate, khw_of
-    model = zoo.MODELS[args.model]()
-    shapes = [tuple(m.weight.shape) for m in zoo.target_layers(model)]
+    shapes = model_shapes(model)
     per_copy = sum(int(torch.Size(s).numel()) for s in shapes)
-    copies = args.copies or max(1, -(-(2 << 30) // (4 * per_copy)))   # >= 2 GiB of fp32 weights
-    gen = torch.Generator(device=dev).manual_seed(1234 + int(os.environ.get("RANK", "0")))
+    copies = copies or max(1, -(-(2 << 30) // (4 * per_copy)))
+    gen = torch.Generator(device=dev).manual_seed(seed + int(os.environ.get("RANK", "0")))
     items = []
     for c in range(copies):
         for s in shapes:
-            if len(s) == 4:
-                std = (2.0 / (s[2] * s[3] * s[0])) ** 0.5
-            else:
-                std = 0.01
-            w = torch.randn(s, device=dev, generator=gen) * std
-            items.append(allocate(w, bits=args.bits, per_channel=args.granularity == "channel",
-                                  symmetric=not args.asym, khw=khw_of(w), want_esum=not args.no_esum,
+            w = synth_weight(s, dev, gen)
+            items.append(allocate(w, bits=bits, per_channel=channel, symmetric=sym, khw=khw_of(w), want_esum=esum,
                                   clip=(-15.0, 15.0)))
     return items, shapes, per_copy, copies
+
+
+def time_plan(plan, stream, dev, steps, warmup):
+    """Device ms per execute() of ``plan`` (all its launches; HIP events on its stream)."""
+    for _ in range(warmup):
+        plan.execute(stream)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        plan.execute(stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) / steps
+
+
+SECONDARY = [
+    # (name, model, bits, channel, sym, esum) -- BASELINE.json configs[2..4]
+    ("resnet50 per-ch sym INT8 + clip + BC error sums", "resnet50", 8, True, True, True),
+    ("deeplab per-ch sym INT8 + clip + BC error sums", "deeplab", 8, True, True, True),
+    ("resnet50 per-ch asym INT4 + clip", "resnet50", 4, True, False, False),
+    ("mobilenetv2 per-tensor asym INT8 (quantize_targ_layer) + clip", "mobilenetv2", 8, False, False, False),
+]
+
+
+def secondary_configs(dev, stream, steps=20):
+    """The other BASELINE configs on this GPU (>= 2 GiB batches): algorithmic
+    GB/s of the sweep kernel and weight-GB/s, so the >= 60 % roofline target is
+    checked on ResNet-50 as well as MobileNetV2."""
+    from data_free_quantization_amd.sweep import SweepPlan
+    out = []
+    for name, model, bits, ch, sym, es in SECONDARY:
+        items, _, per_copy, copies = build_batch(model, dev, bits=bits, channel=ch, sym=sym, esum=es, seed=99)
+        plan = SweepPlan(items)
+        ms = time_plan(plan, stream, dev, steps, 3)
+        st = plan.stats
+        out.append({"config": name, "copies": copies, "algo_GBs": round(st["algo_bytes"] / ms / 1e6, 1),
+                    "frac": round(st["algo_bytes"] / ms / 1e6 / HBM_PEAK_GBS, 4),
+                    "weight_GBs": round(4 * per_copy * copies / ms / 1e6, 1),
+                    "step_ms": round(ms, 4), "launches": st["launches"], "reduce_tasks": st["n_tasks_reduce"]})
+        plan.destroy()
+        del items, plan
+        torch.cuda.empty_cache()
+    return out
+
+
+def sharded_single_model(dev, stream, world, reps=20):
+    """BASELINE configs[4]: ONE ResNet-50 weight set (INT4 per-channel asym +
+    clip), its layer list LPT-sharded over the ranks; ms per pass with the
+    outputs left sharded and with a packed all-gather to every rank."""
+    import torch.distributed as dist
+    from data_free_quantization_amd import distributed as D
+    from data_free_quantization_amd.sweep import khw_of
+    gen = torch.Generator(device=dev).manual_seed(7)            # same weights on every rank
+    ws = [synth_weight(s, dev, gen) for s in model_shapes("resnet50")]
+    specs = [D.output_spec(w, True, 4, False, khw_of(w), False) for w in ws]
+    compute = D.gpu_sweep(ws, bits=4, per_channel=True, symmetric=False, want_esum=False, clip=(-15.0, 15.0),
+                          reuse=True)
+    res = {}
+    for gather in ("none", "all"):
+        for _ in range(3):
+            D.sharded_sweep(ws, compute, specs, gather=gather)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            D.sharded_sweep(ws, compute, specs, gather=gather)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t = D.max_over_ranks(time.perf_counter() - t0, dev) / reps
+        res[f"ms_gather_{gather}"] = round(t * 1e3, 4)
+    res["weights"] = sum(w.numel() for w in ws)
+    res["note"] = "host-timed per pass (sweep launch + packing + all_gather_into_tensor); single-model sizes " \
+                  "are latency bound"
+    return res
 
 
 def cpu_baseline(args, shapes, seconds):
@@ -183,15 +265,18 @@ def main():
     args = parse()
     world, rank, dev = setup_dist(args)
     from data_free_quantization_amd.sweep import SweepPlan
-    items, shapes, per_copy, copies = build_batch(args, dev)
+    from data_free_quantization_amd.distributed import max_over_ranks
+    items, shapes, per_copy, copies = build_batch(args.model, dev, args.copies, args.bits,
+                                                  args.granularity == "channel", not args.asym, not args.no_esum)
     plan = SweepPlan(items)
     st = plan.stats
     stream = torch.cuda.current_stream(dev)
+    if world > 1:
+        import torch.distributed as dist
     for _ in range(args.warmup):
         plan.execute(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
-        import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -206,12 +291,14 @@ def main():
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)          # device time of the K launches on this stream
-    from data_free_quantization_amd.distributed import max_over_ranks
     t_step = max_over_ranks(wall, dev) / args.steps
     weight_bytes = 4 * per_copy * copies * world
     value = weight_bytes / t_step / 1e9
-    launch_ms = dev_ms / (args.steps * st["launches"])
+    launch_ms = dev_ms / args.steps          # device time of one execute() (st["launches"] kernels)
     achieved = st["algo_bytes"] / (launch_ms / 1e3) / 1e9
+    plan.destroy()
+    del plan, items
+    torch.cuda.empty_cache()
     traffic = None
     tj = Path(args.traffic_json)
     if tj.exists():
@@ -219,9 +306,11 @@ def main():
             traffic = json.loads(tj.read_text()).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    sharded = sharded_single_model(dev, stream, world) if world > 1 and not args.no_secondary else None
     res = None
-    probe = same_mix_probe(per_copy * copies, dev, stream) if rank == 0 else None
     if rank == 0:
+        probe = same_mix_probe(per_copy * copies, dev, stream)
+        second = None if args.no_secondary else secondary_configs(dev, stream)
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
         pipe = None if args.no_pipeline else pipeline_timing(dev)
         res = {
@@ -257,6 +346,7 @@ def main():
                 "traffic": traffic,
                 "algo_bytes_per_launch": st["algo_bytes"],
                 "launch_ms": round(launch_ms, 4),
+                "launches": st["launches"],
                 "kernel": "sweep_main_kernel",
                 "tasks": st["n_tasks_main"],
                 "grid_blocks": st["grid_blocks"],
@@ -264,14 +354,16 @@ def main():
                 "same_mix_probe_GBs": probe,
             },
             "cpu_baseline": cpu,
+            "secondary_configs": second,
+            "sharded_single_model": sharded,
             "pipeline_ms": pipe,
             "top1_delta": None,
             "notes": "top-1 needs ImageNet-val + the pretrained checkpoint (absent offline); weight outputs are "
                      "bit-exact with the reference CPU path (tests/test_gpu_pipeline.py)",
         }
         print(json.dumps(res), flush=True)
-    plan.destroy()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
     return res
 

@@ -53,6 +53,15 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup LDS hand-off: this wave's ds_writes complete, then s_barrier.  No
+// vmcnt wait (unlike __syncthreads' fence), so in-flight global stores stay in flight.
+__device__ __forceinline__ void block_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Quantizer parameters, exactly as UniformQuantize.forward builds them

@@ -10,8 +10,14 @@
 // kChunk (2048) contiguous fp32 elements.  A task is either
 //   - "whole rows": up to kMaxRows complete rows; the wave reduces each row's
 //     min/max itself (CHANNEL modes, row_len <= kChunk), or
+//   - a "block-row piece": rows longer than kChunk (up to 4 pieces, e.g. the
+//     4608-element rows of ResNet-50's 512x512x3x3 convs) and small per-tensor
+//     ranges are split over the 4 waves of ONE workgroup: the 4 pieces sit at
+//     list positions 4k..4k+3, so the 4 waves of a block meet them in the same
+//     grid-stride iteration, combine their partial (min, max) through LDS with
+//     one s_barrier, and each quantizes its own piece -- a single HBM pass, or
 //   - a "piece": its (min, max) come from a workspace slot filled by the
-//     reduce launch (TENSOR modes; CHANNEL rows longer than kChunk).
+//     reduce launch (large TENSOR-mode ranges; rows longer than 4 pieces).
 // One wave owns one task at a time (no workgroup barriers): it streams the chunk
 // HBM -> VGPRs with 16-B loads, stages it in a wave-private LDS region for the
 // per-row reductions and the KHW error sums, and writes dq (16 B/lane), codes
@@ -22,6 +28,7 @@
 #include <cstdlib>
 #include <new>
 #include <numeric>
+#include <type_traits>
 #include <vector>
 
 namespace dfq {
@@ -75,7 +82,7 @@ struct alignas(16) DevTask {
     int32_t tensor;
     int32_t n;           // elements in the task
     int32_t row0;        // first row of a whole-row task / the row of a long-row piece
-    int32_t nrows;       // > 0: whole rows; 0: piece
+    int32_t nrows;       // > 0: whole rows; 0: slot piece; -1: block-row piece
     int32_t slot;        // workspace (min,max) slot for pieces, -1 = given range
     int32_t first;       // this piece writes scale/zero for its slot
 };
@@ -207,7 +214,8 @@ __device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTas
 template <int MAXROWS, bool VEC, bool NT = false>
 __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& task, float* data, float* ls,
                                              float* lmn, const uint32_t* __restrict__ slot_min,
-                                             const uint32_t* __restrict__ slot_max, int lane) {
+                                             const uint32_t* __restrict__ slot_max, int lane, float bmn = 0.f,
+                                             float bmx = 0.f) {
     const int n = task.n;
     const bool sym = is_sym(T.mode);
     const int len = (int)T.row_len;
@@ -259,7 +267,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         }
         wave_lds_sync();
     } else {
-        float mn = 0.f, mx = 0.f;
+        float mn = bmn, mx = bmx;   // block-row piece: the workgroup's combined range
         if (task.slot >= 0) {
             mn = dec_ord(slot_min[task.slot]);
             mx = dec_ord(slot_max[task.slot]);
@@ -350,9 +358,25 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         wave_lds_sync();
         const int np = n / khw;
         const int64_t pbase = base / khw;
-        for (int pi = lane; pi < np; pi += kWave) {
-            const float* e = data + pi * khw;   // torch.sum(eps.view(O, I, -1), -1) order
-            st<false>(T.esum + pbase + pi, aten_inner_sum([&](int64_t k) { return e[k]; }, khw));
+        // torch.sum(eps.view(O, I, -1), -1) order; the common kernel sizes get a
+        // compile-time length so the ATen cascade unrolls into straight adds.
+        auto esums = [&](auto kconst) {
+            constexpr int K = decltype(kconst)::value;
+            for (int pi = lane; pi < np; pi += kWave) {
+                const float* e = data + pi * K;
+                st<false>(T.esum + pbase + pi, aten_inner_sum([&](int64_t k) { return e[k]; }, (int64_t)K));
+            }
+        };
+        switch (khw) {
+            case 9: esums(std::integral_constant<int, 9>{}); break;     // 3x3
+            case 49: esums(std::integral_constant<int, 49>{}); break;   // 7x7
+            case 25: esums(std::integral_constant<int, 25>{}); break;   // 5x5
+            case 4: esums(std::integral_constant<int, 4>{}); break;     // 2x2
+            default:
+                for (int pi = lane; pi < np; pi += kWave) {
+                    const float* e = data + pi * khw;
+                    st<false>(T.esum + pbase + pi, aten_inner_sum([&](int64_t k) { return e[k]; }, khw));
+                }
         }
     }
     wave_lds_sync();  // LDS is reused by this wave's next task
@@ -382,8 +406,44 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
             if (t + nwaves < ntasks) next = tasks[t + nwaves];
             vm_wait_all();
             wave_lds_sync();
-            if (T.vec4) compute_task<MAXROWS, true, NT>(T, task, wl, ls, lmn, slot_min, slot_max, lane);
-            else compute_task<MAXROWS, false, NT>(T, task, wl, ls, lmn, slot_min, slot_max, lane);
+            float bmn = 0.f, bmx = 0.f;
+            if (task.nrows < 0) {   // block-row piece: all 4 waves of this block are here
+                float vmin = INFINITY, vmax = -INFINITY;
+                if (T.vec4) {
+                    for (int j = lane; j < (task.n >> 2); j += kWave) {
+                        const float4 v = reinterpret_cast<const float4*>(wl)[j];
+                        vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+                        vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+                    }
+                } else {
+                    for (int e = lane; e < task.n; e += kWave) {
+                        vmin = fminf(vmin, wl[e]);
+                        vmax = fmaxf(vmax, wl[e]);
+                    }
+                }
+                vmin = wave_min(vmin);
+                vmax = wave_max(vmax);
+                // partial (min, max) in this wave's own row-parameter slots (unused by
+                // block-row pieces), read by the block's other waves after the barrier
+                if (lane == 0) {
+                    ls[0] = vmin;
+                    ls[1] = vmax;
+                }
+                block_lds_sync();
+                constexpr int P = Lay::kPerWave;
+                if (task.nrows == -kWavesPerBlock) {
+                    const float* b0 = lds + NB * CHUNK;
+                    bmn = fminf(fminf(b0[0], b0[P]), fminf(b0[2 * P], b0[3 * P]));
+                    bmx = fmaxf(fmaxf(b0[1], b0[P + 1]), fmaxf(b0[2 * P + 1], b0[3 * P + 1]));
+                } else {   // pairs of waves (0,1), (2,3)
+                    const float* b0 = lds + (w & ~1) * P + NB * CHUNK;
+                    bmn = fminf(b0[0], b0[P]);
+                    bmx = fmaxf(b0[1], b0[P + 1]);
+                }
+                block_lds_sync();   // the slots are rewritten by the next task
+            }
+            if (T.vec4) compute_task<MAXROWS, true, NT>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
+            else compute_task<MAXROWS, false, NT>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
             task = next;
         }
     } else {
@@ -433,6 +493,7 @@ static int validate(const dfq_tensor_desc& d) {
 struct Built {
     std::vector<DevTensor> tensors;
     std::vector<DevTask> reduce;
+    std::vector<DevTask> blockrow;   // groups of kWavesPerBlock, placed first in the main list
     std::vector<DevTask> main;
     int64_t slots = 0;
     int64_t elems = 0;
@@ -464,7 +525,14 @@ static int piece_len(int khw, bool vec4, int chunk) {
     return p > 0 ? p : -1;
 }
 
+// DFQ_SWEEP_BLOCKROW=0: long rows through the reduce launch instead (A/B switch).
+static bool blockrow_enabled() {
+    const char* e = getenv("DFQ_SWEEP_BLOCKROW");
+    return !(e && e[0] == '0');
+}
+
 static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Variant& V) {
+    const bool use_blockrow = blockrow_enabled();
     const int kChunk = V.chunk, kMaxRows = V.max_rows;
     for (int32_t ti = 0; ti < n; ++ti) {
         const dfq_tensor_desc& d = descs[ti];
@@ -487,7 +555,36 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
         if (total == 0) continue;
         const int plen = piece_len(d.khw, T.vec4, kChunk);
         if (plen <= 0) return DFQ_ERR_UNSUPPORTED;   // khw > kChunk
-        if (channel && d.row_len <= kChunk) {
+        const bool given = (d.flags & DFQ_GIVEN_RANGE) != 0;
+        const int64_t blen = channel ? d.row_len : total;   // the range's extent
+        const bool block_row = use_blockrow && !V.prefetch && !given && blen <= (int64_t)kWavesPerBlock * plen &&
+                               (!channel || d.row_len > kChunk);
+        if (block_row) {
+            // A group of 4 list entries = 4 waves of one block: one row in 4 pieces,
+            // or (rows <= 2 pieces) two rows in 2 pieces each.  Balanced pieces:
+            // the group waits for its slowest wave.
+            const int64_t nr = channel ? d.rows : 1;
+            const int gs = blen <= 2 * (int64_t)plen ? 2 : kWavesPerBlock;
+            const int64_t unit = T.vec4 ? std::lcm<int64_t>(4, d.khw) : d.khw;
+            const int64_t bpl = ceil_div(ceil_div(blen, unit), (int64_t)gs) * unit;
+            const int64_t rows_per_group = kWavesPerBlock / gs;
+            for (int64_t r0 = 0; r0 < nr; r0 += rows_per_group) {
+                for (int i = 0; i < kWavesPerBlock; ++i) {
+                    const int64_t r = r0 + i / gs;
+                    const int64_t off = (int64_t)(i % gs) * bpl;
+                    DevTask k{};
+                    k.tensor = ti; k.nrows = -gs; k.slot = -1;
+                    if (r < nr) {
+                        k.elem_start = r * blen + std::min<int64_t>(off, blen);
+                        k.n = (int32_t)std::max<int64_t>(0, std::min<int64_t>(bpl, blen - off));
+                        k.row0 = (int32_t)r; k.first = (i % gs == 0);
+                    } else {   // padding half-group: no data, writes nothing
+                        k.elem_start = r0 * blen; k.n = 0; k.row0 = (int32_t)r0; k.first = 0;
+                    }
+                    B.blockrow.push_back(k);
+                }
+            }
+        } else if (channel && d.row_len <= kChunk) {
             const int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(kMaxRows, kChunk / d.row_len));
             for (int64_t r = 0; r < d.rows; r += rpt) {
                 const int64_t nr = std::min<int64_t>(rpt, d.rows - r);
@@ -509,7 +606,6 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                 }
             }
         } else {                // tensor modes: one slot per tensor (none for a given range)
-            const bool given = (d.flags & DFQ_GIVEN_RANGE) != 0;
             const int64_t slot = given ? -1 : B.slots++;
             for (int64_t off = 0; off < total; off += plen) {
                 DevTask k{};
@@ -520,6 +616,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
             }
         }
     }
+    B.main.insert(B.main.begin(), B.blockrow.begin(), B.blockrow.end());
     return DFQ_OK;
 }
 

@@ -123,7 +123,10 @@ def sharded_sweep(weights: Sequence[torch.Tensor], compute: Callable[[List[int]]
             return result
         recv = torch.cat(gl)
     else:
-        dist.all_gather_into_tensor(recv, send, group=group)
+        if dist.get_backend(group) == "gloo":      # gloo: list form (CPU or CUDA tensors)
+            dist.all_gather(list(recv.view(world, cap).unbind(0)), send, group=group)
+        else:                                     # RCCL: one packed all-gather over xGMI
+            dist.all_gather_into_tensor(recv, send, group=group)
         if gather == "rank0" and rank != 0:
             return result
     for r, p in enumerate(parts):
@@ -145,18 +148,27 @@ def max_over_ranks(value: float, device=None, group=None) -> float:
 
 
 def gpu_sweep(weights: Sequence[torch.Tensor], bits=8, per_channel=True, symmetric=True, want_esum=True,
-              clip=None) -> Callable[[List[int]], List[LayerOut]]:
+              clip=None, reuse: bool = False) -> Callable[[List[int]], List[LayerOut]]:
     """The product compute for ``sharded_sweep``: one grouped HIP sweep over the
-    rank's layers (SweepPlan)."""
+    rank's layers (SweepPlan).  ``reuse``: keep the plan and its output buffers
+    for the next call with the same layers (repeated passes overwrite them)."""
     from .sweep import SweepPlan, allocate, khw_of
+    cache: Dict[tuple, tuple] = {}
 
     def run(indices: List[int]) -> List[LayerOut]:
-        items = [allocate(weights[i], bits=bits, per_channel=per_channel, symmetric=symmetric,
-                          khw=khw_of(weights[i]), want_esum=want_esum, clip=clip) for i in indices]
-        if items:
-            plan = SweepPlan(items)
+        key = tuple(indices)
+        if reuse and key in cache:
+            plan, items = cache[key]
+        else:
+            items = [allocate(weights[i], bits=bits, per_channel=per_channel, symmetric=symmetric,
+                              khw=khw_of(weights[i]), want_esum=want_esum, clip=clip) for i in indices]
+            plan = SweepPlan(items) if items else None
+            if reuse:
+                cache[key] = (plan, items)
+        if plan is not None:
             plan.execute()
-            plan.destroy()
+            if not reuse:
+                plan.destroy()
         return [LayerOut(it.dst, it.codes, it.scale, it.zero, it.esum) for it in items]
 
     return run

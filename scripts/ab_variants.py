@@ -26,10 +26,7 @@ def main():
     import bench
     from data_free_quantization_amd.sweep import SweepPlan
     dev = torch.device("cuda:0")
-    args = bench.parse.__wrapped__() if hasattr(bench.parse, "__wrapped__") else None
-    ns = type("A", (), dict(model=a.model, copies=0, bits=8, granularity="channel", asym=a.asym,
-                            no_esum=a.no_esum))()
-    items, shapes, per_copy, copies = bench.build_batch(ns, dev)
+    items, shapes, per_copy, copies = bench.build_batch(a.model, dev, sym=not a.asym, esum=not a.no_esum)
     plans = {}
     for v in [int(x) for x in a.variants.split(",")]:
         os.environ["DFQ_SWEEP_VARIANT"] = str(v)

@@ -137,6 +137,41 @@ def test_long_rows_and_odd_sizes_vs_oracle():
     plan.destroy()
 
 
+def test_block_row_pieces_vs_oracle():
+    """Rows of 2049..4 pieces (one workgroup, single HBM pass) and just past it
+    (slot path), with KH*KW error sums; small per-tensor ranges (block path) next
+    to large ones (reduce launch); odd lengths (scalar loads)."""
+    from data_free_quantization_amd.sweep import allocate, SweepPlan, khw_of
+    rng = np.random.default_rng(11)
+    shapes = [(4, 320, 3, 3), (2, 160, 7, 7), (2, 161, 7, 7), (3, 512, 3, 3), (3, 2051), (2, 8192), (2, 8193),
+              (5, 1025, 1, 1), (1, 3, 3, 3), (64, 32, 3, 3)]
+    items, xs = [], []
+    for shp in shapes:
+        x = rng.normal(0, 1, shp).astype(np.float32)
+        xs.append(x)
+        for mode in range(4):
+            t = torch.from_numpy(x).to(DEV)
+            items.append(allocate(t, bits=8 if mode != 1 else 5, per_channel=mode >= 2, symmetric=mode in (1, 3),
+                                  khw=khw_of(t), want_esum=True, clip=(-1.0, 1.0) if mode == 3 else None))
+    plan = SweepPlan(items)
+    for _ in range(2):
+        plan.execute()
+        torch.cuda.synchronize()
+        k = 0
+        for x in xs:
+            for mode in range(4):
+                it = items[k]
+                k += 1
+                o = O.quantize(x, 8 if mode != 1 else 5, mode, rows=x.shape[0] if mode >= 2 else 1, khw=it.khw,
+                               flags=1 if mode == 3 else 0, clip=(-1.0, 1.0), want_esum=True)
+                assert np.array_equal(it.dst.cpu().numpy(), o["dq"]), (x.shape, mode)
+                assert np.array_equal(it.codes.cpu().numpy().view(o["codes"].dtype), o["codes"]), (x.shape, mode)
+                assert np.array_equal(it.scale.cpu().numpy(), o["scale"]), (x.shape, mode)
+                assert np.array_equal(it.zero.cpu().numpy() + np.float32(0), o["zero"] + np.float32(0))
+                assert np.array_equal(it.esum.cpu().numpy(), o["esum"]), (x.shape, mode)
+    plan.destroy()
+
+
 def test_large_sweep_properties():
     """Full-size (1 GiB) sweep: properties that need no oracle -- codes in range,
     the dequant identity dq == code*s + zero (bit-exact), the rounding bound
