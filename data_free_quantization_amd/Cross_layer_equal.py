@@ -2,13 +2,15 @@
 
 ``_layer_equalization`` runs one relation as HIP kernels (channel-parallel
 ranges + rescale, bit-exact with the reference's sequential channel loop);
-``cross_layer_equalization`` keeps the reference's host loop and stop rule, with
-the per-iteration convergence metric reduced on the GPU (``dfq_diff_plan``)
-instead of a deep copy of the graph.
+``cross_layer_equalization`` runs the reference's loop and stop rule on the
+device (``dfq_cle_plan``); the metric is exact (fp32 torch.mean in ATen's order,
+then numpy's pairwise float64 sum), so the iteration count and every weight match
+the reference.
 """
 from __future__ import annotations
 
 import ctypes as C
+import os
 import warnings
 
 import numpy as np
@@ -73,51 +75,122 @@ class _DiffPlan:
             self._plan = None
 
 
+#: iteration cap of the device loop (the reference's loop has none; a run that
+#: reaches it warns)
+MAX_ITERS = int(os.environ.get("DFQ_CLE_MAX_ITERS", "100000"))
+
+
 def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8], Treshhold=2e-7, Count=20,
                              signed=False, eps=0, Save_state=True):
     """Iterate the relations until the summed mean weight change is <= Treshhold
-    or it stayed within 1e-9 for ``Count`` iterations (Cross_layer_equal.py:81-115)."""
+    or it stayed within 1e-9 for ``Count`` iterations (Cross_layer_equal.py:81-115).
+
+    The loop runs on the device (``dfq_cle_plan``): relations grouped into
+    independent chains, the metric (fp32 torch.mean order + numpy's pairwise sum)
+    and the stop rule evaluated by the GPU.  ``DFQ_CLE_MODE=host`` keeps the
+    relation-by-relation host loop (one C call per relation, metric read back
+    every iteration) for comparison."""
     print("Cross layer equalization")
     if Save_state:
         warnings.warn("Save_state plots (ourplots.save_layer) are visualization, not part of the weight path; "
                       "skipped")
     with torch.no_grad():
-        targets = [graph[k] for k in graph if type(graph[k]) in Target_list]
-        plan = _DiffPlan([t.weight.data for t in targets]) if targets else None
-        diff = 1e8
-        iter_count = 0
-        history = []
-        iters = 0
-        try:
-            if plan is not None:
-                plan.snapshot()
-            while diff > Treshhold and iter_count < Count:
-                for rel in relations:
-                    first, second, bn_idx = rel.get_idxs()
-                    l1, l2 = graph[first], graph[second]
-                    if l1.bias is None:   # :93-94
-                        l1.bias = nn.Parameter(torch.zeros(l1.weight.size(0), dtype=torch.float32,
-                                                           device=l1.weight.device), requires_grad=False)
-                    bn = graph[bn_idx]
-                    first_time = rel.S is None
-                    if first_time:
-                        rel.S = torch.empty(l1.weight.size(0), dtype=torch.float32, device=l1.weight.device)
-                    _cle_into(l1.weight.data, l2.weight.data, l1.bias.data, bn.fake_weight, bn.fake_bias,
-                              s_min_max, signed, eps, rel.S, first_time)
-                diff_list = plan.diffs() if plan is not None else []
-                diff_tmp = np.sum(diff_list)
-                history.append(float(diff_tmp))
-                iters += 1
-                if abs(diff - diff_tmp) > 1e-9:
-                    iter_count = 0
-                    diff = diff_tmp
-                else:
-                    iter_count += 1
-        finally:
-            if plan is not None:
-                plan.close()
-        LAST_RUN.clear()
-        LAST_RUN.update(iterations=iters, diffs=history)
+        if os.environ.get("DFQ_CLE_MODE", "device") == "host":
+            _cle_host_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps)
+        else:
+            _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps)
+
+
+def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps):
+    targets = [graph[k].weight.data for k in graph if type(graph[k]) in Target_list]
+    n = len(relations)
+    descs = (_lib.CleRel * max(n, 1))()
+    for i, rel in enumerate(relations):
+        first, second, bn_idx = rel.get_idxs()
+        l1, l2 = graph[first], graph[second]
+        if l1.bias is None:   # :93-94
+            l1.bias = nn.Parameter(torch.zeros(l1.weight.size(0), dtype=torch.float32, device=l1.weight.device),
+                                   requires_grad=False)
+        bn = graph[bn_idx]
+        W1, W2, B1 = l1.weight.data, l2.weight.data, l1.bias.data
+        bnw, bnb = getattr(bn, "fake_weight", None), getattr(bn, "fake_bias", None)
+        _lib.require_device(W1, W2, B1, bnw, bnb)
+        init = rel.S is None
+        if init:
+            rel.S = torch.empty(W1.size(0), dtype=torch.float32, device=W1.device)
+        d = descs[i]
+        d.w1, d.w2, d.b1 = W1.data_ptr(), W2.data_ptr(), B1.data_ptr()
+        d.bn_w = bnw.data_ptr() if bnw is not None else None
+        d.bn_b = bnb.data_ptr() if bnb is not None else None
+        d.s_acc = rel.S.data_ptr()
+        d.c1, d.len1 = W1.shape[0], W1.numel() // W1.shape[0]
+        d.o2, d.i2 = W2.shape[0], W2.shape[1]
+        d.khw2 = W2.numel() // (W2.shape[0] * W2.shape[1])
+        d.s_acc_init = 1 if init else 0
+    _lib.require_device(*targets)
+    nt = len(targets)
+    tp = (C.c_void_p * max(nt, 1))(*[t.data_ptr() for t in targets])
+    tn = (C.c_int64 * max(nt, 1))(*[t.numel() for t in targets])
+    L = _lib.load()
+    plan = C.c_void_p()
+    _lib.check(L.dfq_cle_plan_create(descs, n, tp, tn, nt, float(s_min_max[0]), float(s_min_max[1]),
+                                     int(bool(signed)), float(eps), _lib.REF_THREADS, C.byref(plan)),
+               "dfq_cle_plan_create", RuntimeError)
+    try:
+        iters = C.c_int32(0)
+        hist = (C.c_double * (MAX_ITERS + 1))()
+        dev = targets[0].device if targets else torch.device("cuda", torch.cuda.current_device())
+        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _lib.check(L.dfq_cle_plan_run(plan, float(Treshhold), int(Count), MAX_ITERS, C.byref(iters), hist, stream),
+                   "dfq_cle_plan_run")
+        chains, steps = C.c_int32(0), C.c_int32(0)
+        L.dfq_cle_plan_info(plan, C.byref(chains), C.byref(steps))
+    finally:
+        L.dfq_cle_plan_destroy(plan)
+    if iters.value >= MAX_ITERS:
+        warnings.warn(f"cross_layer_equalization stopped at DFQ_CLE_MAX_ITERS={MAX_ITERS} iterations")
+    LAST_RUN.clear()
+    LAST_RUN.update(iterations=iters.value, diffs=[hist[i] for i in range(iters.value)], chains=chains.value,
+                    steps=steps.value, mode="device")
+
+
+def _cle_host_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps):
+    targets = [graph[k] for k in graph if type(graph[k]) in Target_list]
+    plan = _DiffPlan([t.weight.data for t in targets]) if targets else None
+    diff = 1e8
+    iter_count = 0
+    history = []
+    iters = 0
+    try:
+        if plan is not None:
+            plan.snapshot()
+        while diff > Treshhold and iter_count < Count:
+            for rel in relations:
+                first, second, bn_idx = rel.get_idxs()
+                l1, l2 = graph[first], graph[second]
+                if l1.bias is None:   # :93-94
+                    l1.bias = nn.Parameter(torch.zeros(l1.weight.size(0), dtype=torch.float32,
+                                                       device=l1.weight.device), requires_grad=False)
+                bn = graph[bn_idx]
+                first_time = rel.S is None
+                if first_time:
+                    rel.S = torch.empty(l1.weight.size(0), dtype=torch.float32, device=l1.weight.device)
+                _cle_into(l1.weight.data, l2.weight.data, l1.bias.data, bn.fake_weight, bn.fake_bias,
+                          s_min_max, signed, eps, rel.S, first_time)
+            diff_list = plan.diffs() if plan is not None else []
+            diff_tmp = np.sum(diff_list)
+            history.append(float(diff_tmp))
+            iters += 1
+            if abs(diff - diff_tmp) > 1e-9:
+                iter_count = 0
+                diff = diff_tmp
+            else:
+                iter_count += 1
+    finally:
+        if plan is not None:
+            plan.close()
+    LAST_RUN.clear()
+    LAST_RUN.update(iterations=iters, diffs=history, mode="host")
 
 
 def _cle_into(W1, W2, B1, bnw, bnb, s_min_max, signed, eps, S_acc, first_time):

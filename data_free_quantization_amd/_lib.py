@@ -29,6 +29,7 @@ EXPORTS = [
     "dfq_bn_fold", "dfq_clamp",
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
+    "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
     "dfq_bias_absorb", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate",
     "dfq_probe_stream",
 ]
@@ -48,6 +49,14 @@ class SweepStats(C.Structure):
         ("n_tensors", C.c_int64), ("n_elems", C.c_int64), ("n_tasks_reduce", C.c_int64),
         ("n_tasks_main", C.c_int64), ("algo_bytes", C.c_int64), ("launches", C.c_int32),
         ("grid_blocks", C.c_int32), ("variant", C.c_int32), ("reserved", C.c_int32),
+    ]
+
+
+class CleRel(C.Structure):
+    _fields_ = [
+        ("w1", C.c_void_p), ("w2", C.c_void_p), ("b1", C.c_void_p), ("bn_w", C.c_void_p), ("bn_b", C.c_void_p),
+        ("s_acc", C.c_void_p), ("c1", C.c_int64), ("len1", C.c_int64), ("o2", C.c_int64), ("i2", C.c_int64),
+        ("khw2", C.c_int64), ("s_acc_init", C.c_int32), ("reserved", C.c_int32),
     ]
 
 
@@ -89,6 +98,11 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_diff_plan_snapshot": ([P, P], C.c_int),
         "dfq_diff_plan_execute": ([P, C.POINTER(F64), P], C.c_int),
         "dfq_diff_plan_destroy": ([P], C.c_int),
+        "dfq_cle_plan_create": ([C.POINTER(CleRel), I32, C.POINTER(P), C.POINTER(I64), I32, F64, F64, I32, F32, I32,
+                                 C.POINTER(P)], C.c_int),
+        "dfq_cle_plan_run": ([P, F64, I32, I32, C.POINTER(I32), C.POINTER(F64), P], C.c_int),
+        "dfq_cle_plan_info": ([P, C.POINTER(I32), C.POINTER(I32)], C.c_int),
+        "dfq_cle_plan_destroy": ([P], C.c_int),
         "dfq_bias_absorb": ([P, P, P, P, P, I64, I64, I64, I64, F32, P], C.c_int),
         "dfq_bc_expect": ([P, P, I64, I32, I32, P, P], C.c_int),
         "dfq_bc_apply": ([P, I64, I64, P, I64, P, P, C.POINTER(I64), P], C.c_int),

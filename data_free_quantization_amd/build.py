@@ -15,7 +15,7 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libdfq_hip.so"
-SOURCES = ["dfq_lib.hip", "dfq_sweep.hip", "dfq_transform.hip", "dfq_probe.hip"]
+SOURCES = ["dfq_lib.hip", "dfq_sweep.hip", "dfq_transform.hip", "dfq_cle.hip", "dfq_probe.hip"]
 ARCH = os.environ.get("DFQ_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: no FMA contraction (bit parity with torch CPU eager ops).

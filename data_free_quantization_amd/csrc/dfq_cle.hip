@@ -1,0 +1,1101 @@
+// Cross-layer equalization on the GPU (gfx950): Cross_layer_equal.py:11-116.
+//
+// Two ways in:
+//   * dfq_cle_relation -- one _layer_equalization call (range kernels + rescale),
+//     driven relation by relation from the host, plus dfq_diff_plan_* for the
+//     convergence metric;
+//   * dfq_cle_plan_* -- the whole cross_layer_equalization loop device-resident:
+//     relations are grouped into independent chains (connected components of the
+//     tensors they touch), the k-th relation of every chain runs in ONE range
+//     launch + ONE rescale launch, and the per-iteration metric
+//     sum_l mean|W_l - W_l_prev| (fp32 torch.mean in ATen's reduction order, then
+//     numpy's pairwise float64 sum) and the stop rule are evaluated on the device.
+//     The host only enqueues iterations in batches and reads the state back.
+// fp32 arithmetic is ordered exactly as the reference's torch CPU ops.
+#include "dfq_common.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <new>
+#include <numeric>
+#include <vector>
+
+namespace dfq {
+
+constexpr int kThreads = 256;
+
+static int blocks_for(int64_t n, int per_thread = 1) {
+    const int64_t b = ceil_div(std::max<int64_t>(n, 1), (int64_t)kThreads * per_thread);
+    return (int)std::min<int64_t>(b, 256 * 8);
+}
+// ---------------------------------------------------------------------------
+// Cross-layer equalization: Cross_layer_equal.py:11-59
+//   ws layout: [mins1 | mins2] (2*c1 uint32, memset 0xFF)  [maxs1 | maxs2] (2*c1, memset 0)
+// ---------------------------------------------------------------------------
+struct CleShape {
+    int64_t c1, len1, o2, i2, khw2, groups, o2g;
+};
+
+// W1 rows: one wave per row.
+__global__ void cle_range_w1_kernel(const float* __restrict__ w1, CleShape sh, uint32_t* __restrict__ mins,
+                                    uint32_t* __restrict__ maxs) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t c = wave; c < sh.c1; c += nwaves) {
+        const float* row = w1 + c * sh.len1;
+        float vmin = INFINITY, vmax = -INFINITY;
+        for (int64_t i = lane; i < sh.len1; i += 64) {
+            const float x = row[i];
+            vmin = fminf(vmin, x);
+            vmax = fmaxf(vmax, x);
+        }
+        vmin = wave_min(vmin);
+        vmax = wave_max(vmax);
+        if (lane == 0) {
+            mins[c] = enc_ord(vmin);
+            maxs[c] = enc_ord(vmax);
+        }
+    }
+}
+
+// W2 "columns" W2[g*o2g:(g+1)*o2g, i, :] for channel c = g*i2 + i.
+// i2 == 1 (depthwise-style groups): the column is contiguous -> one wave per channel.
+__global__ void cle_range_w2_contig_kernel(const float* __restrict__ w2, CleShape sh,
+                                           uint32_t* __restrict__ mins, uint32_t* __restrict__ maxs) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int64_t seg = sh.o2g * sh.khw2;
+    for (int64_t c = wave; c < sh.c1; c += nwaves) {
+        const float* col = w2 + c * seg;   // channel c = group c, rows [c*o2g, (c+1)*o2g)
+        float vmin = INFINITY, vmax = -INFINITY;
+        for (int64_t i = lane; i < seg; i += 64) {
+            const float x = col[i];
+            vmin = fminf(vmin, x);
+            vmax = fmaxf(vmax, x);
+        }
+        vmin = wave_min(vmin);
+        vmax = wave_max(vmax);
+        if (lane == 0) {
+            mins[c] = enc_ord(vmin);
+            maxs[c] = enc_ord(vmax);
+        }
+    }
+}
+
+// i2 > 1: each block takes a tile of W2 rows; a thread owns column i and reduces it
+// over the tile's rows, then one ordered-uint atomic per (block, column).
+constexpr int kColTileRows = 16;
+__global__ void cle_range_w2_cols_kernel(const float* __restrict__ w2, CleShape sh,
+                                         uint32_t* __restrict__ mins, uint32_t* __restrict__ maxs) {
+    const int64_t ntiles = ceil_div(sh.o2, kColTileRows);
+    const int64_t rowlen = sh.i2 * sh.khw2;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tile * kColTileRows;
+        const int64_t r1 = std::min<int64_t>(r0 + kColTileRows, sh.o2);
+        for (int64_t i = threadIdx.x; i < sh.i2; i += blockDim.x) {
+            float vmin = INFINITY, vmax = -INFINITY;
+            int64_t g_prev = -1;
+            for (int64_t o = r0; o < r1; ++o) {
+                const int64_t g = o / sh.o2g;
+                if (g != g_prev && g_prev >= 0) {   // tile straddles groups: flush
+                    const int64_t c = g_prev * sh.i2 + i;
+                    atomicMin(&mins[c], enc_ord(vmin));
+                    atomicMax(&maxs[c], enc_ord(vmax));
+                    vmin = INFINITY; vmax = -INFINITY;
+                }
+                g_prev = g;
+                const float* p = w2 + o * rowlen + i * sh.khw2;
+                for (int64_t k = 0; k < sh.khw2; ++k) {
+                    const float x = p[k];
+                    vmin = fminf(vmin, x);
+                    vmax = fmaxf(vmax, x);
+                }
+            }
+            if (g_prev >= 0) {
+                const int64_t c = g_prev * sh.i2 + i;
+                atomicMin(&mins[c], enc_ord(vmin));
+                atomicMax(&maxs[c], enc_ord(vmax));
+            }
+        }
+    }
+}
+
+struct CleScale {
+    float s;    // stored in S and multiplied into W1 rows, B1, bn_w, bn_b
+    float inv;  // multiplied into W2 columns
+};
+
+// s = (1 / (r1 + eps)) * sqrt(r1 * r2 + eps); s = max(smin, min(smax, s))  (Python builtins)
+__device__ __forceinline__ CleScale cle_scale(const uint32_t* mins, const uint32_t* maxs, int64_t c1, int64_t c,
+                                              int is_signed, float eps, double smin, double smax) {
+    const float mn1 = dec_ord(mins[c]), mx1 = dec_ord(maxs[c]);
+    const float mn2 = dec_ord(mins[c1 + c]), mx2 = dec_ord(maxs[c1 + c]);
+    float r1, r2;
+    if (is_signed) {
+        r1 = fmaxf(fabsf(mn1), fabsf(mx1));
+        r2 = fmaxf(fabsf(mn2), fabsf(mx2));
+    } else {
+        r1 = mx1 - mn1;
+        r2 = mx2 - mn2;
+    }
+    const float s = (1.0f / (r1 + eps)) * sqrtf(r1 * r2 + eps);
+    CleScale out;
+    if (s < (float)smax) {
+        if (s > (float)smin) {
+            out.s = s;
+            out.inv = 1.0f / s;
+        } else {
+            out.s = (float)smin;
+            out.inv = (float)(1.0 / smin);
+        }
+    } else {   // includes NaN (dead channel: 0 * inf)
+        const double v = (smax > smin) ? smax : smin;
+        out.s = (float)v;
+        out.inv = (float)(1.0 / v);
+    }
+    return out;
+}
+
+__global__ void cle_apply_kernel(float* __restrict__ w1, float* __restrict__ w2, float* __restrict__ b1,
+                                 float* __restrict__ bn_w, float* __restrict__ bn_b, float* __restrict__ S,
+                                 float* __restrict__ S_acc, int s_acc_init, CleShape sh,
+                                 const uint32_t* __restrict__ mins, const uint32_t* __restrict__ maxs,
+                                 int is_signed, float eps, double smin, double smax) {
+    const int64_t n1 = sh.c1 * sh.len1;
+    const int64_t n2 = sh.o2 * sh.i2 * sh.khw2;
+    const int64_t total = n1 + n2 + sh.c1;
+    const int64_t rowlen2 = sh.i2 * sh.khw2;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        if (e < n1) {
+            const int64_t c = e / sh.len1;
+            const CleScale cs = cle_scale(mins, maxs, sh.c1, c, is_signed, eps, smin, smax);
+            w1[e] = w1[e] * cs.s;
+        } else if (e < n1 + n2) {
+            const int64_t f = e - n1;
+            const int64_t o = f / rowlen2;
+            const int64_t i = (f - o * rowlen2) / sh.khw2;
+            const int64_t c = (o / sh.o2g) * sh.i2 + i;
+            const CleScale cs = cle_scale(mins, maxs, sh.c1, c, is_signed, eps, smin, smax);
+            w2[f] = w2[f] * cs.inv;
+        } else {
+            const int64_t c = e - n1 - n2;
+            const CleScale cs = cle_scale(mins, maxs, sh.c1, c, is_signed, eps, smin, smax);
+            if (b1) b1[c] = b1[c] * cs.s;
+            if (bn_w) bn_w[c] = bn_w[c] * cs.s;
+            if (bn_b) bn_b[c] = bn_b[c] * cs.s;
+            if (S) S[c] = cs.s;
+            if (S_acc) S_acc[c] = s_acc_init ? cs.s : S_acc[c] * cs.s;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CLE convergence metric: Cross_layer_equal.py:83,107-108
+// ---------------------------------------------------------------------------
+struct DiffLayer {
+    float* w;
+    float* snap;
+    int64_t n;
+    int64_t block0;   // first partial slot of this layer
+    int64_t nblocks;
+};
+constexpr int kDiffPerBlock = 8192;
+
+__global__ void diff_partial_kernel(const DiffLayer* __restrict__ layers, const int32_t* __restrict__ block_layer,
+                                    int64_t nblk, double* __restrict__ partial) {
+    __shared__ double red[kThreads / 64];
+    for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const DiffLayer Ly = layers[block_layer[b]];
+        const int64_t lo = (b - Ly.block0) * kDiffPerBlock;
+        const int64_t hi = std::min<int64_t>(lo + kDiffPerBlock, Ly.n);
+        double acc = 0.0;
+        for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+            const float w = Ly.w[i];
+            acc += (double)fabsf(w - Ly.snap[i]);
+            Ly.snap[i] = w;
+        }
+        acc = wave_sum_d(acc);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0.0;
+            for (int k = 0; k < (int)(blockDim.x / 64); ++k) t += red[k];
+            partial[b] = t;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void diff_final_kernel(const DiffLayer* __restrict__ layers, int32_t nl, const double* __restrict__ partial,
+                                  double* __restrict__ out) {
+    for (int l = blockIdx.x * blockDim.x + threadIdx.x; l < nl; l += gridDim.x * blockDim.x) {
+        const DiffLayer Ly = layers[l];
+        double t = 0.0;
+        for (int64_t k = 0; k < Ly.nblocks; ++k) t += partial[Ly.block0 + k];   // fixed order
+        out[l] = Ly.n > 0 ? (double)(float)(t / (double)Ly.n) : 0.0;
+    }
+}
+
+__global__ void copy_kernel(const DiffLayer* __restrict__ layers, const int32_t* __restrict__ block_layer,
+                            int64_t nblk) {
+    for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const DiffLayer Ly = layers[block_layer[b]];
+        const int64_t lo = (b - Ly.block0) * kDiffPerBlock;
+        const int64_t hi = std::min<int64_t>(lo + kDiffPerBlock, Ly.n);
+        for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) Ly.snap[i] = Ly.w[i];
+    }
+}
+
+
+}  // namespace dfq
+
+using namespace dfq;
+
+extern "C" size_t dfq_cle_ws_bytes(int64_t c1) { return (size_t)(c1 > 0 ? c1 : 0) * 4 * sizeof(uint32_t); }
+
+extern "C" int dfq_cle_relation(float* w1, float* w2, float* b1, float* bn_w, float* bn_b, int64_t c1, int64_t len1,
+                                int64_t o2, int64_t i2, int64_t khw2, double s_min, double s_max, int32_t is_signed,
+                                float eps, float* S, float* S_acc, int32_t s_acc_init, void* ws, size_t ws_bytes,
+                                void* stream) {
+    if (!w1 || !w2 || c1 <= 0 || len1 <= 0 || o2 <= 0 || i2 <= 0 || khw2 <= 0) return DFQ_ERR_INVALID;
+    if (!ws || ws_bytes < dfq_cle_ws_bytes(c1)) return DFQ_ERR_WORKSPACE;
+    // grouping as Cross_layer_equal.py:12-18
+    int64_t groups = 1;
+    if (c1 != i2) {
+        groups = c1 / i2;
+        if (groups <= 0 || groups * i2 != c1) return DFQ_ERR_SHAPE;
+    }
+    if (o2 % groups != 0) return DFQ_ERR_SHAPE;
+    CleShape sh{c1, len1, o2, i2, khw2, groups, o2 / groups};
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    uint32_t* mins = static_cast<uint32_t*>(ws);
+    uint32_t* maxs = mins + 2 * c1;
+    DFQ_HIP_CHECK(hipMemsetAsync(mins, 0xFF, sizeof(uint32_t) * 2 * c1, s));
+    DFQ_HIP_CHECK(hipMemsetAsync(maxs, 0x00, sizeof(uint32_t) * 2 * c1, s));
+    const int wave_blocks = (int)std::min<int64_t>(ceil_div(c1, kThreads / 64), 2048);
+    hipLaunchKernelGGL(cle_range_w1_kernel, dim3(wave_blocks), dim3(kThreads), 0, s, w1, sh, mins, maxs);
+    DFQ_LAUNCH_CHECK();
+    if (i2 == 1) {
+        hipLaunchKernelGGL(cle_range_w2_contig_kernel, dim3(wave_blocks), dim3(kThreads), 0, s, w2, sh, mins + c1,
+                           maxs + c1);
+    } else {
+        const int nt = (int)std::min<int64_t>(ceil_div(o2, kColTileRows), 2048);
+        hipLaunchKernelGGL(cle_range_w2_cols_kernel, dim3(nt), dim3(kThreads), 0, s, w2, sh, mins + c1, maxs + c1);
+    }
+    DFQ_LAUNCH_CHECK();
+    const int64_t total = c1 * len1 + o2 * i2 * khw2 + c1;
+    hipLaunchKernelGGL(cle_apply_kernel, dim3(blocks_for(total, 4)), dim3(kThreads), 0, s, w1, w2, b1, bn_w, bn_b,
+                       S, S_acc, s_acc_init, sh, mins, maxs, is_signed, eps, s_min, s_max);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+struct dfq_diff_plan {
+    DiffLayer* d_layers = nullptr;
+    int32_t* d_block_layer = nullptr;
+    double* d_partial = nullptr;
+    double* d_out = nullptr;
+    double* h_out = nullptr;   // pinned
+    int32_t n = 0;
+    int64_t nblk = 0;
+};
+
+extern "C" int dfq_diff_plan_create(float* const* w, float* const* snap, const int64_t* n, int32_t count,
+                                    dfq_diff_plan** out) {
+    if (!out || count < 0 || (count > 0 && (!w || !snap || !n))) return DFQ_ERR_INVALID;
+    *out = nullptr;
+    std::vector<DiffLayer> layers(count);
+    std::vector<int32_t> block_layer;
+    int64_t nb = 0;
+    for (int32_t l = 0; l < count; ++l) {
+        if (!w[l] || !snap[l] || n[l] < 0) return DFQ_ERR_INVALID;
+        const int64_t k = ceil_div(n[l], kDiffPerBlock);
+        layers[l] = DiffLayer{w[l], snap[l], n[l], nb, k};
+        for (int64_t b = 0; b < k; ++b) block_layer.push_back(l);
+        nb += k;
+    }
+    dfq_diff_plan* p = new (std::nothrow) dfq_diff_plan();
+    if (!p) return DFQ_ERR_NOMEM;
+    p->n = count;
+    p->nblk = nb;
+    auto fail = [&](hipError_t e) {
+        set_last_hip_error(e);
+        (void)hipFree(p->d_layers); (void)hipFree(p->d_block_layer); (void)hipFree(p->d_partial); (void)hipFree(p->d_out);
+        if (p->h_out) (void)hipHostFree(p->h_out);
+        delete p;
+        return DFQ_ERR_HIP;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&p->d_layers, sizeof(DiffLayer) * std::max(count, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&p->d_block_layer, sizeof(int32_t) * std::max<int64_t>(nb, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&p->d_partial, sizeof(double) * std::max<int64_t>(nb, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&p->d_out, sizeof(double) * std::max(count, 1))) != hipSuccess) return fail(e);
+    if ((e = hipHostMalloc(&p->h_out, sizeof(double) * std::max(count, 1))) != hipSuccess) return fail(e);
+    if (count > 0 && (e = hipMemcpy(p->d_layers, layers.data(), sizeof(DiffLayer) * count, hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e);
+    if (nb > 0 && (e = hipMemcpy(p->d_block_layer, block_layer.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e);
+    *out = p;
+    return DFQ_OK;
+}
+
+extern "C" int dfq_diff_plan_snapshot(dfq_diff_plan* p, void* stream) {
+    if (!p) return DFQ_ERR_INVALID;
+    if (p->nblk == 0) return DFQ_OK;
+    hipLaunchKernelGGL(copy_kernel, dim3((int)std::min<int64_t>(p->nblk, 4096)), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), p->d_layers, p->d_block_layer, p->nblk);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+extern "C" int dfq_diff_plan_execute(dfq_diff_plan* p, double* out_mean, void* stream) {
+    if (!p || (p->n > 0 && !out_mean)) return DFQ_ERR_INVALID;
+    if (p->n == 0) return DFQ_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (p->nblk > 0) {
+        hipLaunchKernelGGL(diff_partial_kernel, dim3((int)std::min<int64_t>(p->nblk, 4096)), dim3(kThreads), 0, s,
+                           p->d_layers, p->d_block_layer, p->nblk, p->d_partial);
+        DFQ_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(diff_final_kernel, dim3((int)ceil_div(p->n, kThreads)), dim3(kThreads), 0, s, p->d_layers, p->n,
+                       p->d_partial, p->d_out);
+    DFQ_LAUNCH_CHECK();
+    DFQ_HIP_CHECK(hipMemcpyAsync(p->h_out, p->d_out, sizeof(double) * p->n, hipMemcpyDeviceToHost, s));
+    DFQ_HIP_CHECK(hipStreamSynchronize(s));
+    for (int32_t l = 0; l < p->n; ++l) out_mean[l] = p->h_out[l];
+    return DFQ_OK;
+}
+
+extern "C" int dfq_diff_plan_destroy(dfq_diff_plan* p) {
+    if (!p) return DFQ_OK;
+    (void)hipFree(p->d_layers); (void)hipFree(p->d_block_layer); (void)hipFree(p->d_partial); (void)hipFree(p->d_out);
+    if (p->h_out) (void)hipHostFree(p->h_out);
+    delete p;
+    return DFQ_OK;
+}
+
+
+// ============================================================================
+// Device-resident CLE loop (dfq_cle_plan_*)
+// ============================================================================
+namespace dfq {
+
+struct CleRel {
+    float* w1;
+    float* w2;
+    float* b1;
+    float* bnw;
+    float* bnb;
+    float* sacc;
+    int64_t c1, len1, o2, i2, khw2, o2g;
+    int64_t moff;       // this relation's [W1 | W2] range words inside one parity's mins (and maxs)
+    int32_t sacc_init;
+    int32_t pad;
+};
+
+// Range-launch kinds: W1 rows, W2 contiguous channels (i2 == 1), W2 row tiles
+// (i2 > 1, ordered-uint atomics), reset of the OTHER parity's W2 words.
+// Rescale-launch kinds: W1 elements, W2 elements, per-channel vectors.
+enum : int32_t { kRangeW1 = 0, kRangeW2Contig = 1, kRangeW2Tile = 2, kRangeReset = 3 };
+enum : int32_t { kApplyW1 = 0, kApplyW2 = 1, kApplyChannels = 2 };
+
+struct CleTask {
+    int32_t rel;
+    int32_t kind;
+    int64_t a, b;
+};
+
+struct CleLayer {
+    float* w;
+    float* snap;
+    int64_t n;
+};
+
+// One fp32 torch.mean chunk (a thread's share of at::parallel_for in
+// two_pass_reduction): elements [c0, c0 + len) of layer `layer`, slot t.
+struct CleChunk {
+    int32_t layer;
+    int32_t t;
+    int64_t c0;
+    int64_t len;
+};
+
+struct CleState {
+    double diff;         // Cross_layer_equal.py `diff`
+    double thr;          // Treshhold
+    int32_t iter_count;  // consecutive iterations with |diff - diff_tmp| <= 1e-9
+    int32_t iters;       // iterations run
+    int32_t done;
+    int32_t count;       // Count
+    int32_t max_iters;
+    int32_t pad;
+};
+
+constexpr int kCleW1RowsPerTask = 4;       // one wave per row
+constexpr int kCleW2ChansPerTask = 4;      // one wave per contiguous column
+constexpr int64_t kCleElemsPerTask = 4096;
+constexpr int64_t kCleChansPerTask = 1024;
+
+__global__ void __launch_bounds__(kThreads)
+cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
+                      uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st) {
+    if (st->done) return;
+    const int par = st->iters & 1;
+    uint32_t* mins = rng + (int64_t)par * 2 * M;
+    uint32_t* maxs = mins + M;
+    uint32_t* omins = rng + (int64_t)(par ^ 1) * 2 * M;
+    uint32_t* omaxs = omins + M;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    for (int64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
+        const CleTask tk = tasks[t];
+        const CleRel& R = rels[tk.rel];
+        uint32_t* mn = mins + R.moff;
+        uint32_t* mx = maxs + R.moff;
+        if (tk.kind == kRangeW1) {
+            for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
+                const float* row = R.w1 + c * R.len1;
+                float vmin = INFINITY, vmax = -INFINITY;
+                for (int64_t i = lane; i < R.len1; i += 64) {
+                    const float x = row[i];
+                    vmin = fminf(vmin, x);
+                    vmax = fmaxf(vmax, x);
+                }
+                vmin = wave_min(vmin);
+                vmax = wave_max(vmax);
+                if (lane == 0) {
+                    mn[c] = enc_ord(vmin);
+                    mx[c] = enc_ord(vmax);
+                }
+            }
+        } else if (tk.kind == kRangeW2Contig) {
+            const int64_t seg = R.o2g * R.khw2;
+            for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
+                const float* col = R.w2 + c * seg;
+                float vmin = INFINITY, vmax = -INFINITY;
+                for (int64_t i = lane; i < seg; i += 64) {
+                    const float x = col[i];
+                    vmin = fminf(vmin, x);
+                    vmax = fmaxf(vmax, x);
+                }
+                vmin = wave_min(vmin);
+                vmax = wave_max(vmax);
+                if (lane == 0) {
+                    mn[R.c1 + c] = enc_ord(vmin);
+                    mx[R.c1 + c] = enc_ord(vmax);
+                }
+            }
+        } else if (tk.kind == kRangeW2Tile) {
+            const int64_t rowlen = R.i2 * R.khw2;
+            for (int64_t i = threadIdx.x; i < R.i2; i += kThreads) {
+                float vmin = INFINITY, vmax = -INFINITY;
+                int64_t g_prev = -1;
+                for (int64_t o = tk.a; o < tk.b; ++o) {
+                    const int64_t g = o / R.o2g;
+                    if (g != g_prev && g_prev >= 0) {   // tile straddles groups: flush
+                        atomicMin(&mn[R.c1 + g_prev * R.i2 + i], enc_ord(vmin));
+                        atomicMax(&mx[R.c1 + g_prev * R.i2 + i], enc_ord(vmax));
+                        vmin = INFINITY;
+                        vmax = -INFINITY;
+                    }
+                    g_prev = g;
+                    const float* p = R.w2 + o * rowlen + i * R.khw2;
+                    for (int64_t k = 0; k < R.khw2; ++k) {
+                        vmin = fminf(vmin, p[k]);
+                        vmax = fmaxf(vmax, p[k]);
+                    }
+                }
+                if (g_prev >= 0) {
+                    atomicMin(&mn[R.c1 + g_prev * R.i2 + i], enc_ord(vmin));
+                    atomicMax(&mx[R.c1 + g_prev * R.i2 + i], enc_ord(vmax));
+                }
+            }
+        } else {   // kRangeReset: the other parity's W2 words, for the next iteration's atomics
+            for (int64_t c = tk.a + threadIdx.x; c < tk.b; c += kThreads) {
+                omins[R.moff + R.c1 + c] = 0xFFFFFFFFu;
+                omaxs[R.moff + R.c1 + c] = 0u;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
+                      const uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
+                      float eps, double smin, double smax) {
+    if (st->done) return;
+    const int par = st->iters & 1;
+    const bool first_iter = st->iters == 0;
+    const uint32_t* mins = rng + (int64_t)par * 2 * M;
+    const uint32_t* maxs = mins + M;
+    for (int64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
+        const CleTask tk = tasks[t];
+        const CleRel& R = rels[tk.rel];
+        const uint32_t* mn = mins + R.moff;
+        const uint32_t* mx = maxs + R.moff;
+        if (tk.kind == kApplyW1) {
+            for (int64_t e = tk.a + threadIdx.x; e < tk.b; e += kThreads) {
+                const CleScale cs = cle_scale(mn, mx, R.c1, e / R.len1, is_signed, eps, smin, smax);
+                R.w1[e] = R.w1[e] * cs.s;
+            }
+        } else if (tk.kind == kApplyW2) {
+            const int64_t rowlen2 = R.i2 * R.khw2;
+            for (int64_t f = tk.a + threadIdx.x; f < tk.b; f += kThreads) {
+                const int64_t o = f / rowlen2;
+                const int64_t i = (f - o * rowlen2) / R.khw2;
+                const CleScale cs = cle_scale(mn, mx, R.c1, (o / R.o2g) * R.i2 + i, is_signed, eps, smin, smax);
+                R.w2[f] = R.w2[f] * cs.inv;
+            }
+        } else {
+            for (int64_t c = tk.a + threadIdx.x; c < tk.b; c += kThreads) {
+                const CleScale cs = cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax);
+                if (R.b1) R.b1[c] = R.b1[c] * cs.s;
+                if (R.bnw) R.bnw[c] = R.bnw[c] * cs.s;
+                if (R.bnb) R.bnb[c] = R.bnb[c] * cs.s;
+                if (R.sacc) R.sacc[c] = (R.sacc_init && first_iter) ? cs.s : R.sacc[c] * cs.s;
+            }
+        }
+    }
+}
+
+// snap := W for every target layer (before the first iteration)
+__global__ void cle_loop_snap_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
+                                     int64_t nchunks) {
+    for (int64_t k = blockIdx.x; k < nchunks; k += gridDim.x) {
+        const CleChunk ch = chunks[k];
+        const CleLayer Ly = layers[ch.layer];
+        for (int64_t i = ch.c0 + threadIdx.x; i < ch.c0 + ch.len; i += kThreads) Ly.snap[i] = Ly.w[i];
+    }
+}
+
+// The metric's fp32 sums (torch.mean's vectorized_inner_sum over one chunk) as a
+// fixed tree.  A chunk of len elements is 32 streams (s = 8k + l: 8 vector lanes x
+// ILP 4; stream element i is chunk element 32i + s) of sz = len/32 elements, each
+// a 4-level cascade with 16-element level-0 blocks (step 2^4 for every chunk below
+// 16M elements).  One level-1 group of all 32 streams is 8192 CONTIGUOUS elements:
+//   * cle_loop_diff_tiles_kernel: one workgroup per 8192-element tile stages
+//     |W - snap| in LDS (snap := W on the way), 512 threads-worth of level-0 block
+//     sums, then 32 level-1 sums -> b1buf; the chunk's remainder (partial group,
+//     level-0 tail, row_sum tail vectors, scalar tail) is one more "tail tile";
+//   * cle_loop_diff_combine_kernel: one wave per chunk finishes the cascade in
+//     ATen's order (level 2/3, a0 += a1 += a2 += a3, ILP, lanes, scalar tail).
+constexpr int kCleTile = 8192;            // 32 streams x 16 x 16
+constexpr int kCleTailWords = 64;         // per chunk: 32 stream partials, 24 row-tail, 8 scalar-tail values
+
+struct CleUnit {
+    int32_t chunk;
+    int32_t tile;     // < nb1: full level-1 tile; == nb1: the chunk's tail tile
+};
+
+__global__ void __launch_bounds__(kThreads)
+cle_loop_diff_tiles_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
+                           const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t nunits,
+                           float* __restrict__ b1buf, float* __restrict__ tailbuf, const CleState* __restrict__ st) {
+    __shared__ float d[kCleTile + kCleTailWords];
+    __shared__ float b0[512];
+    if (st->done) return;
+    const int tid = threadIdx.x;
+    for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+        const CleUnit un = units[u];
+        const CleChunk ch = chunks[un.chunk];
+        const CleLayer Ly = layers[ch.layer];
+        const float* __restrict__ w = Ly.w + ch.c0;
+        float* __restrict__ sn = Ly.snap + ch.c0;
+        const int64_t len = ch.len, sz = len / 32, vs = len / 8;
+        const int64_t nb1 = sz / 256;
+        const bool full = un.tile < nb1;
+        const int64_t e0 = (int64_t)un.tile * kCleTile;
+        const int64_t cnt = full ? kCleTile : len - e0;
+        for (int64_t e = tid; e < cnt; e += kThreads) {   // |W - W_prev|, snap := W
+            const float x = w[e0 + e];
+            d[e] = fabsf(x - sn[e0 + e]);
+            sn[e0 + e] = x;
+        }
+        __syncthreads();
+        if (full) {
+            for (int q = tid; q < 512; q += kThreads) {   // level 0: 16 blocks x 32 streams
+                const int s = q & 31, m = q >> 5;
+                float a = 0.f;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) a += d[32 * (16 * m + j) + s];
+                b0[m * 32 + s] = a;
+            }
+            __syncthreads();
+            if (tid < 32) {   // level 1
+                float a = 0.f;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) a += b0[m * 32 + tid];
+                b1buf[b1off[un.chunk] + (int64_t)un.tile * 32 + tid] = a;
+            }
+        } else {
+            const int64_t ni = sz - nb1 * 256;   // stream elements left: rem_b0 blocks + tail0
+            const int64_t rem_b0 = ni / 16, tail0 = ni % 16;
+            float* tb = tailbuf + (int64_t)un.chunk * kCleTailWords;
+            if (tid < 32) {
+                float a1p = 0.f;
+                for (int64_t m = 0; m < rem_b0; ++m) {
+                    float a = 0.f;
+                    for (int j = 0; j < 16; ++j) a += d[32 * (16 * m + j) + tid];
+                    a1p += a;
+                }
+                float a0t = 0.f;
+                for (int64_t j = 0; j < tail0; ++j) a0t += d[32 * (16 * rem_b0 + j) + tid];
+                float p = a0t;   // a0 += a1 (a2 and a3 follow in the combine)
+                p += a1p;
+                tb[tid] = p;
+            } else if (tid < 64) {   // raw row_sum-tail vectors (v in [4sz, vs)) and scalar tail
+                const int t = tid - 32;
+                const int64_t nv = vs - 4 * sz;
+                if (t < 24 && t < nv * 8) tb[32 + t] = d[8 * (4 * sz) + t - e0];
+                if (t < 8 && t < len - 8 * vs) tb[56 + t] = d[8 * vs + t - e0];
+            }
+        }
+        __syncthreads();   // LDS reused by the next unit
+    }
+}
+
+// One wave per chunk: the rest of the cascade, the ILP and lane combines and
+// the scalar tail, in ATen's order; part[layer][t] = 0 + sum.
+__global__ void __launch_bounds__(kThreads)
+cle_loop_diff_combine_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks, int64_t nchunks,
+                             const int64_t* __restrict__ b1off, const float* __restrict__ b1buf,
+                             const float* __restrict__ tailbuf, float* __restrict__ part,
+                             const CleState* __restrict__ st) {
+    if (st->done) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+    for (int64_t k = wave; k < nchunks; k += nwaves) {
+        const CleChunk ch = chunks[k];
+        const int64_t len = ch.len;
+        float fa = 0.f;
+        if (len < 8) {   // tiny chunk: scalar row_sum (no tiles ran for it)
+            if (lane == 0) {
+                const CleLayer Ly = layers[ch.layer];
+                float* w = Ly.w + ch.c0;
+                float* sn = Ly.snap + ch.c0;
+                fa = aten_inner_sum([&](int64_t e) {
+                    const float x = w[e];
+                    const float dd = fabsf(x - sn[e]);
+                    sn[e] = x;
+                    return dd;
+                }, len);
+            }
+        } else {
+            const int64_t sz = len / 32, vs = len / 8;
+            const int64_t nb1 = sz / 256, nb2 = nb1 / 16, rem_b1 = nb1 % 16;
+            const float* b1 = b1buf + b1off[k];
+            const float* tb = tailbuf + k * kCleTailWords;
+            float p = 0.f;
+            if (lane < 32) {
+                float a3 = 0.f;
+                for (int64_t r = 0; r < nb2; ++r) {
+                    float b2 = 0.f;
+                    for (int q = 0; q < 16; ++q) b2 += b1[(r * 16 + q) * 32 + lane];
+                    a3 += b2;
+                }
+                float a2p = 0.f;
+                for (int64_t q = 0; q < rem_b1; ++q) a2p += b1[(nb2 * 16 + q) * 32 + lane];
+                p = tb[lane];   // a0 + a1
+                p += a2p;
+                p += a3;
+            }
+            float ps[32];
+#pragma unroll
+            for (int s = 0; s < 32; ++s) ps[s] = __shfl(p, s, 64);
+            if (lane == 0) {
+                for (int64_t e = 0; e < len - 8 * vs; ++e) fa += tb[56 + e];   // scalar tail first
+                const int64_t nv = vs - 4 * sz;
+                for (int l = 0; l < 8; ++l) {
+                    float p0 = ps[l];
+                    for (int64_t v = 0; v < nv; ++v) p0 += tb[32 + v * 8 + l];   // row_sum tail into p0
+                    p0 += ps[l + 8];
+                    p0 += ps[l + 16];
+                    p0 += ps[l + 24];
+                    fa += p0;
+                }
+            }
+        }
+        if (lane == 0) part[(int64_t)ch.layer * 8 + ch.t] = 0.f + fa;   // buffer[t] starts at 0
+    }
+}
+
+// numpy pairwise float64 sum (identity 0 + pairwise_sum), as np.sum(diff_list).
+__device__ double np_pairwise(const double* a, int64_t n) {
+    // numpy's recursion (blocks of <= 128 with 8 accumulators; split at n/2
+    // rounded down to a multiple of 8) as an explicit post-order walk.
+    struct Frame {
+        int64_t o, n;
+        int state;
+    };
+    Frame fr[48];
+    double acc[48];
+    int fp = 0, ap = 0;
+    fr[fp++] = {0, n, 0};
+    while (fp > 0) {
+        Frame& f = fr[fp - 1];
+        if (f.n <= 128) {
+            const double* x = a + f.o;
+            double res;
+            if (f.n < 8) {
+                res = 0.;
+                for (int64_t i = 0; i < f.n; ++i) res += x[i];
+            } else {
+                double r[8];
+                for (int j = 0; j < 8; ++j) r[j] = x[j];
+                int64_t i;
+                for (i = 8; i < f.n - (f.n % 8); i += 8)
+                    for (int j = 0; j < 8; ++j) r[j] += x[i + j];
+                res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+                for (; i < f.n; ++i) res += x[i];
+            }
+            acc[ap++] = res;
+            --fp;
+        } else if (f.state == 0) {
+            int64_t n2 = f.n / 2;
+            n2 -= n2 % 8;
+            f.state = 1;
+            const Frame left{f.o, n2, 0}, right{f.o + n2, f.n - n2, 0};
+            fr[fp++] = right;   // evaluated second
+            fr[fp++] = left;    // evaluated first
+        } else {
+            const double right = acc[--ap];
+            const double left = acc[--ap];
+            acc[ap++] = left + right;
+            --fp;
+        }
+    }
+    return 0. + acc[0];   // add.reduce starts from the identity
+}
+
+// Per-layer fp32 mean from the chunk sums (final_reduce over the 8-slot buffer,
+// then / n), np.sum over layers, history and the stop rule.  One block.
+__global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32_t nl, const float* __restrict__ part,
+                                      double* __restrict__ means, double* __restrict__ hist, CleState* __restrict__ st) {
+    if (st->done) return;
+    for (int l = threadIdx.x; l < nl; l += blockDim.x) {
+        float acc = 0.f;
+        for (int t = 0; t < 8; ++t) acc += part[(int64_t)l * 8 + t];
+        const float sum = 0.f + acc;
+        means[l] = (double)(sum / (float)layers[l].n);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double dt = nl > 0 ? np_pairwise(means, nl) : 0.0;
+        const int it = st->iters;
+        hist[it] = dt;
+        st->iters = it + 1;
+        if (fabs(st->diff - dt) > 1e-9) {
+            st->iter_count = 0;
+            st->diff = dt;
+        } else {
+            st->iter_count += 1;
+        }
+        const bool cont = (st->diff > st->thr) && (st->iter_count < st->count);
+        st->done = (!cont || st->iters >= st->max_iters) ? 1 : 0;
+    }
+}
+
+}  // namespace dfq
+
+struct dfq_cle_plan {
+    CleRel* d_rels = nullptr;
+    CleTask* d_rtasks = nullptr;
+    CleTask* d_atasks = nullptr;
+    CleLayer* d_layers = nullptr;
+    CleChunk* d_chunks = nullptr;
+    uint32_t* d_rng = nullptr;      // [2 parities][mins M | maxs M]
+    float* d_part = nullptr;        // [layers][8]
+    double* d_means = nullptr;
+    double* d_hist = nullptr;
+    int32_t hist_cap = 0;
+    CleState* d_state = nullptr;
+    CleState* h_state = nullptr;    // pinned
+    std::vector<float*> snaps;
+    std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
+    int64_t M = 0, nchunks = 0;
+    int32_t nl = 0, chains = 0, steps = 0;
+    CleUnit* d_units = nullptr;
+    int64_t* d_b1off = nullptr;
+    float* d_b1 = nullptr;          // level-1 sums, [chunk][nb1][32]
+    float* d_tail = nullptr;        // [chunk][kCleTailWords]
+    int64_t nunits = 0;
+    double smin = 1e-8, smax = 1e8;
+    int32_t is_signed = 0;
+    float eps = 0.f;
+};
+
+static void cle_plan_free(dfq_cle_plan* p) {
+    (void)hipFree(p->d_rels); (void)hipFree(p->d_rtasks); (void)hipFree(p->d_atasks); (void)hipFree(p->d_layers);
+    (void)hipFree(p->d_chunks); (void)hipFree(p->d_rng); (void)hipFree(p->d_part); (void)hipFree(p->d_means);
+    (void)hipFree(p->d_hist); (void)hipFree(p->d_state); (void)hipFree(p->d_units); (void)hipFree(p->d_b1off);
+    (void)hipFree(p->d_b1); (void)hipFree(p->d_tail);
+    if (p->h_state) (void)hipHostFree(p->h_state);
+    for (float* s : p->snaps) (void)hipFree(s);
+    delete p;
+}
+
+template <typename T>
+static hipError_t upload(T** dst, const std::vector<T>& v) {
+    hipError_t e = hipMalloc(dst, sizeof(T) * std::max<size_t>(v.size(), 1));
+    if (e != hipSuccess) return e;
+    if (!v.empty()) e = hipMemcpy(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice);
+    return e;
+}
+
+extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
+                                   const int64_t* target_n, int32_t n_targets, double s_min, double s_max,
+                                   int32_t is_signed, float eps, int32_t ref_threads, dfq_cle_plan** out) {
+    if (!out || n_rel < 0 || n_targets < 0 || (n_rel > 0 && !rels) || (n_targets > 0 && (!targets || !target_n)))
+        return DFQ_ERR_INVALID;
+    *out = nullptr;
+    // relations: shapes as dfq_cle_relation
+    std::vector<CleRel> R(n_rel);
+    int64_t M = 0;
+    for (int32_t r = 0; r < n_rel; ++r) {
+        const dfq_cle_rel& d = rels[r];
+        if (!d.w1 || !d.w2 || !d.b1 || d.c1 <= 0 || d.len1 <= 0 || d.o2 <= 0 || d.i2 <= 0 || d.khw2 <= 0)
+            return DFQ_ERR_INVALID;
+        int64_t groups = 1;
+        if (d.c1 != d.i2) {
+            groups = d.c1 / d.i2;
+            if (groups <= 0 || groups * d.i2 != d.c1) return DFQ_ERR_SHAPE;
+        }
+        if (d.o2 % groups != 0) return DFQ_ERR_SHAPE;
+        CleRel c{};
+        c.w1 = d.w1; c.w2 = d.w2; c.b1 = d.b1; c.bnw = d.bn_w; c.bnb = d.bn_b; c.sacc = d.s_acc;
+        c.c1 = d.c1; c.len1 = d.len1; c.o2 = d.o2; c.i2 = d.i2; c.khw2 = d.khw2; c.o2g = d.o2 / groups;
+        c.moff = M;
+        c.sacc_init = d.s_acc_init;
+        M += 2 * d.c1;
+        R[r] = c;
+    }
+    // chains: connected components over the tensors a relation touches
+    std::vector<int32_t> parent(n_rel);
+    std::iota(parent.begin(), parent.end(), 0);
+    auto find = [&](int32_t x) {
+        while (parent[x] != x) x = parent[x] = parent[parent[x]];
+        return x;
+    };
+    for (int32_t a = 0; a < n_rel; ++a) {
+        const void* pa[5] = {R[a].w1, R[a].w2, R[a].b1, R[a].bnw, R[a].bnb};
+        for (int32_t b = 0; b < a; ++b) {
+            const void* pb[5] = {R[b].w1, R[b].w2, R[b].b1, R[b].bnw, R[b].bnb};
+            bool share = false;
+            for (int i = 0; i < 5 && !share; ++i)
+                for (int j = 0; j < 5 && !share; ++j) share = pa[i] && pa[i] == pb[j];
+            if (share) parent[find(a)] = find(b);
+        }
+    }
+    std::vector<int32_t> step_of(n_rel), comp_len(n_rel, 0);
+    int32_t chains = 0, steps = 0;
+    for (int32_t r = 0; r < n_rel; ++r) {
+        const int32_t c = find(r);
+        if (comp_len[c] == 0) ++chains;
+        step_of[r] = comp_len[c]++;
+        steps = std::max(steps, step_of[r] + 1);
+    }
+    // tasks per step
+    std::vector<CleTask> rt, at;
+    std::vector<int64_t> rstep(1, 0), astep(1, 0);
+    for (int32_t k = 0; k < steps; ++k) {
+        for (int32_t r = 0; r < n_rel; ++r) {
+            if (step_of[r] != k) continue;
+            const CleRel& c = R[r];
+            for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
+                rt.push_back({r, kRangeW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1)});
+            if (c.i2 == 1) {
+                for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
+                    rt.push_back({r, kRangeW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1)});
+            } else {
+                for (int64_t a = 0; a < c.o2; a += kColTileRows)
+                    rt.push_back({r, kRangeW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2)});
+                for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
+                    rt.push_back({r, kRangeReset, a, std::min<int64_t>(a + kCleChansPerTask, c.c1)});
+            }
+            const int64_t n1 = c.c1 * c.len1, n2 = c.o2 * c.i2 * c.khw2;
+            for (int64_t a = 0; a < n1; a += kCleElemsPerTask)
+                at.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleElemsPerTask, n1)});
+            for (int64_t a = 0; a < n2; a += kCleElemsPerTask)
+                at.push_back({r, kApplyW2, a, std::min<int64_t>(a + kCleElemsPerTask, n2)});
+            for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
+                at.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kCleChansPerTask, c.c1)});
+        }
+        rstep.push_back((int64_t)rt.size());
+        astep.push_back((int64_t)at.size());
+    }
+    // metric chunks: torch.mean = sum / n; the sum is two_pass_reduction over
+    // min(threads, ceil(n / 32768)) equal chunks when n >= 32768 (serial below)
+    dfq_cle_plan* p = new (std::nothrow) dfq_cle_plan();
+    if (!p) return DFQ_ERR_NOMEM;
+    std::vector<CleLayer> layers(n_targets);
+    std::vector<CleChunk> chunks;
+    std::vector<CleUnit> units;
+    std::vector<int64_t> b1off;
+    int64_t nb1_total = 0;
+    for (int32_t l = 0; l < n_targets; ++l) {
+        const int64_t n = target_n[l];
+        if (!targets[l] || n <= 0) { cle_plan_free(p); return DFQ_ERR_INVALID; }
+        float* snap = nullptr;
+        hipError_t e = hipMalloc(&snap, sizeof(float) * n);
+        if (e != hipSuccess) { set_last_hip_error(e); cle_plan_free(p); return DFQ_ERR_HIP; }
+        p->snaps.push_back(snap);
+        layers[l] = CleLayer{targets[l], snap, n};
+        int64_t nt = 1;
+        if (n >= 32768 && ref_threads > 1) nt = std::min<int64_t>(ref_threads, ceil_div(n, (int64_t)32768));
+        if (nt > 8) nt = 8;
+        const int64_t chunk = ceil_div(n, nt);
+        for (int64_t t = 0; t < nt; ++t) {
+            const int64_t b = t * chunk;
+            if (b >= n) break;
+            const int64_t len = std::min<int64_t>(n, b + chunk) - b;
+            const int64_t sz = len / 32;
+            if (aten_ceil_log2(sz) / 4 > 4) { cle_plan_free(p); return DFQ_ERR_UNSUPPORTED; }   // > 16M / chunk
+            const int32_t ci = (int32_t)chunks.size();
+            chunks.push_back(CleChunk{l, (int32_t)t, b, len});
+            const int64_t nb1 = sz / 256;
+            b1off.push_back(32 * nb1_total);   // float offset of this chunk's [nb1][32] level-1 sums
+            nb1_total += nb1;
+            if (len >= 8)
+                for (int64_t g = 0; g <= nb1; ++g) units.push_back(CleUnit{ci, (int32_t)g});
+        }
+    }
+    p->nunits = (int64_t)units.size();
+    p->M = M;
+    p->nl = n_targets;
+    p->nchunks = (int64_t)chunks.size();
+    p->chains = chains;
+    p->steps = steps;
+    p->rstep = rstep;
+    p->astep = astep;
+    p->smin = s_min; p->smax = s_max; p->is_signed = is_signed; p->eps = eps;
+    hipError_t e;
+    auto fail = [&](hipError_t err) { set_last_hip_error(err); cle_plan_free(p); return DFQ_ERR_HIP; };
+    if ((e = upload(&p->d_rels, R)) != hipSuccess) return fail(e);
+    if ((e = upload(&p->d_rtasks, rt)) != hipSuccess) return fail(e);
+    if ((e = upload(&p->d_atasks, at)) != hipSuccess) return fail(e);
+    if ((e = upload(&p->d_layers, layers)) != hipSuccess) return fail(e);
+    if ((e = upload(&p->d_chunks, chunks)) != hipSuccess) return fail(e);
+    if ((e = upload(&p->d_units, units)) != hipSuccess) return fail(e);
+    if ((e = upload(&p->d_b1off, b1off)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&p->d_b1, sizeof(float) * 32 * std::max<int64_t>(nb1_total, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&p->d_tail, sizeof(float) * kCleTailWords * std::max<int64_t>((int64_t)chunks.size(), 1))) !=
+        hipSuccess)
+        return fail(e);
+    if ((e = hipMalloc(&p->d_rng, sizeof(uint32_t) * 4 * std::max<int64_t>(M, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&p->d_part, sizeof(float) * 8 * std::max(n_targets, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&p->d_means, sizeof(double) * std::max(n_targets, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&p->d_state, sizeof(CleState))) != hipSuccess) return fail(e);
+    if ((e = hipHostMalloc(&p->h_state, sizeof(CleState))) != hipSuccess) return fail(e);
+    *out = p;
+    return DFQ_OK;
+}
+
+extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count, int32_t max_iters,
+                                int32_t* iterations, double* diffs, void* stream) {
+    if (!p || max_iters < 0) return DFQ_ERR_INVALID;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (p->hist_cap < max_iters + 1) {
+        (void)hipFree(p->d_hist);
+        p->d_hist = nullptr;
+        DFQ_HIP_CHECK(hipMalloc(&p->d_hist, sizeof(double) * (max_iters + 1)));
+        p->hist_cap = max_iters + 1;
+    }
+    CleState init{};
+    init.diff = 1e8;
+    init.thr = threshold;
+    init.iter_count = 0;
+    init.iters = 0;
+    init.count = count;
+    init.max_iters = max_iters;
+    init.done = !((init.diff > threshold) && (0 < count)) || max_iters == 0;
+    *p->h_state = init;
+    DFQ_HIP_CHECK(hipMemcpyAsync(p->d_state, p->h_state, sizeof(CleState), hipMemcpyHostToDevice, s));
+    // both parities' ranges: mins = +inf code (0xFF..), maxs = 0
+    for (int par = 0; par < 2; ++par) {
+        DFQ_HIP_CHECK(hipMemsetAsync(p->d_rng + (int64_t)par * 2 * p->M, 0xFF, sizeof(uint32_t) * p->M, s));
+        DFQ_HIP_CHECK(hipMemsetAsync(p->d_rng + (int64_t)par * 2 * p->M + p->M, 0x00, sizeof(uint32_t) * p->M, s));
+    }
+    DFQ_HIP_CHECK(hipMemsetAsync(p->d_part, 0, sizeof(float) * 8 * std::max(p->nl, 1), s));
+    if (p->nchunks > 0) {
+        hipLaunchKernelGGL(cle_loop_snap_kernel, dim3((int)std::min<int64_t>(p->nchunks * 8, 2048)), dim3(kThreads), 0,
+                           s, p->d_layers, p->d_chunks, p->nchunks);
+        DFQ_LAUNCH_CHECK();
+    }
+    int32_t launched = 0;
+    int32_t batch = 4;
+    while (!init.done) {
+        const int32_t nb = std::min(batch, max_iters - launched);
+        for (int32_t it = 0; it < nb; ++it) {
+            for (int32_t k = 0; k < p->steps; ++k) {
+                const int64_t r0 = p->rstep[k], r1 = p->rstep[k + 1];
+                const int64_t a0 = p->astep[k], a1 = p->astep[k + 1];
+                if (r1 > r0) {
+                    hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(r1 - r0, 2048)),
+                                       dim3(kThreads), 0, s, p->d_rels, p->d_rtasks, r0, r1, p->d_rng, p->M,
+                                       p->d_state);
+                    DFQ_LAUNCH_CHECK();
+                }
+                if (a1 > a0) {
+                    hipLaunchKernelGGL(cle_loop_apply_kernel, dim3((int)std::min<int64_t>(a1 - a0, 2048)),
+                                       dim3(kThreads), 0, s, p->d_rels, p->d_atasks, a0, a1, p->d_rng, p->M,
+                                       p->d_state, p->is_signed, p->eps, p->smin, p->smax);
+                    DFQ_LAUNCH_CHECK();
+                }
+            }
+            if (p->nchunks > 0) {
+                if (p->nunits > 0) {
+                    hipLaunchKernelGGL(cle_loop_diff_tiles_kernel, dim3((int)std::min<int64_t>(p->nunits, 4096)),
+                                       dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->d_b1off, p->d_units,
+                                       p->nunits, p->d_b1, p->d_tail, p->d_state);
+                    DFQ_LAUNCH_CHECK();
+                }
+                hipLaunchKernelGGL(cle_loop_diff_combine_kernel,
+                                   dim3((int)ceil_div(p->nchunks, (int64_t)(kThreads / 64))), dim3(kThreads), 0, s,
+                                   p->d_layers, p->d_chunks, p->nchunks, p->d_b1off, p->d_b1, p->d_tail, p->d_part,
+                                   p->d_state);
+                DFQ_LAUNCH_CHECK();
+            }
+            hipLaunchKernelGGL(cle_loop_final_kernel, dim3(1), dim3(kThreads), 0, s, p->d_layers, p->nl, p->d_part,
+                               p->d_means, p->d_hist, p->d_state);
+            DFQ_LAUNCH_CHECK();
+        }
+        launched += nb;
+        DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
+        DFQ_HIP_CHECK(hipStreamSynchronize(s));
+        init = *p->h_state;
+        if (launched >= max_iters) break;
+        batch = 8;
+    }
+    const CleState fin = *p->h_state;
+    if (getenv("DFQ_CLE_DEBUG")) {   // per-layer chunk sums of the last iteration run
+        std::vector<float> part(8 * std::max(p->nl, 1));
+        DFQ_HIP_CHECK(hipMemcpy(part.data(), p->d_part, sizeof(float) * part.size(), hipMemcpyDeviceToHost));
+        for (int32_t l = 0; l < p->nl; ++l) {
+            fprintf(stderr, "DFQ_CLE_DEBUG layer %d:", l);
+            for (int t = 0; t < 8; ++t) fprintf(stderr, " %.9g", part[8 * l + t]);
+            fprintf(stderr, "\n");
+        }
+    }
+    if (iterations) *iterations = fin.iters;
+    if (diffs && fin.iters > 0)
+        DFQ_HIP_CHECK(hipMemcpy(diffs, p->d_hist, sizeof(double) * fin.iters, hipMemcpyDeviceToHost));
+    return DFQ_OK;
+}
+
+extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t* steps) {
+    if (!p) return DFQ_ERR_INVALID;
+    if (chains) *chains = p->chains;
+    if (steps) *steps = p->steps;
+    return DFQ_OK;
+}
+
+extern "C" int dfq_cle_plan_destroy(dfq_cle_plan* p) {
+    if (!p) return DFQ_OK;
+    cle_plan_free(p);
+    return DFQ_OK;
+}

@@ -153,6 +153,36 @@ int dfq_diff_plan_snapshot(dfq_diff_plan* plan, void* stream);  /* snap := W, as
 int dfq_diff_plan_execute(dfq_diff_plan* plan, double* out_mean, void* stream);
 int dfq_diff_plan_destroy(dfq_diff_plan* plan);
 
+/* Device-resident cross_layer_equalization loop (Cross_layer_equal.py:63-116).
+ * One relation of the loop (:86-104); pointers are device memory, in place. */
+typedef struct dfq_cle_rel {
+    float* w1;          /* graph[layer_first].weight, [c1, len1] */
+    float* w2;          /* graph[layer_second].weight, [o2, i2, khw2] */
+    float* b1;          /* graph[layer_first].bias [c1] (the caller adds the zero bias of :93-94) */
+    float* bn_w;        /* graph[bn_idx].fake_weight [c1] or NULL */
+    float* bn_b;        /* graph[bn_idx].fake_bias [c1] or NULL */
+    float* s_acc;       /* Relation.S [c1] (set_scale_vec, utils/relation.py:26-30) or NULL */
+    int64_t c1, len1, o2, i2, khw2;
+    int32_t s_acc_init; /* Relation.S was None: the first iteration stores s */
+    int32_t reserved;
+} dfq_cle_rel;
+typedef struct dfq_cle_plan dfq_cle_plan;
+/* targets: the weights of every Target_list layer in graph order (the diff list of
+ * :107); ref_threads: torch's intra-op thread count whose fp32 mean order the
+ * metric reproduces. Relations touching a common tensor keep their order; the
+ * others run concurrently (bit-identical: they commute). */
+int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
+                        const int64_t* target_n, int32_t n_targets, double s_min, double s_max,
+                        int32_t is_signed, float eps, int32_t ref_threads, dfq_cle_plan** plan);
+/* Runs the loop `while diff > threshold and iter_count < count` (at most
+ * max_iters iterations); blocking.  iterations = iterations run; diffs[i] (room for
+ * max_iters doubles, may be NULL) = the per-iteration diff (np.sum of the list). */
+int dfq_cle_plan_run(dfq_cle_plan* plan, double threshold, int32_t count, int32_t max_iters,
+                     int32_t* iterations, double* diffs, void* stream);
+/* chains = independent relation groups, steps = launches pairs per iteration */
+int dfq_cle_plan_info(const dfq_cle_plan* plan, int32_t* chains, int32_t* steps);
+int dfq_cle_plan_destroy(dfq_cle_plan* plan);
+
 /* ---- high-bias absorption (bias_absorption.py:147-197) ------------------
  * c = max(bn_b - N*bn_w, 0) (bn_* = the BN's fake_weight / fake_bias);
  * b2[o] += sum_i (sum_k W2[o,i,k]) * c[g*i2 + i];  b1 -= c;  bn_b -= c.

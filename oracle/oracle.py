@@ -41,6 +41,10 @@ def lib():
         L.oracle_bc_expect.argtypes = [P, P, I64, I32, I32, P]
         L.oracle_bc_apply.argtypes = [P, I64, I64, P, I64, P, P, C.POINTER(I64)]
         L.oracle_bc_propagate.argtypes = [P, I64, P, I64, I32]
+        L.oracle_mean_abs_diff.argtypes = [P, P, I64, I32]
+        L.oracle_mean_abs_diff.restype = C.c_float
+        L.oracle_np_sum.argtypes = [P, I64]
+        L.oracle_np_sum.restype = C.c_double
         _lib = L
     return _lib
 
@@ -144,3 +148,15 @@ def bc_propagate(vec, fake_b, threads=8):
     if rc:
         raise RuntimeError(f"oracle_bc_propagate rc={rc}")
     return fake_b
+
+
+def mean_abs_diff(a, b, threads=8):
+    """float(torch.mean(torch.abs(a - b))) in ATen's CPU order (Cross_layer_equal.py:107)."""
+    a, b = _f32(a), _f32(b)
+    return float(lib().oracle_mean_abs_diff(_p(a), _p(b), a.size, threads))
+
+
+def np_sum(values):
+    """np.sum(list_of_floats) (numpy pairwise summation), restated."""
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    return float(lib().oracle_np_sum(_p(v), v.size))

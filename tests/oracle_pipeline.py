@@ -44,7 +44,8 @@ class OracleDFQ:
                     s.update(g=gg, b=bb, m=mm, v=vv, fw=fw, fb=fb, eps=0.0)
                     break
 
-    def cle(self, threshold=2e-7, count=20, max_iters=None):
+    def cle(self, threshold=2e-7, count=20, max_iters=None, threads=8):
+        self.threads = threads
         rels = create_relation(self.graph, self.bottoms, TARG)
         self.rels = rels
         self.S = {}
@@ -60,8 +61,8 @@ class OracleDFQ:
                 self.W[a], self.W[b], self.B[a] = w1, w2, b1
                 s.update(fw=fw, fb=fb)
                 self.S[a] = S if a not in self.S else (self.S[a] * S).astype(np.float32)
-            d = [float(np.float32(np.abs(self.W[k] - old[k]).astype(np.float64).mean())) for k in self.tkeys]
-            dt = np.sum(d)
+            d = [O.mean_abs_diff(self.W[k], old[k], self.threads) for k in self.tkeys]
+            dt = O.np_sum(d)
             self.cle_diffs.append(float(dt))
             it += 1
             if abs(diff - dt) > 1e-9:

@@ -1,0 +1,153 @@
+"""Device-resident CLE loop (dfq_cle_plan) vs the oracle's sequential replay of
+Cross_layer_equal.py:63-116 on hand-made graphs: several independent chains
+(dense, depthwise, grouped, Linear), signed ranges, eps, custom scale limits, a
+dead channel, a relation without BN stats, a layer shared by two relations in
+one chain and a large layer (multi-chunk metric).  Weights, biases, BN fake
+stats, Relation.S, iteration count and every per-iteration diff: bit-exact."""
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+class _BN:
+    def __init__(self, c, rng, with_stats=True):
+        self.fake_weight = torch.from_numpy(rng.uniform(0.5, 1.5, c).astype(np.float32)).to(DEV) if with_stats \
+            else None
+        self.fake_bias = torch.from_numpy(rng.normal(0, 0.5, c).astype(np.float32)).to(DEV) if with_stats \
+            else None
+
+
+def _conv(o, i, k, groups=1, rng=None, bias=True, dead=None):
+    m = nn.Conv2d(i, o, k, groups=groups, bias=bias)
+    w = rng.normal(0, 1, m.weight.shape).astype(np.float32)
+    if dead is not None:
+        w[dead] = 0.0
+    m.weight.data = torch.from_numpy(w)
+    if bias:
+        m.bias.data = torch.from_numpy(rng.normal(0, 0.1, o).astype(np.float32))
+    return m.to(DEV)
+
+
+def _graph(seed):
+    from data_free_quantization_amd.utils.relation import Relation
+    rng = np.random.default_rng(seed)
+    g = OrderedDict()
+    g["Data"] = "Data"
+    # chain A: dense 3x3 -> 1x1 (tile path) -> grouped(2) 3x3, with a dead channel
+    g["a1"] = _conv(16, 3, 3, rng=rng, dead=5)
+    g["a1bn"] = _BN(16, rng)
+    g["a2"] = _conv(24, 16, 1, rng=rng, bias=False)
+    g["a2bn"] = _BN(24, rng)
+    g["a3"] = _conv(32, 24, 3, groups=2, rng=rng)
+    # chain B: pointwise -> depthwise (contiguous columns) -> pointwise
+    g["b1"] = _conv(40, 8, 1, rng=rng)
+    g["b1bn"] = _BN(40, rng)
+    g["b2"] = _conv(40, 40, 3, groups=40, rng=rng)
+    g["b2bn"] = _BN(40, rng, with_stats=False)
+    g["b3"] = _conv(20, 40, 1, rng=rng)
+    # chain C: one big layer (metric over several 32768-element chunks) -> Linear
+    g["c1"] = _conv(256, 64, 3, rng=rng)
+    g["c1bn"] = _BN(256, rng)
+    lin = nn.Linear(256, 10)
+    lin.weight.data = torch.from_numpy(rng.normal(0, 0.05, (10, 256)).astype(np.float32))
+    g["c2"] = lin.to(DEV)
+    # a target that no relation touches
+    g["d1"] = _conv(4, 4, 1, rng=rng)
+    rels = [Relation("a1", "a2", "a1bn"), Relation("b1", "b2", "b1bn"), Relation("a2", "a3", "a2bn"),
+            Relation("c1", "c2", "c1bn"), Relation("b2", "b3", "b2bn")]
+    return g, rels
+
+
+def _replay(g, rels, s_min_max, thr, count, signed, eps):
+    """The reference loop with the oracle's _layer_equalization and metric."""
+    tk = [k for k in g if type(g[k]) in (nn.Conv2d, nn.Linear)]
+    W = {k: g[k].weight.detach().cpu().numpy().copy() for k in tk}
+    B = {k: (g[k].bias.detach().cpu().numpy().copy() if g[k].bias is not None else None) for k in tk}
+    BN = {k: [None if v is None else v.cpu().numpy().copy() for v in (g[k].fake_weight, g[k].fake_bias)]
+          for k in g if isinstance(g[k], _BN)}
+    S = {}
+    diff, it_count, diffs = 1e8, 0, []
+    while diff > thr and it_count < count:
+        old = {k: W[k].copy() for k in tk}
+        for i, r in enumerate(rels):
+            a, b, bn = r.get_idxs()
+            if B[a] is None:
+                B[a] = np.zeros(W[a].shape[0], np.float32)
+            w1, w2, b1, fw, fb, s = O.cle_relation(W[a], W[b], B[a], BN[bn][0], BN[bn][1], s_min_max[0],
+                                                   s_min_max[1], signed, eps)
+            W[a], W[b], B[a], BN[bn] = w1, w2, b1, [fw, fb]
+            with np.errstate(over="ignore"):   # the dead channel: s = 1e8 every iteration
+                S[i] = s if i not in S else (S[i] * s).astype(np.float32)
+        dt = O.np_sum([O.mean_abs_diff(W[k], old[k]) for k in tk])
+        diffs.append(dt)
+        if abs(diff - dt) > 1e-9:
+            it_count, diff = 0, dt
+        else:
+            it_count += 1
+    return W, B, BN, S, diffs
+
+
+@pytest.mark.parametrize("signed,eps,smm,thr,count", [
+    (False, 0.0, (1e-8, 1e8), 2e-7, 20),
+    (True, 0.0, (1e-8, 1e8), 2e-7, 20),
+    (False, 1e-3, (0.5, 2.0), 1e-6, 5),
+    (False, 0.0, (1e-8, 1e8), 1e3, 20),     # stops after one iteration
+])
+def test_device_cle_matches_oracle(signed, eps, smm, thr, count, monkeypatch):
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    monkeypatch.setenv("DFQ_CLE_MODE", "device")
+    g, rels = _graph(0)
+    W, B, BN, S, diffs = _replay(g, rels, smm, thr, count, signed, eps)
+    cle.cross_layer_equalization(g, rels, [nn.Conv2d, nn.Linear], s_min_max=list(smm), Treshhold=thr, Count=count,
+                                 signed=signed, eps=eps, Save_state=False)
+    torch.cuda.synchronize()
+    assert cle.LAST_RUN["chains"] == 3 and cle.LAST_RUN["steps"] == 2
+    assert cle.LAST_RUN["diffs"] == diffs
+    for k in W:
+        assert np.array_equal(g[k].weight.detach().cpu().numpy(), W[k]), k
+        if B[k] is not None:
+            assert np.array_equal(g[k].bias.detach().cpu().numpy(), B[k]), k
+    for k, (fw, fb) in BN.items():
+        if fw is not None:
+            assert np.array_equal(g[k].fake_weight.cpu().numpy(), fw), k
+            assert np.array_equal(g[k].fake_bias.cpu().numpy(), fb), k
+    for i, r in enumerate(rels):
+        assert np.array_equal(r.S.cpu().numpy(), S[i]), i
+
+
+def test_device_cle_accumulates_existing_scale(monkeypatch):
+    """A second call multiplies into Relation.S (set_scale_vec) instead of storing."""
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    monkeypatch.setenv("DFQ_CLE_MODE", "device")
+    g, rels = _graph(1)
+    cle.cross_layer_equalization(g, rels, [nn.Conv2d, nn.Linear], Treshhold=1e3, Save_state=False)
+    s1 = [r.S.clone() for r in rels]
+    g2, rels2 = _graph(1)
+    cle.cross_layer_equalization(g2, rels2, [nn.Conv2d, nn.Linear], Treshhold=1e3, Save_state=False)
+    cle.cross_layer_equalization(g2, rels2, [nn.Conv2d, nn.Linear], Treshhold=1e3, Save_state=False)
+    g3, rels3 = _graph(1)
+    cle.cross_layer_equalization(g3, rels3, [nn.Conv2d, nn.Linear], Treshhold=1e3, Save_state=False)
+    for r in rels3:
+        r.S = None
+    cle.cross_layer_equalization(g3, rels3, [nn.Conv2d, nn.Linear], Treshhold=1e3, Save_state=False)
+    for a, r2, r3 in zip(s1, rels2, rels3):
+        assert torch.equal(r2.S, a * r3.S)
+
+
+def test_device_cle_no_relations(monkeypatch):
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    monkeypatch.setenv("DFQ_CLE_MODE", "device")
+    g, _ = _graph(2)
+    before = {k: g[k].weight.detach().clone() for k in g if isinstance(g[k], (nn.Conv2d, nn.Linear))}
+    cle.cross_layer_equalization(g, [], [nn.Conv2d, nn.Linear], Save_state=False)
+    assert cle.LAST_RUN["iterations"] == 1 and cle.LAST_RUN["diffs"] == [0.0]
+    for k, w in before.items():
+        assert torch.equal(g[k].weight, w)

@@ -17,8 +17,10 @@ pytestmark = pytest.mark.gpu
 TARG = (nn.Conv2d, nn.Linear)
 
 
+@pytest.mark.parametrize("cle_mode", ["device", "host"])
 @pytest.mark.parametrize("name", ["mobilenetv2", "resnet50", "deeplab"])
-def test_pipeline_matches_reference(name):
+def test_pipeline_matches_reference(name, cle_mode, monkeypatch):
+    monkeypatch.setenv("DFQ_CLE_MODE", cle_mode)
     from data_free_quantization_amd import zoo
     from data_free_quantization_amd import Cross_layer_equal as cle
     from data_free_quantization_amd.pipeline import run_dfq
@@ -62,9 +64,14 @@ def test_pipeline_matches_reference(name):
             check(stage)
         if stage == "cle":
             assert not failures, failures
+            assert cle.LAST_RUN["mode"] == cle_mode
             assert cle.LAST_RUN["iterations"] == len(P["cle_diffs"])
-            # per-layer means: fp64 on the GPU vs torch's fp32 cascade sum on the CPU
-            np.testing.assert_allclose(cle.LAST_RUN["diffs"], P["cle_diffs"], rtol=1e-5)
+            if cle_mode == "device":
+                # fp32 torch.mean in ATen's two-pass order + numpy's pairwise sum: exact
+                assert cle.LAST_RUN["diffs"] == list(P["cle_diffs"])
+            else:
+                # host loop: per-layer means accumulated in fp64 (dfq_diff_plan)
+                np.testing.assert_allclose(cle.LAST_RUN["diffs"], P["cle_diffs"], rtol=1e-5)
 
     bc_error = str(P["bc_error"])
     if bc_error:

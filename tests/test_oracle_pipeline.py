@@ -31,7 +31,7 @@ def test_oracle_pipeline_matches_reference(name):
     assert np.array_equal(_bias_hashes(R), P["bn1_bh"])
     R.cle()
     assert len(R.cle_diffs) == len(P["cle_diffs"])
-    np.testing.assert_allclose(R.cle_diffs, P["cle_diffs"], rtol=1e-5)
+    assert R.cle_diffs == list(P["cle_diffs"])   # fp32 torch.mean order + numpy pairwise sum, bit-exact
     assert np.array_equal(_stage_hashes(R), P["cle_wh"])
     assert np.array_equal(_bias_hashes(R), P["cle_bh"])
     R.absorb()
