@@ -394,6 +394,8 @@ struct CleRel {
     int64_t c1, len1, o2, i2, khw2, o2g;
     int64_t moff;       // this relation's [W1 | W2] range words inside one parity's mins (and maxs)
     int32_t sacc_init;
+    int32_t vec1;       // W1 rows 16-B aligned (float4 path)
+    int32_t vec2;       // W2 contiguous channel segments 16-B aligned (i2 == 1)
     int32_t pad;
 };
 
@@ -401,7 +403,7 @@ struct CleRel {
 // (i2 > 1, ordered-uint atomics), reset of the OTHER parity's W2 words.
 // Rescale-launch kinds: W1 elements, W2 elements, per-channel vectors.
 enum : int32_t { kRangeW1 = 0, kRangeW2Contig = 1, kRangeW2Tile = 2, kRangeReset = 3 };
-enum : int32_t { kApplyW1 = 0, kApplyW2 = 1, kApplyChannels = 2 };
+enum : int32_t { kApplyW1 = 0, kApplyW2Contig = 1, kApplyW2Tile = 2, kApplyChannels = 3 };
 
 struct CleTask {
     int32_t rel;
@@ -437,8 +439,78 @@ struct CleState {
 
 constexpr int kCleW1RowsPerTask = 4;       // one wave per row
 constexpr int kCleW2ChansPerTask = 4;      // one wave per contiguous column
-constexpr int64_t kCleElemsPerTask = 4096;
 constexpr int64_t kCleChansPerTask = 1024;
+
+// min / max of n floats at p, one wave, 4 loads in flight per lane
+__device__ __forceinline__ void wave_range(const float* __restrict__ p, int64_t n, bool vec, int lane, float& vmin,
+                                           float& vmax) {
+    vmin = INFINITY;
+    vmax = -INFINITY;
+    if (vec) {
+        const float4* p4 = reinterpret_cast<const float4*>(p);
+        const int64_t n4 = n >> 2;
+        for (int64_t i = lane; i < n4; i += 4 * 64) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n4) v[u] = p4[i + 64 * u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n4) {
+                    vmin = fminf(vmin, fminf(fminf(v[u].x, v[u].y), fminf(v[u].z, v[u].w)));
+                    vmax = fmaxf(vmax, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
+                }
+        }
+    } else {
+        for (int64_t i = lane; i < n; i += 4 * 64) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n) v[u] = p[i + 64 * u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n) {
+                    vmin = fminf(vmin, v[u]);
+                    vmax = fmaxf(vmax, v[u]);
+                }
+        }
+    }
+    vmin = wave_min(vmin);
+    vmax = wave_max(vmax);
+}
+
+// p[0..n) *= f, one wave; 4 loads in flight per lane before the stores
+__device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, bool vec, float f, int lane) {
+    if (vec) {
+        float4* p4 = reinterpret_cast<float4*>(p);
+        const int64_t n4 = n >> 2;
+        for (int64_t i = lane; i < n4; i += 4 * 64) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n4) v[u] = p4[i + 64 * u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n4) {
+                    v[u].x = v[u].x * f;
+                    v[u].y = v[u].y * f;
+                    v[u].z = v[u].z * f;
+                    v[u].w = v[u].w * f;
+                    p4[i + 64 * u] = v[u];
+                }
+        }
+    } else {
+        for (int64_t i = lane; i < n; i += 4 * 64) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n) v[u] = p[i + 64 * u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n) p[i + 64 * u] = v[u] * f;
+        }
+    }
+}
 
 __global__ void __launch_bounds__(kThreads)
 cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
@@ -456,43 +528,46 @@ cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
         const CleRel& R = rels[tk.rel];
         uint32_t* mn = mins + R.moff;
         uint32_t* mx = maxs + R.moff;
-        if (tk.kind == kRangeW1) {
+        if (tk.kind == kRangeW1) {   // one wave per W1 row
             for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
-                const float* row = R.w1 + c * R.len1;
-                float vmin = INFINITY, vmax = -INFINITY;
-                for (int64_t i = lane; i < R.len1; i += 64) {
-                    const float x = row[i];
-                    vmin = fminf(vmin, x);
-                    vmax = fmaxf(vmax, x);
-                }
-                vmin = wave_min(vmin);
-                vmax = wave_max(vmax);
+                float vmin, vmax;
+                wave_range(R.w1 + c * R.len1, R.len1, R.vec1, lane, vmin, vmax);
                 if (lane == 0) {
                     mn[c] = enc_ord(vmin);
                     mx[c] = enc_ord(vmax);
                 }
             }
-        } else if (tk.kind == kRangeW2Contig) {
+        } else if (tk.kind == kRangeW2Contig) {   // one wave per contiguous W2 channel
             const int64_t seg = R.o2g * R.khw2;
             for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
-                const float* col = R.w2 + c * seg;
-                float vmin = INFINITY, vmax = -INFINITY;
-                for (int64_t i = lane; i < seg; i += 64) {
-                    const float x = col[i];
-                    vmin = fminf(vmin, x);
-                    vmax = fmaxf(vmax, x);
-                }
-                vmin = wave_min(vmin);
-                vmax = wave_max(vmax);
+                float vmin, vmax;
+                wave_range(R.w2 + c * seg, seg, R.vec2, lane, vmin, vmax);
                 if (lane == 0) {
                     mn[R.c1 + c] = enc_ord(vmin);
                     mx[R.c1 + c] = enc_ord(vmax);
                 }
             }
-        } else if (tk.kind == kRangeW2Tile) {
+        } else if (tk.kind == kRangeW2Tile) {   // rows [a, b) of W2, one thread per column
             const int64_t rowlen = R.i2 * R.khw2;
+            const bool one_group = (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
             for (int64_t i = threadIdx.x; i < R.i2; i += kThreads) {
                 float vmin = INFINITY, vmax = -INFINITY;
+                if (one_group && R.khw2 == 1) {   // 1x1 / Linear: the tile's column, 16 loads in flight
+                    float v[kColTileRows];
+#pragma unroll
+                    for (int j = 0; j < kColTileRows; ++j)
+                        if (tk.a + j < tk.b) v[j] = R.w2[(tk.a + j) * rowlen + i];
+#pragma unroll
+                    for (int j = 0; j < kColTileRows; ++j)
+                        if (tk.a + j < tk.b) {
+                            vmin = fminf(vmin, v[j]);
+                            vmax = fmaxf(vmax, v[j]);
+                        }
+                    const int64_t c = R.c1 + (tk.a / R.o2g) * R.i2 + i;
+                    atomicMin(&mn[c], enc_ord(vmin));
+                    atomicMax(&mx[c], enc_ord(vmax));
+                    continue;
+                }
                 int64_t g_prev = -1;
                 for (int64_t o = tk.a; o < tk.b; ++o) {
                     const int64_t g = o / R.o2g;
@@ -532,23 +607,51 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
     const bool first_iter = st->iters == 0;
     const uint32_t* mins = rng + (int64_t)par * 2 * M;
     const uint32_t* maxs = mins + M;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
     for (int64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
         const CleTask tk = tasks[t];
         const CleRel& R = rels[tk.rel];
         const uint32_t* mn = mins + R.moff;
         const uint32_t* mx = maxs + R.moff;
-        if (tk.kind == kApplyW1) {
-            for (int64_t e = tk.a + threadIdx.x; e < tk.b; e += kThreads) {
-                const CleScale cs = cle_scale(mn, mx, R.c1, e / R.len1, is_signed, eps, smin, smax);
-                R.w1[e] = R.w1[e] * cs.s;
+        if (tk.kind == kApplyW1) {   // W1[c, :] *= s[c], one wave per row
+            for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
+                const CleScale cs = cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax);
+                wave_scale(R.w1 + c * R.len1, R.len1, R.vec1, cs.s, lane);
             }
-        } else if (tk.kind == kApplyW2) {
-            const int64_t rowlen2 = R.i2 * R.khw2;
-            for (int64_t f = tk.a + threadIdx.x; f < tk.b; f += kThreads) {
-                const int64_t o = f / rowlen2;
-                const int64_t i = (f - o * rowlen2) / R.khw2;
-                const CleScale cs = cle_scale(mn, mx, R.c1, (o / R.o2g) * R.i2 + i, is_signed, eps, smin, smax);
-                R.w2[f] = R.w2[f] * cs.inv;
+        } else if (tk.kind == kApplyW2Contig) {   // W2 channel segment *= 1/s[c]
+            const int64_t seg = R.o2g * R.khw2;
+            for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
+                const CleScale cs = cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax);
+                wave_scale(R.w2 + c * seg, seg, R.vec2, cs.inv, lane);
+            }
+        } else if (tk.kind == kApplyW2Tile) {   // rows [a, b) of W2, one thread per column
+            const int64_t rowlen = R.i2 * R.khw2;
+            const bool one_group = (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
+            for (int64_t i = threadIdx.x; i < R.i2; i += kThreads) {
+                if (one_group && R.khw2 == 1) {   // 1x1 / Linear: the tile's column, loads first
+                    const float inv = cle_scale(mn, mx, R.c1, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin,
+                                                smax).inv;
+                    float v[kColTileRows];
+#pragma unroll
+                    for (int j = 0; j < kColTileRows; ++j)
+                        if (tk.a + j < tk.b) v[j] = R.w2[(tk.a + j) * rowlen + i];
+#pragma unroll
+                    for (int j = 0; j < kColTileRows; ++j)
+                        if (tk.a + j < tk.b) R.w2[(tk.a + j) * rowlen + i] = v[j] * inv;
+                    continue;
+                }
+                int64_t g_prev = -1;
+                float inv = 0.f;
+                for (int64_t o = tk.a; o < tk.b; ++o) {
+                    const int64_t g = o / R.o2g;
+                    if (g != g_prev) {
+                        inv = cle_scale(mn, mx, R.c1, g * R.i2 + i, is_signed, eps, smin, smax).inv;
+                        g_prev = g;
+                    }
+                    float* p = R.w2 + o * rowlen + i * R.khw2;
+                    for (int64_t k = 0; k < R.khw2; ++k) p[k] = p[k] * inv;
+                }
             }
         } else {
             for (int64_t c = tk.a + threadIdx.x; c < tk.b; c += kThreads) {
@@ -871,6 +974,8 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         c.c1 = d.c1; c.len1 = d.len1; c.o2 = d.o2; c.i2 = d.i2; c.khw2 = d.khw2; c.o2g = d.o2 / groups;
         c.moff = M;
         c.sacc_init = d.s_acc_init;
+        c.vec1 = (d.len1 % 4 == 0 && reinterpret_cast<uintptr_t>(d.w1) % 16 == 0) ? 1 : 0;
+        c.vec2 = (d.i2 == 1 && (c.o2g * d.khw2) % 4 == 0 && reinterpret_cast<uintptr_t>(d.w2) % 16 == 0) ? 1 : 0;
         M += 2 * d.c1;
         R[r] = c;
     }
@@ -917,11 +1022,15 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
                     rt.push_back({r, kRangeReset, a, std::min<int64_t>(a + kCleChansPerTask, c.c1)});
             }
-            const int64_t n1 = c.c1 * c.len1, n2 = c.o2 * c.i2 * c.khw2;
-            for (int64_t a = 0; a < n1; a += kCleElemsPerTask)
-                at.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleElemsPerTask, n1)});
-            for (int64_t a = 0; a < n2; a += kCleElemsPerTask)
-                at.push_back({r, kApplyW2, a, std::min<int64_t>(a + kCleElemsPerTask, n2)});
+            for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
+                at.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1)});
+            if (c.i2 == 1) {
+                for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
+                    at.push_back({r, kApplyW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1)});
+            } else {
+                for (int64_t a = 0; a < c.o2; a += kColTileRows)
+                    at.push_back({r, kApplyW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2)});
+            }
             for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
                 at.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kCleChansPerTask, c.c1)});
         }

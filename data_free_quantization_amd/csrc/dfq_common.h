@@ -207,6 +207,128 @@ __host__ __device__ inline float aten_inner_sum(Get get, int64_t n) {
     return fa;
 }
 
+// --- wave-parallel forms of the same orders (bit-identical results) -------
+// aten_cascade by one wave: level-0 blocks of 16 (one lane each), level-1 groups
+// of 16 blocks, then the level-2/3 combine and the tails on lane 0.  b0s / b1s:
+// this wave's LDS scratch (>= size/16 and size/256 floats).  Sizes whose cascade
+// step is not 16 (>= 2^20) or that exceed the scratch run on lane 0.
+template <typename Get>
+__device__ inline float wave_cascade(Get get, int64_t size, int lane, float* b0s, float* b1s, int64_t b0cap) {
+    float res = 0.f;
+    if (aten_ceil_log2(size) / 4 > 4 || (size >> 4) > b0cap) {
+        if (lane == 0) res = aten_cascade(get, size);
+        return __shfl(res, 0, 64);
+    }
+    const int64_t nb0 = size >> 4, tail = size & 15, nb1 = nb0 >> 4, rem_b0 = nb0 & 15;
+    const int64_t nb2 = nb1 >> 4, rem_b1 = nb1 & 15;
+    for (int64_t m = lane; m < nb0; m += 64) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a += get(m * 16 + j);
+        b0s[m] = a;
+    }
+    wave_lds_sync();
+    for (int64_t q = lane; q < nb1; q += 64) {
+        float a = 0.f;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) a += b0s[q * 16 + m];
+        b1s[q] = a;
+    }
+    wave_lds_sync();
+    if (lane == 0) {
+        float a3 = 0.f;
+        for (int64_t r = 0; r < nb2; ++r) {
+            float b2 = 0.f;
+            for (int q = 0; q < 16; ++q) b2 += b1s[r * 16 + q];
+            a3 += b2;
+        }
+        float a2p = 0.f;
+        for (int64_t q = 0; q < rem_b1; ++q) a2p += b1s[nb2 * 16 + q];
+        float a1p = 0.f;
+        for (int64_t m = 0; m < rem_b0; ++m) a1p += b0s[nb1 * 16 + m];
+        float a0t = 0.f;
+        for (int64_t j = 0; j < tail; ++j) a0t += get(nb0 * 16 + j);
+        res = a0t;   // a0 += a1; a0 += a2; a0 += a3
+        res += a1p;
+        res += a2p;
+        res += a3;
+    }
+    wave_lds_sync();   // scratch reused by the caller's next cascade
+    return __shfl(res, 0, 64);
+}
+
+// aten_row_sum by one wave (4 ILP streams, each a wave_cascade).
+template <typename Get>
+__device__ inline float wave_row_sum(Get get, int64_t size, int lane, float* b0s, float* b1s, int64_t b0cap) {
+    const int64_t sz = size / 4;
+    float p[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] = wave_cascade([&](int64_t i) { return get(4 * i + k); }, sz, lane, b0s, b1s, b0cap);
+    float p0 = p[0];
+    for (int64_t i = 4 * sz; i < size; ++i) p0 += get(i);
+    p0 += p[1];
+    p0 += p[2];
+    p0 += p[3];
+    return p0;
+}
+
+// aten_inner_sum by one wave when every stream is short: lanes 0..31 each run one
+// of the 32 (vector lane, ILP) cascades sequentially; the combine follows on lane 0.
+template <typename Get>
+__device__ inline float wave_inner_sum(Get get, int64_t n, int lane) {
+    float r = 0.f;
+    if (n < 8) {
+        if (lane == 0) r = aten_row_sum(get, n);
+        return __shfl(r, 0, 64);
+    }
+    const int64_t vs = n / 8, sz = vs / 4;
+    float p = 0.f;
+    if (lane < 32) {
+        const int l = lane & 7, k = lane >> 3;
+        p = aten_cascade([&](int64_t i) { return get(8 * (4 * i + k) + l); }, sz);
+        if (k == 0)
+            for (int64_t v = 4 * sz; v < vs; ++v) p += get(8 * v + l);   // row_sum tail into p0
+    }
+    float ps[32];
+#pragma unroll
+    for (int s = 0; s < 32; ++s) ps[s] = __shfl(p, s, 64);
+    if (lane == 0) {
+        float fa = 0.f;
+        for (int64_t e = 8 * vs; e < n; ++e) fa += get(e);
+        for (int l = 0; l < 8; ++l) {
+            float p0 = ps[l];
+            p0 += ps[l + 8];
+            p0 += ps[l + 16];
+            p0 += ps[l + 24];
+            fa += p0;
+        }
+        r = fa;
+    }
+    return __shfl(r, 0, 64);
+}
+
+// Which reduction aten_outer_col_sum uses for column c: true = the 32-column
+// multi_row_sum cascade, false = row_sum (ILP 4).
+__host__ __device__ inline bool aten_outer_col_is_cascade(int64_t R, int64_t F, int64_t c, int threads) {
+    int64_t c0 = 0, c1 = F;
+    if (R * F >= 32768 && threads > 1) {
+        const int64_t nt = F < threads ? F : threads;
+        const int64_t chunk = ceil_div(F, nt);
+        c0 = c1 = -1;
+        for (int64_t t = 0; t < nt; ++t) {
+            int64_t b = t * chunk, e = b + chunk < F ? b + chunk : F;
+            if (b >= F) break;
+            b = b >= F ? b : b - b % 32;
+            e = e >= F ? e : e - e % 32;
+            if (b <= c && c < e) { c0 = b; c1 = e; break; }
+        }
+        if (c0 < 0) { c0 = 0; c1 = F; }
+    }
+    const int64_t w = c1 - c0;
+    const int64_t g = w >= 8 ? 32 : 4;
+    return (c - c0) < g * (w / g);
+}
+
 // Column c of a row-major [R, F] summed over R (vectorized_outer_sum /
 // scalar_outer_sum inside TensorIterator::parallel_reduce with `threads`).
 __host__ __device__ inline float aten_outer_col_sum(const float* a, int64_t R, int64_t F, int64_t c, int threads) {

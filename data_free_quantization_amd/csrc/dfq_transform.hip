@@ -143,26 +143,44 @@ __global__ void bc_expect_kernel(const float* __restrict__ w, const float* __res
     }
 }
 
-// One thread per output row: bias_vec[r, :] = E (+) expect, bias[r] += mean in
-// ATen's order (bias.view(O, -1).mean(dim=1)).
-__global__ void bc_apply_kernel(const float* __restrict__ E, int64_t o, int64_t i2, const float* __restrict__ ex,
-                                int64_t f, int64_t bcols, float* __restrict__ bias, float* __restrict__ bias_vec) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < o; r += (int64_t)gridDim.x * blockDim.x) {
+// One wave per output row: bias_vec[r, :] = E (+) expect, bias[r] += mean in
+// ATen's order (bias.view(O, -1).mean(dim=1)): the 32 (vector lane, ILP) streams
+// of the row run on 32 lanes, the combine on lane 0 (wave_inner_sum).
+__global__ void __launch_bounds__(kThreads)
+bc_apply_kernel(const float* __restrict__ E, int64_t o, int64_t i2, const float* __restrict__ ex, int64_t f,
+                int64_t bcols, float* __restrict__ bias, float* __restrict__ bias_vec) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+    for (int64_t r = wave; r < o; r += nwaves) {
         auto get = [&](int64_t j) { return E[r * i2 + (i2 > 1 ? j : 0)] + ex[f > 1 ? j : 0]; };
         if (bias_vec)
-            for (int64_t j = 0; j < bcols; ++j) bias_vec[r * bcols + j] = get(j);
-        const float sum = aten_inner_sum(get, bcols);
-        bias[r] = bias[r] + sum / (float)bcols;
+            for (int64_t j = lane; j < bcols; j += 64) bias_vec[r * bcols + j] = get(j);
+        const float sum = wave_inner_sum(get, bcols, lane);
+        if (lane == 0) bias[r] = bias[r] + sum / (float)bcols;
     }
 }
 
-// One thread per BN channel: fake_b[c] += mean_r(-bias_vec[r*f + c]) in ATen's
-// order for bias_prev.view(-1, F).mean(0) with `threads` intra-op threads.
-__global__ void bc_propagate_kernel(const float* __restrict__ bias_vec, int64_t nrows, int64_t f, int threads,
-                                    float* __restrict__ fake_b) {
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < f; c += (int64_t)gridDim.x * blockDim.x) {
-        const float s = -aten_outer_col_sum(bias_vec, nrows, f, c, threads);   // sum(-v) == -sum(v) exactly
-        fake_b[c] = fake_b[c] + s / (float)nrows;
+// One wave per BN channel: fake_b[c] += mean_r(-bias_vec[r*f + c]) in ATen's
+// order for bias_prev.view(-1, F).mean(0) with `threads` intra-op threads (the
+// column's cascade or ILP row_sum as a wave-parallel tree).
+constexpr int64_t kBcScratch = 1024;
+__global__ void __launch_bounds__(kThreads)
+bc_propagate_kernel(const float* __restrict__ bias_vec, int64_t nrows, int64_t f, int threads,
+                    float* __restrict__ fake_b) {
+    __shared__ float scratch[kThreads / 64][kBcScratch + kBcScratch / 16];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    float* b0s = scratch[wv];
+    float* b1s = b0s + kBcScratch;
+    const int64_t wave = (int64_t)blockIdx.x * (kThreads / 64) + wv;
+    const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+    for (int64_t c = wave; c < f; c += nwaves) {
+        auto get = [&](int64_t r) { return bias_vec[r * f + c]; };
+        const float sum = aten_outer_col_is_cascade(nrows, f, c, threads)
+                              ? wave_cascade(get, nrows, lane, b0s, b1s, kBcScratch)
+                              : wave_row_sum(get, nrows, lane, b0s, b1s, kBcScratch);
+        if (lane == 0) fake_b[c] = fake_b[c] + (-sum) / (float)nrows;   // sum(-v) == -sum(v) exactly
     }
 }
 
@@ -235,7 +253,8 @@ extern "C" int dfq_bc_apply(const float* E, int64_t o, int64_t i2, const float* 
     if (bcols_out) *bcols_out = bcols;
     // _apply_bias_correction: sizes never equal (2-D vs 1-D); numel must exceed o
     if (o * bcols <= o) return DFQ_ERR_SHAPE;
-    hipLaunchKernelGGL(bc_apply_kernel, dim3(blocks_for(o)), dim3(kThreads), 0, static_cast<hipStream_t>(stream), E,
+    hipLaunchKernelGGL(bc_apply_kernel, dim3((int)std::min<int64_t>(ceil_div(o, (int64_t)4), 2048)), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), E,
                        o, i2, expect, f, bcols, bias, bias_vec);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
@@ -245,7 +264,8 @@ extern "C" int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fak
                                 void* stream) {
     if (!bias_vec || !fake_b || numel <= 0 || f <= 0 || ref_threads < 1) return DFQ_ERR_INVALID;
     if (numel % f != 0) return DFQ_ERR_SHAPE;   // .view(-1, F) fails
-    hipLaunchKernelGGL(bc_propagate_kernel, dim3(blocks_for(f)), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(bc_propagate_kernel, dim3((int)std::min<int64_t>(ceil_div(f, (int64_t)4), 2048)), dim3(kThreads),
+                       0, static_cast<hipStream_t>(stream),
                        bias_vec, numel / f, f, (int)ref_threads, fake_b);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
