@@ -408,7 +408,8 @@ enum : int32_t { kApplyW1 = 0, kApplyW2Contig = 1, kApplyW2Tile = 2, kApplyChann
 struct CleTask {
     int32_t rel;
     int32_t kind;
-    int64_t a, b;
+    int64_t a, b;     // rows / channels / elements [a, b)
+    int64_t c0, c1;   // W2 tiles: columns [c0, c1) (one thread each)
 };
 
 struct CleLayer {
@@ -550,7 +551,7 @@ cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
         } else if (tk.kind == kRangeW2Tile) {   // rows [a, b) of W2, one thread per column
             const int64_t rowlen = R.i2 * R.khw2;
             const bool one_group = (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
-            for (int64_t i = threadIdx.x; i < R.i2; i += kThreads) {
+            for (int64_t i = tk.c0 + threadIdx.x; i < tk.c1; i += kThreads) {
                 float vmin = INFINITY, vmax = -INFINITY;
                 if (one_group && R.khw2 == 1) {   // 1x1 / Linear: the tile's column, 16 loads in flight
                     float v[kColTileRows];
@@ -628,7 +629,7 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
         } else if (tk.kind == kApplyW2Tile) {   // rows [a, b) of W2, one thread per column
             const int64_t rowlen = R.i2 * R.khw2;
             const bool one_group = (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
-            for (int64_t i = threadIdx.x; i < R.i2; i += kThreads) {
+            for (int64_t i = tk.c0 + threadIdx.x; i < tk.c1; i += kThreads) {
                 if (one_group && R.khw2 == 1) {   // 1x1 / Linear: the tile's column, loads first
                     const float inv = cle_scale(mn, mx, R.c1, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin,
                                                 smax).inv;
@@ -665,16 +666,6 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
     }
 }
 
-// snap := W for every target layer (before the first iteration)
-__global__ void cle_loop_snap_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
-                                     int64_t nchunks) {
-    for (int64_t k = blockIdx.x; k < nchunks; k += gridDim.x) {
-        const CleChunk ch = chunks[k];
-        const CleLayer Ly = layers[ch.layer];
-        for (int64_t i = ch.c0 + threadIdx.x; i < ch.c0 + ch.len; i += kThreads) Ly.snap[i] = Ly.w[i];
-    }
-}
-
 // The metric's fp32 sums (torch.mean's vectorized_inner_sum over one chunk) as a
 // fixed tree.  A chunk of len elements is 32 streams (s = 8k + l: 8 vector lanes x
 // ILP 4; stream element i is chunk element 32i + s) of sz = len/32 elements, each
@@ -693,6 +684,29 @@ struct CleUnit {
     int32_t chunk;
     int32_t tile;     // < nb1: full level-1 tile; == nb1: the chunk's tail tile
 };
+
+// snap := W for every target layer (before the first iteration): one workgroup
+// per metric tile (chunks of < 8 elements by the first workgroup)
+__global__ void cle_loop_snap_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
+                                     int64_t nchunks, const CleUnit* __restrict__ units, int64_t nunits) {
+    for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+        const CleUnit un = units[u];
+        const CleChunk ch = chunks[un.chunk];
+        const CleLayer Ly = layers[ch.layer];
+        const int64_t nb1 = (ch.len / 32) / 256;
+        const int64_t e0 = (int64_t)un.tile * 8192;
+        const int64_t e1 = un.tile < nb1 ? e0 + 8192 : ch.len;
+        for (int64_t i = e0 + threadIdx.x; i < e1; i += kThreads) Ly.snap[ch.c0 + i] = Ly.w[ch.c0 + i];
+    }
+    if (blockIdx.x == 0)
+        for (int64_t k = 0; k < nchunks; ++k) {
+            const CleChunk ch = chunks[k];
+            if (ch.len >= 8) continue;
+            const CleLayer Ly = layers[ch.layer];
+            for (int64_t i = threadIdx.x; i < ch.len; i += kThreads) Ly.snap[ch.c0 + i] = Ly.w[ch.c0 + i];
+        }
+}
+
 
 __global__ void __launch_bounds__(kThreads)
 cle_loop_diff_tiles_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
@@ -713,10 +727,20 @@ cle_loop_diff_tiles_kernel(const CleLayer* __restrict__ layers, const CleChunk* 
         const bool full = un.tile < nb1;
         const int64_t e0 = (int64_t)un.tile * kCleTile;
         const int64_t cnt = full ? kCleTile : len - e0;
-        for (int64_t e = tid; e < cnt; e += kThreads) {   // |W - W_prev|, snap := W
-            const float x = w[e0 + e];
-            d[e] = fabsf(x - sn[e0 + e]);
-            sn[e0 + e] = x;
+        for (int64_t e = tid; e < cnt; e += 8 * kThreads) {   // |W - W_prev|, snap := W; 8 loads in flight
+            float x[8], y[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (e + u * kThreads < cnt) {
+                    x[u] = w[e0 + e + u * kThreads];
+                    y[u] = sn[e0 + e + u * kThreads];
+                }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (e + u * kThreads < cnt) {
+                    d[e + u * kThreads] = fabsf(x[u] - y[u]);
+                    sn[e0 + e + u * kThreads] = x[u];
+                }
         }
         __syncthreads();
         if (full) {
@@ -918,6 +942,8 @@ struct dfq_cle_plan {
     int32_t hist_cap = 0;
     CleState* d_state = nullptr;
     CleState* h_state = nullptr;    // pinned
+    hipStream_t st = nullptr;       // the loop's stream
+    hipGraphExec_t gexec = nullptr; // kCleBatch iterations
     std::vector<float*> snaps;
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
     int64_t M = 0, nchunks = 0;
@@ -939,6 +965,8 @@ static void cle_plan_free(dfq_cle_plan* p) {
     (void)hipFree(p->d_b1); (void)hipFree(p->d_tail);
     if (p->h_state) (void)hipHostFree(p->h_state);
     for (float* s : p->snaps) (void)hipFree(s);
+    if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
+    if (p->st) (void)hipStreamDestroy(p->st);
     delete p;
 }
 
@@ -1012,27 +1040,31 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             if (step_of[r] != k) continue;
             const CleRel& c = R[r];
             for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
-                rt.push_back({r, kRangeW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1)});
+                rt.push_back({r, kRangeW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
             if (c.i2 == 1) {
                 for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
-                    rt.push_back({r, kRangeW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1)});
+                    rt.push_back({r, kRangeW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), 0, 0});
             } else {
                 for (int64_t a = 0; a < c.o2; a += kColTileRows)
-                    rt.push_back({r, kRangeW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2)});
+                    for (int64_t i0 = 0; i0 < c.i2; i0 += kThreads)
+                        rt.push_back({r, kRangeW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2), i0,
+                                      std::min<int64_t>(i0 + kThreads, c.i2)});
                 for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
-                    rt.push_back({r, kRangeReset, a, std::min<int64_t>(a + kCleChansPerTask, c.c1)});
+                    rt.push_back({r, kRangeReset, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
             }
             for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
-                at.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1)});
+                at.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
             if (c.i2 == 1) {
                 for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
-                    at.push_back({r, kApplyW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1)});
+                    at.push_back({r, kApplyW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), 0, 0});
             } else {
                 for (int64_t a = 0; a < c.o2; a += kColTileRows)
-                    at.push_back({r, kApplyW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2)});
+                    for (int64_t i0 = 0; i0 < c.i2; i0 += kThreads)
+                        at.push_back({r, kApplyW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2), i0,
+                                      std::min<int64_t>(i0 + kThreads, c.i2)});
             }
             for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
-                at.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kCleChansPerTask, c.c1)});
+                at.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
         }
         rstep.push_back((int64_t)rt.size());
         astep.push_back((int64_t)at.size());
@@ -1104,15 +1136,60 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     return DFQ_OK;
 }
 
+// One CLE iteration's launches (steps, metric, stop rule) on stream s.
+static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
+    for (int32_t k = 0; k < p->steps; ++k) {
+        const int64_t r0 = p->rstep[k], r1 = p->rstep[k + 1];
+        const int64_t a0 = p->astep[k], a1 = p->astep[k + 1];
+        if (r1 > r0) {
+            hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(r1 - r0, 2048)), dim3(kThreads), 0, s,
+                               p->d_rels, p->d_rtasks, r0, r1, p->d_rng, p->M, p->d_state);
+            DFQ_LAUNCH_CHECK();
+        }
+        if (a1 > a0) {
+            hipLaunchKernelGGL(cle_loop_apply_kernel, dim3((int)std::min<int64_t>(a1 - a0, 2048)), dim3(kThreads), 0, s,
+                               p->d_rels, p->d_atasks, a0, a1, p->d_rng, p->M, p->d_state, p->is_signed, p->eps,
+                               p->smin, p->smax);
+            DFQ_LAUNCH_CHECK();
+        }
+    }
+    if (p->nchunks > 0) {
+        if (p->nunits > 0) {
+            hipLaunchKernelGGL(cle_loop_diff_tiles_kernel, dim3((int)std::min<int64_t>(p->nunits, 4096)), dim3(kThreads),
+                               0, s, p->d_layers, p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail,
+                               p->d_state);
+            DFQ_LAUNCH_CHECK();
+        }
+        hipLaunchKernelGGL(cle_loop_diff_combine_kernel, dim3((int)ceil_div(p->nchunks, (int64_t)(kThreads / 64))),
+                           dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_b1off, p->d_b1, p->d_tail,
+                           p->d_part, p->d_state);
+        DFQ_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(cle_loop_final_kernel, dim3(1), dim3(kThreads), 0, s, p->d_layers, p->nl, p->d_part, p->d_means,
+                       p->d_hist, p->d_state);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+constexpr int32_t kCleBatch = 8;   // iterations enqueued between state read-backs
+
 extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count, int32_t max_iters,
                                 int32_t* iterations, double* diffs, void* stream) {
     if (!p || max_iters < 0) return DFQ_ERR_INVALID;
-    hipStream_t s = static_cast<hipStream_t>(stream);
+    // The loop runs on the plan's own stream (graph capture needs a non-default
+    // stream): wait for the caller's producers first; the call is blocking.
+    DFQ_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    if (!p->st) DFQ_HIP_CHECK(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+    hipStream_t s = p->st;
     if (p->hist_cap < max_iters + 1) {
         (void)hipFree(p->d_hist);
         p->d_hist = nullptr;
         DFQ_HIP_CHECK(hipMalloc(&p->d_hist, sizeof(double) * (max_iters + 1)));
         p->hist_cap = max_iters + 1;
+        if (p->gexec) {   // captured with the old history pointer
+            (void)hipGraphExecDestroy(p->gexec);
+            p->gexec = nullptr;
+        }
     }
     CleState init{};
     init.diff = 1e8;
@@ -1131,55 +1208,46 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     }
     DFQ_HIP_CHECK(hipMemsetAsync(p->d_part, 0, sizeof(float) * 8 * std::max(p->nl, 1), s));
     if (p->nchunks > 0) {
-        hipLaunchKernelGGL(cle_loop_snap_kernel, dim3((int)std::min<int64_t>(p->nchunks * 8, 2048)), dim3(kThreads), 0,
-                           s, p->d_layers, p->d_chunks, p->nchunks);
+        hipLaunchKernelGGL(cle_loop_snap_kernel, dim3((int)std::min<int64_t>(std::max<int64_t>(p->nunits, 1), 4096)),
+                           dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_units, p->nunits);
         DFQ_LAUNCH_CHECK();
     }
-    int32_t launched = 0;
-    int32_t batch = 4;
-    while (!init.done) {
-        const int32_t nb = std::min(batch, max_iters - launched);
-        for (int32_t it = 0; it < nb; ++it) {
-            for (int32_t k = 0; k < p->steps; ++k) {
-                const int64_t r0 = p->rstep[k], r1 = p->rstep[k + 1];
-                const int64_t a0 = p->astep[k], a1 = p->astep[k + 1];
-                if (r1 > r0) {
-                    hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(r1 - r0, 2048)),
-                                       dim3(kThreads), 0, s, p->d_rels, p->d_rtasks, r0, r1, p->d_rng, p->M,
-                                       p->d_state);
-                    DFQ_LAUNCH_CHECK();
-                }
-                if (a1 > a0) {
-                    hipLaunchKernelGGL(cle_loop_apply_kernel, dim3((int)std::min<int64_t>(a1 - a0, 2048)),
-                                       dim3(kThreads), 0, s, p->d_rels, p->d_atasks, a0, a1, p->d_rng, p->M,
-                                       p->d_state, p->is_signed, p->eps, p->smin, p->smax);
-                    DFQ_LAUNCH_CHECK();
-                }
-            }
-            if (p->nchunks > 0) {
-                if (p->nunits > 0) {
-                    hipLaunchKernelGGL(cle_loop_diff_tiles_kernel, dim3((int)std::min<int64_t>(p->nunits, 4096)),
-                                       dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->d_b1off, p->d_units,
-                                       p->nunits, p->d_b1, p->d_tail, p->d_state);
-                    DFQ_LAUNCH_CHECK();
-                }
-                hipLaunchKernelGGL(cle_loop_diff_combine_kernel,
-                                   dim3((int)ceil_div(p->nchunks, (int64_t)(kThreads / 64))), dim3(kThreads), 0, s,
-                                   p->d_layers, p->d_chunks, p->nchunks, p->d_b1off, p->d_b1, p->d_tail, p->d_part,
-                                   p->d_state);
-                DFQ_LAUNCH_CHECK();
-            }
-            hipLaunchKernelGGL(cle_loop_final_kernel, dim3(1), dim3(kThreads), 0, s, p->d_layers, p->nl, p->d_part,
-                               p->d_means, p->d_hist, p->d_state);
-            DFQ_LAUNCH_CHECK();
+    // kCleBatch iterations as one HIP graph (kernels of finished runs return at
+    // once: the stop rule lives in d_state); DFQ_CLE_GRAPH=0: eager launches.
+    const char* ge = getenv("DFQ_CLE_GRAPH");
+    const bool use_graph = !(ge && ge[0] == '0');
+    if (use_graph && !p->gexec && !init.done) {
+        DFQ_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        int rc = DFQ_OK;
+        for (int32_t it = 0; it < kCleBatch && rc == DFQ_OK; ++it) rc = cle_enqueue_iteration(p, s);
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(s, &g);
+        if (rc != DFQ_OK) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
         }
-        launched += nb;
+        DFQ_HIP_CHECK(ec);
+        const hipError_t ei = hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        DFQ_HIP_CHECK(ei);
+    }
+    int32_t launched = 0;
+    while (!init.done) {
+        if (use_graph) {
+            DFQ_HIP_CHECK(hipGraphLaunch(p->gexec, s));
+        } else {
+            for (int32_t it = 0; it < kCleBatch; ++it) {
+                const int rc = cle_enqueue_iteration(p, s);
+                if (rc != DFQ_OK) return rc;
+            }
+        }
+        launched += kCleBatch;
         DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
         DFQ_HIP_CHECK(hipStreamSynchronize(s));
         init = *p->h_state;
         if (launched >= max_iters) break;
-        batch = 8;
     }
+    DFQ_HIP_CHECK(hipStreamSynchronize(s));
     const CleState fin = *p->h_state;
     if (getenv("DFQ_CLE_DEBUG")) {   // per-layer chunk sums of the last iteration run
         std::vector<float> part(8 * std::max(p->nl, 1));
