@@ -177,33 +177,64 @@ def sharded_single_model(dev, stream, world, reps=20):
 
 
 def cpu_baseline(args, shapes, seconds):
-    """The CPU port (oracle/dfq_oracle.c, scalar, 1 thread) on a bounded sample of
-    the same workload: whole MobileNetV2 weight sets, same mode/flags."""
+    """The reference's CPU arithmetic on the GPU box's host cores, on a bounded
+    sample of the same workload (whole weight sets of the model):
+
+    * value: oracle/torch_port.py -- the reference's own torch CPU op sequence
+      (UniformQuantize.forward per output channel, clip_weight's clamp, the BC
+      error sums), torch.get_num_threads() intra-op threads;
+    * per_tensor_GBs: quantize_targ_layer's per-tensor sweep, same threads;
+    * oracle_c_1thread_GBs: the scalar C port (oracle/dfq_oracle.c), 1 thread."""
     import numpy as np
     from oracle import oracle as O
+    from oracle import torch_port as TP
     rng = np.random.default_rng(0)
     ws = []
     for s in shapes:
         std = (2.0 / (s[2] * s[3] * s[0])) ** 0.5 if len(s) == 4 else 0.01
         ws.append(rng.normal(0, std, s).astype(np.float32))
+    tw = [torch.from_numpy(w) for w in ws]
+    elems = sum(w.size for w in ws)
+    sym = not args.asym
+
+    def timed(fn, budget):
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return passes, el
+
+    def port_pass():
+        for w in tw:
+            TP.per_channel_sweep(w, args.bits, sym, clip=(-15.0, 15.0), want_esum=not args.no_esum)
+
+    def per_tensor_pass():
+        for w in tw:
+            TP.per_tensor_sweep(w, args.bits, False)
+
     mode = (O.CHANNEL_ASYM if args.asym else O.CHANNEL_SYM) if args.granularity == "channel" else \
         (O.TENSOR_ASYM if args.asym else O.TENSOR_SYM)
-    elems = sum(w.size for w in ws)
-    passes = 0
-    t0 = time.perf_counter()
-    while True:
+
+    def c_pass():
         for w in ws:
             rows = w.shape[0] if mode >= 2 else 1
             khw = w.shape[2] * w.shape[3] if w.ndim == 4 else 1
             O.quantize(w, args.bits, mode, rows=rows, khw=khw, flags=O.F_CLIP, clip=(-15.0, 15.0),
                        want_esum=not args.no_esum)
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": round(4.0 * elems * passes / el / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{args.model} x1 weight set ({len(ws)} layers, {elems} weights) x {passes} passes, "
-                      f"{el:.1f} s, scalar C port (oracle/dfq_oracle.c), 1 thread"}
+
+    threads = torch.get_num_threads()
+    p1, e1 = timed(port_pass, seconds)
+    p2, e2 = timed(per_tensor_pass, max(1.0, seconds / 5))
+    p3, e3 = timed(c_pass, max(1.0, seconds / 5))
+    gbs = lambda p, e: round(4.0 * elems * p / e / 1e9, 4)
+    return {"value": gbs(p1, e1), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{args.model} x1 weight set ({len(ws)} layers, {elems} weights) x {p1} passes in {e1:.1f} s: "
+                      f"the reference's torch CPU ops (oracle/torch_port.py: quantize() per output channel + "
+                      f"clamp + BC error sums), {threads} intra-op threads",
+            "per_tensor_GBs": gbs(p2, e2), "per_tensor_sample": f"{p2} passes, quantize_targ_layer arithmetic",
+            "oracle_c_1thread_GBs": gbs(p3, e3)}
 
 
 def pipeline_timing(dev):
