@@ -50,9 +50,12 @@ constexpr Variant kVariants[] = {
     {1024, 128, false},   // 3: 5 KB / wave, 28 waves / CU
     {4096, 256, false},   // 4: 18 KB / wave, 8 waves / CU
     {2048, 256, false},   // 5: variant 0 with non-temporal loads and stores
+    {2048, 256, false},   // 6: variant 5, KH*KW sums specialised for 3x3 only (fewer VGPRs)
+    {2048, 256, false},   // 7: variant 5, generic KH*KW sums only
+    {2560, 256, false},   // 8: variant 6 with 2560-element tasks (12 waves / CU)
 };
-constexpr int kNumVariants = 6;
-constexpr int kDefaultVariant = 5;   // fastest in the A/B (profiles/r01/ab_*.json)
+constexpr int kNumVariants = 9;
+constexpr int kDefaultVariant = 6;   // = 5 with 87 instead of 105 VGPRs (profiles/r01/ab_*_v568.json)
 
 struct alignas(16) DevTensor {
     const float* src;
@@ -211,7 +214,8 @@ __device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTas
 }
 
 // Steps 2-4 on a chunk that has landed in ``data``.
-template <int MAXROWS, bool VEC, bool NT = false>
+// ESPEC: compile-time KH*KW error sums -- 2: 3x3/5x5/7x7/2x2, 1: 3x3, 0: none
+template <int MAXROWS, bool VEC, bool NT = false, int ESPEC = 2>
 __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& task, float* data, float* ls,
                                              float* lmn, const uint32_t* __restrict__ slot_min,
                                              const uint32_t* __restrict__ slot_max, int lane, float bmn = 0.f,
@@ -367,22 +371,31 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
                 st<false>(T.esum + pbase + pi, aten_inner_sum([&](int64_t k) { return e[k]; }, (int64_t)K));
             }
         };
-        switch (khw) {
-            case 9: esums(std::integral_constant<int, 9>{}); break;     // 3x3
-            case 49: esums(std::integral_constant<int, 49>{}); break;   // 7x7
-            case 25: esums(std::integral_constant<int, 25>{}); break;   // 5x5
-            case 4: esums(std::integral_constant<int, 4>{}); break;     // 2x2
-            default:
-                for (int pi = lane; pi < np; pi += kWave) {
-                    const float* e = data + pi * khw;
-                    st<false>(T.esum + pbase + pi, aten_inner_sum([&](int64_t k) { return e[k]; }, khw));
-                }
+        auto generic = [&]() {
+            for (int pi = lane; pi < np; pi += kWave) {
+                const float* e = data + pi * khw;
+                st<false>(T.esum + pbase + pi, aten_inner_sum([&](int64_t k) { return e[k]; }, khw));
+            }
+        };
+        if constexpr (ESPEC == 2) {
+            switch (khw) {
+                case 9: esums(std::integral_constant<int, 9>{}); break;     // 3x3
+                case 49: esums(std::integral_constant<int, 49>{}); break;   // 7x7
+                case 25: esums(std::integral_constant<int, 25>{}); break;   // 5x5
+                case 4: esums(std::integral_constant<int, 4>{}); break;     // 2x2
+                default: generic();
+            }
+        } else if constexpr (ESPEC == 1) {
+            if (khw == 9) esums(std::integral_constant<int, 9>{});
+            else generic();
+        } else {
+            generic();
         }
     }
     wave_lds_sync();  // LDS is reused by this wave's next task
 }
 
-template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false>
+template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false, int ESPEC = 2>
 __global__ void __launch_bounds__(kBlockThreads)
 sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restrict__ tasks, int64_t ntasks,
                   const uint32_t* __restrict__ slot_min, const uint32_t* __restrict__ slot_max) {
@@ -442,8 +455,10 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                 }
                 block_lds_sync();   // the slots are rewritten by the next task
             }
-            if (T.vec4) compute_task<MAXROWS, true, NT>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
-            else compute_task<MAXROWS, false, NT>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
+            if (T.vec4)
+                compute_task<MAXROWS, true, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
+            else
+                compute_task<MAXROWS, false, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
             task = next;
         }
     } else {
@@ -658,6 +673,18 @@ static void launch_main(int variant, int grid, hipStream_t s, const DevTensor* t
         case 4:
             hipLaunchKernelGGL((sweep_main_kernel<4096, 256, false>), dim3(grid), dim3(kBlockThreads), 0, s, t, k,
                                n, smin, smax);
+            break;
+        case 6:
+            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false, true, 1>), dim3(grid), dim3(kBlockThreads), 0, s,
+                               t, k, n, smin, smax);
+            break;
+        case 7:
+            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false, true, 0>), dim3(grid), dim3(kBlockThreads), 0, s,
+                               t, k, n, smin, smax);
+            break;
+        case 8:
+            hipLaunchKernelGGL((sweep_main_kernel<2560, 256, false, true, 1>), dim3(grid), dim3(kBlockThreads), 0, s,
+                               t, k, n, smin, smax);
             break;
         case 5:
             hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false, true>), dim3(grid), dim3(kBlockThreads), 0, s,
