@@ -509,7 +509,11 @@ struct Built {
     std::vector<DevTensor> tensors;
     std::vector<DevTask> reduce;
     std::vector<DevTask> blockrow;   // groups of kWavesPerBlock, placed first in the main list
-    std::vector<DevTask> main;
+    std::vector<DevTask> main;       // block rows, then tasks needing no reduce, then slot pieces
+    std::vector<DevTask> slotted;    // slot pieces, in reduce order (appended to main at the end)
+    // slabs of the two-pass (reduce -> quantize) work: reduce[rslab[k], rslab[k+1]) and
+    // the main list's slot pieces [mslab[k], mslab[k+1]) (offsets into `slotted`)
+    std::vector<int64_t> rslab, mslab;
     int64_t slots = 0;
     int64_t elems = 0;
     int64_t algo_bytes = 0;
@@ -546,8 +550,27 @@ static bool blockrow_enabled() {
     return !(e && e[0] == '0');
 }
 
+// DFQ_SWEEP_SLAB_MB: split the two-pass (reduce -> quantize) tensors into slabs of
+// about this many MB, each reduced and quantized back to back, so the second read
+// of a slab can still hit the 256 MB Infinity Cache (0: one slab).
+static int64_t slab_bytes() {
+    const char* e = getenv("DFQ_SWEEP_SLAB_MB");
+    return (e && *e) ? (int64_t)atoll(e) << 20 : 0;
+}
+
 static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Variant& V) {
     const bool use_blockrow = blockrow_enabled();
+    const int64_t slab = slab_bytes();
+    int64_t slab_used = 0;
+    B.rslab.assign(1, 0);
+    B.mslab.assign(1, 0);
+    auto close_slab_if_full = [&](int64_t next_bytes) {
+        if (slab > 0 && slab_used > 0 && slab_used + next_bytes > slab) {
+            B.rslab.push_back((int64_t)B.reduce.size());
+            B.mslab.push_back((int64_t)B.slotted.size());
+            slab_used = 0;
+        }
+    };
     const int kChunk = V.chunk, kMaxRows = V.max_rows;
     for (int32_t ti = 0; ti < n; ++ti) {
         const dfq_tensor_desc& d = descs[ti];
@@ -609,6 +632,8 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                 B.main.push_back(k);
             }
         } else if (channel) {   // long rows: one slot per row
+            close_slab_if_full(4 * total);
+            slab_used += 4 * total;
             for (int64_t r = 0; r < d.rows; ++r) {
                 const int64_t slot = B.slots++;
                 for (int64_t off = 0; off < d.row_len; off += plen) {
@@ -617,21 +642,34 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                     k.n = (int32_t)std::min<int64_t>(plen, d.row_len - off);
                     k.row0 = (int32_t)r; k.nrows = 0; k.slot = (int32_t)slot; k.first = (off == 0);
                     B.reduce.push_back(k);
-                    B.main.push_back(k);
+                    B.slotted.push_back(k);
                 }
             }
         } else {                // tensor modes: one slot per tensor (none for a given range)
             const int64_t slot = given ? -1 : B.slots++;
+            if (!given) {
+                close_slab_if_full(4 * total);
+                slab_used += 4 * total;
+            }
             for (int64_t off = 0; off < total; off += plen) {
                 DevTask k{};
                 k.elem_start = off; k.tensor = ti; k.n = (int32_t)std::min<int64_t>(plen, total - off);
                 k.row0 = 0; k.nrows = 0; k.slot = (int32_t)slot; k.first = (off == 0);
-                if (!given) B.reduce.push_back(k);
-                B.main.push_back(k);
+                if (!given) {
+                    B.reduce.push_back(k);
+                    B.slotted.push_back(k);
+                } else {
+                    B.main.push_back(k);
+                }
             }
         }
     }
+    B.rslab.push_back((int64_t)B.reduce.size());
+    B.mslab.push_back((int64_t)B.slotted.size());
     B.main.insert(B.main.begin(), B.blockrow.begin(), B.blockrow.end());
+    const int64_t base = (int64_t)B.main.size();   // slot pieces follow the single-pass tasks
+    for (auto& m : B.mslab) m += base;
+    B.main.insert(B.main.end(), B.slotted.begin(), B.slotted.end());
     return DFQ_OK;
 }
 
@@ -708,6 +746,7 @@ struct dfq_sweep_plan {
     DevTask* d_main = nullptr;
     uint32_t* d_slots = nullptr;   // [slots] mins then [slots] maxs
     int64_t n_reduce = 0, n_main = 0, n_slots = 0, n_tensors = 0, n_elems = 0, algo_bytes = 0;
+    std::vector<int64_t> rslab, mslab;   // slab boundaries (Built)
 };
 
 extern "C" int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, dfq_sweep_plan** out) {
@@ -726,6 +765,8 @@ extern "C" int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, df
     p->n_tensors = n;
     p->n_elems = B.elems;
     p->algo_bytes = B.algo_bytes;
+    p->rslab = B.rslab;
+    p->mslab = B.mslab;
     auto fail = [&](hipError_t e) {
         set_last_hip_error(e);
         (void)hipFree(p->d_tensors); (void)hipFree(p->d_reduce); (void)hipFree(p->d_main); (void)hipFree(p->d_slots);
@@ -758,14 +799,36 @@ extern "C" int dfq_sweep_plan_execute(dfq_sweep_plan* p, void* stream) {
     if (p->n_reduce > 0) {
         DFQ_HIP_CHECK(hipMemsetAsync(p->d_slots, 0xFF, sizeof(uint32_t) * p->n_slots, s));
         DFQ_HIP_CHECK(hipMemsetAsync(p->d_slots + p->n_slots, 0x00, sizeof(uint32_t) * p->n_slots, s));
-        hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for(p->n_reduce)), dim3(kBlockThreads), 0, s,
-                           p->d_tensors, p->d_reduce, p->n_reduce, p->d_slots, p->d_slots + p->n_slots);
-        DFQ_LAUNCH_CHECK();
     }
-    if (p->n_main > 0) {
-        launch_main(p->variant, grid_for(p->n_main, kVariants[p->variant]), s, p->d_tensors, p->d_main, p->n_main,
-                    p->d_slots, p->d_slots + p->n_slots);
-        DFQ_LAUNCH_CHECK();
+    const size_t nslab = p->rslab.size() - 1;
+    if (nslab <= 1) {   // one reduce launch over every slot piece, then one main launch
+        if (p->n_reduce > 0) {
+            hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for(p->n_reduce)), dim3(kBlockThreads), 0, s,
+                               p->d_tensors, p->d_reduce, p->n_reduce, p->d_slots, p->d_slots + p->n_slots);
+            DFQ_LAUNCH_CHECK();
+        }
+        if (p->n_main > 0) {
+            launch_main(p->variant, grid_for(p->n_main, kVariants[p->variant]), s, p->d_tensors, p->d_main, p->n_main,
+                        p->d_slots, p->d_slots + p->n_slots);
+            DFQ_LAUNCH_CHECK();
+        }
+        return DFQ_OK;
+    }
+    // slabs: reduce(k), then quantize slab k (the first main launch also takes the
+    // single-pass tasks)
+    for (size_t k = 0; k < nslab; ++k) {
+        const int64_t r0 = p->rslab[k], r1 = p->rslab[k + 1];
+        if (r1 > r0) {
+            hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for(r1 - r0)), dim3(kBlockThreads), 0, s, p->d_tensors,
+                               p->d_reduce + r0, r1 - r0, p->d_slots, p->d_slots + p->n_slots);
+            DFQ_LAUNCH_CHECK();
+        }
+        const int64_t m0 = k == 0 ? 0 : p->mslab[k], m1 = p->mslab[k + 1];
+        if (m1 > m0) {
+            launch_main(p->variant, grid_for(m1 - m0, kVariants[p->variant]), s, p->d_tensors, p->d_main + m0, m1 - m0,
+                        p->d_slots, p->d_slots + p->n_slots);
+            DFQ_LAUNCH_CHECK();
+        }
     }
     return DFQ_OK;
 }
@@ -777,7 +840,15 @@ extern "C" int dfq_sweep_plan_stats(const dfq_sweep_plan* p, dfq_sweep_stats* st
     st->n_tasks_reduce = p->n_reduce;
     st->n_tasks_main = p->n_main;
     st->algo_bytes = p->algo_bytes;
-    st->launches = (p->n_reduce > 0 ? 1 : 0) + (p->n_main > 0 ? 1 : 0);
+    if (p->rslab.size() > 2) {
+        int32_t l = 0;
+        for (size_t k = 0; k + 1 < p->rslab.size(); ++k)
+            l += (p->rslab[k + 1] > p->rslab[k] ? 1 : 0) +
+                 ((p->mslab[k + 1] > (k == 0 ? 0 : p->mslab[k])) ? 1 : 0);
+        st->launches = l;
+    } else {
+        st->launches = (p->n_reduce > 0 ? 1 : 0) + (p->n_main > 0 ? 1 : 0);
+    }
     st->grid_blocks = p->n_main > 0 ? grid_for(p->n_main, kVariants[p->variant]) : 0;
     st->variant = p->variant;
     return DFQ_OK;
