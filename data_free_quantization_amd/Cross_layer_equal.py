@@ -143,15 +143,15 @@ def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count,
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         _lib.check(L.dfq_cle_plan_run(plan, float(Treshhold), int(Count), MAX_ITERS, C.byref(iters), hist, stream),
                    "dfq_cle_plan_run")
-        chains, steps = C.c_int32(0), C.c_int32(0)
-        L.dfq_cle_plan_info(plan, C.byref(chains), C.byref(steps))
+        chains, steps, launches = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        L.dfq_cle_plan_info(plan, C.byref(chains), C.byref(steps), C.byref(launches))
     finally:
         L.dfq_cle_plan_destroy(plan)
     if iters.value >= MAX_ITERS:
         warnings.warn(f"cross_layer_equalization stopped at DFQ_CLE_MAX_ITERS={MAX_ITERS} iterations")
     LAST_RUN.clear()
     LAST_RUN.update(iterations=iters.value, diffs=[hist[i] for i in range(iters.value)], chains=chains.value,
-                    steps=steps.value, mode="device")
+                    steps=steps.value, launches_per_iteration=launches.value, mode="device")
 
 
 def _cle_host_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps):

@@ -101,7 +101,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_cle_plan_create": ([C.POINTER(CleRel), I32, C.POINTER(P), C.POINTER(I64), I32, F64, F64, I32, F32, I32,
                                  C.POINTER(P)], C.c_int),
         "dfq_cle_plan_run": ([P, F64, I32, I32, C.POINTER(I32), C.POINTER(F64), P], C.c_int),
-        "dfq_cle_plan_info": ([P, C.POINTER(I32), C.POINTER(I32)], C.c_int),
+        "dfq_cle_plan_info": ([P, C.POINTER(I32), C.POINTER(I32), C.POINTER(I32)], C.c_int),
         "dfq_cle_plan_destroy": ([P], C.c_int),
         "dfq_bias_absorb": ([P, P, P, P, P, I64, I64, I64, I64, F32, P], C.c_int),
         "dfq_bc_expect": ([P, P, I64, I32, I32, P, P], C.c_int),

@@ -396,13 +396,14 @@ struct CleRel {
     int32_t sacc_init;
     int32_t vec1;       // W1 rows 16-B aligned (float4 path)
     int32_t vec2;       // W2 contiguous channel segments 16-B aligned (i2 == 1)
-    int32_t pad;
+    int32_t fuse_next;  // >= 0: this relation's W2 is that relation's W1 -- the rescale
+                        // of W2 also produces its row ranges (fused schedule)
 };
 
 // Range-launch kinds: W1 rows, W2 contiguous channels (i2 == 1), W2 row tiles
 // (i2 > 1, ordered-uint atomics), reset of the OTHER parity's W2 words.
 // Rescale-launch kinds: W1 elements, W2 elements, per-channel vectors.
-enum : int32_t { kRangeW1 = 0, kRangeW2Contig = 1, kRangeW2Tile = 2, kRangeReset = 3 };
+enum : int32_t { kRangeW1 = 0, kRangeW2Contig = 1, kRangeW2Tile = 2, kRangeReset = 3, kRangeResetW1 = 4 };
 enum : int32_t { kApplyW1 = 0, kApplyW2Contig = 1, kApplyW2Tile = 2, kApplyChannels = 3 };
 
 struct CleTask {
@@ -513,6 +514,22 @@ __device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, boo
     }
 }
 
+// p[0..n) *= f and the (min, max) of the products, one wave (scalar loads:
+// used for short depthwise rows)
+__device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t n, float f, int lane, float& vmin,
+                                                 float& vmax) {
+    vmin = INFINITY;
+    vmax = -INFINITY;
+    for (int64_t i = lane; i < n; i += 64) {
+        const float y = p[i] * f;
+        p[i] = y;
+        vmin = fminf(vmin, y);
+        vmax = fmaxf(vmax, y);
+    }
+    vmin = wave_min(vmin);
+    vmax = wave_max(vmax);
+}
+
 __global__ void __launch_bounds__(kThreads)
 cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
                       uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st) {
@@ -590,10 +607,11 @@ cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
                     atomicMax(&mx[R.c1 + g_prev * R.i2 + i], enc_ord(vmax));
                 }
             }
-        } else {   // kRangeReset: the other parity's W2 words, for the next iteration's atomics
+        } else {   // kRangeReset(W1): the other parity's W2 (W1) words, for the next iteration's atomics
+            const int64_t off = R.moff + (tk.kind == kRangeReset ? R.c1 : 0);
             for (int64_t c = tk.a + threadIdx.x; c < tk.b; c += kThreads) {
-                omins[R.moff + R.c1 + c] = 0xFFFFFFFFu;
-                omaxs[R.moff + R.c1 + c] = 0u;
+                omins[off + c] = 0xFFFFFFFFu;
+                omaxs[off + c] = 0u;
             }
         }
     }
@@ -601,13 +619,14 @@ cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
 
 __global__ void __launch_bounds__(kThreads)
 cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
-                      const uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
+                      uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
                       float eps, double smin, double smax) {
+    __shared__ float red[2][kThreads / 64][kColTileRows];
     if (st->done) return;
     const int par = st->iters & 1;
     const bool first_iter = st->iters == 0;
-    const uint32_t* mins = rng + (int64_t)par * 2 * M;
-    const uint32_t* maxs = mins + M;
+    uint32_t* mins = rng + (int64_t)par * 2 * M;
+    uint32_t* maxs = mins + M;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     for (int64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
@@ -624,8 +643,72 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
             const int64_t seg = R.o2g * R.khw2;
             for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
                 const CleScale cs = cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax);
-                wave_scale(R.w2 + c * seg, seg, R.vec2, cs.inv, lane);
+                if (R.fuse_next >= 0) {   // o2g == 1: the segment is row c of W2 = row c of the next W1
+                    float vmin, vmax;
+                    wave_scale_range(R.w2 + c * seg, seg, cs.inv, lane, vmin, vmax);
+                    if (lane == 0) {
+                        const int64_t off = rels[R.fuse_next].moff;
+                        mins[off + c] = enc_ord(vmin);
+                        maxs[off + c] = enc_ord(vmax);
+                    }
+                } else {
+                    wave_scale(R.w2 + c * seg, seg, R.vec2, cs.inv, lane);
+                }
             }
+        } else if (tk.kind == kApplyW2Tile && R.fuse_next >= 0) {
+            // rows [a, b) x columns [c0, c0 + 256) of W2, one thread per column, and the
+            // tile's per-row (min, max) of the results -> the next relation's W1 rows
+            const int64_t rowlen = R.i2 * R.khw2;
+            const int64_t i = tk.c0 + threadIdx.x;
+            float rmn[kColTileRows], rmx[kColTileRows];
+#pragma unroll
+            for (int j = 0; j < kColTileRows; ++j) {
+                rmn[j] = INFINITY;
+                rmx[j] = -INFINITY;
+            }
+            if (i < tk.c1) {
+                int64_t g_prev = -1;
+                float inv = 0.f;
+#pragma unroll
+                for (int j = 0; j < kColTileRows; ++j) {
+                    const int64_t o = tk.a + j;
+                    if (o < tk.b) {
+                        const int64_t g = o / R.o2g;
+                        if (g != g_prev) {
+                            inv = cle_scale(mn, mx, R.c1, g * R.i2 + i, is_signed, eps, smin, smax).inv;
+                            g_prev = g;
+                        }
+                        float* p = R.w2 + o * rowlen + i * R.khw2;
+                        for (int64_t k = 0; k < R.khw2; ++k) {
+                            const float y = p[k] * inv;
+                            p[k] = y;
+                            rmn[j] = fminf(rmn[j], y);
+                            rmx[j] = fmaxf(rmx[j], y);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kColTileRows; ++j) {
+                const float a = wave_min(rmn[j]), b = wave_max(rmx[j]);
+                if (lane == 0) {
+                    red[0][wv][j] = a;
+                    red[1][wv][j] = b;
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x < tk.b - tk.a) {
+                const int j = threadIdx.x;
+                float a = red[0][0][j], b = red[1][0][j];
+                for (int w = 1; w < kThreads / 64; ++w) {
+                    a = fminf(a, red[0][w][j]);
+                    b = fmaxf(b, red[1][w][j]);
+                }
+                const int64_t off = rels[R.fuse_next].moff + tk.a + j;
+                atomicMin(&mins[off], enc_ord(a));
+                atomicMax(&maxs[off], enc_ord(b));
+            }
+            __syncthreads();   // red is reused by the next task
         } else if (tk.kind == kApplyW2Tile) {   // rows [a, b) of W2, one thread per column
             const int64_t rowlen = R.i2 * R.khw2;
             const bool one_group = (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
@@ -948,6 +1031,7 @@ struct dfq_cle_plan {
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
     int64_t M = 0, nchunks = 0;
     int32_t nl = 0, chains = 0, steps = 0;
+    bool fused = false;   // one range launch per iteration (see dfq_cle_plan_create)
     CleUnit* d_units = nullptr;
     int64_t* d_b1off = nullptr;
     float* d_b1 = nullptr;          // level-1 sums, [chunk][nb1][32]
@@ -1004,6 +1088,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         c.sacc_init = d.s_acc_init;
         c.vec1 = (d.len1 % 4 == 0 && reinterpret_cast<uintptr_t>(d.w1) % 16 == 0) ? 1 : 0;
         c.vec2 = (d.i2 == 1 && (c.o2g * d.khw2) % 4 == 0 && reinterpret_cast<uintptr_t>(d.w2) % 16 == 0) ? 1 : 0;
+        c.fuse_next = -1;
         M += 2 * d.c1;
         R[r] = c;
     }
@@ -1032,25 +1117,78 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         step_of[r] = comp_len[c]++;
         steps = std::max(steps, step_of[r] + 1);
     }
-    // tasks per step
+    // Fused schedule: a relation's W2 must be untouched by the earlier relations of
+    // its chain (its column range can be taken at the start of the iteration), and
+    // its W1 untouched too, or the W2 of the immediately preceding relation -- whose
+    // rescale then produces the W1 row ranges.  Otherwise: per-step range launches.
+    std::vector<int32_t> w1_src(n_rel, -1);
+    bool fused = true;
+    {
+        const char* fe = getenv("DFQ_CLE_FUSED");
+        if (fe && fe[0] == '0') fused = false;
+        std::vector<std::vector<int32_t>> chain_of(n_rel);
+        for (int32_t r = 0; r < n_rel; ++r) chain_of[find(r)].push_back(r);
+        for (const auto& L : chain_of) {
+            for (size_t j = 0; j < L.size() && fused; ++j) {
+                const CleRel& cr = R[L[j]];
+                for (size_t i = 0; i < j && fused; ++i) {
+                    const CleRel& cq = R[L[i]];
+                    if (cq.w1 == cr.w2 || cq.w2 == cr.w2) fused = false;
+                    if (cq.w1 == cr.w1 || cq.w2 == cr.w1) {
+                        const bool ok = i + 1 == j && cq.w2 == cr.w1 && cq.w1 != cr.w1 && w1_src[L[j]] < 0 &&
+                                        (cq.i2 > 1 || cq.o2g == 1) && cr.c1 == cq.o2 && cr.len1 == cq.i2 * cq.khw2;
+                        if (ok) w1_src[L[j]] = L[i];
+                        else fused = false;
+                    }
+                }
+            }
+        }
+        if (fused)
+            for (int32_t r = 0; r < n_rel; ++r)
+                if (w1_src[r] >= 0) R[w1_src[r]].fuse_next = r;
+    }
+    // tasks: per-step range + rescale launches, or (fused) one range launch for
+    // every relation's W2 (and untouched W1) followed by the rescale launches
     std::vector<CleTask> rt, at;
     std::vector<int64_t> rstep(1, 0), astep(1, 0);
+    auto w2_range_tasks = [&](int32_t r) {
+        const CleRel& c = R[r];
+        if (c.i2 == 1) {
+            for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
+                rt.push_back({r, kRangeW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), 0, 0});
+        } else {
+            for (int64_t a = 0; a < c.o2; a += kColTileRows)
+                for (int64_t i0 = 0; i0 < c.i2; i0 += kThreads)
+                    rt.push_back({r, kRangeW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2), i0,
+                                  std::min<int64_t>(i0 + kThreads, c.i2)});
+            for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
+                rt.push_back({r, kRangeReset, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
+        }
+    };
+    auto w1_range_tasks = [&](int32_t r) {
+        const CleRel& c = R[r];
+        if (fused && w1_src[r] >= 0) {   // produced by the previous relation's rescale: reset the next parity
+            for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
+                rt.push_back({r, kRangeResetW1, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
+        } else {
+            for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
+                rt.push_back({r, kRangeW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
+        }
+    };
+    if (fused) {
+        for (int32_t r = 0; r < n_rel; ++r) {
+            w1_range_tasks(r);
+            w2_range_tasks(r);
+        }
+        rstep.push_back((int64_t)rt.size());
+    }
     for (int32_t k = 0; k < steps; ++k) {
         for (int32_t r = 0; r < n_rel; ++r) {
             if (step_of[r] != k) continue;
             const CleRel& c = R[r];
-            for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
-                rt.push_back({r, kRangeW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
-            if (c.i2 == 1) {
-                for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
-                    rt.push_back({r, kRangeW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), 0, 0});
-            } else {
-                for (int64_t a = 0; a < c.o2; a += kColTileRows)
-                    for (int64_t i0 = 0; i0 < c.i2; i0 += kThreads)
-                        rt.push_back({r, kRangeW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2), i0,
-                                      std::min<int64_t>(i0 + kThreads, c.i2)});
-                for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
-                    rt.push_back({r, kRangeReset, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
+            if (!fused) {
+                w1_range_tasks(r);
+                w2_range_tasks(r);
             }
             for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
                 at.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
@@ -1066,7 +1204,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
                 at.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
         }
-        rstep.push_back((int64_t)rt.size());
+        if (!fused) rstep.push_back((int64_t)rt.size());
         astep.push_back((int64_t)at.size());
     }
     // metric chunks: torch.mean = sum / n; the sum is two_pass_reduction over
@@ -1111,6 +1249,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->nchunks = (int64_t)chunks.size();
     p->chains = chains;
     p->steps = steps;
+    p->fused = fused;
     p->rstep = rstep;
     p->astep = astep;
     p->smin = s_min; p->smax = s_max; p->is_signed = is_signed; p->eps = eps;
@@ -1139,7 +1278,8 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
 // One CLE iteration's launches (steps, metric, stop rule) on stream s.
 static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
     for (int32_t k = 0; k < p->steps; ++k) {
-        const int64_t r0 = p->rstep[k], r1 = p->rstep[k + 1];
+        const int64_t r0 = p->fused ? (k == 0 ? p->rstep[0] : 0) : p->rstep[k];
+        const int64_t r1 = p->fused ? (k == 0 ? p->rstep[1] : 0) : p->rstep[k + 1];
         const int64_t a0 = p->astep[k], a1 = p->astep[k + 1];
         if (r1 > r0) {
             hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(r1 - r0, 2048)), dim3(kThreads), 0, s,
@@ -1264,10 +1404,12 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     return DFQ_OK;
 }
 
-extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t* steps) {
+extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t* steps, int32_t* launches) {
     if (!p) return DFQ_ERR_INVALID;
     if (chains) *chains = p->chains;
     if (steps) *steps = p->steps;
+    if (launches)   // per iteration: range + rescale launches, then the metric (2) and the stop rule
+        *launches = (p->fused ? 1 + p->steps : 2 * p->steps) + (p->nunits > 0 ? 1 : 0) + (p->nchunks > 0 ? 1 : 0) + 1;
     return DFQ_OK;
 }
 

@@ -107,7 +107,7 @@ typedef struct dfq_sweep_stats {
     int64_t n_tasks_reduce;   /* wave tasks of the range-reduction launch (0 = launch skipped) */
     int64_t n_tasks_main;     /* wave tasks of the quantize launch */
     int64_t algo_bytes;       /* algorithmic HBM bytes of one execute */
-    int32_t launches;         /* kernel launches per execute (1 or 2) */
+    int32_t launches;         /* kernel launches per execute (1, 2, or 2 per slab under DFQ_SWEEP_SLAB_MB) */
     int32_t grid_blocks;      /* blocks of the quantize launch */
     int32_t variant;          /* kernel variant (env DFQ_SWEEP_VARIANT at create) */
     int32_t reserved;
@@ -179,8 +179,10 @@ int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* ta
  * max_iters doubles, may be NULL) = the per-iteration diff (np.sum of the list). */
 int dfq_cle_plan_run(dfq_cle_plan* plan, double threshold, int32_t count, int32_t max_iters,
                      int32_t* iterations, double* diffs, void* stream);
-/* chains = independent relation groups, steps = launches pairs per iteration */
-int dfq_cle_plan_info(const dfq_cle_plan* plan, int32_t* chains, int32_t* steps);
+/* chains = independent relation groups, steps = relations per chain (max),
+ * launches = kernel launches per iteration (fused schedule: one range launch for
+ * the whole iteration; DFQ_CLE_FUSED=0: one per step) */
+int dfq_cle_plan_info(const dfq_cle_plan* plan, int32_t* chains, int32_t* steps, int32_t* launches);
 int dfq_cle_plan_destroy(dfq_cle_plan* plan);
 
 /* ---- high-bias absorption (bias_absorption.py:147-197) ------------------

@@ -26,4 +26,6 @@ for rep in range(2):
         run_dfq(m, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel", symmetric=True,
                 bc_mode="fused", timings=t)
     torch.cuda.synchronize()
-    print(rep, {k: round(v * 1e3, 3) for k, v in t.items()}, round((time.perf_counter() - t0) * 1e3, 3), flush=True)
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    print(rep, {k: round(v * 1e3, 3) for k, v in t.items()}, round((time.perf_counter() - t0) * 1e3, 3),
+          {k: v for k, v in cle.LAST_RUN.items() if k != "diffs"}, flush=True)

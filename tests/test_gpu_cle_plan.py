@@ -4,6 +4,7 @@ Cross_layer_equal.py:63-116 on hand-made graphs: several independent chains
 dead channel, a relation without BN stats, a layer shared by two relations in
 one chain and a large layer (multi-chunk metric).  Weights, biases, BN fake
 stats, Relation.S, iteration count and every per-iteration diff: bit-exact."""
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -110,6 +111,9 @@ def test_device_cle_matches_oracle(signed, eps, smm, thr, count, monkeypatch):
                                  signed=signed, eps=eps, Save_state=False)
     torch.cuda.synchronize()
     assert cle.LAST_RUN["chains"] == 3 and cle.LAST_RUN["steps"] == 2
+    # fused schedule: one range launch + 2 rescale steps + metric (2) + stop rule
+    expect = 6 if os.environ.get("DFQ_CLE_FUSED", "1") != "0" else 7
+    assert cle.LAST_RUN["launches_per_iteration"] == expect
     assert cle.LAST_RUN["diffs"] == diffs
     for k in W:
         assert np.array_equal(g[k].weight.detach().cpu().numpy(), W[k]), k
