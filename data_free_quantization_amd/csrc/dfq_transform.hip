@@ -184,6 +184,105 @@ bc_propagate_kernel(const float* __restrict__ bias_vec, int64_t nrows, int64_t f
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Activation ranges from BN statistics: set_quant_minmax,
+// utils/layer_transform.py:356-618.  Rectified-Gaussian moments with scipy's
+// pdf / ndtr in float64 on the fp32 argument, every fp32 op in the reference's
+// expression order (:396-410).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float std_pdf(float x) {
+    const double xd = (double)x;
+    return (float)(exp(-(xd * xd) / 2.0) / 2.5066282746310002);
+}
+__device__ __forceinline__ float std_cdf(float x) { return (float)ndtr_d((double)x); }
+
+// kind 0: mean = b, var = w*w; 1: calculate_mean / calculate_var (ReLU);
+// 2: calculate_mean_6 / calculate_var_6 (ReLU6).  sqrt_w: w := sqrt(w + eps)
+// (torch.sqrt(var + eps)).  accumulate: mean += m, var += v.  mean/var may alias w/b.
+__global__ void act_moments_kernel(const float* w_in, const float* b_in, int64_t n, int kind, int sqrt_w, float eps,
+                                   int accumulate, float* mean, float* var) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        const float w = sqrt_w ? sqrtf(w_in[j] + eps) : w_in[j];
+        const float b = b_in[j];
+        float m, v;
+        if (kind == 0) {
+            m = b;
+            v = w * w;
+        } else if (kind == 1) {
+            const float x0 = (-b) / w;
+            const float P0 = std_pdf(x0), C0 = std_cdf(x0);
+            m = w * P0 + b * (1.0f - C0);
+            const float B = ((b * b + w * w) + m * m) - (2.0f * m) * b;
+            v = ((1.0f - C0) * B + (w * (b - 2.0f * m)) * P0) + (m * m) * C0;
+        } else {
+            const float x0 = (-b) / w, x6 = (6.0f - b) / w;
+            const float P0 = std_pdf(x0), C0 = std_cdf(x0), P6 = std_pdf(x6), C6 = std_cdf(x6);
+            m = (w * (P0 - P6) + b * (C6 - C0)) + 6.0f * (1.0f - C6);
+            const float B = ((b * b + w * w) + m * m) - (2.0f * m) * b;
+            const float d6 = 6.0f - m;
+            v = ((((C6 - C0) * B + (w * -6.0f) * P6) + (w * (b - 2.0f * m)) * (P0 - P6)) + (m * m) * C0) +
+                (d6 * d6) * (1.0f - C6);
+        }
+        if (accumulate) {
+            m = mean[j] + m;
+            v = var[j] + v;
+        }
+        mean[j] = m;
+        var[j] = v;
+    }
+}
+
+// out = {min(a - N*w), max(a + N*w)} (get_min_value / get_max_value, :391-392);
+// w_is_var: w := sqrt(w + eps).  One block.
+__global__ void act_minmax_kernel(const float* a, const float* w_in, int64_t n, int w_is_var, float eps, float nsig,
+                                  float* out) {
+    __shared__ float smin[4], smax[4];
+    float vmin = INFINITY, vmax = -INFINITY;
+    for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
+        const float w = w_is_var ? sqrtf(w_in[j] + eps) : w_in[j];
+        const float nw = nsig * w;
+        vmin = fminf(vmin, a[j] - nw);
+        vmax = fmaxf(vmax, a[j] + nw);
+    }
+    vmin = wave_min(vmin);
+    vmax = wave_max(vmax);
+    if ((threadIdx.x & 63) == 0) {
+        smin[threadIdx.x >> 6] = vmin;
+        smax[threadIdx.x >> 6] = vmax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x / 64); ++k) {
+            vmin = fminf(vmin, smin[k]);
+            vmax = fmaxf(vmax, smax[k]);
+        }
+        out[0] = fminf(smin[0], vmin);
+        out[1] = fmaxf(smax[0], vmax);
+    }
+}
+
+// Case (d.) of set_quant_minmax (:470-481): a BN statistic vector pushed through a
+// conv (weights summed over KH*KW, ATen order) or linear layer with its bias:
+// out[o] = sum_i Wsum[o, i] * x[g*I + i] (+ bias[o]).  One wave per output.
+__global__ void act_affine_kernel(const float* x, const float* w, const float* bias, int64_t o, int64_t i2,
+                                  int64_t khw, int64_t og, float* out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t r = wave; r < o; r += nwaves) {
+        const int64_t g = r / og;
+        float acc = 0.f;
+        for (int64_t i = lane; i < i2; i += 64) {
+            const float* p = w + (r * i2 + i) * khw;
+            const float ws = khw == 1 ? p[0] : aten_inner_sum([&](int64_t k) { return p[k]; }, khw);
+            acc += ws * x[g * i2 + i];
+        }
+        acc = wave_sum_f(acc);
+        if (lane == 0) out[r] = bias ? acc + bias[r] : acc;
+    }
+}
+
 }  // namespace dfq
 
 using namespace dfq;
@@ -267,6 +366,34 @@ extern "C" int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fak
     hipLaunchKernelGGL(bc_propagate_kernel, dim3((int)std::min<int64_t>(ceil_div(f, (int64_t)4), 2048)), dim3(kThreads),
                        0, static_cast<hipStream_t>(stream),
                        bias_vec, numel / f, f, (int)ref_threads, fake_b);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+extern "C" int dfq_act_moments(const float* w, const float* b, int64_t n, int32_t kind, int32_t sqrt_w, float eps,
+                               int32_t accumulate, float* mean, float* var, void* stream) {
+    if (!w || !b || !mean || !var || n < 0 || kind < 0 || kind > 2) return DFQ_ERR_INVALID;
+    if (n == 0) return DFQ_OK;
+    hipLaunchKernelGGL(act_moments_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, static_cast<hipStream_t>(stream), w,
+                       b, n, (int)kind, (int)sqrt_w, eps, (int)accumulate, mean, var);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+extern "C" int dfq_act_minmax(const float* a, const float* w, int64_t n, int32_t w_is_var, float eps, float nsig,
+                              float* out2, void* stream) {
+    if (!a || !w || !out2 || n <= 0) return DFQ_ERR_INVALID;
+    hipLaunchKernelGGL(act_minmax_kernel, dim3(1), dim3(kThreads), 0, static_cast<hipStream_t>(stream), a, w, n,
+                       (int)w_is_var, eps, nsig, out2);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+extern "C" int dfq_act_affine(const float* x, const float* w, const float* bias, int64_t o, int64_t i2, int64_t khw,
+                              int64_t groups, float* out, void* stream) {
+    if (!x || !w || !out || o <= 0 || i2 <= 0 || khw <= 0 || groups <= 0 || o % groups) return DFQ_ERR_INVALID;
+    hipLaunchKernelGGL(act_affine_kernel, dim3((int)std::min<int64_t>(ceil_div(o, (int64_t)4), 2048)), dim3(kThreads),
+                       0, static_cast<hipStream_t>(stream), x, w, bias, o, i2, khw, o / groups, out);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }

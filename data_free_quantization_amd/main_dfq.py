@@ -29,7 +29,8 @@ from .bias_absorption import bias_absorption
 from .bias_correction import bias_correction
 from .clip_weight import clip_weight
 from .Cross_layer_equal import cross_layer_equalization
-from .utils.layer_transform import merge_batchnorm, quantize_targ_layer, replace_op, restore_op, switch_layers
+from .utils.layer_transform import (merge_batchnorm, quantize_targ_layer, replace_op, restore_op, set_quant_minmax,
+                                    switch_layers)
 from .utils.quantize import QuantConv2d, QuantLinear, QuantMeasure, set_layer_bits
 from .utils.relation import create_relation
 from .utils.tracer import TorchTransformer
@@ -145,6 +146,7 @@ def main(argv=None):
         graph = quantize_targ_layer(graph, args.bits_weight, args.bits_bias, targ_layer,
                                     granularity=args.granularity, symmetric=args.symmetric, clip=fused_clip,
                                     state=state)
+        set_quant_minmax(graph, bottoms)   # main_dfq.py:217
     if args.clip_weight and not (args.quantize and args.bc_mode == "fused"):
         clip_weight(graph, range_clip=[-15, 15], targ_type=targ_layer)
     if args.correction:

@@ -4,6 +4,9 @@
 * ``quantize_targ_layer`` (utils/layer_transform.py:288-305) -> one grouped HIP sweep
 * ``find_prev_bn``        (utils/layer_transform.py:308-353) host graph walk
 * ``switch_layers``       (utils/layer_transform.py:161-197) with this package's tracer
+* ``set_quant_minmax``    (utils/layer_transform.py:356-618) -> HIP ``dfq_act_*``
+* ``replace_op`` / ``restore_op`` (utils/layer_transform.py:128-158): tensor-op
+  input quantization during inference
 
 Graph/bottoms follow SURVEY.md 8b.  Target tensors must be on a ROCm device.
 """
@@ -52,8 +55,35 @@ def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d]):
                 bn.register_buffer("fake_weight", fake_w)
                 bn.register_buffer("fake_bias", fake_b)
                 bn.eps = 0
+                _identity_forward_hooks(bn)
                 break
     return model
+
+
+_TINY = float(torch.finfo(torch.float32).tiny)
+
+
+def _identity_forward_hooks(bn):
+    """The folded BN (weight 1, bias 0, mean 0, var 1, eps 0 -- the reference's
+    state) is an identity, but torch >= 2 rejects eps == 0 in F.batch_norm.  Run
+    its forward with the smallest normal fp32 eps (1 + eps == 1 in fp32, so the
+    result is unchanged) and put eps = 0 back afterwards."""
+    if getattr(bn, "_dfq_identity_hooks", False):
+        return
+
+    def pre(mod, args):
+        if mod.eps == 0:
+            mod.eps = _TINY
+            mod._dfq_eps_swapped = True
+
+    def post(mod, args, out):
+        if getattr(mod, "_dfq_eps_swapped", False):
+            mod.eps = 0
+            mod._dfq_eps_swapped = False
+
+    bn.register_forward_pre_hook(pre)
+    bn.register_forward_hook(post)
+    bn._dfq_identity_hooks = True
 
 
 def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, granularity="tensor",
@@ -148,27 +178,358 @@ def find_prev_bn(bn_module, relu_attached, graph, bottoms, bot):
     return bn_list, relu_attach_list, connect_type_list, targ_without_bn
 
 
+#: the tensor-op quantizers installed by switch_layers(quant_op=True) (the
+#: reference keeps the same module-level global, utils/layer_transform.py:186)
+module_tensor_op = None
+
+# tensor ops whose inputs get QuantMeasures (utils/layer_transform.py:8-13), as
+# this package's tracer names their graph nodes
+_QUANT_OPS = ("add", "cat", "mean", "interpolate", "softmax")
+_QUANT_OP_PREFIXES = ("add_", "torch.cat_", "torch.mean_", "F.interpolate_", "F.softmax_")
+
+
+class CustomTensorOP(nn.Module):
+    """QuantMeasures for the inputs of the graph's tensor-op nodes (add / cat /
+    mean / interpolate / softmax), one per tensor input, in graph order
+    (utils/layer_transform.py:199-236).  The reference finds a call's quantizers
+    by cycling an index over the ops PyTransformer recorded; here they are keyed by
+    the graph's op node, and ``replace_op`` matches calls to nodes in execution
+    order."""
+
+    def __init__(self, graph, bottoms, ignore_op=("pad",)):
+        super().__init__()
+        self.quants = nn.ModuleList()
+        self.offsets: Dict[str, tuple] = {}
+        self.names = []
+        for key, node in graph.items():
+            if type(node) != str or bottoms.get(key) is None:
+                continue
+            if any(ig in key for ig in ignore_op) or not key.startswith(_QUANT_OP_PREFIXES):
+                continue
+            n = len(bottoms[key])
+            self.offsets[key] = (len(self.quants), n)
+            self.names.append(key)
+            for _ in range(n):
+                self.quants.append(QuantMeasure(num_bits=8, momentum=0.1))
+        self.idx_name_tensor_op = 0
+
+    def get(self, key):
+        o, n = self.offsets[key]
+        return [self.quants[o + i] for i in range(n)]
+
+    def next_name(self):
+        """The op node the next intercepted call belongs to (execution order)."""
+        key = self.names[self.idx_name_tensor_op]
+        self.idx_name_tensor_op = (self.idx_name_tensor_op + 1) % len(self.names)
+        return key
+
+
 def switch_layers(model, transformer, data, module_dict, ignore_layer=[], ignore_op=["pad"], quant_op=True):
-    """Swap layer types (module_dict {1: [(Conv2d, QuantConv2d), ...], 0: [(ReLU6, ReLU)]})
-    and build the graph (utils/layer_transform.py:161-197).  Activation-op
-    interception (CustomTensorOP) is not on the weight path and is not installed."""
+    """Swap layer types (module_dict {1: [(Conv2d, QuantConv2d), ...], 0: [(ReLU6, ReLU)]}),
+    build the graph and, with ``quant_op``, install the tensor-op quantizers
+    (utils/layer_transform.py:161-197)."""
+    global module_tensor_op
     for key in module_dict:
         for source, target in module_dict[key]:
             transformer.register(source, target)
         model = transformer.trans_layers(model, update=(key == 1))
-    transformer._build_graph(model, data, ignore_layer)
+    g = transformer._build_graph(model, data, ignore_layer)
+    if not quant_op:
+        return model, transformer
+    module_tensor_op = CustomTensorOP(g.getGraph(), g.getBottoms(), tuple(ignore_op))
+    dev = next((p.device for p in model.parameters()), torch.device("cpu"))
+    module_tensor_op.to(dev)
+    model.add_module("custom_tensor_op", module_tensor_op)
     return model, transformer
 
 
-def replace_op():
-    """Activation-op interception (utils/layer_transform.py:128-144) belongs to the
-    activation/inference path, out of scope for the weight path."""
+# ---------------------------------------------------------------------------
+# set_quant_minmax (utils/layer_transform.py:356-618): QuantMeasure ranges from
+# the BN statistics feeding each quantized input.  The per-channel statistics
+# (rectified-Gaussian moments, min/max of mean -/+ N*std, the case (d.) affine)
+# are HIP kernels; the branch walk and the scalar combination stay Python, as in
+# the reference.
+# ---------------------------------------------------------------------------
+_EPS = 1e-6
+#: QuantMeasures the last set_quant_minmax set through case (d.) (a conv/linear
+#: between the BN and the quantizer; its GEMV order is MKL's in the reference)
+CASE_D = []
+
+
+def _moments(weight, bias, kind, sqrt_w=False, into=None):
+    """(mean, var) of one BN branch: kind 0 (no activation), 1 (ReLU), 2 (ReLU6);
+    ``into``: (mean, var) accumulated in place (mean += m; var += v)."""
+    _lib.require_device(weight, bias)
+    n = bias.numel()
+    if into is None:
+        mean = torch.empty(n, dtype=torch.float32, device=bias.device)
+        var = torch.empty_like(mean)
+        acc = 0
+    else:
+        mean, var = into
+        acc = 1
+    rc = _lib.load().dfq_act_moments(_lib.ptr(weight), _lib.ptr(bias), n, kind, int(sqrt_w), _EPS, acc,
+                                     _lib.ptr(mean), _lib.ptr(var), _lib.stream_of(bias))
+    _lib.check(rc, "dfq_act_moments")
+    return mean, var
+
+
+def _moments_inplace(mean, var, kind):
+    """mean, var <- calculate_mean(_6)(sqrt(var + eps), mean), calculate_var(_6)(...)."""
+    rc = _lib.load().dfq_act_moments(_lib.ptr(var), _lib.ptr(mean), mean.numel(), kind, 1, _EPS, 0,
+                                     _lib.ptr(mean), _lib.ptr(var), _lib.stream_of(mean))
+    _lib.check(rc, "dfq_act_moments")
+
+
+def _minmax(a, w, n_sigma, w_is_var=False):
+    """(float(min(a - N*w)), float(max(a + N*w))), w := sqrt(w + eps) if w_is_var."""
+    _lib.require_device(a, w)
+    out = torch.empty(2, dtype=torch.float32, device=a.device)
+    rc = _lib.load().dfq_act_minmax(_lib.ptr(a), _lib.ptr(w), a.numel(), int(w_is_var), _EPS, float(n_sigma),
+                                    _lib.ptr(out), _lib.stream_of(a))
+    _lib.check(rc, "dfq_act_minmax")
+    lo, hi = out.tolist()
+    return lo, hi
+
+
+def _get_min_value(bias, weight, n):
+    return _minmax(bias, weight, n)[0]
+
+
+def _get_max_value(bias, weight, n):
+    return _minmax(bias, weight, n)[1]
+
+
+def _through_layer(vec, layer_type, layer):
+    """Case (d.): a statistic vector pushed through a conv (weight summed over
+    KH*KW, groups) or linear layer with its bias (utils/layer_transform.py:470-479)."""
+    w = layer.weight.detach().data
+    b = layer.bias.detach().data   # AttributeError on a bias-less layer, as the reference
+    o, i2 = w.shape[0], w.shape[1]
+    khw = w.numel() // (o * i2)
+    groups = getattr(layer, "groups", 1) if layer_type == "conv" else 1
+    out = torch.empty(o, dtype=torch.float32, device=w.device)
+    _lib.require_device(vec, w, b)
+    rc = _lib.load().dfq_act_affine(_lib.ptr(vec), _lib.ptr(w.contiguous()), _lib.ptr(b), o, i2, khw, groups,
+                                    _lib.ptr(out), _lib.stream_of(w))
+    _lib.check(rc, "dfq_act_affine")
+    return out
+
+
+def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchNorm2d, N=6, verbose=True):
+    """Set every QuantMeasure's running_min / running_max from the statistics of
+    the BatchNorms feeding it (utils/layer_transform.py:356-618): 1-to-1, 1-to-many
+    (add: Gaussian moment sums; cat: min/max), many-to-many, and layers without a
+    BN in between (case d.)."""
+    if verbose:
+        print("SET QUANT MIN MAX")
+    CASE_D.clear()
+
+    def get_quant_module(layer, key):
+        if type(layer) == str:
+            if module_tensor_op is not None and key in module_tensor_op.offsets:
+                return module_tensor_op.get(key)
+            return None
+        if hasattr(layer, "quant"):
+            return [getattr(layer, "quant")]
+        return None
+
+    def kind_of(use_relu):
+        return 1 if use_relu == "relu" else 2 if use_relu == "relu6" else 0
+
+    bn_module, relu_attached = {}, {}
+    for idx_layer in graph:
+        bot = bottoms[idx_layer]
+        if bot is None:
+            continue
+        node = graph[idx_layer]
+        if type(node) == bn_type:
+            bn_module[idx_layer] = node
+            relu_attached[idx_layer] = "none"
+            continue
+        if type(node) == torch.nn.ReLU:
+            relu_attached[bot[0]] = "relu"
+        elif type(node) == torch.nn.ReLU6:
+            relu_attached[bot[0]] = "relu6"
+        quant_module = get_quant_module(node, idx_layer)
+        if len(bot) == 1 and bot[0] == "Data":
+            if is_detection:
+                quant_module[0].running_max.fill_(1)
+                quant_module[0].running_min.fill_(-1)
+            else:   # (1 - mean) / std and (0 - mean) / std of the data preprocessing
+                quant_module[0].running_max.fill_(2.64)
+                quant_module[0].running_min.fill_(-2.11790393)
+        elif quant_module is not None:
+            bn_list, relu_attach_list, connect_type_list, targ_without_bn = find_prev_bn(
+                bn_module, relu_attached, graph, bottoms, bot[:])
+            if len(quant_module) == len(bn_list):   # 1 to 1
+                for idx in range(len(bn_list)):
+                    bias = getattr(bn_list[idx][0], "fake_bias").view(-1)
+                    weight = getattr(bn_list[idx][0], "fake_weight").view(-1)
+                    if bn_list[idx][1][0] in targ_without_bn:   # case (d.)
+                        CASE_D.append(quant_module[idx])
+                        layer_type, obj_layer = targ_without_bn[bn_list[idx][1][0]]
+                        bias = _through_layer(bias, layer_type, obj_layer)
+                        weight = _through_layer(weight, layer_type, obj_layer)
+                        value_max = _get_max_value(bias, weight, N)
+                        value_min = _get_min_value(bias, weight, N)
+                    else:
+                        lo, hi = _minmax(bias, weight, N)
+                        value_min = max(0., lo) if "relu" in relu_attach_list[idx] else lo
+                        value_max = min(6., hi) if "relu6" in relu_attach_list[idx] else hi
+                    quant_module[idx].running_max.fill_(value_max)
+                    quant_module[idx].running_min.fill_(value_min)
+            else:   # 1 to many or many to many
+                bn_branch = {}
+                for idx, tmp in enumerate(bn_list):
+                    _, bid = tmp
+                    bn_branch.setdefault(bid[0], []).append((tmp, relu_attach_list[idx], connect_type_list[idx]))
+                bn_res = {}
+                for key in bn_branch:
+                    tmp_list = sorted(bn_branch[key], key=lambda x: len(x[0][1]), reverse=True)
+                    node_cur, use_relu, connect_type = tmp_list[0]
+                    layer_cur, bid = node_cur
+                    depth = len(bid)
+                    tmp_list.pop(0)
+                    bias = layer_cur.fake_bias.detach().clone()
+                    weight = layer_cur.fake_weight.detach().clone()
+                    mean = var = None
+                    value_min = value_max = None
+                    if "add" in connect_type:
+                        mean, var = _moments(weight, bias, kind_of(use_relu))
+                    else:
+                        lo, hi = _minmax(bias, weight, N)
+                        value_min = max(0., lo) if "relu" in use_relu else lo
+                        value_max = min(6., hi) if "relu6" in use_relu else hi
+                    while len(tmp_list) > 0:
+                        idx_bound = 0
+                        while idx_bound < len(tmp_list) and len(tmp_list[idx_bound][0][1]) == depth:
+                            idx_bound += 1
+                        if idx_bound == 0 and len(tmp_list) > 0:   # cut depth
+                            depth = len(tmp_list[idx_bound][0][1])
+                        else:
+                            for idx in range(idx_bound):
+                                node_tmp, use_relu_tmp, connect_type = tmp_list[idx]
+                                bias = node_tmp[0].fake_bias.detach().clone()
+                                weight = node_tmp[0].fake_weight.detach().clone()
+                                if "add" in connect_type:
+                                    _moments(weight, bias, kind_of(use_relu_tmp), into=(mean, var))
+                                    if "relu6" in connect_type:
+                                        _moments_inplace(mean, var, 2)
+                                    elif "relu" in connect_type:
+                                        _moments_inplace(mean, var, 1)
+                                else:
+                                    lo, hi = _minmax(bias, weight, N)
+                                    if "cat" == connect_type:
+                                        value_min = min(value_min, max(0., lo) if "relu" in use_relu_tmp else lo)
+                                        value_max = max(value_max, min(6., hi) if "relu6" in use_relu_tmp else hi)
+                                    else:
+                                        value_min += max(0., lo) if use_relu_tmp else lo
+                                        value_max += hi
+                            tmp_list = tmp_list[idx_bound:]
+                            if "one" == connect_type:
+                                value_min /= (idx_bound + 1)
+                                value_max /= (idx_bound + 1)
+                    if "add" in connect_type:
+                        bn_res[key] = (connect_type, mean, var)
+                    else:
+                        bn_res[key] = (connect_type, value_min, value_max)
+
+                if len(quant_module) == 1 and len(quant_module) < len(bn_list):   # 1 to many
+                    assert len(list(bn_res.keys())) == 1, "Error occurs when setting min/max, should be 1 to many"
+                    first = list(bn_res.values())[0]
+                    if "add" in first[0]:
+                        _, mean, var = first
+                        value_min, value_max = _minmax(mean, var, N, w_is_var=True)
+                    else:
+                        _, value_min, value_max = first
+                    quant_module[0].running_max.fill_(value_max)
+                    quant_module[0].running_min.fill_(value_min)
+                elif len(quant_module) < len(bn_list):   # many to many
+                    assert len(bn_res) == len(quant_module), "LENGTH NOT EQUAL {} vs {}".format(
+                        len(bn_res), len(quant_module))
+                    for idx in range(len(bn_res)):
+                        entry = bn_res[str(idx)]
+                        if "add" in entry[0]:
+                            _, mean, var = entry
+                            value_min, value_max = _minmax(mean, var, N, w_is_var=True)
+                        else:
+                            _, value_min, value_max = entry
+                        quant_module[idx].running_max.fill_(value_max)
+                        quant_module[idx].running_min.fill_(value_min)
+                else:
+                    assert False, "Unknown error occured while setting min/max"
+
+
+_RAW_OPS = {}
+_MODE = None
+
+
+def _quantized_call(func, args, kwargs):
+    """Apply the op node's QuantMeasures to the call's tensor inputs (the reference's
+    ___add__ / torch_cat / torch_mean / F_interpolate / F_softmax,
+    utils/layer_transform.py:18-124)."""
+    key = module_tensor_op.next_name()
+    qs = module_tensor_op.get(key)
+    if func in _ADD_FUNCS:
+        args = (qs[0](args[0]), qs[1](args[1])) + tuple(args[2:])
+    elif func is torch.cat:
+        seq = args[0] if args else kwargs.pop("tensors")
+        args = (type(seq)(q(t) for q, t in zip(qs, seq)),) + tuple(args[1:])
+    else:
+        args = (qs[0](args[0]),) + tuple(args[1:])
+    return func(*args, **kwargs)
+
+
+def _op_kind(func):
+    if func in _ADD_FUNCS:
+        return "add"
+    if func is torch.cat:
+        return "cat"
+    if func is torch.mean:
+        return "mean"
+    if func is torch.nn.functional.interpolate:
+        return "interpolate"
+    if func is torch.nn.functional.softmax:
+        return "softmax"
     return None
+
+
+_ADD_FUNCS = (torch.Tensor.__add__, torch.Tensor.add, torch.Tensor.__iadd__, torch.add)
+
+
+class _TensorOpMode(torch.overrides.TorchFunctionMode):
+    """Routes add / cat / mean / interpolate / softmax calls through the
+    quantizers of the graph node they execute (replace_op)."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        kind = _op_kind(func)
+        if kind is not None and module_tensor_op is not None and module_tensor_op.names:
+            expect = module_tensor_op.names[module_tensor_op.idx_name_tensor_op]
+            if kind in expect:
+                return _quantized_call(func, args, kwargs)
+        return func(*args, **kwargs)
+
+
+def replace_op():
+    """Quantize the inputs of tensor ops during inference
+    (utils/layer_transform.py:128-144): a TorchFunctionMode that matches each
+    add / cat / mean / interpolate / softmax call to the next op node of the graph
+    instead of monkey-patching torch and inspecting the call stack."""
+    global _MODE
+    if _MODE is None:
+        _MODE = _TensorOpMode()
+        _MODE.__enter__()
 
 
 def restore_op():
-    return None
+    """Undo replace_op (utils/layer_transform.py:147-158)."""
+    global _MODE
+    if _MODE is not None:
+        _MODE.__exit__(None, None, None)
+        _MODE = None
 
 
 __all__ = ["merge_batchnorm", "quantize_targ_layer", "find_prev_bn", "switch_layers", "replace_op", "restore_op",
-           "TorchTransformer", "QuantMeasure"]
+           "set_quant_minmax", "CustomTensorOP", "TorchTransformer", "QuantMeasure"]

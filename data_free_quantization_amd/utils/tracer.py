@@ -39,7 +39,7 @@ _TRANSPARENT_FUNCS = {operator.getitem, getattr, torch.flatten, torch.reshape}
 _OPS = {
     operator.add: "add", operator.iadd: "add", torch.add: "add",
     torch.cat: "torch.cat", torch.mean: "torch.mean",
-    F.pad: "F.pad", F.interpolate: "F.interpolate",
+    F.pad: "F.pad", F.interpolate: "F.interpolate", F.softmax: "F.softmax",
 }
 _METHOD_OPS = {"add": "add", "add_": "add", "__add__": "add", "__iadd__": "add", "mean": "torch.mean"}
 

@@ -220,6 +220,23 @@ int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_
 int dfq_probe_stream(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t blocks,
                      void* stream);
 
+/* ---- activation ranges from BN statistics (set_quant_minmax,
+ *      utils/layer_transform.py:356-618) ---------------------------------------
+ * Per channel j, with w = sqrt_w ? sqrt(w[j] + eps) : w[j], b = b[j]:
+ *   kind 0: m = b, v = w*w;  1: calculate_mean / calculate_var (ReLU, :396-399);
+ *   2: calculate_mean_6 / calculate_var_6 (ReLU6, :400-410);
+ *   accumulate ? (mean += m, var += v) : (mean = m, var = v).  mean/var may alias w/b. */
+int dfq_act_moments(const float* w, const float* b, int64_t n, int32_t kind, int32_t sqrt_w, float eps,
+                    int32_t accumulate, float* mean, float* var, void* stream);
+/* out2 = {min(a - nsig*w), max(a + nsig*w)} (get_min_value / get_max_value, :391-392),
+ * w := sqrt(w + eps) when w_is_var.  out2: 2 device floats. */
+int dfq_act_minmax(const float* a, const float* w, int64_t n, int32_t w_is_var, float eps, float nsig,
+                   float* out2, void* stream);
+/* Case (d.) (:470-481): out[o] = sum_i (sum_k W[o,i,k]) * x[g*i2 + i] (+ bias[o]),
+ * W = [o, i2, khw] (khw = 1 for Linear), g = o / (o / groups). */
+int dfq_act_affine(const float* x, const float* w, const float* bias, int64_t o, int64_t i2, int64_t khw,
+                   int64_t groups, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

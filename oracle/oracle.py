@@ -45,6 +45,9 @@ def lib():
         L.oracle_mean_abs_diff.restype = C.c_float
         L.oracle_np_sum.argtypes = [P, I64]
         L.oracle_np_sum.restype = C.c_double
+        L.oracle_act_moments.argtypes = [P, P, I64, I32, I32, F32, I32, P, P]
+        L.oracle_act_minmax.argtypes = [P, P, I64, I32, F32, F32, P]
+        L.oracle_act_affine.argtypes = [P, P, P, I64, I64, I64, I64, P]
         _lib = L
     return _lib
 
@@ -160,3 +163,33 @@ def np_sum(values):
     """np.sum(list_of_floats) (numpy pairwise summation), restated."""
     v = np.ascontiguousarray(values, dtype=np.float64)
     return float(lib().oracle_np_sum(_p(v), v.size))
+
+
+def act_moments(w, b, kind, sqrt_w=False, eps=1e-6, into=None):
+    """set_quant_minmax's (mean, var) of one BN branch (utils/layer_transform.py:396-410)."""
+    w, b = _f32(w), _f32(b)
+    if into is None:
+        mean, var, acc = np.empty_like(b), np.empty_like(b), 0
+    else:
+        mean, var = into
+        acc = 1
+    lib().oracle_act_moments(_p(w), _p(b), b.size, kind, int(sqrt_w), eps, acc, _p(mean), _p(var))
+    return mean, var
+
+
+def act_minmax(a, w, nsig, w_is_var=False, eps=1e-6):
+    a, w = _f32(a), _f32(w)
+    out = np.empty(2, np.float32)
+    lib().oracle_act_minmax(_p(a), _p(w), a.size, int(w_is_var), eps, float(nsig), _p(out))
+    return float(out[0]), float(out[1])
+
+
+def act_affine(x, w, bias, groups=1):
+    """Case (d.) of set_quant_minmax: x pushed through W (summed over KH*KW) + bias."""
+    x, w = _f32(x), _f32(w)
+    b = None if bias is None else _f32(bias)
+    o, i2 = w.shape[0], w.shape[1]
+    khw = w.size // (o * i2)
+    out = np.empty(o, np.float32)
+    lib().oracle_act_affine(_p(x), _p(w), _p(b), o, i2, khw, groups, _p(out))
+    return out

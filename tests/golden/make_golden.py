@@ -400,6 +400,47 @@ def pipeline(name: str, seed: int = 0, per_channel: bool = False):
     print(name, "relations", len(res), "cle iters", len(spy.diffs), "bc", str(P["bc_error"]), stats)
 
 
+def act_ranges(name: str, seed: int = 0):
+    """set_quant_minmax (utils/layer_transform.py:356-618) on the graph after the
+    first merge_batchnorm (random BN statistics) and after the second one (the
+    main_dfq order: fake stats reset to 1 / 0).  Every target layer carries a
+    QuantMeasure (as QuantConv2d / QuantLinear would); every add / cat / mean /
+    interpolate node one per tensor input (the reference's CustomTensorOP, in graph
+    order -- PyTransformer, which would record them, is absent)."""
+    import utils.layer_transform as ref_lt
+    from utils.quantize import QuantMeasure as RefQM
+    from data_free_quantization_amd.utils.layer_transform import CustomTensorOP as OurCTO
+    model = zoo.build(name, seed=seed, relu=True)
+    g = build_graph(model, "positional")
+    graph, bottoms = g.getGraph(), g.getBottoms()
+    tkeys = [k for k in graph if type(graph[k]) in TARG]
+    for k in tkeys:
+        graph[k].quant = RefQM(num_bits=8)
+    ops = OurCTO(graph, bottoms)
+    A = {"targets": np.array(tkeys, dtype=np.int64), "op_keys": np.array(ops.names),
+         "op_counts": np.array([ops.offsets[k][1] for k in ops.names], dtype=np.int64)}
+
+    def run(tag):
+        qms = [RefQM(num_bits=8) for _ in range(len(ops.quants))]
+        ref_lt.module_tensor_op = ref_lt.CustomTensorOP(qms, [(k, f"{k}_{ops.offsets[k][1]}") for k in ops.names])
+        try:
+            ref_lt.set_quant_minmax(graph, bottoms, verbose=False)
+            A[f"{tag}_error"] = np.array("")
+        except Exception as e:
+            A[f"{tag}_error"] = np.array(f"{type(e).__name__}: {e}")
+        mods = [graph[k].quant for k in tkeys] + qms
+        A[f"{tag}_min"] = np.array([float(q.running_min) for q in mods], dtype=np.float32)
+        A[f"{tag}_max"] = np.array([float(q.running_max) for q in mods], dtype=np.float32)
+
+    ref_merge_bn(model, graph, bottoms, TARG)
+    run("bn1")
+    ref_merge_bn(model, graph, bottoms, TARG)
+    run("bn2")
+    np.savez_compressed(HERE / f"act_ranges_{name}.npz", **A)
+    print(name, "act ranges:", len(tkeys), "layer quantizers,", len(ops.quants), "op quantizers",
+          str(A["bn1_error"]), str(A["bn2_error"]))
+
+
 def literal_bc(name="mobilenetv2"):
     """Opaque (PyTransformer-like) keys: bias_correction skips every layer (Q2)."""
     model = zoo.build(name, seed=0, relu=True)
@@ -422,5 +463,8 @@ if __name__ == "__main__":
     for m in ("mobilenetv2", "resnet50", "deeplab"):
         if m in which:
             pipeline(m, per_channel=(m == "mobilenetv2"))
+    for m in ("mobilenetv2", "resnet50", "deeplab"):
+        if "act" in which or f"act_{m}" in which:
+            act_ranges(m)
     if "literal" in which:
         print("literal bias_correction is a no-op:", literal_bc())

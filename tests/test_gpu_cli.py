@@ -24,3 +24,10 @@ def test_main_dfq_full_flags(extra, tmp_path, monkeypatch):
         if "--granularity" not in extra:   # per-tensor 8-bit grid: at most 256 distinct values
             assert torch.unique(w).numel() <= 256
     assert (tmp_path / "dfq_result.txt").read_text().startswith("task: cls")
+    # set_quant_minmax ran (main_dfq.py:217): every activation quantizer has a range;
+    # after the second BN fold the statistics are N(0, 1) -> ReLU inputs [0, 6]
+    from data_free_quantization_amd.utils import layer_transform as L
+    qs = [m.quant for m in targets] + list(L.module_tensor_op.quants)
+    assert all(float(q.running_max) > float(q.running_min) for q in qs)
+    assert float(targets[0].quant.running_max) == np.float32(2.64)
+    assert sum(float(q.running_min) == 0.0 and float(q.running_max) == 6.0 for q in qs) > 30
