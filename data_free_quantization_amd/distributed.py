@@ -68,26 +68,34 @@ def output_spec(weight: torch.Tensor, per_channel: bool, bits: int, symmetric: b
     return spec
 
 
-def _pack(outs: List[LayerOut], specs: List[Dict], device) -> torch.Tensor:
-    total = sum(nb for s in specs for (_, _, _, nb) in _layout(s))
-    buf = torch.zeros(max(total, 16), dtype=torch.uint8, device=device)
-    off = 0
+def _pack(outs: List[LayerOut], specs: List[Dict], device, cap: int = 0) -> torch.Tensor:
+    """All fields of all layers, each at a 16-B aligned offset, in ONE byte buffer
+    of max(cap, 16) bytes, written by a single concatenation kernel.  Padding and
+    the tail are never read (``_unpack`` reads each field's own bytes), so they are
+    left uninitialised."""
+    parts = []
+    total = 0
     for o, s in zip(outs, specs):
         for name, shp, dt, nb in _layout(s):
-            t = getattr(o, name).contiguous()
-            raw = t.view(-1).view(torch.uint8)
-            buf[off:off + raw.numel()].copy_(raw)
-            off += nb
+            raw = getattr(o, name).contiguous().view(-1).view(torch.uint8)
+            parts.append(raw)
+            if nb > raw.numel():
+                parts.append(torch.empty(nb - raw.numel(), dtype=torch.uint8, device=device))
+            total += nb
+    buf = torch.empty(max(cap, total, 16), dtype=torch.uint8, device=device)
+    if parts:
+        torch.cat(parts, out=buf[:total])
     return buf
 
 
 def _unpack(buf: torch.Tensor, specs: List[Dict]) -> List[LayerOut]:
+    """Views into ``buf`` (no copies): the gathered layers alias the receive buffer."""
     outs, off = [], 0
     for s in specs:
         vals = {}
         for name, shp, dt, nb in _layout(s):
             n = int(torch.Size(shp).numel()) * torch.empty(0, dtype=dt).element_size()
-            vals[name] = buf[off:off + n].clone().view(dt).view(shp)
+            vals[name] = buf[off:off + n].view(dt).view(shp)
             off += nb
         outs.append(LayerOut(**vals))
     return outs
@@ -110,11 +118,9 @@ def sharded_sweep(weights: Sequence[torch.Tensor], compute: Callable[[List[int]]
     if world == 1 or gather == "none":
         return result
     dev = weights[0].device
-    my_buf = _pack(local, [specs[i] for i in mine], dev)
     sizes_b = [sum(nb for i in p for (_, _, _, nb) in _layout(specs[i])) for p in parts]
     cap = max(max(sizes_b), 16)
-    send = torch.zeros(cap, dtype=torch.uint8, device=dev)
-    send[:my_buf.numel()].copy_(my_buf[:cap])
+    send = _pack(local, [specs[i] for i in mine], dev, cap)
     recv = torch.empty(cap * world, dtype=torch.uint8, device=dev)
     if gather == "rank0" and dist.get_backend(group) == "gloo":
         gl = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
