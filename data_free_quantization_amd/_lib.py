@@ -26,7 +26,7 @@ EXPORTS = [
     "dfq_abi_version", "dfq_error_string", "dfq_last_hip_error",
     "dfq_quantize_ws_bytes", "dfq_quantize_tensor",
     "dfq_sweep_plan_create", "dfq_sweep_plan_execute", "dfq_sweep_plan_stats", "dfq_sweep_plan_destroy",
-    "dfq_bn_fold", "dfq_clamp",
+    "dfq_bn_fold", "dfq_bn_fold_batch", "dfq_clamp",
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
     "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
@@ -50,6 +50,14 @@ class SweepStats(C.Structure):
         ("n_tensors", C.c_int64), ("n_elems", C.c_int64), ("n_tasks_reduce", C.c_int64),
         ("n_tasks_main", C.c_int64), ("algo_bytes", C.c_int64), ("launches", C.c_int32),
         ("grid_blocks", C.c_int32), ("variant", C.c_int32), ("reserved", C.c_int32),
+    ]
+
+
+class BnFoldDesc(C.Structure):
+    _fields_ = [
+        ("w", C.c_void_p), ("bias", C.c_void_p), ("bn_w", C.c_void_p), ("bn_b", C.c_void_p),
+        ("bn_mean", C.c_void_p), ("bn_var", C.c_void_p), ("fake_w", C.c_void_p), ("fake_b", C.c_void_p),
+        ("eps", C.c_float), ("reserved", C.c_int32), ("rows", C.c_int64), ("row_len", C.c_int64),
     ]
 
 
@@ -92,6 +100,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_sweep_plan_destroy": ([P], C.c_int),
         "dfq_bn_fold": ([P, P, P, P, P, P, P, P, F32, I64, I64, P], C.c_int),
         "dfq_clamp": ([P, I64, F32, F32, P], C.c_int),
+        "dfq_bn_fold_batch": ([C.POINTER(BnFoldDesc), I32, P], C.c_int),
         "dfq_cle_ws_bytes": ([I64], SZ),
         "dfq_cle_relation": ([P, P, P, P, P, I64, I64, I64, I64, I64, F64, F64, I32, F32, P, P, I32, P, SZ, P],
                              C.c_int),

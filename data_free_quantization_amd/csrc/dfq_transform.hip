@@ -283,6 +283,59 @@ __global__ void act_affine_kernel(const float* x, const float* w, const float* b
     }
 }
 
+
+// Batched BN fold: every (BN, producer layer) pair of a model in two launches.
+struct BnFoldJob {
+    float* w;
+    float* bias;
+    float* g;
+    float* b;
+    float* m;
+    float* v;
+    float* fake_w;
+    float* fake_b;
+    float eps;
+    int32_t pad;
+    int64_t rows, row_len;
+};
+struct BnFoldChunk {
+    int32_t job;
+    int32_t pad;
+    int64_t e0, e1;   // element range of the job's weight
+};
+
+__global__ void bn_fold_weight_batch_kernel(const BnFoldJob* __restrict__ jobs, const BnFoldChunk* __restrict__ chunks,
+                                            int64_t nchunks) {
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const BnFoldChunk ch = chunks[c];
+        const BnFoldJob J = jobs[ch.job];
+        for (int64_t i = ch.e0 + threadIdx.x; i < ch.e1; i += blockDim.x) {
+            const int64_t o = i / J.row_len;
+            J.w[i] = J.w[i] * bn_factor(J.g[o], J.v[o], J.eps);
+        }
+    }
+}
+
+// One block per job: the per-channel bias / fake-stat / BN-reset update (after
+// every weight has used the old BN parameters: a separate launch).
+__global__ void bn_fold_channel_batch_kernel(const BnFoldJob* __restrict__ jobs, int32_t njobs) {
+    for (int32_t j = blockIdx.x; j < njobs; j += gridDim.x) {
+        const BnFoldJob J = jobs[j];
+        for (int64_t o = threadIdx.x; o < J.rows; o += blockDim.x) {
+            const float go = J.g[o], bo = J.b[o], mo = J.m[o], vo = J.v[o];
+            const float f = bn_factor(go, vo, J.eps);
+            const float shift = bo - (go * mo) / sqrtf(vo + J.eps);
+            J.bias[o] = J.bias[o] * f + shift;
+            if (J.fake_w) J.fake_w[o] = fabsf(go);
+            if (J.fake_b) J.fake_b[o] = bo;
+            J.g[o] = 1.0f;
+            J.v[o] = 1.0f;
+            J.b[o] = 0.0f;
+            J.m[o] = 0.0f;
+        }
+    }
+}
+
 }  // namespace dfq
 
 using namespace dfq;
@@ -395,5 +448,48 @@ extern "C" int dfq_act_affine(const float* x, const float* w, const float* bias,
     hipLaunchKernelGGL(act_affine_kernel, dim3((int)std::min<int64_t>(ceil_div(o, (int64_t)4), 2048)), dim3(kThreads),
                        0, static_cast<hipStream_t>(stream), x, w, bias, o, i2, khw, o / groups, out);
     DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+extern "C" int dfq_bn_fold_batch(const dfq_bn_fold_desc* d, int32_t n, void* stream) {
+    if (n < 0 || (n > 0 && !d)) return DFQ_ERR_INVALID;
+    if (n == 0) return DFQ_OK;
+    std::vector<BnFoldJob> jobs(n);
+    std::vector<BnFoldChunk> chunks;
+    for (int32_t j = 0; j < n; ++j) {
+        const dfq_bn_fold_desc& x = d[j];
+        if (!x.w || !x.bias || !x.bn_w || !x.bn_b || !x.bn_mean || !x.bn_var || x.rows < 0 || x.row_len < 0)
+            return DFQ_ERR_INVALID;
+        for (int32_t k = 0; k < j; ++k)   // each weight folded once per call (sequential semantics otherwise)
+            if (d[k].w == x.w) return DFQ_ERR_INVALID;
+        jobs[j] = BnFoldJob{x.w, x.bias, x.bn_w, x.bn_b, x.bn_mean, x.bn_var, x.fake_w, x.fake_b, x.eps, 0, x.rows,
+                            x.row_len};
+        const int64_t ne = x.rows * x.row_len;
+        for (int64_t e = 0; e < ne; e += 8192) chunks.push_back(BnFoldChunk{j, 0, e, std::min<int64_t>(e + 8192, ne)});
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    BnFoldJob* dj = nullptr;
+    BnFoldChunk* dc = nullptr;
+    DFQ_HIP_CHECK(hipMalloc(&dj, sizeof(BnFoldJob) * n));
+    hipError_t e = hipMalloc(&dc, sizeof(BnFoldChunk) * std::max<size_t>(chunks.size(), 1));
+    if (e == hipSuccess) e = hipMemcpyAsync(dj, jobs.data(), sizeof(BnFoldJob) * n, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && !chunks.empty())
+        e = hipMemcpyAsync(dc, chunks.data(), sizeof(BnFoldChunk) * chunks.size(), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && !chunks.empty()) {
+        hipLaunchKernelGGL(bn_fold_weight_batch_kernel, dim3((int)std::min<size_t>(chunks.size(), 4096)),
+                           dim3(kThreads), 0, s, dj, dc, (int64_t)chunks.size());
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(bn_fold_channel_batch_kernel, dim3(std::min(n, 2048)), dim3(kThreads), 0, s, dj, n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);   // the tables die with this call
+    (void)hipFree(dj);
+    (void)hipFree(dc);
+    if (e != hipSuccess) {
+        set_last_hip_error(e);
+        return DFQ_ERR_HIP;
+    }
     return DFQ_OK;
 }

@@ -30,34 +30,55 @@ _LINEAR_TYPES = (nn.Linear, QLinear, QuantLinear, QuantNLinear)
 
 def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d]):
     """Fold each BatchNorm2d into the target layer feeding it, keep |gamma| and beta
-    as ``fake_weight``/``fake_bias`` buffers, and turn the BN into an identity."""
-    with torch.no_grad():
-        for layer_idx in graph:
-            if bottoms[layer_idx] is None:
+    as ``fake_weight``/``fake_bias`` buffers, and turn the BN into an identity
+    (utils/layer_transform.py:240-285).  Every fold of the model runs in one
+    ``dfq_bn_fold_batch`` call (two launches)."""
+    pairs = []
+    for layer_idx in graph:
+        if bottoms[layer_idx] is None:
+            continue
+        for bot_idx in bottoms[layer_idx]:
+            bn, layer = graph[layer_idx], graph[bot_idx]
+            if type(bn) != nn.BatchNorm2d or type(layer) not in targ_type:
                 continue
-            for bot_idx in bottoms[layer_idx]:
-                bn, layer = graph[layer_idx], graph[bot_idx]
-                if type(bn) != nn.BatchNorm2d or type(layer) not in targ_type:
-                    continue
-                w = layer.weight
-                _lib.require_device(w, bn.weight, bn.bias, bn.running_mean, bn.running_var)
-                if layer.bias is None:   # :262-263
-                    layer.bias = nn.Parameter(torch.zeros(w.size(0), dtype=torch.float32, device=w.device),
-                                              requires_grad=False)
-                fake_w = torch.empty_like(bn.weight)
-                fake_b = torch.empty_like(bn.bias)
-                rows = w.size(0)
-                rc = _lib.load().dfq_bn_fold(
-                    _lib.ptr(w), _lib.ptr(layer.bias), _lib.ptr(bn.weight), _lib.ptr(bn.bias),
-                    _lib.ptr(bn.running_mean), _lib.ptr(bn.running_var), _lib.ptr(fake_w), _lib.ptr(fake_b),
-                    float(bn.eps), rows, w.numel() // rows, _lib.stream_of(w))
-                _lib.check(rc, "dfq_bn_fold")
-                bn.register_buffer("fake_weight", fake_w)
-                bn.register_buffer("fake_bias", fake_b)
-                bn.eps = 0
-                _identity_forward_hooks(bn)
-                break
+            pairs.append((bn, layer))
+            break
+    if not pairs:
+        return model
+    # a layer feeding two BNs is folded twice in sequence by the reference: one
+    # batch call per fold then, in graph order
+    if len({id(layer.weight) for _, layer in pairs}) < len(pairs):
+        for pair in pairs:
+            _fold_batch([pair])
+    else:
+        _fold_batch(pairs)
     return model
+
+
+def _fold_batch(pairs):
+    with torch.no_grad():
+        descs = (_lib.BnFoldDesc * len(pairs))()
+        for j, (bn, layer) in enumerate(pairs):
+            w = layer.weight
+            _lib.require_device(w, bn.weight, bn.bias, bn.running_mean, bn.running_var)
+            if layer.bias is None:   # :262-263
+                layer.bias = nn.Parameter(torch.zeros(w.size(0), dtype=torch.float32, device=w.device),
+                                          requires_grad=False)
+            bn.register_buffer("fake_weight", torch.empty_like(bn.weight))
+            bn.register_buffer("fake_bias", torch.empty_like(bn.bias))
+            d = descs[j]
+            d.w, d.bias = w.data_ptr(), layer.bias.data_ptr()
+            d.bn_w, d.bn_b = bn.weight.data_ptr(), bn.bias.data_ptr()
+            d.bn_mean, d.bn_var = bn.running_mean.data_ptr(), bn.running_var.data_ptr()
+            d.fake_w, d.fake_b = bn.fake_weight.data_ptr(), bn.fake_bias.data_ptr()
+            d.eps = float(bn.eps)
+            d.rows = w.size(0)
+            d.row_len = w.numel() // w.size(0)
+        rc = _lib.load().dfq_bn_fold_batch(descs, len(pairs), _lib.stream_of(pairs[0][1].weight))
+        _lib.check(rc, "dfq_bn_fold_batch")
+        for bn, _ in pairs:
+            bn.eps = 0
+            _identity_forward_hooks(bn)
 
 
 _TINY = float(torch.finfo(torch.float32).tiny)

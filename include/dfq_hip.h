@@ -126,6 +126,24 @@ int dfq_bn_fold(float* w, float* bias, float* bn_w, float* bn_b, float* bn_mean,
                 float* fake_w, float* fake_b, float eps, int64_t rows, int64_t row_len,
                 void* stream);
 
+/* All BN folds of a model in two launches (blocking): one descriptor per
+ * (BN, producer layer) pair, each weight at most once per call; eps per BN. */
+typedef struct dfq_bn_fold_desc {
+    float* w;
+    float* bias;
+    float* bn_w;
+    float* bn_b;
+    float* bn_mean;
+    float* bn_var;
+    float* fake_w;      /* may be NULL */
+    float* fake_b;      /* may be NULL */
+    float  eps;
+    int32_t reserved;
+    int64_t rows;
+    int64_t row_len;
+} dfq_bn_fold_desc;
+int dfq_bn_fold_batch(const dfq_bn_fold_desc* descs, int32_t n, void* stream);
+
 /* ---- weight clipping (clip_weight.py:18-29): w = min(max(w, lo), hi), in place */
 int dfq_clamp(float* w, int64_t n, float lo, float hi, void* stream);
 
