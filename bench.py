@@ -237,9 +237,9 @@ def cpu_baseline(args, shapes, seconds):
             "oracle_c_1thread_GBs": gbs(p3, e3)}
 
 
-def pipeline_timing(dev):
-    """One-off: the full main_dfq stage order on one MobileNetV2 (per-channel
-    sym INT8, fused BC) on the GPU; seconds per stage (after a warm-up run)."""
+def pipeline_timing(dev, model="mobilenetv2"):
+    """One-off: the full main_dfq stage order on one model (per-channel sym INT8,
+    fused BC) on the GPU; milliseconds per stage (after a warm-up run)."""
     import torch.nn as nn
     from data_free_quantization_amd import zoo, Cross_layer_equal as cle
     from data_free_quantization_amd.pipeline import run_dfq
@@ -250,7 +250,7 @@ def pipeline_timing(dev):
     logging.getLogger("data_free_quantization_amd.bias_correction").setLevel(logging.ERROR)
     out = {}
     for rep in range(2):
-        m = zoo.build("mobilenetv2", seed=0, relu=True).to(dev)
+        m = zoo.build(model, seed=0, relu=True).to(dev)
         g = build_graph(m, "positional")
         t = {}
         t0 = time.perf_counter()
@@ -343,7 +343,7 @@ def main():
         probe = same_mix_probe(per_copy * copies, dev, stream)
         second = None if args.no_secondary else secondary_configs(dev, stream)
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
-        pipe = None if args.no_pipeline else pipeline_timing(dev)
+        pipe = None if args.no_pipeline else {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")}
         res = {
             "metric": METRIC,
             "value": round(value, 2),

@@ -44,6 +44,3 @@ for (c1, l1, o2) in [(4, 2, 3), (16, 27, 8), (64, 200, 16), (128, 128, 4), (256,
     print((c1, l1, o2), "n1", c1 * l1, "n2", o2 * c1, "weights ok", ok1, ok2, "diff", got, ref, got == ref,
           "m1", m1, "m2", m2, flush=True)
 
-# per-chunk sums for the failing size, CPU restatement
-if len(sys.argv) > 1:
-    sys.path.insert(0, "/tmp")
