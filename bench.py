@@ -145,6 +145,22 @@ def secondary_configs(dev, stream, steps=20):
     return out
 
 
+def single_model_latency(dev, stream, reps=200):
+    """ONE weight set per model (cache-resident: MobileNetV2
+    45 MB algorithmic), per-channel sym INT8 + codes + clip + BC sums; device
+    microseconds per execute() and the algorithmic GB/s that implies."""
+    from data_free_quantization_amd.sweep import SweepPlan
+    out = {}
+    for model in ("mobilenetv2", "resnet50", "deeplab"):
+        items, _, _, _ = build_batch(model, dev, copies=1, seed=5)
+        plan = SweepPlan(items)
+        ms = time_plan(plan, stream, dev, reps, 20)
+        out[model] = {"us": round(ms * 1e3, 2), "algo_GBs": round(plan.stats["algo_bytes"] / ms / 1e6, 1),
+                      "launches": plan.stats["launches"]}
+        plan.destroy()
+    return out
+
+
 def sharded_single_model(dev, stream, world, reps=20):
     """BASELINE configs[4]: ONE ResNet-50 weight set (INT4 per-channel asym +
     clip), its layer list LPT-sharded over the ranks; ms per pass with the
@@ -342,6 +358,7 @@ def main():
     if rank == 0:
         probe = same_mix_probe(per_copy * copies, dev, stream)
         second = None if args.no_secondary else secondary_configs(dev, stream)
+        single = None if args.no_secondary else single_model_latency(dev, stream)
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
         pipe = None if args.no_pipeline else {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")}
         res = {
@@ -386,6 +403,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "secondary_configs": second,
+            "single_model_latency": single,
             "sharded_single_model": sharded,
             "pipeline_ms": pipe,
             "top1_delta": None,

@@ -623,7 +623,11 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                 }
             }
         } else if (channel && d.row_len <= kChunk) {
-            const int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(kMaxRows, kChunk / d.row_len));
+            // short rows (depthwise 3x3: 9 elements) are reduced one lane per row and run
+            // the scalar path: at most one row per lane keeps such a task's latency
+            // near a vector task's (single-model sweeps are latency-bound)
+            const int64_t row_cap = d.row_len < 32 ? kWave : kMaxRows;
+            const int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(row_cap, kChunk / d.row_len));
             for (int64_t r = 0; r < d.rows; r += rpt) {
                 const int64_t nr = std::min<int64_t>(rpt, d.rows - r);
                 DevTask k{};
