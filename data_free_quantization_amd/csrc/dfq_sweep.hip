@@ -53,8 +53,12 @@ constexpr Variant kVariants[] = {
     {2048, 256, false},   // 6: variant 5, KH*KW sums specialised for 3x3 only (fewer VGPRs)
     {2048, 256, false},   // 7: variant 5, generic KH*KW sums only
     {2560, 256, false},   // 8: variant 6 with 2560-element tasks (12 waves / CU)
+    {1024, 128, false},   // 9: variant 6 with 1024-element tasks (32 waves / CU)
+    {1536, 192, false},   // 10: variant 6 with 1536-element tasks (20 waves / CU)
+    {1024, 128, true},    // 11: 1024-element tasks, next task's DMA in flight (16 waves / CU), NT
+    {1024, 128, false},   // 12: variant 9 with the generic E sums (fewer VGPRs)
 };
-constexpr int kNumVariants = 9;
+constexpr int kNumVariants = 13;
 constexpr int kDefaultVariant = 6;   // = 5 with 87 instead of 105 VGPRs (profiles/r01/ab_*_v568.json)
 
 struct alignas(16) DevTensor {
@@ -467,7 +471,7 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
         int64_t t = wave0;
         if (t < ntasks) {
             const DevTask task = tasks[t];
-            issue_task_load(tensors[task.tensor], task, wl, lane);
+            issue_task_load<NT>(tensors[task.tensor], task, wl, lane);
         }
         for (; t < ntasks; t += nwaves) {
             const DevTask task = tasks[t];
@@ -477,11 +481,11 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
             const int64_t tn = t + nwaves;
             if (tn < ntasks) {
                 const DevTask nt = tasks[tn];
-                issue_task_load(tensors[nt.tensor], nt, wl + (cur ^ 1) * CHUNK, lane);
+                issue_task_load<NT>(tensors[nt.tensor], nt, wl + (cur ^ 1) * CHUNK, lane);
             }
             float* data = wl + cur * CHUNK;
-            if (T.vec4) compute_task<MAXROWS, true>(T, task, data, ls, lmn, slot_min, slot_max, lane);
-            else compute_task<MAXROWS, false>(T, task, data, ls, lmn, slot_min, slot_max, lane);
+            if (T.vec4) compute_task<MAXROWS, true, NT, ESPEC>(T, task, data, ls, lmn, slot_min, slot_max, lane);
+            else compute_task<MAXROWS, false, NT, ESPEC>(T, task, data, ls, lmn, slot_min, slot_max, lane);
             cur ^= 1;
         }
     }
@@ -677,19 +681,6 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
     return DFQ_OK;
 }
 
-static int lds_bytes(const Variant& V) {
-    return 4 * kWavesPerBlock * ((V.prefetch ? 2 : 1) * V.chunk + 2 * V.max_rows);
-}
-
-// Persistent grid: as many blocks per CU as LDS admits (<= 8), on 256 CUs; fewer
-// if there is little work.
-static int grid_for(int64_t ntasks, const Variant& V) {
-    const int per_cu = std::max(1, std::min(8, (160 * 1024) / lds_bytes(V)));
-    const int64_t want = ceil_div(ntasks, kWavesPerBlock);
-    return (int)std::max<int64_t>(1, std::min<int64_t>(want, 256 * per_cu));
-}
-static int grid_for(int64_t ntasks) { return grid_for(ntasks, kVariants[kDefaultVariant]); }
-
 static int variant_from_env() {
     const char* e = getenv("DFQ_SWEEP_VARIANT");
     if (!e || !*e) return kDefaultVariant;
@@ -697,46 +688,55 @@ static int variant_from_env() {
     return (v >= 0 && v < kNumVariants) ? v : kDefaultVariant;
 }
 
+
+static int lds_bytes(const Variant& V) {
+    return 4 * kWavesPerBlock * ((V.prefetch ? 2 : 1) * V.chunk + 2 * V.max_rows);
+}
+
+using MainKernel = void (*)(const DevTensor*, const DevTask*, int64_t, const uint32_t*, const uint32_t*);
+
+static MainKernel main_kernel(int variant) {
+    switch (variant) {
+        case 1: return sweep_main_kernel<1024, 128, true>;
+        case 2: return sweep_main_kernel<2048, 256, true>;
+        case 3: return sweep_main_kernel<1024, 128, false>;
+        case 4: return sweep_main_kernel<4096, 256, false>;
+        case 5: return sweep_main_kernel<2048, 256, false, true>;
+        case 6: return sweep_main_kernel<2048, 256, false, true, 1>;
+        case 7: return sweep_main_kernel<2048, 256, false, true, 0>;
+        case 8: return sweep_main_kernel<2560, 256, false, true, 1>;
+        case 9: return sweep_main_kernel<1024, 128, false, true, 1>;
+        case 10: return sweep_main_kernel<1536, 192, false, true, 1>;
+        case 11: return sweep_main_kernel<1024, 128, true, true, 1>;
+        case 12: return sweep_main_kernel<1024, 128, false, true, 0>;
+        default: return sweep_main_kernel<2048, 256, false>;
+    }
+}
+
+// Grid: up to 64 blocks per CU (16384 blocks), far more than are resident (4-5
+// per CU for the sweep kernels).  Each wave's grid-stride list is then only a
+// few tasks long and the dispatcher hands CUs new blocks as old ones retire --
+// dynamic load balance over tasks of uneven cost.  Measured against resident-
+// only grids (profiles/r01/ab_grid.txt): MobileNetV2 +25 %, ResNet-50 / DeepLab
+// +4-6 %; 32-128 per CU are within a few %, fully unrolled grids (one block per
+// 4 tasks) lose 10 %.  DFQ_SWEEP_BLOCKS_PER_CU overrides (A/B).
+constexpr int kBlocksPerCu = 64;
+static int blocks_per_cu() {
+    static const int v = [] {
+        const char* e = getenv("DFQ_SWEEP_BLOCKS_PER_CU");
+        return e && *e ? std::max(1, std::min(1024, atoi(e))) : kBlocksPerCu;
+    }();
+    return v;
+}
+static int grid_for(int64_t ntasks) {
+    const int64_t want = ceil_div(ntasks, kWavesPerBlock);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(want, 256 * (int64_t)blocks_per_cu()));
+}
+static int grid_for_variant(int64_t ntasks, int) { return grid_for(ntasks); }
+
 static void launch_main(int variant, int grid, hipStream_t s, const DevTensor* t, const DevTask* k, int64_t n,
                         const uint32_t* smin, const uint32_t* smax) {
-    switch (variant) {
-        case 1:
-            hipLaunchKernelGGL((sweep_main_kernel<1024, 128, true>), dim3(grid), dim3(kBlockThreads), 0, s, t, k, n,
-                               smin, smax);
-            break;
-        case 2:
-            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, true>), dim3(grid), dim3(kBlockThreads), 0, s, t, k, n,
-                               smin, smax);
-            break;
-        case 3:
-            hipLaunchKernelGGL((sweep_main_kernel<1024, 128, false>), dim3(grid), dim3(kBlockThreads), 0, s, t, k,
-                               n, smin, smax);
-            break;
-        case 4:
-            hipLaunchKernelGGL((sweep_main_kernel<4096, 256, false>), dim3(grid), dim3(kBlockThreads), 0, s, t, k,
-                               n, smin, smax);
-            break;
-        case 6:
-            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false, true, 1>), dim3(grid), dim3(kBlockThreads), 0, s,
-                               t, k, n, smin, smax);
-            break;
-        case 7:
-            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false, true, 0>), dim3(grid), dim3(kBlockThreads), 0, s,
-                               t, k, n, smin, smax);
-            break;
-        case 8:
-            hipLaunchKernelGGL((sweep_main_kernel<2560, 256, false, true, 1>), dim3(grid), dim3(kBlockThreads), 0, s,
-                               t, k, n, smin, smax);
-            break;
-        case 5:
-            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false, true>), dim3(grid), dim3(kBlockThreads), 0, s,
-                               t, k, n, smin, smax);
-            break;
-        default:
-            hipLaunchKernelGGL((sweep_main_kernel<2048, 256, false>), dim3(grid), dim3(kBlockThreads), 0, s, t, k,
-                               n, smin, smax);
-            break;
-    }
+    hipLaunchKernelGGL(main_kernel(variant), dim3(grid), dim3(kBlockThreads), 0, s, t, k, n, smin, smax);
 }
 
 }  // namespace dfq
@@ -812,7 +812,7 @@ extern "C" int dfq_sweep_plan_execute(dfq_sweep_plan* p, void* stream) {
             DFQ_LAUNCH_CHECK();
         }
         if (p->n_main > 0) {
-            launch_main(p->variant, grid_for(p->n_main, kVariants[p->variant]), s, p->d_tensors, p->d_main, p->n_main,
+            launch_main(p->variant, grid_for_variant(p->n_main, p->variant), s, p->d_tensors, p->d_main, p->n_main,
                         p->d_slots, p->d_slots + p->n_slots);
             DFQ_LAUNCH_CHECK();
         }
@@ -829,7 +829,7 @@ extern "C" int dfq_sweep_plan_execute(dfq_sweep_plan* p, void* stream) {
         }
         const int64_t m0 = k == 0 ? 0 : p->mslab[k], m1 = p->mslab[k + 1];
         if (m1 > m0) {
-            launch_main(p->variant, grid_for(m1 - m0, kVariants[p->variant]), s, p->d_tensors, p->d_main + m0, m1 - m0,
+            launch_main(p->variant, grid_for_variant(m1 - m0, p->variant), s, p->d_tensors, p->d_main + m0, m1 - m0,
                         p->d_slots, p->d_slots + p->n_slots);
             DFQ_LAUNCH_CHECK();
         }
@@ -853,7 +853,7 @@ extern "C" int dfq_sweep_plan_stats(const dfq_sweep_plan* p, dfq_sweep_stats* st
     } else {
         st->launches = (p->n_reduce > 0 ? 1 : 0) + (p->n_main > 0 ? 1 : 0);
     }
-    st->grid_blocks = p->n_main > 0 ? grid_for(p->n_main, kVariants[p->variant]) : 0;
+    st->grid_blocks = p->n_main > 0 ? grid_for_variant(p->n_main, p->variant) : 0;
     st->variant = p->variant;
     return DFQ_OK;
 }
@@ -925,7 +925,8 @@ extern "C" int dfq_quantize_tensor(const dfq_tensor_desc* d, void* ws, size_t ws
         DFQ_LAUNCH_CHECK();
     }
     if (!B.main.empty()) {
-        launch_main(kDefaultVariant, grid_for((int64_t)B.main.size()), s, dt, dm, (int64_t)B.main.size(), slots,
+        launch_main(kDefaultVariant, grid_for_variant((int64_t)B.main.size(), kDefaultVariant), s, dt, dm,
+                    (int64_t)B.main.size(), slots,
                     slots + B.slots);
         DFQ_LAUNCH_CHECK();
     }

@@ -237,6 +237,10 @@ int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_
  * the sweep's traffic mix; not part of the reference interface. */
 int dfq_probe_stream(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t blocks,
                      void* stream);
+/* The sweep's memory pattern without arithmetic: 2048-element wave tasks through
+ * LDS-DMA, non-temporal dq / codes / E stores (copy_only: dq only).  n % 2048 == 0. */
+int dfq_probe_lds(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t copy_only,
+                  int32_t blocks, void* stream);
 
 /* ---- activation ranges from BN statistics (set_quant_minmax,
  *      utils/layer_transform.py:356-618) ---------------------------------------
