@@ -132,14 +132,20 @@ def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count,
     tp = (C.c_void_p * max(nt, 1))(*[t.data_ptr() for t in targets])
     tn = (C.c_int64 * max(nt, 1))(*[t.numel() for t in targets])
     L = _lib.load()
+    dev = targets[0].device if targets else torch.device("cuda", torch.cuda.current_device())
+    # W_prev snapshots from torch's caching allocator (no hipMalloc / hipFree per call)
+    ws_bytes = int(L.dfq_cle_plan_ws_bytes(tn, nt))
+    if ws_bytes < 0:
+        raise RuntimeError("dfq_cle_plan_ws_bytes: invalid target sizes")
+    ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=dev)
     plan = C.c_void_p()
     _lib.check(L.dfq_cle_plan_create(descs, n, tp, tn, nt, float(s_min_max[0]), float(s_min_max[1]),
-                                     int(bool(signed)), float(eps), _lib.REF_THREADS, C.byref(plan)),
+                                     int(bool(signed)), float(eps), _lib.REF_THREADS, ws.data_ptr(), ws.numel(),
+                                     C.byref(plan)),
                "dfq_cle_plan_create", RuntimeError)
     try:
         iters = C.c_int32(0)
         hist = (C.c_double * (MAX_ITERS + 1))()
-        dev = targets[0].device if targets else torch.device("cuda", torch.cuda.current_device())
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         _lib.check(L.dfq_cle_plan_run(plan, float(Treshhold), int(Count), MAX_ITERS, C.byref(iters), hist, stream),
                    "dfq_cle_plan_run")

@@ -29,7 +29,7 @@ EXPORTS = [
     "dfq_bn_fold", "dfq_bn_fold_batch", "dfq_clamp",
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
-    "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
+    "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
     "dfq_bias_absorb", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate",
     "dfq_probe_stream", "dfq_probe_lds",
     "dfq_act_moments", "dfq_act_minmax", "dfq_act_affine",
@@ -108,8 +108,9 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_diff_plan_snapshot": ([P, P], C.c_int),
         "dfq_diff_plan_execute": ([P, C.POINTER(F64), P], C.c_int),
         "dfq_diff_plan_destroy": ([P], C.c_int),
+        "dfq_cle_plan_ws_bytes": ([C.POINTER(I64), I32], C.c_int64),
         "dfq_cle_plan_create": ([C.POINTER(CleRel), I32, C.POINTER(P), C.POINTER(I64), I32, F64, F64, I32, F32, I32,
-                                 C.POINTER(P)], C.c_int),
+                                 P, I64, C.POINTER(P)], C.c_int),
         "dfq_cle_plan_run": ([P, F64, I32, I32, C.POINTER(I32), C.POINTER(F64), P], C.c_int),
         "dfq_cle_plan_info": ([P, C.POINTER(I32), C.POINTER(I32), C.POINTER(I32)], C.c_int),
         "dfq_cle_plan_destroy": ([P], C.c_int),

@@ -118,6 +118,19 @@ def _error_sums(weight, bits, signed, precomputed=None):
     return r.esum.view(o, i2), o, i2
 
 
+def _snapshot(tensors):
+    """{name: t.clone()} as views of ONE buffer filled by one concatenation."""
+    if not tensors:
+        return {}
+    vals = list(tensors.values())
+    flat = torch.cat([t.reshape(-1) for t in vals])
+    out, off = {}, 0
+    for name, t in tensors.items():
+        out[name] = flat[off:off + t.numel()].view(t.shape)
+        off += t.numel()
+    return out
+
+
 def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.BatchNorm2d, signed=False, *,
                     error_sums=None):
     """Returns (bias_before_correction, bias_after_correction) keyed "layer_<idx>".
@@ -133,15 +146,19 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
     bias = None             # persists across layers like the reference's local
     before, after = {}, {}
     keys = list(graph.keys())
+    after_src = {}
     with torch.no_grad():
+        # The walk only writes the bias of the layer it is on, after recording it, so
+        # every "before" value is the bias at entry: one batched copy instead of a
+        # clone per layer (and likewise for "after", at the end).
+        before = _snapshot({f"layer_{i}": l.bias.data for i, l in enumerate(graph.values())
+                            if i in bottoms and isinstance(l, targ_type) and getattr(l, "bias", None) is not None})
         for idx_layer, layer in enumerate(graph.values()):
             layer_name = f"layer_{idx_layer}"
             if idx_layer not in bottoms:
                 logger.warning(f"Layer index {idx_layer} not found in bottoms")
                 continue
             bot = bottoms[idx_layer]
-            if isinstance(layer, targ_type) and getattr(layer, "bias", None) is not None:
-                before[layer_name] = layer.bias.data.clone()
             if bot is None or bot[0] == "Data":
                 continue
             node = graph[idx_layer]
@@ -178,6 +195,7 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                     raise UnboundLocalError("local variable 'bias' referenced before assignment")
                 bias_prev = bias
                 if getattr(layer, "bias", None) is not None:
-                    after[layer_name] = layer.bias.data.clone()
+                    after_src[layer_name] = layer.bias.data
+        after = _snapshot(after_src)
     logger.info("Bias correction completed.")
     return before, after

@@ -15,9 +15,12 @@
 #include "dfq_common.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
 #include <new>
 #include <numeric>
 #include <vector>
@@ -481,8 +484,13 @@ __device__ __forceinline__ void wave_range(const float* __restrict__ p, int64_t 
     vmax = wave_max(vmax);
 }
 
-// p[0..n) *= f, one wave; 4 loads in flight per lane before the stores
-__device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, bool vec, float f, int lane) {
+// p[0..n) *= f(), one wave; 4 loads in flight per lane before the stores.  The
+// factor (range-table reads) is evaluated after the first loads are issued, so
+// the data and the range words are one memory round trip, not two.
+template <class F>
+__device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, bool vec, int lane, F&& factor) {
+    float f = 0.f;
+    bool have = false;
     if (vec) {
         float4* p4 = reinterpret_cast<float4*>(p);
         const int64_t n4 = n >> 2;
@@ -491,6 +499,10 @@ __device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, boo
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (i + 64 * u < n4) v[u] = p4[i + 64 * u];
+            if (!have) {
+                f = factor();
+                have = true;
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (i + 64 * u < n4) {
@@ -507,6 +519,10 @@ __device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, boo
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (i + 64 * u < n) v[u] = p[i + 64 * u];
+            if (!have) {
+                f = factor();
+                have = true;
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (i + 64 * u < n) p[i + 64 * u] = v[u] * f;
@@ -514,14 +530,22 @@ __device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, boo
     }
 }
 
-// p[0..n) *= f and the (min, max) of the products, one wave (scalar loads:
-// used for short depthwise rows)
-__device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t n, float f, int lane, float& vmin,
-                                                 float& vmax) {
+// p[0..n) *= f() and the (min, max) of the products, one wave (scalar loads:
+// used for short depthwise rows); the factor is read after the first load
+template <class F>
+__device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t n, int lane, float& vmin, float& vmax,
+                                                 F&& factor) {
     vmin = INFINITY;
     vmax = -INFINITY;
+    float f = 0.f;
+    bool have = false;
     for (int64_t i = lane; i < n; i += 64) {
-        const float y = p[i] * f;
+        const float x = p[i];
+        if (!have) {
+            f = factor();
+            have = true;
+        }
+        const float y = x * f;
         p[i] = y;
         vmin = fminf(vmin, y);
         vmax = fmaxf(vmax, y);
@@ -530,9 +554,69 @@ __device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t 
     vmax = wave_max(vmax);
 }
 
+// W2 row tiles with KH*KW = khw in (1, kTileMaxKhw] and one group: thread t owns
+// the tile's flattened positions p = t + 256 m (m < khw) -- consecutive threads
+// on consecutive floats, khw independent loads per row in flight -- instead of
+// one thread per column walking its khw floats serially.
+constexpr int kTileMaxKhw = 9;   // 3x3 (and 2x2); larger kernels keep the per-column walk
+
+__device__ __forceinline__ bool tile_by_position(const CleRel& R, const CleTask& tk) {
+    return R.khw2 > 1 && R.khw2 <= kTileMaxKhw && (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
+}
+
+// Column ranges of the tile: per-position (min, max) over its rows, then over each
+// column's khw positions through LDS (tl: 2 * kThreads * kTileMaxKhw floats).
+__device__ void tile_range_by_position(const CleRel& R, const CleTask& tk, uint32_t* __restrict__ mn,
+                                       uint32_t* __restrict__ mx, float* __restrict__ tl) {
+    const int t = threadIdx.x;
+    const int khw = (int)R.khw2;
+    const int64_t rowlen = R.i2 * R.khw2;
+    const int ncol = (int)(tk.c1 - tk.c0);
+    const int npos = ncol * khw;
+    const float* base = R.w2 + tk.c0 * R.khw2;
+    float vmn[kTileMaxKhw], vmx[kTileMaxKhw];
+#pragma unroll
+    for (int m = 0; m < kTileMaxKhw; ++m) {
+        vmn[m] = INFINITY;
+        vmx[m] = -INFINITY;
+    }
+    for (int64_t o = tk.a; o < tk.b; ++o) {
+        const float* rp = base + o * rowlen;
+        float v[kTileMaxKhw];
+#pragma unroll
+        for (int m = 0; m < kTileMaxKhw; ++m)
+            if (m < khw && t + kThreads * m < npos) v[m] = rp[t + kThreads * m];
+#pragma unroll
+        for (int m = 0; m < kTileMaxKhw; ++m)
+            if (m < khw && t + kThreads * m < npos) {
+                vmn[m] = fminf(vmn[m], v[m]);
+                vmx[m] = fmaxf(vmx[m], v[m]);
+            }
+    }
+#pragma unroll
+    for (int m = 0; m < kTileMaxKhw; ++m)
+        if (m < khw && t + kThreads * m < npos) {
+            tl[t + kThreads * m] = vmn[m];
+            tl[kThreads * kTileMaxKhw + t + kThreads * m] = vmx[m];
+        }
+    __syncthreads();
+    if (t < ncol) {
+        float a = INFINITY, b = -INFINITY;
+        for (int k = 0; k < khw; ++k) {
+            a = fminf(a, tl[t * khw + k]);
+            b = fmaxf(b, tl[kThreads * kTileMaxKhw + t * khw + k]);
+        }
+        const int64_t c = R.c1 + (tk.a / R.o2g) * R.i2 + tk.c0 + t;
+        atomicMin(&mn[c], enc_ord(a));
+        atomicMax(&mx[c], enc_ord(b));
+    }
+    __syncthreads();   // tl is reused by the next task
+}
+
 __global__ void __launch_bounds__(kThreads)
 cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
                       uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st) {
+    __shared__ float tl[2 * kThreads * kTileMaxKhw];
     if (st->done) return;
     const int par = st->iters & 1;
     uint32_t* mins = rng + (int64_t)par * 2 * M;
@@ -566,6 +650,10 @@ cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
                 }
             }
         } else if (tk.kind == kRangeW2Tile) {   // rows [a, b) of W2, one thread per column
+            if (tile_by_position(R, tk)) {
+                tile_range_by_position(R, tk, mn, mx, tl);
+                continue;
+            }
             const int64_t rowlen = R.i2 * R.khw2;
             const bool one_group = (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
             for (int64_t i = tk.c0 + threadIdx.x; i < tk.c1; i += kThreads) {
@@ -622,6 +710,8 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
                       uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
                       float eps, double smin, double smax) {
     __shared__ float red[2][kThreads / 64][kColTileRows];
+    __shared__ float inv_s[kThreads];
+    __shared__ float inv_pos[kThreads * kTileMaxKhw];
     if (st->done) return;
     const int par = st->iters & 1;
     const bool first_iter = st->iters == 0;
@@ -636,43 +726,114 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
         const uint32_t* mx = maxs + R.moff;
         if (tk.kind == kApplyW1) {   // W1[c, :] *= s[c], one wave per row
             for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
-                const CleScale cs = cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax);
-                wave_scale(R.w1 + c * R.len1, R.len1, R.vec1, cs.s, lane);
+                wave_scale(R.w1 + c * R.len1, R.len1, R.vec1, lane,
+                           [&] { return cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax).s; });
             }
         } else if (tk.kind == kApplyW2Contig) {   // W2 channel segment *= 1/s[c]
             const int64_t seg = R.o2g * R.khw2;
             for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
-                const CleScale cs = cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax);
+                auto inv = [&] { return cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax).inv; };
                 if (R.fuse_next >= 0) {   // o2g == 1: the segment is row c of W2 = row c of the next W1
                     float vmin, vmax;
-                    wave_scale_range(R.w2 + c * seg, seg, cs.inv, lane, vmin, vmax);
+                    wave_scale_range(R.w2 + c * seg, seg, lane, vmin, vmax, inv);
                     if (lane == 0) {
                         const int64_t off = rels[R.fuse_next].moff;
                         mins[off + c] = enc_ord(vmin);
                         maxs[off + c] = enc_ord(vmax);
                     }
                 } else {
-                    wave_scale(R.w2 + c * seg, seg, R.vec2, cs.inv, lane);
+                    wave_scale(R.w2 + c * seg, seg, R.vec2, lane, inv);
                 }
             }
+        } else if (tk.kind == kApplyW2Tile && tile_by_position(R, tk)) {
+            // position-parallel tile (KH*KW > 1): the columns' 1/s into LDS, then each
+            // row's positions scaled; fused: the rows' (min, max) for the next W1
+            const int t = threadIdx.x;
+            const int khw = (int)R.khw2;
+            const int64_t rowlen = R.i2 * R.khw2;
+            const int ncol = (int)(tk.c1 - tk.c0);
+            const int npos = ncol * khw;
+            float* base = R.w2 + tk.c0 * R.khw2;
+            const bool fuse = R.fuse_next >= 0;
+            if (t < ncol)
+                inv_s[t] = cle_scale(mn, mx, R.c1, (tk.a / R.o2g) * R.i2 + tk.c0 + t, is_signed, eps, smin, smax).inv;
+            __syncthreads();
+            for (int q = t; q < npos; q += kThreads) inv_pos[q] = inv_s[q / khw];   // 1/s per position
+            __syncthreads();
+            for (int64_t o = tk.a; o < tk.b; ++o) {
+                float* rp = base + o * rowlen;
+                float v[kTileMaxKhw];
+#pragma unroll
+                for (int m = 0; m < kTileMaxKhw; ++m)
+                    if (m < khw && t + kThreads * m < npos) v[m] = rp[t + kThreads * m];
+                float lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+                for (int m = 0; m < kTileMaxKhw; ++m)
+                    if (m < khw && t + kThreads * m < npos) {
+                        const float y = v[m] * inv_pos[t + kThreads * m];
+                        rp[t + kThreads * m] = y;
+                        lo = fminf(lo, y);
+                        hi = fmaxf(hi, y);
+                    }
+                if (fuse) {
+                    lo = wave_min(lo);
+                    hi = wave_max(hi);
+                    if (lane == 0) {
+                        red[0][wv][o - tk.a] = lo;
+                        red[1][wv][o - tk.a] = hi;
+                    }
+                }
+            }
+            __syncthreads();
+            if (fuse && t < tk.b - tk.a) {
+                float a = red[0][0][t], b = red[1][0][t];
+                for (int w = 1; w < kThreads / 64; ++w) {
+                    a = fminf(a, red[0][w][t]);
+                    b = fmaxf(b, red[1][w][t]);
+                }
+                const int64_t off = rels[R.fuse_next].moff + tk.a + t;
+                atomicMin(&mins[off], enc_ord(a));
+                atomicMax(&maxs[off], enc_ord(b));
+            }
+            __syncthreads();   // inv_s / red are reused by the next task
         } else if (tk.kind == kApplyW2Tile && R.fuse_next >= 0) {
             // rows [a, b) x columns [c0, c0 + 256) of W2, one thread per column, and the
             // tile's per-row (min, max) of the results -> the next relation's W1 rows
+            // (each row's wave reduction in uniform control flow: no per-row arrays)
             const int64_t rowlen = R.i2 * R.khw2;
             const int64_t i = tk.c0 + threadIdx.x;
-            float rmn[kColTileRows], rmx[kColTileRows];
+            const bool act = i < tk.c1;
+            const bool one_group = (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
+            const int nr = (int)(tk.b - tk.a);
+            if (one_group && R.khw2 == 1) {   // 1x1 / Linear: the column's loads first
+                float v[kColTileRows];
 #pragma unroll
-            for (int j = 0; j < kColTileRows; ++j) {
-                rmn[j] = INFINITY;
-                rmx[j] = -INFINITY;
-            }
-            if (i < tk.c1) {
-                int64_t g_prev = -1;
-                float inv = 0.f;
+                for (int j = 0; j < kColTileRows; ++j)
+                    if (act && j < nr) v[j] = R.w2[(tk.a + j) * rowlen + i];
+                const float inv =
+                    act ? cle_scale(mn, mx, R.c1, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin, smax).inv : 0.f;
 #pragma unroll
                 for (int j = 0; j < kColTileRows; ++j) {
+                    if (j < nr) {   // uniform
+                        float y = 0.f;
+                        if (act) {
+                            y = v[j] * inv;
+                            R.w2[(tk.a + j) * rowlen + i] = y;
+                        }
+                        const float a = wave_min(act ? y : INFINITY), b = wave_max(act ? y : -INFINITY);
+                        if (lane == 0) {
+                            red[0][wv][j] = a;
+                            red[1][wv][j] = b;
+                        }
+                    }
+                }
+            } else {
+                int64_t g_prev = -1;
+                float inv = 0.f;
+                for (int j = 0; j < nr; ++j) {
                     const int64_t o = tk.a + j;
-                    if (o < tk.b) {
+                    float lo = INFINITY, hi = -INFINITY;
+                    if (act) {
                         const int64_t g = o / R.o2g;
                         if (g != g_prev) {
                             inv = cle_scale(mn, mx, R.c1, g * R.i2 + i, is_signed, eps, smin, smax).inv;
@@ -682,18 +843,15 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
                         for (int64_t k = 0; k < R.khw2; ++k) {
                             const float y = p[k] * inv;
                             p[k] = y;
-                            rmn[j] = fminf(rmn[j], y);
-                            rmx[j] = fmaxf(rmx[j], y);
+                            lo = fminf(lo, y);
+                            hi = fmaxf(hi, y);
                         }
                     }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < kColTileRows; ++j) {
-                const float a = wave_min(rmn[j]), b = wave_max(rmx[j]);
-                if (lane == 0) {
-                    red[0][wv][j] = a;
-                    red[1][wv][j] = b;
+                    const float a = wave_min(lo), b = wave_max(hi);
+                    if (lane == 0) {
+                        red[0][wv][j] = a;
+                        red[1][wv][j] = b;
+                    }
                 }
             }
             __syncthreads();
@@ -714,12 +872,12 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
             const bool one_group = (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
             for (int64_t i = tk.c0 + threadIdx.x; i < tk.c1; i += kThreads) {
                 if (one_group && R.khw2 == 1) {   // 1x1 / Linear: the tile's column, loads first
-                    const float inv = cle_scale(mn, mx, R.c1, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin,
-                                                smax).inv;
                     float v[kColTileRows];
 #pragma unroll
                     for (int j = 0; j < kColTileRows; ++j)
                         if (tk.a + j < tk.b) v[j] = R.w2[(tk.a + j) * rowlen + i];
+                    const float inv = cle_scale(mn, mx, R.c1, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin,
+                                                smax).inv;
 #pragma unroll
                     for (int j = 0; j < kColTileRows; ++j)
                         if (tk.a + j < tk.b) R.w2[(tk.a + j) * rowlen + i] = v[j] * inv;
@@ -1012,6 +1170,8 @@ __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32
 
 }  // namespace dfq
 
+constexpr int32_t kCleHistCap = 1025;   // per-iteration diffs kept in the plan's tables
+
 struct dfq_cle_plan {
     CleRel* d_rels = nullptr;
     CleTask* d_rtasks = nullptr;
@@ -1024,10 +1184,9 @@ struct dfq_cle_plan {
     double* d_hist = nullptr;
     int32_t hist_cap = 0;
     CleState* d_state = nullptr;
-    CleState* h_state = nullptr;    // pinned
-    hipStream_t st = nullptr;       // the loop's stream
+    CleState* h_state = nullptr;    // pinned (the device context's, set by run)
+    hipStream_t st = nullptr;       // the loop's stream (the device context's)
     hipGraphExec_t gexec = nullptr; // kCleBatch iterations
-    std::vector<float*> snaps;
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
     int64_t M = 0, nchunks = 0;
     int32_t nl = 0, chains = 0, steps = 0;
@@ -1040,33 +1199,77 @@ struct dfq_cle_plan {
     double smin = 1e-8, smax = 1e8;
     int32_t is_signed = 0;
     float eps = 0.f;
+    void* d_tables = nullptr;       // every device table above but d_hist: ONE allocation
+    void* d_snap_owned = nullptr;   // snapshots when the caller passed no workspace
+    double* d_hist_owned = nullptr; // history beyond kCleHistCap iterations
 };
 
+// DFQ_CLE_TIMING: host-side phase times of create / run / destroy on stderr.
+static bool cle_timing() {
+    static const bool on = getenv("DFQ_CLE_TIMING") != nullptr;
+    return on;
+}
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Per-device loop stream and pinned state word, shared by every plan of the
+// process (creating and destroying them per call cost ~0.6 ms); plan_run holds
+// the device's lock while it uses them.
+struct CleDeviceCtx {
+    std::mutex mu;
+    hipStream_t st = nullptr;
+    CleState* h_state = nullptr;
+};
+static CleDeviceCtx& cle_device_ctx(int dev) {
+    static CleDeviceCtx ctx[64];
+    return ctx[dev & 63];
+}
+
 static void cle_plan_free(dfq_cle_plan* p) {
-    (void)hipFree(p->d_rels); (void)hipFree(p->d_rtasks); (void)hipFree(p->d_atasks); (void)hipFree(p->d_layers);
-    (void)hipFree(p->d_chunks); (void)hipFree(p->d_rng); (void)hipFree(p->d_part); (void)hipFree(p->d_means);
-    (void)hipFree(p->d_hist); (void)hipFree(p->d_state); (void)hipFree(p->d_units); (void)hipFree(p->d_b1off);
-    (void)hipFree(p->d_b1); (void)hipFree(p->d_tail);
-    if (p->h_state) (void)hipHostFree(p->h_state);
-    for (float* s : p->snaps) (void)hipFree(s);
+    const double t0 = now_us();
+    (void)hipFree(p->d_tables);
+    (void)hipFree(p->d_snap_owned);
+    (void)hipFree(p->d_hist_owned);
+    const double t1 = now_us();
     if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
-    if (p->st) (void)hipStreamDestroy(p->st);
+    const double t2 = now_us();
+    if (cle_timing()) fprintf(stderr, "DFQ_CLE_TIMING free: device %.1f us, graph %.1f\n", t1 - t0, t2 - t1);
     delete p;
 }
 
-template <typename T>
-static hipError_t upload(T** dst, const std::vector<T>& v) {
-    hipError_t e = hipMalloc(dst, sizeof(T) * std::max<size_t>(v.size(), 1));
-    if (e != hipSuccess) return e;
-    if (!v.empty()) e = hipMemcpy(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice);
-    return e;
+static int64_t snap_bytes(int64_t n) { return ceil_div(n * (int64_t)sizeof(float), (int64_t)256) * 256; }
+
+// Byte layout of the plan's device tables (one allocation, one host->device copy).
+struct TableLayout {
+    int64_t total = 0;
+    template <typename T>
+    int64_t add(int64_t count) {
+        const int64_t off = total;
+        total += ceil_div((int64_t)sizeof(T) * std::max<int64_t>(count, 1), (int64_t)256) * 256;
+        return off;
+    }
+};
+
+extern "C" int64_t dfq_cle_plan_ws_bytes(const int64_t* target_n, int32_t n_targets) {
+    if (n_targets < 0 || (n_targets > 0 && !target_n)) return -1;
+    int64_t b = 0;
+    for (int32_t l = 0; l < n_targets; ++l) {
+        if (target_n[l] < 0) return -1;
+        b += snap_bytes(target_n[l]);
+    }
+    return b;
 }
 
 extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
                                    const int64_t* target_n, int32_t n_targets, double s_min, double s_max,
-                                   int32_t is_signed, float eps, int32_t ref_threads, dfq_cle_plan** out) {
+                                   int32_t is_signed, float eps, int32_t ref_threads, void* ws, int64_t ws_bytes,
+                                   dfq_cle_plan** out) {
     if (!out || n_rel < 0 || n_targets < 0 || (n_rel > 0 && !rels) || (n_targets > 0 && (!targets || !target_n)))
         return DFQ_ERR_INVALID;
+    const int64_t need_ws = dfq_cle_plan_ws_bytes(target_n, n_targets);
+    if (need_ws < 0) return DFQ_ERR_INVALID;
+    if (ws && (ws_bytes < need_ws || reinterpret_cast<uintptr_t>(ws) % 256 != 0)) return DFQ_ERR_INVALID;
     *out = nullptr;
     // relations: shapes as dfq_cle_relation
     std::vector<CleRel> R(n_rel);
@@ -1216,13 +1419,18 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     std::vector<CleUnit> units;
     std::vector<int64_t> b1off;
     int64_t nb1_total = 0;
+    char* snap_base = static_cast<char*>(ws);
+    if (!snap_base && need_ws > 0) {   // no caller workspace: the plan owns its snapshots
+        hipError_t e = hipMalloc(&p->d_snap_owned, need_ws);
+        if (e != hipSuccess) { set_last_hip_error(e); cle_plan_free(p); return DFQ_ERR_HIP; }
+        snap_base = static_cast<char*>(p->d_snap_owned);
+    }
+    int64_t snap_off = 0;
     for (int32_t l = 0; l < n_targets; ++l) {
         const int64_t n = target_n[l];
         if (!targets[l] || n <= 0) { cle_plan_free(p); return DFQ_ERR_INVALID; }
-        float* snap = nullptr;
-        hipError_t e = hipMalloc(&snap, sizeof(float) * n);
-        if (e != hipSuccess) { set_last_hip_error(e); cle_plan_free(p); return DFQ_ERR_HIP; }
-        p->snaps.push_back(snap);
+        float* snap = reinterpret_cast<float*>(snap_base + snap_off);
+        snap_off += snap_bytes(n);
         layers[l] = CleLayer{targets[l], snap, n};
         int64_t nt = 1;
         if (n >= 32768 && ref_threads > 1) nt = std::min<int64_t>(ref_threads, ceil_div(n, (int64_t)32768));
@@ -1255,22 +1463,47 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->smin = s_min; p->smax = s_max; p->is_signed = is_signed; p->eps = eps;
     hipError_t e;
     auto fail = [&](hipError_t err) { set_last_hip_error(err); cle_plan_free(p); return DFQ_ERR_HIP; };
-    if ((e = upload(&p->d_rels, R)) != hipSuccess) return fail(e);
-    if ((e = upload(&p->d_rtasks, rt)) != hipSuccess) return fail(e);
-    if ((e = upload(&p->d_atasks, at)) != hipSuccess) return fail(e);
-    if ((e = upload(&p->d_layers, layers)) != hipSuccess) return fail(e);
-    if ((e = upload(&p->d_chunks, chunks)) != hipSuccess) return fail(e);
-    if ((e = upload(&p->d_units, units)) != hipSuccess) return fail(e);
-    if ((e = upload(&p->d_b1off, b1off)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&p->d_b1, sizeof(float) * 32 * std::max<int64_t>(nb1_total, 1))) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&p->d_tail, sizeof(float) * kCleTailWords * std::max<int64_t>((int64_t)chunks.size(), 1))) !=
-        hipSuccess)
-        return fail(e);
-    if ((e = hipMalloc(&p->d_rng, sizeof(uint32_t) * 4 * std::max<int64_t>(M, 1))) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&p->d_part, sizeof(float) * 8 * std::max(n_targets, 1))) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&p->d_means, sizeof(double) * std::max(n_targets, 1))) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&p->d_state, sizeof(CleState))) != hipSuccess) return fail(e);
-    if ((e = hipHostMalloc(&p->h_state, sizeof(CleState))) != hipSuccess) return fail(e);
+    // every table in one allocation; the host-built ones in one copy
+    TableLayout T;
+    const int64_t o_rels = T.add<CleRel>((int64_t)R.size());
+    const int64_t o_rt = T.add<CleTask>((int64_t)rt.size());
+    const int64_t o_at = T.add<CleTask>((int64_t)at.size());
+    const int64_t o_layers = T.add<CleLayer>((int64_t)layers.size());
+    const int64_t o_chunks = T.add<CleChunk>((int64_t)chunks.size());
+    const int64_t o_units = T.add<CleUnit>((int64_t)units.size());
+    const int64_t o_b1off = T.add<int64_t>((int64_t)b1off.size());
+    const int64_t host_bytes = T.total;   // the tables above are built on the host
+    const int64_t o_b1 = T.add<float>(32 * nb1_total);
+    const int64_t o_tail = T.add<float>(kCleTailWords * (int64_t)chunks.size());
+    const int64_t o_rng = T.add<uint32_t>(4 * M);
+    const int64_t o_part = T.add<float>(8 * (int64_t)n_targets);
+    const int64_t o_means = T.add<double>(n_targets);
+    const int64_t o_state = T.add<CleState>(1);
+    const int64_t o_hist = T.add<double>(kCleHistCap);
+    if ((e = hipMalloc(&p->d_tables, T.total)) != hipSuccess) return fail(e);
+    char* base = static_cast<char*>(p->d_tables);
+    std::vector<char> blob(host_bytes, 0);
+    auto put = [&](int64_t off, const auto& v) {
+        if (!v.empty()) std::memcpy(blob.data() + off, v.data(), sizeof(v[0]) * v.size());
+    };
+    put(o_rels, R); put(o_rt, rt); put(o_at, at); put(o_layers, layers); put(o_chunks, chunks); put(o_units, units);
+    put(o_b1off, b1off);
+    if ((e = hipMemcpy(base, blob.data(), host_bytes, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    p->d_rels = reinterpret_cast<CleRel*>(base + o_rels);
+    p->d_rtasks = reinterpret_cast<CleTask*>(base + o_rt);
+    p->d_atasks = reinterpret_cast<CleTask*>(base + o_at);
+    p->d_layers = reinterpret_cast<CleLayer*>(base + o_layers);
+    p->d_chunks = reinterpret_cast<CleChunk*>(base + o_chunks);
+    p->d_units = reinterpret_cast<CleUnit*>(base + o_units);
+    p->d_b1off = reinterpret_cast<int64_t*>(base + o_b1off);
+    p->d_b1 = reinterpret_cast<float*>(base + o_b1);
+    p->d_tail = reinterpret_cast<float*>(base + o_tail);
+    p->d_rng = reinterpret_cast<uint32_t*>(base + o_rng);
+    p->d_part = reinterpret_cast<float*>(base + o_part);
+    p->d_means = reinterpret_cast<double*>(base + o_means);
+    p->d_state = reinterpret_cast<CleState*>(base + o_state);
+    p->d_hist = reinterpret_cast<double*>(base + o_hist);
+    p->hist_cap = kCleHistCap;
     *out = p;
     return DFQ_OK;
 }
@@ -1319,12 +1552,24 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     // The loop runs on the plan's own stream (graph capture needs a non-default
     // stream): wait for the caller's producers first; the call is blocking.
     DFQ_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-    if (!p->st) DFQ_HIP_CHECK(hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking));
+    int dev = 0;
+    DFQ_HIP_CHECK(hipGetDevice(&dev));
+    CleDeviceCtx& ctx = cle_device_ctx(dev);
+    std::lock_guard<std::mutex> lock(ctx.mu);
+    if (!ctx.st) DFQ_HIP_CHECK(hipStreamCreateWithFlags(&ctx.st, hipStreamNonBlocking));
+    if (!ctx.h_state) DFQ_HIP_CHECK(hipHostMalloc(&ctx.h_state, sizeof(CleState)));
+    if (p->st && p->st != ctx.st && p->gexec) {   // captured on another device's stream: recapture
+        (void)hipGraphExecDestroy(p->gexec);
+        p->gexec = nullptr;
+    }
+    p->st = ctx.st;
+    p->h_state = ctx.h_state;
     hipStream_t s = p->st;
     if (p->hist_cap < max_iters + 1) {
-        (void)hipFree(p->d_hist);
-        p->d_hist = nullptr;
-        DFQ_HIP_CHECK(hipMalloc(&p->d_hist, sizeof(double) * (max_iters + 1)));
+        (void)hipFree(p->d_hist_owned);
+        p->d_hist_owned = nullptr;
+        DFQ_HIP_CHECK(hipMalloc(&p->d_hist_owned, sizeof(double) * (max_iters + 1)));
+        p->d_hist = p->d_hist_owned;
         p->hist_cap = max_iters + 1;
         if (p->gexec) {   // captured with the old history pointer
             (void)hipGraphExecDestroy(p->gexec);
@@ -1356,6 +1601,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     // once: the stop rule lives in d_state); DFQ_CLE_GRAPH=0: eager launches.
     const char* ge = getenv("DFQ_CLE_GRAPH");
     const bool use_graph = !(ge && ge[0] == '0');
+    const double tc0 = now_us();
     if (use_graph && !p->gexec && !init.done) {
         DFQ_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         int rc = DFQ_OK;
@@ -1371,6 +1617,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         (void)hipGraphDestroy(g);
         DFQ_HIP_CHECK(ei);
     }
+    const double tc1 = now_us();
     int32_t launched = 0;
     while (!init.done) {
         if (use_graph) {
@@ -1388,6 +1635,9 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         if (launched >= max_iters) break;
     }
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
+    if (cle_timing())
+        fprintf(stderr, "DFQ_CLE_TIMING run: capture+instantiate %.1f us, loop %.1f us (%d iterations launched)\n",
+                tc1 - tc0, now_us() - tc1, launched);
     const CleState fin = *p->h_state;
     if (getenv("DFQ_CLE_DEBUG")) {   // per-layer chunk sums of the last iteration run
         std::vector<float> part(8 * std::max(p->nl, 1));

@@ -185,13 +185,20 @@ typedef struct dfq_cle_rel {
     int32_t reserved;
 } dfq_cle_rel;
 typedef struct dfq_cle_plan dfq_cle_plan;
+/* Workspace bytes for the plan's weight snapshots (the `W_prev` of :83,107):
+ * one fp32 copy of every target, each 256-B aligned; -1 on bad arguments. */
+int64_t dfq_cle_plan_ws_bytes(const int64_t* target_n, int32_t n_targets);
 /* targets: the weights of every Target_list layer in graph order (the diff list of
  * :107); ref_threads: torch's intra-op thread count whose fp32 mean order the
  * metric reproduces. Relations touching a common tensor keep their order; the
- * others run concurrently (bit-identical: they commute). */
+ * others run concurrently (bit-identical: they commute).
+ * ws: caller-owned device workspace of >= dfq_cle_plan_ws_bytes bytes, 256-B
+ * aligned, alive until destroy (e.g. from the framework's caching allocator), or
+ * NULL: the plan allocates it. */
 int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
                         const int64_t* target_n, int32_t n_targets, double s_min, double s_max,
-                        int32_t is_signed, float eps, int32_t ref_threads, dfq_cle_plan** plan);
+                        int32_t is_signed, float eps, int32_t ref_threads, void* ws, int64_t ws_bytes,
+                        dfq_cle_plan** plan);
 /* Runs the loop `while diff > threshold and iter_count < count` (at most
  * max_iters iterations); blocking.  iterations = iterations run; diffs[i] (room for
  * max_iters doubles, may be NULL) = the per-iteration diff (np.sum of the list). */
