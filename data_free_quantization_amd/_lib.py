@@ -25,8 +25,9 @@ DFQ_ERR_NOMEM, DFQ_ERR_SHAPE, DFQ_ERR_WORKSPACE = -4, -5, -6
 EXPORTS = [
     "dfq_abi_version", "dfq_error_string", "dfq_last_hip_error",
     "dfq_quantize_ws_bytes", "dfq_quantize_tensor",
-    "dfq_sweep_plan_create", "dfq_sweep_plan_execute", "dfq_sweep_plan_stats", "dfq_sweep_plan_destroy",
-    "dfq_bn_fold", "dfq_bn_fold_batch", "dfq_clamp",
+    "dfq_sweep_plan_create", "dfq_sweep_plan_ws_bytes", "dfq_sweep_plan_create_ws", "dfq_sweep_plan_execute",
+    "dfq_sweep_plan_stats", "dfq_sweep_plan_destroy",
+    "dfq_bn_fold", "dfq_bn_fold_ws_bytes", "dfq_bn_fold_batch", "dfq_clamp",
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
     "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
@@ -95,12 +96,15 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_quantize_ws_bytes": ([C.POINTER(TensorDesc), C.POINTER(SZ)], C.c_int),
         "dfq_quantize_tensor": ([C.POINTER(TensorDesc), P, SZ, P], C.c_int),
         "dfq_sweep_plan_create": ([C.POINTER(TensorDesc), I32, C.POINTER(P)], C.c_int),
+        "dfq_sweep_plan_ws_bytes": ([C.POINTER(TensorDesc), I32], C.c_int64),
+        "dfq_sweep_plan_create_ws": ([C.POINTER(TensorDesc), I32, P, I64, P, C.POINTER(P)], C.c_int),
         "dfq_sweep_plan_execute": ([P, P], C.c_int),
         "dfq_sweep_plan_stats": ([P, C.POINTER(SweepStats)], C.c_int),
         "dfq_sweep_plan_destroy": ([P], C.c_int),
         "dfq_bn_fold": ([P, P, P, P, P, P, P, P, F32, I64, I64, P], C.c_int),
         "dfq_clamp": ([P, I64, F32, F32, P], C.c_int),
-        "dfq_bn_fold_batch": ([C.POINTER(BnFoldDesc), I32, P], C.c_int),
+        "dfq_bn_fold_ws_bytes": ([C.POINTER(BnFoldDesc), I32], C.c_int64),
+        "dfq_bn_fold_batch": ([C.POINTER(BnFoldDesc), I32, P, I64, P], C.c_int),
         "dfq_cle_ws_bytes": ([I64], SZ),
         "dfq_cle_relation": ([P, P, P, P, P, I64, I64, I64, I64, I64, F64, F64, I32, F32, P, P, I32, P, SZ, P],
                              C.c_int),

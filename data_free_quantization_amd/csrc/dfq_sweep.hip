@@ -25,6 +25,7 @@
 #include "dfq_common.h"
 
 #include <algorithm>
+#include <cstring>
 #include <cstdlib>
 #include <new>
 #include <numeric>
@@ -749,17 +750,49 @@ struct dfq_sweep_plan {
     DevTask* d_reduce = nullptr;
     DevTask* d_main = nullptr;
     uint32_t* d_slots = nullptr;   // [slots] mins then [slots] maxs
+    void* d_owned = nullptr;       // the tables' allocation when no workspace was given
     int64_t n_reduce = 0, n_main = 0, n_slots = 0, n_tensors = 0, n_elems = 0, algo_bytes = 0;
     std::vector<int64_t> rslab, mslab;   // slab boundaries (Built)
 };
 
-extern "C" int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, dfq_sweep_plan** out) {
+namespace dfq {
+// Device layout of a plan's tables: [tensors | reduce tasks | main tasks | slots],
+// each 256-B aligned (one allocation or one caller workspace).
+struct PlanLayout {
+    int64_t o_tensors = 0, o_reduce = 0, o_main = 0, o_slots = 0, total = 0;
+};
+static int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
+static PlanLayout plan_layout(const Built& B, int64_t n) {
+    PlanLayout L;
+    L.o_tensors = 0;
+    L.o_reduce = L.o_tensors + align256((int64_t)sizeof(DevTensor) * n);
+    L.o_main = L.o_reduce + align256((int64_t)sizeof(DevTask) * (int64_t)B.reduce.size());
+    L.o_slots = L.o_main + align256((int64_t)sizeof(DevTask) * (int64_t)B.main.size());
+    L.total = L.o_slots + align256((int64_t)sizeof(uint32_t) * 2 * B.slots);
+    return L;
+}
+}  // namespace dfq
+
+extern "C" int64_t dfq_sweep_plan_ws_bytes(const dfq_tensor_desc* descs, int32_t n) {
+    if ((n > 0 && !descs) || n < 0) return -1;
+    Built B;
+    if (build(descs, n, B, kVariants[variant_from_env()])) return -1;
+    return plan_layout(B, n).total;
+}
+
+// ws == NULL: the plan owns one hipMalloc'ed table block (blocking copy).  Else the
+// tables go to the caller's stream-ordered workspace: one copy on `stream`, then a
+// sync of that stream (the host staging dies with the call).
+static int sweep_plan_create_impl(const dfq_tensor_desc* descs, int32_t n, void* ws, int64_t ws_bytes,
+                                  hipStream_t stream, dfq_sweep_plan** out) {
     if (!out || (n > 0 && !descs) || n < 0) return DFQ_ERR_INVALID;
     *out = nullptr;
     const int variant = variant_from_env();
     Built B;
     int rc = build(descs, n, B, kVariants[variant]);
     if (rc) return rc;
+    const PlanLayout Lo = plan_layout(B, n);
+    if (ws && (ws_bytes < Lo.total || reinterpret_cast<uintptr_t>(ws) % 256 != 0)) return DFQ_ERR_WORKSPACE;
     dfq_sweep_plan* p = new (std::nothrow) dfq_sweep_plan();
     if (!p) return DFQ_ERR_NOMEM;
     p->variant = variant;
@@ -771,30 +804,47 @@ extern "C" int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, df
     p->algo_bytes = B.algo_bytes;
     p->rslab = B.rslab;
     p->mslab = B.mslab;
-    auto fail = [&](hipError_t e) {
+    hipError_t e = hipSuccess;
+    char* base = static_cast<char*>(ws);
+    if (!base) {
+        e = hipMalloc(&p->d_owned, Lo.total);
+        base = static_cast<char*>(p->d_owned);
+    }
+    p->d_tensors = reinterpret_cast<DevTensor*>(base + Lo.o_tensors);
+    p->d_reduce = reinterpret_cast<DevTask*>(base + Lo.o_reduce);
+    p->d_main = reinterpret_cast<DevTask*>(base + Lo.o_main);
+    p->d_slots = reinterpret_cast<uint32_t*>(base + Lo.o_slots);
+    if (e == hipSuccess) {
+        std::vector<char> blob(Lo.o_slots, 0);   // the host-built tables
+        if (n > 0) std::memcpy(blob.data() + Lo.o_tensors, B.tensors.data(), sizeof(DevTensor) * n);
+        if (!B.reduce.empty())
+            std::memcpy(blob.data() + Lo.o_reduce, B.reduce.data(), sizeof(DevTask) * B.reduce.size());
+        if (!B.main.empty()) std::memcpy(blob.data() + Lo.o_main, B.main.data(), sizeof(DevTask) * B.main.size());
+        if (ws) {
+            e = hipMemcpyAsync(base, blob.data(), Lo.o_slots, hipMemcpyHostToDevice, stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        } else {
+            e = hipMemcpy(base, blob.data(), Lo.o_slots, hipMemcpyHostToDevice);
+        }
+    }
+    if (e != hipSuccess) {
         set_last_hip_error(e);
-        (void)hipFree(p->d_tensors); (void)hipFree(p->d_reduce); (void)hipFree(p->d_main); (void)hipFree(p->d_slots);
+        (void)hipFree(p->d_owned);
         delete p;
         return DFQ_ERR_HIP;
-    };
-    hipError_t e;
-    if (n > 0) {
-        if ((e = hipMalloc(&p->d_tensors, sizeof(DevTensor) * n)) != hipSuccess) return fail(e);
-        if ((e = hipMemcpy(p->d_tensors, B.tensors.data(), sizeof(DevTensor) * n, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
-    }
-    if (p->n_reduce > 0) {
-        if ((e = hipMalloc(&p->d_reduce, sizeof(DevTask) * p->n_reduce)) != hipSuccess) return fail(e);
-        if ((e = hipMemcpy(p->d_reduce, B.reduce.data(), sizeof(DevTask) * p->n_reduce, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
-    }
-    if (p->n_main > 0) {
-        if ((e = hipMalloc(&p->d_main, sizeof(DevTask) * p->n_main)) != hipSuccess) return fail(e);
-        if ((e = hipMemcpy(p->d_main, B.main.data(), sizeof(DevTask) * p->n_main, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
-    }
-    if (p->n_slots > 0) {
-        if ((e = hipMalloc(&p->d_slots, sizeof(uint32_t) * 2 * p->n_slots)) != hipSuccess) return fail(e);
     }
     *out = p;
     return DFQ_OK;
+}
+
+extern "C" int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, dfq_sweep_plan** out) {
+    return sweep_plan_create_impl(descs, n, nullptr, 0, nullptr, out);
+}
+
+extern "C" int dfq_sweep_plan_create_ws(const dfq_tensor_desc* descs, int32_t n, void* ws, int64_t ws_bytes,
+                                        void* stream, dfq_sweep_plan** out) {
+    if (!ws) return DFQ_ERR_WORKSPACE;
+    return sweep_plan_create_impl(descs, n, ws, ws_bytes, static_cast<hipStream_t>(stream), out);
 }
 
 extern "C" int dfq_sweep_plan_execute(dfq_sweep_plan* p, void* stream) {
@@ -860,7 +910,7 @@ extern "C" int dfq_sweep_plan_stats(const dfq_sweep_plan* p, dfq_sweep_stats* st
 
 extern "C" int dfq_sweep_plan_destroy(dfq_sweep_plan* p) {
     if (!p) return DFQ_OK;
-    (void)hipFree(p->d_tensors); (void)hipFree(p->d_reduce); (void)hipFree(p->d_main); (void)hipFree(p->d_slots);
+    (void)hipFree(p->d_owned);   // NULL for workspace-backed plans
     delete p;
     return DFQ_OK;
 }

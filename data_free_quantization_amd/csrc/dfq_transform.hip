@@ -5,6 +5,8 @@
 // torch CPU ops (one rounding per op; -ffp-contract=off, IEEE div/sqrt).
 #include "dfq_common.h"
 
+#include <cstring>
+
 #include <algorithm>
 #include <cmath>
 #include <new>
@@ -451,11 +453,10 @@ extern "C" int dfq_act_affine(const float* x, const float* w, const float* bias,
     return DFQ_OK;
 }
 
-extern "C" int dfq_bn_fold_batch(const dfq_bn_fold_desc* d, int32_t n, void* stream) {
-    if (n < 0 || (n > 0 && !d)) return DFQ_ERR_INVALID;
-    if (n == 0) return DFQ_OK;
-    std::vector<BnFoldJob> jobs(n);
-    std::vector<BnFoldChunk> chunks;
+// Tables of one batched fold: the jobs, and 8192-element weight chunks.
+static int bn_fold_tables(const dfq_bn_fold_desc* d, int32_t n, std::vector<BnFoldJob>& jobs,
+                          std::vector<BnFoldChunk>& chunks) {
+    jobs.resize(n);
     for (int32_t j = 0; j < n; ++j) {
         const dfq_bn_fold_desc& x = d[j];
         if (!x.w || !x.bias || !x.bn_w || !x.bn_b || !x.bn_mean || !x.bn_var || x.rows < 0 || x.row_len < 0)
@@ -467,14 +468,45 @@ extern "C" int dfq_bn_fold_batch(const dfq_bn_fold_desc* d, int32_t n, void* str
         const int64_t ne = x.rows * x.row_len;
         for (int64_t e = 0; e < ne; e += 8192) chunks.push_back(BnFoldChunk{j, 0, e, std::min<int64_t>(e + 8192, ne)});
     }
+    return DFQ_OK;
+}
+
+static int64_t round256(int64_t b) { return ceil_div(b, (int64_t)256) * 256; }
+
+extern "C" int64_t dfq_bn_fold_ws_bytes(const dfq_bn_fold_desc* d, int32_t n) {
+    if (n < 0 || (n > 0 && !d)) return -1;
+    int64_t nchunks = 0;
+    for (int32_t j = 0; j < n; ++j) {
+        if (d[j].rows < 0 || d[j].row_len < 0) return -1;
+        nchunks += ceil_div(d[j].rows * d[j].row_len, (int64_t)8192);
+    }
+    return round256((int64_t)sizeof(BnFoldJob) * n) + round256((int64_t)sizeof(BnFoldChunk) * nchunks);
+}
+
+extern "C" int dfq_bn_fold_batch(const dfq_bn_fold_desc* d, int32_t n, void* ws, int64_t ws_bytes, void* stream) {
+    if (n < 0 || (n > 0 && !d)) return DFQ_ERR_INVALID;
+    if (n == 0) return DFQ_OK;
+    std::vector<BnFoldJob> jobs;
+    std::vector<BnFoldChunk> chunks;
+    const int rc = bn_fold_tables(d, n, jobs, chunks);
+    if (rc != DFQ_OK) return rc;
+    const int64_t jb = round256((int64_t)sizeof(BnFoldJob) * n);
+    const int64_t need = jb + round256((int64_t)sizeof(BnFoldChunk) * (int64_t)chunks.size());
+    if (ws && (ws_bytes < need || reinterpret_cast<uintptr_t>(ws) % 256 != 0)) return DFQ_ERR_INVALID;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    BnFoldJob* dj = nullptr;
-    BnFoldChunk* dc = nullptr;
-    DFQ_HIP_CHECK(hipMalloc(&dj, sizeof(BnFoldJob) * n));
-    hipError_t e = hipMalloc(&dc, sizeof(BnFoldChunk) * std::max<size_t>(chunks.size(), 1));
-    if (e == hipSuccess) e = hipMemcpyAsync(dj, jobs.data(), sizeof(BnFoldJob) * n, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && !chunks.empty())
-        e = hipMemcpyAsync(dc, chunks.data(), sizeof(BnFoldChunk) * chunks.size(), hipMemcpyHostToDevice, s);
+    void* own = nullptr;
+    if (!ws) {   // no caller workspace: a private one, freed after a stream sync
+        DFQ_HIP_CHECK(hipMalloc(&own, need));
+        ws = own;
+    }
+    char* base = static_cast<char*>(ws);
+    BnFoldJob* dj = reinterpret_cast<BnFoldJob*>(base);
+    BnFoldChunk* dc = reinterpret_cast<BnFoldChunk*>(base + jb);
+    // one staging blob, one copy
+    std::vector<char> blob(need, 0);
+    std::memcpy(blob.data(), jobs.data(), sizeof(BnFoldJob) * n);
+    if (!chunks.empty()) std::memcpy(blob.data() + jb, chunks.data(), sizeof(BnFoldChunk) * chunks.size());
+    hipError_t e = hipMemcpyAsync(base, blob.data(), need, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && !chunks.empty()) {
         hipLaunchKernelGGL(bn_fold_weight_batch_kernel, dim3((int)std::min<size_t>(chunks.size(), 4096)),
                            dim3(kThreads), 0, s, dj, dc, (int64_t)chunks.size());
@@ -484,9 +516,10 @@ extern "C" int dfq_bn_fold_batch(const dfq_bn_fold_desc* d, int32_t n, void* str
         hipLaunchKernelGGL(bn_fold_channel_batch_kernel, dim3(std::min(n, 2048)), dim3(kThreads), 0, s, dj, n);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(s);   // the tables die with this call
-    (void)hipFree(dj);
-    (void)hipFree(dc);
+    // The staging blob dies with this call (and private tables with it): wait for
+    // the stream rather than lean on pageable-copy staging semantics.
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (own) (void)hipFree(own);
     if (e != hipSuccess) {
         set_last_hip_error(e);
         return DFQ_ERR_HIP;

@@ -85,12 +85,25 @@ class SweepPlan:
             if it.clip is not None:
                 d.clip_lo, d.clip_hi = float(it.clip[0]), float(it.clip[1])
         self._plan = C.c_void_p()
-        _lib.check(L.dfq_sweep_plan_create(descs, len(self.items), C.byref(self._plan)), "dfq_sweep_plan_create",
-                   ValueError)
+        self._device = self.items[0].src.device if self.items else None
+        self._ws = None
+        if self.items:
+            # task tables in torch's caching allocator (stream-ordered): no hipMalloc /
+            # hipFree per plan, and destroy() needs no device sync
+            nb = int(L.dfq_sweep_plan_ws_bytes(descs, len(self.items)))
+            if nb < 0:
+                _lib.check(L.dfq_sweep_plan_create(descs, len(self.items), C.byref(self._plan)),
+                           "dfq_sweep_plan_create", ValueError)   # raises with the planner's error
+            self._stream = torch.cuda.current_stream(self._device)
+            self._ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=self._device)
+            _lib.check(L.dfq_sweep_plan_create_ws(descs, len(self.items), self._ws.data_ptr(), self._ws.numel(),
+                                                  C.c_void_p(self._stream.cuda_stream), C.byref(self._plan)),
+                       "dfq_sweep_plan_create_ws", ValueError)
+        else:
+            _lib.check(L.dfq_sweep_plan_create(descs, 0, C.byref(self._plan)), "dfq_sweep_plan_create", ValueError)
         st = _lib.SweepStats()
         _lib.check(L.dfq_sweep_plan_stats(self._plan, C.byref(st)), "dfq_sweep_plan_stats")
         self.stats = {f: getattr(st, f) for f, _ in _lib.SweepStats._fields_}
-        self._device = self.items[0].src.device if self.items else None
 
     def execute(self, stream: Optional[torch.cuda.Stream] = None):
         if self._plan is None:
@@ -98,14 +111,18 @@ class SweepPlan:
         if not self.items:
             return
         s = stream if stream is not None else torch.cuda.current_stream(self._device)
+        if s != self._stream:   # the tables must outlive work queued on another stream
+            self._ws.record_stream(s)
         _lib.check(_lib.load().dfq_sweep_plan_execute(self._plan, C.c_void_p(s.cuda_stream)),
                    "dfq_sweep_plan_execute")
 
     def destroy(self):
         if self._plan is not None and self._plan.value:
-            torch.cuda.synchronize(self._device)
+            # workspace-backed: the C plan holds no device memory, and the tables are
+            # released to torch's allocator in stream order (no sync needed)
             _lib.load().dfq_sweep_plan_destroy(self._plan)
         self._plan = None
+        self._ws = None
 
     def __del__(self):
         try:

@@ -55,17 +55,32 @@ def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d]):
     return model
 
 
+def _carve(total_sizes, fill_zero, device):
+    """Views of ONE allocation, one per size (a model's worth of small vectors in a
+    single allocator call instead of one each)."""
+    n = sum(total_sizes)
+    flat = (torch.zeros if fill_zero else torch.empty)(max(n, 1), dtype=torch.float32, device=device)
+    out, off = [], 0
+    for k in total_sizes:
+        out.append(flat[off:off + k])
+        off += k
+    return out
+
+
 def _fold_batch(pairs):
     with torch.no_grad():
         descs = (_lib.BnFoldDesc * len(pairs))()
+        dev = pairs[0][1].weight.device
+        for bn, layer in pairs:
+            _lib.require_device(layer.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var)
+        need_bias = [layer for _, layer in pairs if layer.bias is None]
+        for layer, z in zip(need_bias, _carve([l.weight.size(0) for l in need_bias], True, dev)):   # :262-263
+            layer.bias = nn.Parameter(z, requires_grad=False)
+        fakes = _carve([bn.weight.numel() for bn, _ in pairs] * 2, False, dev)
         for j, (bn, layer) in enumerate(pairs):
             w = layer.weight
-            _lib.require_device(w, bn.weight, bn.bias, bn.running_mean, bn.running_var)
-            if layer.bias is None:   # :262-263
-                layer.bias = nn.Parameter(torch.zeros(w.size(0), dtype=torch.float32, device=w.device),
-                                          requires_grad=False)
-            bn.register_buffer("fake_weight", torch.empty_like(bn.weight))
-            bn.register_buffer("fake_bias", torch.empty_like(bn.bias))
+            bn.register_buffer("fake_weight", fakes[j].view_as(bn.weight))
+            bn.register_buffer("fake_bias", fakes[len(pairs) + j].view_as(bn.bias))
             d = descs[j]
             d.w, d.bias = w.data_ptr(), layer.bias.data_ptr()
             d.bn_w, d.bn_b = bn.weight.data_ptr(), bn.bias.data_ptr()
@@ -74,7 +89,13 @@ def _fold_batch(pairs):
             d.eps = float(bn.eps)
             d.rows = w.size(0)
             d.row_len = w.numel() // w.size(0)
-        rc = _lib.load().dfq_bn_fold_batch(descs, len(pairs), _lib.stream_of(pairs[0][1].weight))
+        L = _lib.load()
+        nb = int(L.dfq_bn_fold_ws_bytes(descs, len(pairs)))
+        if nb < 0:
+            raise RuntimeError("dfq_bn_fold_ws_bytes: invalid layer shapes")
+        dev = pairs[0][1].weight.device
+        ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=dev)   # stream-ordered (caching allocator)
+        rc = L.dfq_bn_fold_batch(descs, len(pairs), ws.data_ptr(), ws.numel(), _lib.stream_of(pairs[0][1].weight))
         _lib.check(rc, "dfq_bn_fold_batch")
         for bn, _ in pairs:
             bn.eps = 0
@@ -135,15 +156,8 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
         rows = w.size(0) if per_channel else 1
         npar = rows
         khw = khw_of(w)
-        want = state is not None
         it = SweepItem(src=w, dst=w, bits=bit_weight, per_channel=per_channel, symmetric=symmetric, clip=clip,
                        khw=khw, rows=rows)
-        if want:
-            cdt = (torch.int8 if symmetric else torch.uint8) if bit_weight <= 8 else torch.int16
-            it.codes = torch.empty(w.shape, dtype=cdt, device=w.device)
-            it.scale = torch.empty(npar, dtype=torch.float32, device=w.device)
-            it.zero = torch.empty(npar, dtype=torch.float32, device=w.device)
-            it.esum = torch.empty(w.numel() // khw, dtype=torch.float32, device=w.device)
         items.append(it)
         keys.append(layer_idx)
         if layer.bias is not None and bits_bias < 32:
@@ -152,9 +166,26 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
             keys.append(None)
     if not items:
         return graph
+    if state is not None:   # codes / scale / zero / E of every layer: views of two allocations
+        wl = [it for it, k in zip(items, keys) if k is not None]
+        dev = wl[0].src.device
+        cdt = (torch.int8 if symmetric else torch.uint8) if bit_weight <= 8 else torch.int16
+        up = lambda k: -(-k // 16) * 16   # noqa: E731  -- 16-element aligned pieces (vector paths)
+        codes = torch.empty(sum(up(it.src.numel()) for it in wl), dtype=cdt, device=dev)
+        f32 = torch.empty(sum(2 * up(it.rows) + up(it.src.numel() // it.khw) for it in wl), dtype=torch.float32,
+                          device=dev)
+        co = fo = 0
+        for it in wl:
+            n, r, ne = it.src.numel(), it.rows, it.src.numel() // it.khw
+            it.codes = codes[co:co + n].view(it.src.shape)
+            it.scale = f32[fo:fo + r]
+            it.zero = f32[fo + up(r):fo + up(r) + r]
+            it.esum = f32[fo + 2 * up(r):fo + 2 * up(r) + ne]
+            co += up(n)
+            fo += 2 * up(r) + up(ne)
     plan = SweepPlan(items)
     plan.execute()
-    plan.destroy()   # synchronises before releasing the task tables
+    plan.destroy()   # stream-ordered: the task tables return to torch's allocator
     if state is not None:
         for k, it in zip(keys, items):
             if k is not None:

@@ -114,6 +114,13 @@ typedef struct dfq_sweep_stats {
 } dfq_sweep_stats;
 /* Blocking (uploads the descriptor/task tables once).  descs is copied. */
 int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, dfq_sweep_plan** plan);
+/* The same with the tables in a caller workspace of >= dfq_sweep_plan_ws_bytes
+ * bytes (256-B aligned, stream-ordered with `stream`, alive while the plan runs;
+ * e.g. the framework's caching allocator): no hipMalloc / hipFree, and destroy
+ * needs no device sync.  The upload is on `stream`, which is synchronized. */
+int64_t dfq_sweep_plan_ws_bytes(const dfq_tensor_desc* descs, int32_t n);
+int dfq_sweep_plan_create_ws(const dfq_tensor_desc* descs, int32_t n, void* ws, int64_t ws_bytes, void* stream,
+                             dfq_sweep_plan** plan);
 int dfq_sweep_plan_execute(dfq_sweep_plan* plan, void* stream);
 int dfq_sweep_plan_stats(const dfq_sweep_plan* plan, dfq_sweep_stats* stats);
 int dfq_sweep_plan_destroy(dfq_sweep_plan* plan);
@@ -142,7 +149,12 @@ typedef struct dfq_bn_fold_desc {
     int64_t rows;
     int64_t row_len;
 } dfq_bn_fold_desc;
-int dfq_bn_fold_batch(const dfq_bn_fold_desc* descs, int32_t n, void* stream);
+/* Device workspace bytes for dfq_bn_fold_batch's job tables (-1: bad arguments). */
+int64_t dfq_bn_fold_ws_bytes(const dfq_bn_fold_desc* descs, int32_t n);
+/* ws: >= dfq_bn_fold_ws_bytes bytes, 256-B aligned, stream-ordered with `stream`
+ * (e.g. the framework's caching allocator), or NULL: private tables (a
+ * hipMalloc / hipFree per call).  Blocking: the stream is synchronized. */
+int dfq_bn_fold_batch(const dfq_bn_fold_desc* descs, int32_t n, void* ws, int64_t ws_bytes, void* stream);
 
 /* ---- weight clipping (clip_weight.py:18-29): w = min(max(w, lo), hi), in place */
 int dfq_clamp(float* w, int64_t n, float lo, float hi, void* stream);
