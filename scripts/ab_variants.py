@@ -22,11 +22,13 @@ def main():
     p.add_argument("--model", default="mobilenetv2")
     p.add_argument("--no-esum", action="store_true")
     p.add_argument("--asym", action="store_true")
+    p.add_argument("--tensor", action="store_true", help="per-tensor ranges (quantize_targ_layer's mode)")
     a = p.parse_args()
     import bench
     from data_free_quantization_amd.sweep import SweepPlan
     dev = torch.device("cuda:0")
-    items, shapes, per_copy, copies = bench.build_batch(a.model, dev, sym=not a.asym, esum=not a.no_esum)
+    items, shapes, per_copy, copies = bench.build_batch(a.model, dev, channel=not a.tensor, sym=not a.asym,
+                                                          esum=not a.no_esum)
     plans = {}
     for v in [int(x) for x in a.variants.split(",")]:
         os.environ["DFQ_SWEEP_VARIANT"] = str(v)
