@@ -338,6 +338,54 @@ __global__ void bn_fold_channel_batch_kernel(const BnFoldJob* __restrict__ jobs,
     }
 }
 
+// ---------------------------------------------------------------------------
+// quantize()'s data range with num_chunks (utils/quantize.py:26-37):
+// y = x.view(rows, -1); min = y.min(-1)[0].mean(-1), max likewise (fp32).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads)
+chunk_row_range_kernel(const float* __restrict__ x, int64_t rows, int64_t row_len, float* __restrict__ mins,
+                       float* __restrict__ maxs) {
+    __shared__ float smn[kThreads / kWave], smx[kThreads / kWave];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+    for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+        const float* row = x + r * row_len;
+        float a = INFINITY, b = -INFINITY;
+        for (int64_t i = threadIdx.x; i < row_len; i += kThreads) {
+            const float v = row[i];
+            a = fminf(a, v);
+            b = fmaxf(b, v);
+        }
+        a = wave_min(a);
+        b = wave_max(b);
+        if (lane == 0) {
+            smn[w] = a;
+            smx[w] = b;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int k = 1; k < kThreads / kWave; ++k) {
+                a = fminf(a, smn[k]);
+                b = fmaxf(b, smx[k]);
+            }
+            mins[r] = a;
+            maxs[r] = b;
+        }
+        __syncthreads();
+    }
+}
+
+// One wave: torch.mean over the rows' mins / maxs in ATen's order (sum, then / n).
+__global__ void chunk_mean_kernel(const float* __restrict__ mins, const float* __restrict__ maxs, int64_t rows,
+                                  float* __restrict__ out2) {
+    const int lane = threadIdx.x;
+    const float smn = wave_inner_sum([&](int64_t i) { return mins[i]; }, rows, lane);
+    const float smx = wave_inner_sum([&](int64_t i) { return maxs[i]; }, rows, lane);
+    if (lane == 0) {
+        out2[0] = smn / (float)rows;
+        out2[1] = smx / (float)rows;
+    }
+}
+
 }  // namespace dfq
 
 using namespace dfq;
@@ -524,5 +572,19 @@ extern "C" int dfq_bn_fold_batch(const dfq_bn_fold_desc* d, int32_t n, void* ws,
         set_last_hip_error(e);
         return DFQ_ERR_HIP;
     }
+    return DFQ_OK;
+}
+
+extern "C" int dfq_chunk_range(const float* x, int64_t rows, int64_t row_len, float* rowbuf, float* out2,
+                               void* stream) {
+    if (!x || !rowbuf || !out2 || rows < 1) return DFQ_ERR_INVALID;
+    if (row_len < 1) return DFQ_ERR_SHAPE;   // torch: min over an empty dim raises
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int grid = (int)std::min<int64_t>(rows, 4096);
+    hipLaunchKernelGGL(chunk_row_range_kernel, dim3(grid), dim3(kThreads), 0, s, x, rows, row_len, rowbuf,
+                       rowbuf + rows);
+    DFQ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(chunk_mean_kernel, dim3(1), dim3(kWave), 0, s, rowbuf, rowbuf + rows, rows, out2);
+    DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }

@@ -91,6 +91,57 @@ def fake_quant(x: torch.Tensor, num_bits: int = 8, *, per_channel: bool = False,
     return QuantResult(dq, codes, scale, zero, esum)
 
 
+def _chunk_range(x: torch.Tensor, rows: int):
+    """(min, max) as quantize() builds them when a bound is None
+    (utils/quantize.py:26-37): mean over x.view(rows, -1)'s rows of each row's
+    min / max, fp32 (0-d tensors in the reference)."""
+    if rows == 1:
+        return _data_range(x)
+    xc = x.detach().contiguous()
+    rowbuf = torch.empty(2 * rows, dtype=torch.float32, device=x.device)
+    out2 = torch.empty(2, dtype=torch.float32, device=x.device)
+    _lib.check(_lib.load().dfq_chunk_range(_lib.ptr(xc), rows, xc.numel() // rows, _lib.ptr(rowbuf), _lib.ptr(out2),
+                                           _lib.stream_of(xc)), "dfq_chunk_range", RuntimeError)
+    mn, mx = out2.tolist()
+    return mn, mx
+
+
+def _resolve_range(input, min_value, max_value, num_chunks, symmetric):
+    """The (min, max) quantize() ends up using and whether its scale is built in
+    fp32 (0-d tensor arithmetic) or in double (Python floats), as
+    utils/quantize.py:26-68 does.  None: both bounds from the whole tensor, taken
+    inside the kernel."""
+    B = input.shape[0]   # the reference indexes shape[0] too (IndexError for 0-d)
+    if min_value is None or max_value is None:
+        nc = B if num_chunks is None else num_chunks
+        rows = B // nc
+        n = input.numel()
+        if rows == 0 or n % rows != 0:
+            raise RuntimeError(f"shape '[{rows}, -1]' is invalid for input of size {n}")
+        if n == 0:
+            raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0")
+        if min_value is None and max_value is None and rows == 1:
+            return None
+        mn, mx = _chunk_range(input, rows)
+        t_min, v_min = (True, mn) if min_value is None else (_is_tensor_value(min_value), float(min_value))
+        t_max, v_max = (True, mx) if max_value is None else (_is_tensor_value(max_value), float(max_value))
+    else:
+        t_min, v_min = _is_tensor_value(min_value), float(min_value)
+        t_max, v_max = _is_tensor_value(max_value), float(max_value)
+    if not symmetric:
+        return v_min, v_max, t_min or t_max
+    # max_value = abs(max); min_value = abs(min); if max < min: max = min;
+    # scale = max / qmax -- a tensor winner divides in fp32, a float one in double.
+    # A tensor-vs-float comparison runs in fp32 (the float is cast to the tensor's dtype).
+    a_max, a_min = abs(v_max), abs(v_min)
+    if t_min or t_max:
+        less = bool(torch.tensor(a_max, dtype=torch.float32) < torch.tensor(a_min, dtype=torch.float32))
+    else:
+        less = a_max < a_min
+    w, t = (a_min, t_min) if less else (a_max, t_max)
+    return w, w, t
+
+
 class UniformQuantize(InplaceFunction):
     """Uniform quantize -> dequantize with a straight-through backward
     (utils/quantize.py:16-85)."""
@@ -98,16 +149,7 @@ class UniformQuantize(InplaceFunction):
     @staticmethod
     def forward(ctx, input, num_bits=8, min_value=None, max_value=None, inplace=False, symmetric=False,
                 num_chunks=None):
-        scale_f32 = False
-        if min_value is None or max_value is None:
-            # utils/quantize.py:26-37: range from the data as 0-d fp32 tensors
-            num_chunks = input.shape[0] if num_chunks is None else num_chunks
-            if input.shape[0] // num_chunks != 1:
-                raise NotImplementedError(
-                    "chunked range statistics (num_chunks < batch) belong to the activation path")
-            scale_f32 = True
-        if _is_tensor_value(min_value) or _is_tensor_value(max_value):
-            scale_f32 = True
+        rng = _resolve_range(input, min_value, max_value, num_chunks, symmetric)
         ctx.inplace = inplace
         ctx.num_bits = num_bits
         ctx.min_value = min_value
@@ -117,17 +159,11 @@ class UniformQuantize(InplaceFunction):
             out = input
         else:
             out = torch.empty_like(input)
-        given_min = given_max = None
-        if min_value is not None or max_value is not None:
-            # one given, one from data: compute the missing one on the device range path
-            if min_value is None or max_value is None:
-                mn, mx = _data_range(input)
-                given_min = float(mn) if min_value is None else float(min_value)
-                given_max = float(mx) if max_value is None else float(max_value)
-            else:
-                given_min, given_max = float(min_value), float(max_value)
-        fake_quant(input.detach(), num_bits, symmetric=symmetric, min_value=given_min, max_value=given_max,
-                   out=out, want_codes=False, scale_f32=scale_f32)
+        if rng is None:   # 0-d fp32 range of the whole tensor, reduced in the kernel
+            fake_quant(input.detach(), num_bits, symmetric=symmetric, out=out, want_codes=False, scale_f32=True)
+        else:
+            fake_quant(input.detach(), num_bits, symmetric=symmetric, min_value=rng[0], max_value=rng[1], out=out,
+                       want_codes=False, scale_f32=rng[2])
         return out
 
     @staticmethod

@@ -96,6 +96,11 @@ int dfq_quantize_ws_bytes(const dfq_tensor_desc* desc, size_t* bytes);
 /* Blocking (returns after the stream drains: the reference quantize() is
  * synchronous too).  ws: device memory of >= dfq_quantize_ws_bytes bytes. */
 int dfq_quantize_tensor(const dfq_tensor_desc* desc, void* ws, size_t ws_bytes, void* stream);
+/* quantize()'s data range when min/max are None and num_chunks splits the batch
+ * (utils/quantize.py:26-37): x viewed as [rows = B // num_chunks, row_len];
+ * out2 = {mean_r min(x[r]), mean_r max(x[r])} in fp32, the mean in ATen's sum
+ * order.  rowbuf: 2*rows device floats of scratch.  Async on `stream`. */
+int dfq_chunk_range(const float* x, int64_t rows, int64_t row_len, float* rowbuf, float* out2, void* stream);
 
 /* ---- grouped sweep over many tensors (replaces quantize_targ_layer,
  *      utils/layer_transform.py:288-305, fused with clip_weight.py:4-33 and the

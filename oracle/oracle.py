@@ -36,6 +36,7 @@ def lib():
         P, I64, I32, F32, F64 = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_double
         L.oracle_quantize.argtypes = [P, I64, I64, I32, I32, I32, I32, F32, F32, F64, F64, P, P, P, P, P]
         L.oracle_bn_fold.argtypes = [P, P, P, P, P, P, P, P, F32, I64, I64]
+        L.oracle_chunk_range.argtypes = [P, I64, I64, P]
         L.oracle_cle_relation.argtypes = [P, P, P, P, P, I64, I64, I64, I64, I64, F64, F64, I32, F32, P]
         L.oracle_bias_absorb.argtypes = [P, P, P, P, P, I64, I64, I64, I64, F32]
         L.oracle_bc_expect.argtypes = [P, P, I64, I32, I32, P]
@@ -84,6 +85,17 @@ def quantize(x, bits=8, mode=TENSOR_ASYM, rows=None, khw=1, flags=0, clip=(0.0, 
     if want_esum:
         out["esum"] = esum
     return out
+
+
+def chunk_range(x, rows):
+    """quantize()'s range for min/max None (utils/quantize.py:26-37): mean over the
+    rows of x.view(rows, -1) of each row's min / max, as fp32."""
+    x = _f32(x)
+    out = np.empty(2, np.float32)
+    rc = lib().oracle_chunk_range(_p(x), rows, x.size // rows, _p(out))
+    if rc:
+        raise RuntimeError(f"oracle_chunk_range rc={rc}")
+    return out[0], out[1]
 
 
 def bn_fold(w, bias, g, b, m, v, eps):

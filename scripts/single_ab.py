@@ -1,0 +1,28 @@
+"""Single-model sweep latency per kernel variant: one weight set,
+per-channel sym INT8 + codes + clip + BC sums, device us per execute (diagnostic).
+usage: python scripts/single_ab.py [variants...]   (env DFQ_SWEEP_BLOCKS_PER_CU applies)"""
+import json
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import bench  # noqa: E402
+from data_free_quantization_amd.sweep import SweepPlan  # noqa: E402
+
+variants = [int(v) for v in sys.argv[1:]] or [6]
+dev = torch.device("cuda:0")
+stream = torch.cuda.current_stream(dev)
+for model in ("mobilenetv2", "resnet50", "deeplab"):
+    items, _, _, _ = bench.build_batch(model, dev, copies=1, seed=5)
+    row = {"model": model, "bpc": os.environ.get("DFQ_SWEEP_BLOCKS_PER_CU", "64")}
+    for v in variants:
+        os.environ["DFQ_SWEEP_VARIANT"] = str(v)
+        plan = SweepPlan(items)
+        ms = bench.time_plan(plan, stream, dev, 200, 20)
+        row[f"v{v}"] = round(ms * 1e3, 2)
+        row[f"v{v}_grid"] = plan.stats["grid_blocks"]
+        plan.destroy()
+    print(json.dumps(row), flush=True)

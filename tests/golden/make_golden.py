@@ -9,6 +9,8 @@ Outputs (all plain arrays, loadable with numpy allow_pickle=False):
   quant_cases.npz     quantize()/UniformQuantize on unit and edge-case tensors,
                       per-tensor (reference call shape of utils/layer_transform.py:298)
                       and per-channel (reference quantize() per W[o] slice)
+  chunk_cases.npz     quantize() with min/max None and num_chunks (the chunked
+                      data range, utils/quantize.py:25-37)
   transform_cases.npz merge_batchnorm, _layer_equalization, bias_absorption,
                       bias_correction helpers on small layers
   pipeline_<model>.npz  main_dfq stage order on the synthetic models of
@@ -164,6 +166,45 @@ def quant_cases():
     arrays["meta"] = np.array(json.dumps(meta))
     np.savez_compressed(HERE / "quant_cases.npz", **arrays)
     print("quant cases:", len(meta))
+
+
+def chunk_cases():
+    """quantize() with min/max None and num_chunks (utils/quantize.py:25-37): the
+    range is the mean over x.view(B // num_chunks, -1)'s rows of each row's min /
+    max (0-d fp32 tensors); one bound may be given as a Python float."""
+    rng = np.random.Generator(np.random.PCG64(4321))
+    arrays, meta = {}, []
+    specs = [((32, 3, 5, 5), 16), ((32, 3, 5, 5), 8), ((32, 3, 5, 5), 4), ((32, 3, 5, 5), 1), ((32, 3, 5, 5), 32),
+             ((1000, 7), 1), ((64, 40), 2), ((48, 33), 3), ((20, 6), 40), ((18, 5), 4)]
+    for k, (shp, nc) in enumerate(specs):
+        x = np.ascontiguousarray(rng.normal(0, 0.4, shp), dtype=np.float32)
+        arrays[f"in{k}"] = x
+        for bits in (8, 4):
+            for sym in (False, True):
+                for given in (None, ("min", -0.25), ("max", 0.3), ("max", 3.3000015069999997), ("min", -3.3000015069999997)):
+                    if given is not None and (bits != 8 or k % 3):
+                        continue
+                    xt = torch.from_numpy(x.copy())
+                    kw = {} if given is None else {f"{given[0]}_value": given[1]}
+                    idx = len(meta)
+                    entry = dict(input=k, shape=list(shp), num_chunks=nc, bits=bits, sym=sym,
+                                 given=None if given is None else list(given), error=None)
+                    try:
+                        out = ref_quantize(xt, bits, symmetric=sym, num_chunks=nc, **kw)
+                    except Exception as e:   # the reference's own error (e.g. view(0, -1))
+                        entry["error"] = type(e).__name__
+                        meta.append(entry)
+                        continue
+                    y = xt.view(shp[0] // nc, -1)
+                    arrays[f"range{idx}"] = np.array([float(y.min(-1)[0].mean(-1)), float(y.max(-1)[0].mean(-1))],
+                                                     dtype=np.float32)
+                    dq = t2n(out)
+                    arrays[f"dq{idx}"] = dq
+                    arrays[f"dqh{idx}"] = np.array(h(dq))
+                    meta.append(entry)
+    arrays["meta"] = np.array(json.dumps(meta))
+    np.savez_compressed(HERE / "chunk_cases.npz", **arrays)
+    print("chunk cases:", len(meta), "errors:", sum(m["error"] is not None for m in meta))
 
 
 # ---------------------------------------------------------------------------
@@ -458,6 +499,8 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["quant", "transform", "mobilenetv2", "resnet50", "deeplab"]
     if "quant" in which:
         quant_cases()
+    if "quant" in which or "chunks" in which:
+        chunk_cases()
     if "transform" in which:
         transform_cases()
     for m in ("mobilenetv2", "resnet50", "deeplab"):

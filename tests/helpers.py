@@ -67,3 +67,28 @@ def recover_codes_consistent(dq, codes, scale, zero):
     z = np.float32(zero)
     regen = (codes.astype(np.float32) * s).astype(np.float32) + z
     return np.array_equal(regen.astype(np.float32), dq)
+
+
+def chunk_cases():
+    """quantize() with num_chunks / a None bound (tests/golden/chunk_cases.npz)."""
+    z = np.load(GOLDEN / "chunk_cases.npz", allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    out = []
+    for i, m in enumerate(meta):
+        case = dict(m)
+        case["idx"] = i
+        case["x"] = z[f"in{m['input']}"]
+        if m["error"] is None:
+            case["range"] = z[f"range{i}"]
+            case["dq"] = z[f"dq{i}"]
+            case["dqh"] = str(z[f"dqh{i}"])
+        out.append(case)
+    return out
+
+
+def chunk_kwargs(case):
+    """quantize() keyword arguments of a chunk case."""
+    kw = dict(symmetric=case["sym"], num_chunks=case["num_chunks"])
+    if case["given"] is not None:
+        kw[f"{case['given'][0]}_value"] = case["given"][1]
+    return kw

@@ -212,3 +212,106 @@ def test_reference_quantize_api_on_gpu():
     y = quantize(x, 8, float(x.min()), float(x.max()))
     y.sum().backward()
     assert torch.equal(x.grad, torch.ones_like(x))
+
+
+def test_large_ranges_vs_oracle(monkeypatch):
+    """Per-tensor ranges from one workgroup (8192) up to 4M elements and just past,
+    long per-channel rows, KH*KW sums, a single outlier setting a whole tensor's
+    range: bit-exact with the oracle, and identical with block-row pieces off
+    (DFQ_SWEEP_BLOCKROW=0: every range > one wave task through the reduce launch)."""
+    from data_free_quantization_amd.sweep import allocate, SweepPlan, khw_of
+    rng = np.random.default_rng(23)
+    big = 512 * 4 * 2048
+    shapes = [(8193,), (3, 4097, 3, 3), (1000, 1000), (big,), (big + 4,), (4, 20000), (2, 70001),
+              (96, 144, 1, 1), (320, 1280)]
+    xs = [rng.normal(0, 1, s).astype(np.float32) for s in shapes]
+    xs[2][17, 3] = 40.0
+    modes = [0, 1, 2, 3]
+
+    def run():
+        items = []
+        for x in xs:
+            for mode in modes:
+                t = torch.from_numpy(x).to(DEV)
+                items.append(allocate(t, bits=8 if mode != 1 else 4, per_channel=mode >= 2 and x.ndim > 1,
+                                      symmetric=mode in (1, 3), khw=khw_of(t) if x.ndim > 2 else 1, want_esum=True,
+                                      clip=(-2.0, 2.0) if mode == 3 else None))
+        plan = SweepPlan(items)
+        for _ in range(2):   # replay re-initialises the range slots
+            plan.execute()
+        torch.cuda.synchronize()
+        return plan, items
+
+    plan, items = run()
+    k = 0
+    for x in xs:
+        for mode in modes:
+            it = items[k]
+            k += 1
+            ch = mode >= 2 and x.ndim > 1
+            m = mode if (ch or mode < 2) else mode - 2
+            o = O.quantize(x, 8 if mode != 1 else 4, m, rows=x.shape[0] if ch else 1, khw=it.khw,
+                           flags=1 if mode == 3 else 0, clip=(-2.0, 2.0), want_esum=True)
+            assert np.array_equal(it.dst.cpu().numpy(), o["dq"]), (x.shape, mode)
+            assert np.array_equal(it.codes.cpu().numpy().view(o["codes"].dtype), o["codes"]), (x.shape, mode)
+            assert np.array_equal(it.scale.cpu().numpy(), o["scale"]), (x.shape, mode)
+            assert np.array_equal(it.esum.cpu().numpy(), o["esum"]), (x.shape, mode)
+    monkeypatch.setenv("DFQ_SWEEP_BLOCKROW", "0")
+    plan2, items2 = run()
+    for a, b in zip(items, items2):
+        assert torch.equal(a.dst, b.dst) and torch.equal(a.codes, b.codes) and torch.equal(a.esum, b.esum)
+    plan.destroy()
+    plan2.destroy()
+
+
+def test_many_models_per_tensor():
+    """quantize_targ_layer's mode over 24 MobileNetV2 weight sets in one plan
+    (reduce launch + quantize launch); every layer bit-exact with the oracle."""
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd.sweep import allocate, SweepPlan, khw_of
+    m = zoo.build("mobilenetv2", seed=9)
+    layers = [l.weight.detach() for l in zoo.target_layers(m)]
+    ref = [O.quantize(w.numpy(), 8, O.TENSOR_ASYM, rows=1, khw=khw_of(w), flags=1, clip=(-0.3, 0.3),
+                      want_esum=True) for w in layers]
+    items = []
+    for c in range(24):
+        for w in layers:
+            wd = (w.to(DEV) if c == 0 else w.to(DEV).clone()).contiguous()
+            items.append(allocate(wd, bits=8, per_channel=False, symmetric=False, khw=khw_of(wd), want_esum=True,
+                                  clip=(-0.3, 0.3)))
+    plan = SweepPlan(items)
+    plan.execute()
+    torch.cuda.synchronize()
+    assert plan.stats["launches"] == 2
+    for i, it in enumerate(items):
+        o = ref[i % len(layers)]
+        assert np.array_equal(it.dst.cpu().numpy(), o["dq"])
+        assert np.array_equal(it.codes.cpu().numpy(), o["codes"])
+        assert np.array_equal(it.esum.cpu().numpy(), o["esum"])
+    plan.destroy()
+
+
+def _chunk_cases():
+    from tests.helpers import chunk_cases
+    return chunk_cases()
+
+
+@pytest.mark.parametrize("case", _chunk_cases(), ids=lambda c: f"chunk{c['idx']}")
+def test_quantize_num_chunks_matches_reference(case):
+    """quantize() with num_chunks / one None bound on the GPU (dfq_chunk_range +
+    the sweep): bit-exact with the reference's output; the chunk range itself equals
+    the reference's y.min(-1)[0].mean(-1) / y.max(-1)[0].mean(-1); shapes the
+    reference rejects raise RuntimeError."""
+    from data_free_quantization_amd.utils.quantize import _chunk_range, quantize
+    from tests.helpers import chunk_kwargs
+    x = torch.from_numpy(case["x"]).to(DEV)
+    if case["error"] is not None:
+        with pytest.raises(RuntimeError):
+            quantize(x, case["bits"], **chunk_kwargs(case))
+        return
+    rows = case["x"].shape[0] // case["num_chunks"]
+    assert np.array_equal(np.array(_chunk_range(x, rows), np.float32), case["range"])
+    y = quantize(x, case["bits"], **chunk_kwargs(case))
+    torch.cuda.synchronize()
+    assert h(y.cpu().numpy()) == case["dqh"]
+    assert np.array_equal(y.cpu().numpy(), case["dq"])
