@@ -89,6 +89,39 @@ def _apply_bias_correction_E(layer, E, o, i2, connect_type, expect):
     return vec
 
 
+def _compute_final_bias_correction(eps, bn_values):
+    """bias_correction.py:61-80: eps (+) expect, or torch.cat for a 'cat' branch
+    (which raises for a 2-D eps, as in the reference)."""
+    connect_type, expect = bn_values
+    if connect_type == "cat":
+        return torch.cat([eps, expect])
+    return eps + expect
+
+
+def _apply_bias_correction(layer, bias):
+    """bias_correction.py:82-106: add ``bias`` to ``layer.bias`` -- directly when the
+    shapes match, else its per-output-channel mean (``bias.view(O, -1).mean(1)`` in
+    ATen's order, ``dfq_bc_apply`` with a zero expectation)."""
+    if layer.bias is None:   # :89-90 references an undefined `nn`
+        raise NameError("name 'nn' is not defined")
+    if bias.size() == layer.bias.size():
+        layer.bias.data.add_(bias)
+        return
+    if bias.numel() <= layer.bias.data.numel():
+        raise ValueError("Bias correction shape mismatch that cannot be handled automatically.")
+    o = layer.bias.size(0)
+    if bias.numel() % o:
+        raise RuntimeError(f"shape '[{o}, -1]' is invalid for input of size {bias.numel()}")
+    E = bias.detach().contiguous().view(-1)
+    _lib.require_device(E, layer.bias.data)
+    zero = torch.zeros(1, dtype=torch.float32, device=E.device)
+    vec = torch.empty_like(E)
+    out_cols = C.c_int64(0)
+    rc = _lib.load().dfq_bc_apply(_lib.ptr(E), o, E.numel() // o, _lib.ptr(zero), 1, _lib.ptr(layer.bias.data),
+                                  _lib.ptr(vec), C.byref(out_cols), _lib.stream_of(E))
+    _lib.check(rc, "dfq_bc_apply", ValueError)
+
+
 def _quantize_error(param, num_bits=8, reduction="none", signed=False):
     """bias_correction.py:111-144: Q(param) - param (per-tensor range), reduced."""
     x = param.detach().contiguous()

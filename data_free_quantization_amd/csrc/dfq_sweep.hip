@@ -563,7 +563,27 @@ static int64_t slab_bytes() {
     return (e && *e) ? (int64_t)atoll(e) << 20 : 0;
 }
 
+// Reduce-launch tasks: consecutive pieces of one range merged up to `span`
+// elements per wave task (fewer same-address atomics, longer read streams).
+// DFQ_SWEEP_REDUCE_SPAN overrides (A/B).
+static int64_t reduce_span() {
+    const char* e = getenv("DFQ_SWEEP_REDUCE_SPAN");
+    return (e && *e) ? std::max<int64_t>(1, atoll(e)) : 16384;
+}
+static void push_reduce(std::vector<DevTask>& R, const DevTask& k, int64_t span) {
+    if (!R.empty()) {
+        DevTask& p = R.back();
+        if (p.slot == k.slot && p.tensor == k.tensor && p.elem_start + p.n == k.elem_start &&
+            (int64_t)p.n + k.n <= span) {
+            p.n += k.n;
+            return;
+        }
+    }
+    R.push_back(k);
+}
+
 static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Variant& V) {
+    const int64_t rspan = reduce_span();
     const bool use_blockrow = blockrow_enabled();
     const int64_t slab = slab_bytes();
     int64_t slab_used = 0;
@@ -650,7 +670,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                     k.elem_start = r * d.row_len + off; k.tensor = ti;
                     k.n = (int32_t)std::min<int64_t>(plen, d.row_len - off);
                     k.row0 = (int32_t)r; k.nrows = 0; k.slot = (int32_t)slot; k.first = (off == 0);
-                    B.reduce.push_back(k);
+                    push_reduce(B.reduce, k, rspan);
                     B.slotted.push_back(k);
                 }
             }
@@ -665,7 +685,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                 k.elem_start = off; k.tensor = ti; k.n = (int32_t)std::min<int64_t>(plen, total - off);
                 k.row0 = 0; k.nrows = 0; k.slot = (int32_t)slot; k.first = (off == 0);
                 if (!given) {
-                    B.reduce.push_back(k);
+                    push_reduce(B.reduce, k, rspan);
                     B.slotted.push_back(k);
                 } else {
                     B.main.push_back(k);

@@ -106,6 +106,30 @@ def test_bias_correction_helpers():
         bc._apply_bias_correction_E(layer, E, 32, 64, "cat", T(z["bc_expect_relu"]))
 
 
+def test_bc_reference_named_helpers():
+    """_compute_final_bias_correction + _apply_bias_correction (bias_correction.py:61-106)
+    called by their reference names: same fixtures as the fused path."""
+    from data_free_quantization_amd import bias_correction as bc
+    z, _ = transform_cases()
+    T = lambda a: torch.from_numpy(a).to(DEV)
+    layer = nn.Conv2d(64, 32, 1, bias=True).to(DEV)
+    with torch.no_grad():
+        layer.bias.copy_(T(z["bc_bias"]))
+    bv = bc._compute_final_bias_correction(T(z["bc_E"]), ("one", T(z["bc_expect_relu"])))
+    assert np.array_equal(bv.cpu().numpy().ravel(), z["bc_vec"])
+    bc._apply_bias_correction(layer, bv)
+    assert np.array_equal(layer.bias.detach().cpu().numpy(), z["bc_bias_out"])
+    dw = nn.Conv2d(64, 64, 3, groups=64, bias=True).to(DEV)
+    with torch.no_grad():
+        dw.bias.zero_()
+    bc._apply_bias_correction(dw, bc._compute_final_bias_correction(T(z["bc_Ed"]), ("one", T(z["bc_expect_relu"]))))
+    assert np.array_equal(dw.bias.detach().cpu().numpy(), z["bc_dw_bias_out"])
+    with pytest.raises(RuntimeError):   # torch.cat of a 2-D eps with a 1-D expectation
+        bc._compute_final_bias_correction(T(z["bc_E"]), ("cat", T(z["bc_expect_relu"])))
+    with pytest.raises(ValueError):     # fewer elements than the bias
+        bc._apply_bias_correction(layer, torch.zeros(8, device=DEV))
+
+
 def test_clip_weight():
     from data_free_quantization_amd.clip_weight import clip_weight
     conv = nn.Conv2d(16, 32, 3).to(DEV)
