@@ -32,7 +32,7 @@ EXPORTS = [
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
     "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
     "dfq_bias_absorb", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate",
-    "dfq_probe_stream", "dfq_probe_lds",
+    "dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline",
     "dfq_act_moments", "dfq_act_minmax", "dfq_act_affine",
 ]
 
@@ -124,6 +124,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_bc_apply": ([P, I64, I64, P, I64, P, P, C.POINTER(I64), P], C.c_int),
         "dfq_bc_propagate": ([P, I64, P, I64, I32, P], C.c_int),
         "dfq_probe_stream": ([P, P, P, P, I64, I32, P], C.c_int),
+        "dfq_debug_timeline": ([P, I64], C.c_int),
         "dfq_probe_lds": ([P, P, P, P, I64, I32, I32, P], C.c_int),
         "dfq_act_moments": ([P, P, I64, I32, I32, F32, I32, P, P, P], C.c_int),
         "dfq_act_minmax": ([P, P, I64, I32, F32, F32, P, P], C.c_int),

@@ -44,22 +44,26 @@ struct Variant {
     int max_rows;
     bool prefetch;
 };
+// max_rows: rows of one whole-row task; the host caps rows per task at
+// max(64 (one short row per lane), chunk / 32) (build()), so the per-row
+// parameter arrays (scale, min) take 2 * max_rows floats per wave.
 constexpr Variant kVariants[] = {
-    {2048, 256, false},   // 0: 10 KB LDS / wave, 16 waves / CU
-    {1024, 128, true},    // 1: 2 x 4 KB + 1 KB, next task's DMA in flight during compute
-    {2048, 256, true},    // 2: 2 x 8 KB + 2 KB
-    {1024, 128, false},   // 3: 5 KB / wave, 28 waves / CU
-    {4096, 256, false},   // 4: 18 KB / wave, 8 waves / CU
-    {2048, 256, false},   // 5: variant 0 with non-temporal loads and stores
-    {2048, 256, false},   // 6: variant 5, KH*KW sums specialised for 3x3 only (fewer VGPRs)
-    {2048, 256, false},   // 7: variant 5, generic KH*KW sums only
-    {2560, 256, false},   // 8: variant 6 with 2560-element tasks (12 waves / CU)
-    {1024, 128, false},   // 9: variant 6 with 1024-element tasks (32 waves / CU)
-    {1536, 192, false},   // 10: variant 6 with 1536-element tasks (20 waves / CU)
-    {1024, 128, true},    // 11: 1024-element tasks, next task's DMA in flight (16 waves / CU), NT
-    {1024, 128, false},   // 12: variant 9 with the generic E sums (fewer VGPRs)
+    {2048, 64, false},    // 0: 8.5 KB LDS / wave, 16 waves / CU
+    {1024, 64, true},     // 1: 2 x 4 KB, next task's DMA in flight during compute
+    {2048, 64, true},     // 2: 2 x 8 KB
+    {1024, 64, false},    // 3: 4.5 KB / wave
+    {4096, 128, false},   // 4: 17 KB / wave, 8 waves / CU
+    {2048, 64, false},    // 5: variant 0 with non-temporal loads and stores
+    {2048, 64, false},    // 6: variant 5, KH*KW sums specialised for 3x3 only (fewer VGPRs)
+    {2048, 64, false},    // 7: variant 5, generic KH*KW sums only
+    {2560, 80, false},    // 8: variant 6 with 2560-element tasks (12 waves / CU)
+    {1024, 64, false},    // 9: variant 6 with 1024-element tasks
+    {1536, 64, false},    // 10: variant 6 with 1536-element tasks
+    {1024, 64, true},     // 11: 1024-element tasks, next task's DMA in flight, NT
+    {1024, 64, false},    // 12: variant 9 with the generic E sums (fewer VGPRs)
+    {2048, 64, false},    // 13: variant 6 + per-task timestamps (diagnostics: dfq_debug_timeline)
 };
-constexpr int kNumVariants = 13;
+constexpr int kNumVariants = 14;
 constexpr int kDefaultVariant = 6;   // = 5 with 87 instead of 105 VGPRs (profiles/r01/ab_*_v568.json)
 
 struct alignas(16) DevTensor {
@@ -400,7 +404,12 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
     wave_lds_sync();  // LDS is reused by this wave's next task
 }
 
-template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false, int ESPEC = 2>
+// Diagnostics timeline (variant 13): per main-list task {start, data landed, done}
+// in s_memrealtime ticks (100 MHz) plus the executing wave's hardware ids.
+__device__ uint64_t* g_timeline = nullptr;
+__device__ int64_t g_timeline_cap = 0;
+
+template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false, int ESPEC = 2, bool TL = false>
 __global__ void __launch_bounds__(kBlockThreads)
 sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restrict__ tasks, int64_t ntasks,
                   const uint32_t* __restrict__ slot_min, const uint32_t* __restrict__ slot_max) {
@@ -418,11 +427,14 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
         DevTask task;
         if (wave0 < ntasks) task = tasks[wave0];
         for (int64_t t = wave0; t < ntasks; t += nwaves) {
+            uint64_t tl0 = 0, tl1 = 0;
+            if constexpr (TL) tl0 = wall_clock64();
             const DevTensor T = tensors[task.tensor];
             issue_task_load<NT>(T, task, wl, lane);
             DevTask next = task;   // next record's scalar load overlaps this task
             if (t + nwaves < ntasks) next = tasks[t + nwaves];
             vm_wait_all();
+            if constexpr (TL) tl1 = wall_clock64();
             wave_lds_sync();
             float bmn = 0.f, bmx = 0.f;
             if (task.nrows < 0) {   // block-row piece: all 4 waves of this block are here
@@ -464,6 +476,20 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                 compute_task<MAXROWS, true, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
             else
                 compute_task<MAXROWS, false, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
+            if constexpr (TL) {
+                if (lane == 0 && t < g_timeline_cap) {
+                    uint32_t hw;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                    uint32_t xcc;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                    const uint64_t tl2 = wall_clock64();
+                    uint64_t* r = g_timeline + 4 * t;
+                    r[0] = tl0;
+                    r[1] = tl1;
+                    r[2] = tl2;
+                    r[3] = ((uint64_t)xcc << 32) | hw;
+                }
+            }
             task = next;
         }
     } else {
@@ -717,21 +743,24 @@ static int lds_bytes(const Variant& V) {
 using MainKernel = void (*)(const DevTensor*, const DevTask*, int64_t, const uint32_t*, const uint32_t*);
 
 static MainKernel main_kernel(int variant) {
+#define DFQ_V(i) kVariants[i].chunk, kVariants[i].max_rows, kVariants[i].prefetch
     switch (variant) {
-        case 1: return sweep_main_kernel<1024, 128, true>;
-        case 2: return sweep_main_kernel<2048, 256, true>;
-        case 3: return sweep_main_kernel<1024, 128, false>;
-        case 4: return sweep_main_kernel<4096, 256, false>;
-        case 5: return sweep_main_kernel<2048, 256, false, true>;
-        case 6: return sweep_main_kernel<2048, 256, false, true, 1>;
-        case 7: return sweep_main_kernel<2048, 256, false, true, 0>;
-        case 8: return sweep_main_kernel<2560, 256, false, true, 1>;
-        case 9: return sweep_main_kernel<1024, 128, false, true, 1>;
-        case 10: return sweep_main_kernel<1536, 192, false, true, 1>;
-        case 11: return sweep_main_kernel<1024, 128, true, true, 1>;
-        case 12: return sweep_main_kernel<1024, 128, false, true, 0>;
-        default: return sweep_main_kernel<2048, 256, false>;
+        case 1: return sweep_main_kernel<DFQ_V(1)>;
+        case 2: return sweep_main_kernel<DFQ_V(2)>;
+        case 3: return sweep_main_kernel<DFQ_V(3)>;
+        case 4: return sweep_main_kernel<DFQ_V(4)>;
+        case 5: return sweep_main_kernel<DFQ_V(5), true>;
+        case 6: return sweep_main_kernel<DFQ_V(6), true, 1>;
+        case 7: return sweep_main_kernel<DFQ_V(7), true, 0>;
+        case 8: return sweep_main_kernel<DFQ_V(8), true, 1>;
+        case 9: return sweep_main_kernel<DFQ_V(9), true, 1>;
+        case 10: return sweep_main_kernel<DFQ_V(10), true, 1>;
+        case 11: return sweep_main_kernel<DFQ_V(11), true, 1>;
+        case 12: return sweep_main_kernel<DFQ_V(12), true, 0>;
+        case 13: return sweep_main_kernel<DFQ_V(13), true, 1, true>;
+        default: return sweep_main_kernel<DFQ_V(0)>;
     }
+#undef DFQ_V
 }
 
 // Grid: up to 64 blocks per CU (16384 blocks), far more than are resident (4-5
@@ -1004,5 +1033,14 @@ extern "C" int dfq_quantize_tensor(const dfq_tensor_desc* d, void* ws, size_t ws
     // runtime has consumed them (pageable memcpy is host-synchronous on ROCm, but
     // do not rely on it for correctness).
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
+    return DFQ_OK;
+}
+
+// Diagnostics: point variant 13's timeline at `buf` (4 uint64 per main-list task,
+// `cap` tasks); NULL/0 disables.  Not part of the reference interface.
+extern "C" int dfq_debug_timeline(void* buf, int64_t cap) {
+    uint64_t* p = static_cast<uint64_t*>(buf);
+    DFQ_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), &p, sizeof(p)));
+    DFQ_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_timeline_cap), &cap, sizeof(cap)));
     return DFQ_OK;
 }

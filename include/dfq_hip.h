@@ -261,6 +261,10 @@ int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_
  * the sweep's traffic mix; not part of the reference interface. */
 int dfq_probe_stream(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t blocks,
                      void* stream);
+/* Per-task timeline of sweep variant 13 (DFQ_SWEEP_VARIANT=13): 4 uint64 per
+ * main-list task {start, data landed, done (s_memrealtime, 100 MHz), xcc<<32|hw_id};
+ * buf NULL / cap 0 disables. */
+int dfq_debug_timeline(void* buf, int64_t cap);
 /* The sweep's memory pattern without arithmetic: 2048-element wave tasks through
  * LDS-DMA, non-temporal dq / codes / E stores (copy_only: dq only).  n % 2048 == 0. */
 int dfq_probe_lds(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t copy_only,

@@ -1,0 +1,51 @@
+"""Per-task timeline of one single-model sweep (diagnostic, GPU; variant 13).
+
+usage: python scripts/timeline.py [model] [copies]
+Prints the kernel span and, per phase, when tasks started / had their data /
+finished (us from the first task start), plus latency percentiles.  Timestamps
+are s_memrealtime (100 MHz, 10 ns resolution)."""
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+os.environ["DFQ_SWEEP_VARIANT"] = "13"
+import bench  # noqa: E402
+from data_free_quantization_amd import _lib  # noqa: E402
+from data_free_quantization_amd.sweep import SweepPlan  # noqa: E402
+
+model = sys.argv[1] if len(sys.argv) > 1 else "mobilenetv2"
+copies = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+dev = torch.device("cuda:0")
+stream = torch.cuda.current_stream(dev)
+items, _, _, _ = bench.build_batch(model, dev, copies=copies, seed=5)
+plan = SweepPlan(items)
+n = plan.stats["n_tasks_main"]
+buf = torch.zeros(4 * n, dtype=torch.int64, device=dev)
+L = _lib.load()
+us = bench.time_plan(plan, stream, dev, 100, 10) * 1e3
+_lib.check(L.dfq_debug_timeline(buf.data_ptr(), n), "timeline")
+for _ in range(3):
+    plan.execute(stream)
+torch.cuda.synchronize(dev)
+_lib.check(L.dfq_debug_timeline(None, 0), "timeline off")
+r = buf.view(n, 4).cpu().numpy().astype(np.int64)
+t0 = r[:, 0].min()
+start, landed, done = [(r[:, k] - t0) / 100.0 for k in range(3)]   # us
+q = lambda a: [round(float(np.percentile(a, p)), 2) for p in (0, 10, 50, 90, 99, 100)]
+out = {"model": model, "copies": copies, "tasks": n, "grid": plan.stats["grid_blocks"], "event_us": round(us, 2),
+       "span_us": round(float(done.max()), 2),
+       "start_pct": q(start), "landed_pct": q(landed), "done_pct": q(done),
+       "load_lat_pct": q(landed - start), "compute_pct": q(done - landed)}
+# how many waves were live over time (1 us bins)
+bins = np.arange(0, done.max() + 1.0, 1.0)
+live = [int(((start <= b) & (done > b)).sum()) for b in bins]
+out["live_tasks_per_us"] = live
+xcc = (r[:, 3] >> 32)
+out["tasks_per_xcc"] = np.bincount(xcc, minlength=8).tolist()
+print(json.dumps(out))
+plan.destroy()
