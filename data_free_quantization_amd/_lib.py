@@ -24,7 +24,7 @@ DFQ_ERR_NOMEM, DFQ_ERR_SHAPE, DFQ_ERR_WORKSPACE = -4, -5, -6
 
 EXPORTS = [
     "dfq_abi_version", "dfq_error_string", "dfq_last_hip_error",
-    "dfq_quantize_ws_bytes", "dfq_quantize_tensor", "dfq_chunk_range",
+    "dfq_quantize_ws_bytes", "dfq_quantize_tensor", "dfq_chunk_range", "dfq_range", "dfq_fake_quant_given",
     "dfq_sweep_plan_create", "dfq_sweep_plan_ws_bytes", "dfq_sweep_plan_create_ws", "dfq_sweep_plan_execute",
     "dfq_sweep_plan_stats", "dfq_sweep_plan_destroy",
     "dfq_bn_fold", "dfq_bn_fold_ws_bytes", "dfq_bn_fold_batch", "dfq_clamp",
@@ -96,6 +96,8 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_quantize_ws_bytes": ([C.POINTER(TensorDesc), C.POINTER(SZ)], C.c_int),
         "dfq_quantize_tensor": ([C.POINTER(TensorDesc), P, SZ, P], C.c_int),
         "dfq_chunk_range": ([P, I64, I64, P, P, P], C.c_int),
+        "dfq_range": ([P, I64, P, P], C.c_int),
+        "dfq_fake_quant_given": ([P, P, I64, I32, I32, I32, P, P, P, F64, F64, P], C.c_int),
         "dfq_sweep_plan_create": ([C.POINTER(TensorDesc), I32, C.POINTER(P)], C.c_int),
         "dfq_sweep_plan_ws_bytes": ([C.POINTER(TensorDesc), I32], C.c_int64),
         "dfq_sweep_plan_create_ws": ([C.POINTER(TensorDesc), I32, P, I64, P, C.POINTER(P)], C.c_int),

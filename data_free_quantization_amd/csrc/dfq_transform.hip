@@ -339,6 +339,71 @@ __global__ void bn_fold_channel_batch_kernel(const BnFoldJob* __restrict__ jobs,
 }
 
 // ---------------------------------------------------------------------------
+// Activation fake quant with a given range (QuantMeasure.forward at inference,
+// utils/quantize.py:112-126 -> quantize(input, b, float(min), float(max))):
+// elementwise, async, no workspace.  The range may live in device memory (the
+// observer's running_min / running_max), read as the exact doubles float()
+// would produce, so no host round trip is needed.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads)
+fq_given_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, int bits, int sym, int flags,
+                const float* __restrict__ min_dev, const float* __restrict__ max_dev,
+                const uint32_t* __restrict__ range_enc, double gmin, double gmax, int vec4) {
+    if (min_dev) gmin = (double)min_dev[0];
+    if (max_dev) gmax = (double)max_dev[0];
+    if (range_enc) {   // dfq_range's {~enc(min), enc(max)}
+        gmin = (double)dec_ord(~range_enc[0]);
+        gmax = (double)dec_ord(range_enc[1]);
+    }
+    const QParams p = make_qparams((float)gmin, (float)gmax, bits, sym != 0, flags | DFQ_GIVEN_RANGE, gmin, gmax);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    float q;
+    if (vec4) {
+        const int64_t n4 = n >> 2;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+            const float4 v = reinterpret_cast<const float4*>(x)[i];
+            float4 o;
+            o.x = qdq(v.x, p, q);
+            o.y = qdq(v.y, p, q);
+            o.z = qdq(v.z, p, q);
+            o.w = qdq(v.w, p, q);
+            reinterpret_cast<float4*>(y)[i] = o;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = qdq(x[i], p, q);
+    }
+}
+
+// Whole-tensor (min, max) as order-preserving uints: {max ~enc(x), max enc(x)}, so
+// one zero memset initialises both words (exact, order-independent).
+__global__ void __launch_bounds__(kThreads)
+range_enc_kernel(const float* __restrict__ x, int64_t n, uint32_t* __restrict__ enc) {
+    __shared__ float smn[kThreads / kWave], smx[kThreads / kWave];
+    float a = INFINITY, b = -INFINITY;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        a = fminf(a, v);
+        b = fmaxf(b, v);
+    }
+    a = wave_min(a);
+    b = wave_max(b);
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+    if (lane == 0) {
+        smn[w] = a;
+        smx[w] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kThreads / kWave; ++k) {
+            a = fminf(a, smn[k]);
+            b = fmaxf(b, smx[k]);
+        }
+        atomicMax(&enc[0], ~enc_ord(a));
+        atomicMax(&enc[1], enc_ord(b));
+    }
+}
+
+// ---------------------------------------------------------------------------
 // quantize()'s data range with num_chunks (utils/quantize.py:26-37):
 // y = x.view(rows, -1); min = y.min(-1)[0].mean(-1), max likewise (fp32).
 // ---------------------------------------------------------------------------
@@ -585,6 +650,32 @@ extern "C" int dfq_chunk_range(const float* x, int64_t rows, int64_t row_len, fl
                        rowbuf + rows);
     DFQ_LAUNCH_CHECK();
     hipLaunchKernelGGL(chunk_mean_kernel, dim3(1), dim3(kWave), 0, s, rowbuf, rowbuf + rows, rows, out2);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+extern "C" int dfq_range(const float* x, int64_t n, uint32_t* range_enc, void* stream) {
+    if (n < 1 || !x || !range_enc) return DFQ_ERR_INVALID;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DFQ_HIP_CHECK(hipMemsetAsync(range_enc, 0, 2 * sizeof(uint32_t), s));
+    const int grid = (int)std::min<int64_t>(ceil_div(n, (int64_t)kThreads * 8), 2048);
+    hipLaunchKernelGGL(range_enc_kernel, dim3(std::max(grid, 1)), dim3(kThreads), 0, s, x, n, range_enc);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+extern "C" int dfq_fake_quant_given(const float* x, float* y, int64_t n, int32_t bits, int32_t symmetric,
+                                    int32_t flags, const float* min_dev, const float* max_dev,
+                                    const uint32_t* range_enc, double given_min, double given_max, void* stream) {
+    if (n < 0 || (n > 0 && (!x || !y)) || bits < 2 || bits > 16) return DFQ_ERR_INVALID;
+    if (flags & ~(DFQ_SCALE_F32)) return DFQ_ERR_INVALID;
+    if (n == 0) return DFQ_OK;
+    const int vec4 = (n % 4 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
+                     (reinterpret_cast<uintptr_t>(y) % 16 == 0);
+    const int64_t work = vec4 ? n / 4 : n;
+    const int grid = (int)std::min<int64_t>(ceil_div(work, (int64_t)kThreads * 4), 16384);
+    hipLaunchKernelGGL(fq_given_kernel, dim3(std::max(grid, 1)), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                       x, y, n, bits, symmetric, flags, min_dev, max_dev, range_enc, given_min, given_max, vec4);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }

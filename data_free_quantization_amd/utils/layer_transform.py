@@ -514,73 +514,69 @@ def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchN
 
 
 _RAW_OPS = {}
-_MODE = None
+_IN_QUANT = False   # re-entrancy guard: ops inside a quantizer are never intercepted
 
 
-def _quantized_call(func, args, kwargs):
+def _quantized_call(func, kind, args, kwargs):
     """Apply the op node's QuantMeasures to the call's tensor inputs (the reference's
     ___add__ / torch_cat / torch_mean / F_interpolate / F_softmax,
-    utils/layer_transform.py:18-124)."""
+    utils/layer_transform.py:18-124), then run the original op."""
+    global _IN_QUANT
     key = module_tensor_op.next_name()
     qs = module_tensor_op.get(key)
-    if func in _ADD_FUNCS:
-        args = (qs[0](args[0]), qs[1](args[1])) + tuple(args[2:])
-    elif func is torch.cat:
-        seq = args[0] if args else kwargs.pop("tensors")
-        args = (type(seq)(q(t) for q, t in zip(qs, seq)),) + tuple(args[1:])
-    else:
-        args = (qs[0](args[0]),) + tuple(args[1:])
+    _IN_QUANT = True
+    try:
+        if kind == "add":
+            args = (qs[0](args[0]), qs[1](args[1])) + tuple(args[2:])
+        elif kind == "cat":
+            seq = args[0] if args else kwargs.pop("tensors")
+            args = (type(seq)(q(t) for q, t in zip(qs, seq)),) + tuple(args[1:])
+        else:
+            args = (qs[0](args[0]),) + tuple(args[1:])
+    finally:
+        _IN_QUANT = False
     return func(*args, **kwargs)
 
 
-def _op_kind(func):
-    if func in _ADD_FUNCS:
-        return "add"
-    if func is torch.cat:
-        return "cat"
-    if func is torch.mean:
-        return "mean"
-    if func is torch.nn.functional.interpolate:
-        return "interpolate"
-    if func is torch.nn.functional.softmax:
-        return "softmax"
-    return None
+def _wrap(raw, kind):
+    """The patched op: intercepted only when the graph's next op node is this kind
+    (execution order, as the reference's name check does without inspect.stack)."""
+    def op(*args, **kwargs):
+        m = module_tensor_op
+        if not _IN_QUANT and m is not None and m.names and kind in m.names[m.idx_name_tensor_op]:
+            return _quantized_call(raw, kind, args, kwargs)
+        return raw(*args, **kwargs)
+    op.__name__ = getattr(raw, "__name__", kind)
+    op.__wrapped__ = raw
+    return op
 
 
-_ADD_FUNCS = (torch.Tensor.__add__, torch.Tensor.add, torch.Tensor.__iadd__, torch.add)
-
-
-class _TensorOpMode(torch.overrides.TorchFunctionMode):
-    """Routes add / cat / mean / interpolate / softmax calls through the
-    quantizers of the graph node they execute (replace_op)."""
-
-    def __torch_function__(self, func, types, args=(), kwargs=None):
-        kwargs = kwargs or {}
-        kind = _op_kind(func)
-        if kind is not None and module_tensor_op is not None and module_tensor_op.names:
-            expect = module_tensor_op.names[module_tensor_op.idx_name_tensor_op]
-            if kind in expect:
-                return _quantized_call(func, args, kwargs)
-        return func(*args, **kwargs)
+# (owner, attribute, kind): Tensor.__add__ / __iadd__ / add, torch.add, torch.cat,
+# torch.mean, F.interpolate, F.softmax -- the reference's tensor_magic_op_supported,
+# torch_op_supported and func_op_sopprted lists (utils/layer_transform.py:128-144)
+_PATCHES = [(torch.Tensor, "__add__", "add"), (torch.Tensor, "__iadd__", "add"), (torch.Tensor, "add", "add"),
+            (torch, "add", "add"), (torch, "cat", "cat"), (torch, "mean", "mean"),
+            (torch.nn.functional, "interpolate", "interpolate"), (torch.nn.functional, "softmax", "softmax")]
 
 
 def replace_op():
     """Quantize the inputs of tensor ops during inference
-    (utils/layer_transform.py:128-144): a TorchFunctionMode that matches each
-    add / cat / mean / interpolate / softmax call to the next op node of the graph
-    instead of monkey-patching torch and inspecting the call stack."""
-    global _MODE
-    if _MODE is None:
-        _MODE = _TensorOpMode()
-        _MODE.__enter__()
+    (utils/layer_transform.py:128-144): patch the eight ops above with wrappers that
+    match each call to the next op node of the graph (no call-stack inspection);
+    every other op runs untouched."""
+    if _RAW_OPS:
+        return
+    for owner, name, kind in _PATCHES:
+        raw = getattr(owner, name)
+        _RAW_OPS[(owner, name)] = raw
+        setattr(owner, name, _wrap(raw, kind))
 
 
 def restore_op():
     """Undo replace_op (utils/layer_transform.py:147-158)."""
-    global _MODE
-    if _MODE is not None:
-        _MODE.__exit__(None, None, None)
-        _MODE = None
+    for (owner, name), raw in list(_RAW_OPS.items()):
+        setattr(owner, name, raw)
+    _RAW_OPS.clear()
 
 
 __all__ = ["merge_batchnorm", "quantize_targ_layer", "find_prev_bn", "switch_layers", "replace_op", "restore_op",

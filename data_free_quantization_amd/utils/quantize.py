@@ -179,6 +179,42 @@ def _data_range(x: torch.Tensor):
     return r1.zero[0].item(), -r2.zero[0].item()
 
 
+def _no_autograd(*tensors) -> bool:
+    """True when no STE backward is needed (inference): the async paths apply."""
+    return not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors))
+
+
+def device_range(x: torch.Tensor) -> torch.Tensor:
+    """dfq_range: the whole tensor's (min, max) on the device, async, as the
+    library's 2-word order-preserving encoding (input of fake_quant_given)."""
+    _lib.require_device(x)
+    xc = x.detach().contiguous()
+    enc = torch.empty(2, dtype=torch.int32, device=x.device)
+    _lib.check(_lib.load().dfq_range(_lib.ptr(xc), xc.numel(), _lib.ptr(enc), _lib.stream_of(xc)), "dfq_range",
+               RuntimeError)
+    return enc
+
+
+def fake_quant_given(x: torch.Tensor, num_bits: int = 8, symmetric: bool = False, *, min_dev=None, max_dev=None,
+                     range_enc=None, min_value=None, max_value=None, scale_f32: bool = False,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """quantize(x, num_bits, min, max, symmetric=...) with a given range as ONE
+    async elementwise launch (dfq_fake_quant_given): no workspace, no host sync.
+    The range comes from ``range_enc`` (device_range), or device scalars
+    ``min_dev`` / ``max_dev`` (read as float() would), or Python floats.
+    ``scale_f32``: the bounds were 0-d tensors in the reference call (fp32 scale)."""
+    _lib.require_device(x, out)
+    xc = x.detach().contiguous()
+    y = torch.empty_like(xc) if out is None else out
+    rc = _lib.load().dfq_fake_quant_given(
+        _lib.ptr(xc), _lib.ptr(y), xc.numel(), int(num_bits), int(bool(symmetric)),
+        _lib.DFQ_SCALE_F32 if scale_f32 else 0, _lib.ptr(min_dev), _lib.ptr(max_dev), _lib.ptr(range_enc),
+        float(min_value) if min_value is not None else 0.0, float(max_value) if max_value is not None else 0.0,
+        _lib.stream_of(xc))
+    _lib.check(rc, "dfq_fake_quant_given", ValueError)
+    return y
+
+
 def quantize(x, num_bits=8, min_value=None, max_value=None, inplace=False, symmetric=False, num_chunks=None):
     """utils/quantize.py:88-89."""
     return UniformQuantize.apply(x, num_bits, min_value, max_value, inplace, symmetric, num_chunks)
@@ -206,8 +242,11 @@ class QuantMeasure(nn.Module):
     def forward(self, input):
         flat = input.detach().view(input.size(0), -1)
         if self.update_stat:
-            self.running_max = max(self.running_max, flat.max(-1)[0].mean())
-            self.running_min = min(self.running_min, flat.min(-1)[0].mean())
+            # Python max(a, b) / min(a, b) on tensors: b if b > a (b < a) else a --
+            # as a device select instead of a host round trip
+            mx_new, mn_new = flat.max(-1)[0].mean(), flat.min(-1)[0].mean()
+            self.running_max = torch.where(mx_new > self.running_max, mx_new, self.running_max)
+            self.running_min = torch.where(mn_new < self.running_min, mn_new, self.running_min)
         if self.training:
             mn = flat.min(-1)[0].mean()
             mx = flat.max(-1)[0].mean()
@@ -215,6 +254,9 @@ class QuantMeasure(nn.Module):
             self.running_max.mul_(1 - self.momentum).add_(mx * self.momentum)
         else:
             mn, mx = self.running_min, self.running_max
+            if _no_autograd(input):   # inference: float(mn)/float(mx) read on the device, one async launch
+                input.shape[0]        # the reference's quantize() indexes shape[0]
+                return fake_quant_given(input, self.num_bits, min_dev=mn, max_dev=mx)
         return quantize(input, self.num_bits, min_value=float(mn), max_value=float(mx), num_chunks=16)
 
     def set_update_stat(self, update_stat):
@@ -226,6 +268,14 @@ class _QuantWeightMixin:
     fake-quant with float(min)/float(max), bias fake-quant with the data range."""
 
     def _qparams(self, weight, bias):
+        if _no_autograd(weight, bias):
+            # inference: float(weight.min()) / float(weight.max()) and the bias's own
+            # 0-d fp32 range stay on the device (dfq_range), one async launch each
+            qweight = fake_quant_given(weight, self.num_bits, range_enc=device_range(weight))
+            qbias = None
+            if bias is not None:
+                qbias = fake_quant_given(bias, self.num_bits_bias, range_enc=device_range(bias), scale_f32=True)
+            return qweight, qbias
         qweight = quantize(weight, num_bits=self.num_bits, min_value=float(weight.min()),
                            max_value=float(weight.max()))
         qbias = quantize(bias, num_bits=self.num_bits_bias) if bias is not None else None

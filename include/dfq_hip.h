@@ -101,6 +101,20 @@ int dfq_quantize_tensor(const dfq_tensor_desc* desc, void* ws, size_t ws_bytes, 
  * out2 = {mean_r min(x[r]), mean_r max(x[r])} in fp32, the mean in ATen's sum
  * order.  rowbuf: 2*rows device floats of scratch.  Async on `stream`. */
 int dfq_chunk_range(const float* x, int64_t rows, int64_t row_len, float* rowbuf, float* out2, void* stream);
+/* Whole-tensor (min, max) on the device, async: range_enc (2 device uint32) =
+ * {~enc(min), enc(max)} in the library's order-preserving encoding (the input of
+ * dfq_fake_quant_given); it is zeroed on `stream` first. */
+int dfq_range(const float* x, int64_t n, uint32_t* range_enc, void* stream);
+/* quantize(x, bits, min, max, symmetric) with a GIVEN range, elementwise and async
+ * (QuantMeasure.forward at inference, utils/quantize.py:112-126, and the Quant*
+ * layers' weight/bias fake quant, :225-238): the range is, by priority,
+ * range_enc (dfq_range's output), min_dev[0] / max_dev[0] (device floats, e.g. the
+ * observer's running_min / running_max, read as float() would: exact doubles), or
+ * given_min / given_max.  flags: 0 (scale in double: Python-float bounds) or
+ * DFQ_SCALE_F32 (0-d tensor bounds).  No workspace, no host synchronisation. */
+int dfq_fake_quant_given(const float* x, float* y, int64_t n, int32_t bits, int32_t symmetric, int32_t flags,
+                         const float* min_dev, const float* max_dev, const uint32_t* range_enc, double given_min,
+                         double given_max, void* stream);
 
 /* ---- grouped sweep over many tensors (replaces quantize_targ_layer,
  *      utils/layer_transform.py:288-305, fused with clip_weight.py:4-33 and the

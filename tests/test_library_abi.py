@@ -71,3 +71,10 @@ def test_product_rejects_cpu_tensors():
     from data_free_quantization_amd.utils.quantize import quantize
     with pytest.raises(RuntimeError, match="ROCm GPU"):
         quantize(torch.randn(4, 4), 8, -1.0, 1.0)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: a missing libdfq_hip.so raises instead of degrading."""
+    from data_free_quantization_amd import _lib
+    with pytest.raises(_lib.DFQLibraryError, match="no CPU fallback"):
+        _lib.load(tmp_path / "libdfq_hip.so")
