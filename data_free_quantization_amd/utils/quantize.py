@@ -254,9 +254,12 @@ class QuantMeasure(nn.Module):
             self.running_max.mul_(1 - self.momentum).add_(mx * self.momentum)
         else:
             mn, mx = self.running_min, self.running_max
-            if _no_autograd(input):   # inference: float(mn)/float(mx) read on the device, one async launch
-                input.shape[0]        # the reference's quantize() indexes shape[0]
-                return fake_quant_given(input, self.num_bits, min_dev=mn, max_dev=mx)
+        if _no_autograd(input):
+            # no STE backward: float(mn) / float(mx) are read on the device by one
+            # async launch (the reference's main_dfq runs its observers in training
+            # mode at inference -- set_layer_bits makes new ones -- so both branches)
+            input.shape[0]   # the reference's quantize() indexes shape[0]
+            return fake_quant_given(input, self.num_bits, min_dev=mn, max_dev=mx)
         return quantize(input, self.num_bits, min_value=float(mn), max_value=float(mx), num_chunks=16)
 
     def set_update_stat(self, update_stat):

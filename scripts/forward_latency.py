@@ -41,13 +41,19 @@ targ = (QuantConv2d, QuantLinear)
 L.merge_batchnorm(model, graph, bottoms, targ)
 set_layer_bits(graph, 8, 8, 8, targ)
 L.set_quant_minmax(graph, bottoms, verbose=False)
-model.eval()   # inference_all's model.eval(): set_layer_bits made new (training-mode) observers
+L.replace_op()
+try:   # as the reference's main_dfq runs it: set_layer_bits made new observers, left in training mode
+    train_obs_ms = timed(lambda: model(x))
+finally:
+    L.restore_op()
+model.eval()
 L.replace_op()
 try:
     q_ms = timed(lambda: model(x))
 finally:
     L.restore_op()
-print(json.dumps({"batch": batch, "fp32_ms": round(fp32_ms, 3), "quant_ms": round(q_ms, 3)}))
+print(json.dumps({"batch": batch, "fp32_ms": round(fp32_ms, 3), "quant_ms": round(q_ms, 3),
+                  "quant_training_mode_observers_ms": round(train_obs_ms, 3)}))
 
 # breakdown: observers frozen (no update_stat), then without the op interception
 for m in graph.values():
