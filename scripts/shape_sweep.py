@@ -24,6 +24,10 @@ FAMILIES = {
     "3x3_512x512(row4608)": (512, 512, 3, 3),
     "dw3x3_960x1": (960, 1, 3, 3),
     "fc_256x4096(row4096)": (256, 4096),
+    "fc_256x1024(row1024)": (256, 1024),
+    "fc_256x1152(row1152)": (256, 1152),
+    "fc_256x2304(row2304)": (256, 2304),
+    "fc_256x576(row576)": (256, 576),
 }
 
 
