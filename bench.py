@@ -372,13 +372,15 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (int8 codes)",
+            "dtype": "f32",
+            "codes": f"{args.bits}-bit grid indices stored as "
+                     f"{'int16' if args.bits > 8 else ('uint8' if args.asym else 'int8')}",
             "data": "synthetic random-init weights of the reference shapes (no checkpoints offline)",
             "config": {
                 "workload": f"{args.model} x{copies} weight sets per GPU: {args.granularity} "
                             f"{'asym' if args.asym else 'sym'} INT{args.bits} quantize-dequantize + codes + "
                             f"clip[-15,15]" + ("" if args.no_esum else " + bias-correction error sums"),
-                "model": args.model,
+                "weight_shapes": f"{args.model} target layers (SURVEY.md 8, synthetic init)",
                 "copies_per_gpu": copies,
                 "layers_per_copy": len(shapes),
                 "weights_per_copy": per_copy,
