@@ -83,7 +83,7 @@ def synth_weight(s, dev, gen):
     return torch.randn(s, device=dev, generator=gen) * std
 
 
-def build_batch(model, dev, copies=0, bits=8, channel=True, sym=True, esum=True, seed=1234):
+def build_batch(model, dev, copies=0, bits=8, channel=True, sym=True, esum=True, seed=1234, pack=False):
     """Synthetic weight sets of the model's target-layer shapes, generated on the
     GPU; ``copies`` = 0 picks enough for >= 2 GiB of fp32 weights (past the
     256 MB Infinity Cache)."""
@@ -97,7 +97,7 @@ def build_batch(model, dev, copies=0, bits=8, channel=True, sym=True, esum=True,
         for s in shapes:
             w = synth_weight(s, dev, gen)
             items.append(allocate(w, bits=bits, per_channel=channel, symmetric=sym, khw=khw_of(w), want_esum=esum,
-                                  clip=(-15.0, 15.0)))
+                                  clip=(-15.0, 15.0), pack_int4=pack))
     return items, shapes, per_copy, copies
 
 
@@ -120,6 +120,7 @@ SECONDARY = [
     ("resnet50 per-ch sym INT8 + clip + BC error sums", "resnet50", 8, True, True, True),
     ("deeplab per-ch sym INT8 + clip + BC error sums", "deeplab", 8, True, True, True),
     ("resnet50 per-ch asym INT4 + clip", "resnet50", 4, True, False, False),
+    ("resnet50 per-ch asym INT4 + clip, packed int4 codes", "resnet50", 4, True, False, False, True),
     ("mobilenetv2 per-tensor asym INT8 (quantize_targ_layer) + clip", "mobilenetv2", 8, False, False, False),
 ]
 
@@ -130,8 +131,9 @@ def secondary_configs(dev, stream, steps=20):
     checked on ResNet-50 as well as MobileNetV2."""
     from data_free_quantization_amd.sweep import SweepPlan
     out = []
-    for name, model, bits, ch, sym, es in SECONDARY:
-        items, _, per_copy, copies = build_batch(model, dev, bits=bits, channel=ch, sym=sym, esum=es, seed=99)
+    for name, model, bits, ch, sym, es, *pack in SECONDARY:
+        items, _, per_copy, copies = build_batch(model, dev, bits=bits, channel=ch, sym=sym, esum=es, seed=99,
+                                                 pack=bool(pack and pack[0]))
         plan = SweepPlan(items)
         ms = time_plan(plan, stream, dev, steps, 3)
         st = plan.stats
@@ -170,9 +172,9 @@ def sharded_single_model(dev, stream, world, reps=20):
     from data_free_quantization_amd.sweep import khw_of
     gen = torch.Generator(device=dev).manual_seed(7)            # same weights on every rank
     ws = [synth_weight(s, dev, gen) for s in model_shapes("resnet50")]
-    specs = [D.output_spec(w, True, 4, False, khw_of(w), False) for w in ws]
+    specs = [D.output_spec(w, True, 4, False, khw_of(w), False, pack_int4=True) for w in ws]
     compute = D.gpu_sweep(ws, bits=4, per_channel=True, symmetric=False, want_esum=False, clip=(-15.0, 15.0),
-                          reuse=True)
+                          reuse=True, pack_int4=True)
     res = {}
     for gather in ("none", "all"):
         for _ in range(3):

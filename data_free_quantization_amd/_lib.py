@@ -18,7 +18,7 @@ PKG = Path(__file__).resolve().parent
 LIB_PATH = PKG / "libdfq_hip.so"
 
 DFQ_TENSOR_ASYM, DFQ_TENSOR_SYM, DFQ_CHANNEL_ASYM, DFQ_CHANNEL_SYM = 0, 1, 2, 3
-DFQ_CLIP, DFQ_GIVEN_RANGE, DFQ_SCALE_F32 = 0x1, 0x2, 0x4
+DFQ_CLIP, DFQ_GIVEN_RANGE, DFQ_SCALE_F32, DFQ_PACK_INT4 = 0x1, 0x2, 0x4, 0x8
 DFQ_OK, DFQ_ERR_INVALID, DFQ_ERR_HIP, DFQ_ERR_UNSUPPORTED = 0, -1, -2, -3
 DFQ_ERR_NOMEM, DFQ_ERR_SHAPE, DFQ_ERR_WORKSPACE = -4, -5, -6
 

@@ -339,6 +339,10 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
                     const uint32_t c = ((uint32_t)(uint8_t)(int)q0) | ((uint32_t)(uint8_t)(int)q1 << 8) |
                                        ((uint32_t)(uint8_t)(int)q2 << 16) | ((uint32_t)(uint8_t)(int)q3 << 24);
                     st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, c);
+                } else if (T.code_bytes == 0) {   // DFQ_PACK_INT4: 4 codes -> 2 bytes (base % 4 == 0)
+                    const uint32_t c = ((uint32_t)(int)q0 & 0xFu) | (((uint32_t)(int)q1 & 0xFu) << 4) |
+                                       (((uint32_t)(int)q2 & 0xFu) << 8) | (((uint32_t)(int)q3 & 0xFu) << 12);
+                    st<NT>(reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(T.codes) + base / 2) + j, (uint16_t)c);
                 } else {
                     const uint64_t c = ((uint64_t)(uint16_t)(int)q0) | ((uint64_t)(uint16_t)(int)q1 << 16) |
                                        ((uint64_t)(uint16_t)(int)q2 << 32) | ((uint64_t)(uint16_t)(int)q3 << 48);
@@ -350,6 +354,29 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
                 if (khw == 1) st<NT>(reinterpret_cast<float4*>(T.esum + base) + j, ev);
                 else reinterpret_cast<float4*>(data)[j] = ev;
             }
+        }
+    } else if (T.codes && T.code_bytes == 0) {
+        // packed nibbles on the scalar path: the task starts at an even element
+        // (build()), so even lanes own a byte and take the odd neighbour's code by
+        // a shuffle; every lane runs every step so the shuffle sees defined values
+        for (int e0 = 0; e0 < n; e0 += kWave) {
+            const int e = e0 + lane;
+            const bool ok = e < n;
+            uint32_t qi = 0;
+            if (ok) {
+                const float xv = data[e];
+                float qv;
+                const float yv = one(xv, params_for(e), qv);
+                if (T.dst) st<false>(T.dst + base + e, yv);
+                qi = (uint32_t)(int)qv & 0xFu;
+                if (want_e) {
+                    if (khw == 1) st<false>(T.esum + base + e, yv - xv);
+                    else data[e] = yv - xv;
+                }
+            }
+            const uint32_t hi = (uint32_t)__shfl_down((int)qi, 1, kWave);
+            if (ok && (e & 1) == 0)
+                st<false>(static_cast<uint8_t*>(T.codes) + (base + e) / 2, (uint8_t)(qi | (hi << 4)));
         }
     } else {
 #pragma unroll 4
@@ -557,20 +584,21 @@ static DevTensor to_dev(const dfq_tensor_desc& d) {
     t.flags = d.flags; t.clip_lo = d.clip_lo; t.clip_hi = d.clip_hi;
     t.given_min = d.given_min; t.given_max = d.given_max;
     t.inv_len = d.row_len > 0 ? 1.0f / (float)d.row_len : 0.f;
-    t.code_bytes = d.bits <= 8 ? 1 : 2;
+    t.code_bytes = (d.flags & DFQ_PACK_INT4) ? 0 : (d.bits <= 8 ? 1 : 2);   // 0: packed nibbles
     const int64_t n = d.rows * d.row_len;
     const bool channel = d.mode >= DFQ_CHANNEL_ASYM;
     bool v = (n % 4 == 0) && aligned(d.src, 16) && (!d.dst || aligned(d.dst, 16)) &&
-             (!d.codes || aligned(d.codes, 4 * t.code_bytes)) &&
+             (!d.codes || aligned(d.codes, t.code_bytes ? 4 * t.code_bytes : 2)) &&
              (!d.esum || d.khw > 1 || aligned(d.esum, 16));
     if (channel) v = v && (d.row_len % 4 == 0);
     t.vec4 = v ? 1 : 0;
     return t;
 }
 
-// Piece length: a multiple of khw (E sums never straddle a piece) and of 4 (vec4).
-static int piece_len(int khw, bool vec4, int chunk) {
-    const int unit = vec4 ? std::lcm(4, khw) : khw;
+// Piece length: a multiple of khw (E sums never straddle a piece), of 4 (vec4)
+// and of 2 (packed nibbles: a byte never straddles two tasks).
+static int piece_len(int khw, bool vec4, int chunk, bool packed = false) {
+    const int unit = vec4 ? std::lcm(4, khw) : (packed ? std::lcm(2, khw) : khw);
     int p = (chunk / unit) * unit;
     return p > 0 ? p : -1;
 }
@@ -628,12 +656,19 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
         int rc = validate(d);
         if (rc) return rc;
         DevTensor T = to_dev(d);
+        const bool packed = (d.flags & DFQ_PACK_INT4) != 0;
+        if (packed && d.bits > 4) return DFQ_ERR_INVALID;
+        // packed codes need every task to start at an even element: per channel,
+        // odd rows must come in pairs within one whole-row task (row_len <= chunk/2)
+        if (packed && d.mode >= DFQ_CHANNEL_ASYM && (d.row_len & 1) && 2 * d.row_len > kChunk &&
+            d.rows > 1)
+            return DFQ_ERR_UNSUPPORTED;
         const int64_t total = d.rows * d.row_len;
         B.elems += total;
         // algorithmic bytes: read x, write dq / codes / E / per-row params once
         int64_t bytes = 4 * total;
         if (d.dst) bytes += 4 * total;
-        if (d.codes) bytes += (int64_t)T.code_bytes * total;
+        if (d.codes) bytes += T.code_bytes ? (int64_t)T.code_bytes * total : total / 2;
         if (d.esum) bytes += 4 * (total / d.khw);
         const bool channel = d.mode >= DFQ_CHANNEL_ASYM;
         const int64_t nparams = channel ? d.rows : 1;
@@ -642,7 +677,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
         B.algo_bytes += bytes;
         B.tensors.push_back(T);
         if (total == 0) continue;
-        const int plen = piece_len(d.khw, T.vec4, kChunk);
+        const int plen = piece_len(d.khw, T.vec4, kChunk, packed);
         if (plen <= 0) return DFQ_ERR_UNSUPPORTED;   // khw > kChunk
         const bool given = (d.flags & DFQ_GIVEN_RANGE) != 0;
         const int64_t blen = channel ? d.row_len : total;   // the range's extent
@@ -654,7 +689,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
             // the group waits for its slowest wave.
             const int64_t nr = channel ? d.rows : 1;
             const int gs = blen <= 2 * (int64_t)plen ? 2 : kWavesPerBlock;
-            const int64_t unit = T.vec4 ? std::lcm<int64_t>(4, d.khw) : d.khw;
+            const int64_t unit = T.vec4 ? std::lcm<int64_t>(4, d.khw) : (packed ? std::lcm<int64_t>(2, d.khw) : d.khw);
             const int64_t bpl = ceil_div(ceil_div(blen, unit), (int64_t)gs) * unit;
             const int64_t rows_per_group = kWavesPerBlock / gs;
             for (int64_t r0 = 0; r0 < nr; r0 += rows_per_group) {
@@ -678,7 +713,8 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
             // the scalar path: at most one row per lane keeps such a task's latency
             // near a vector task's (single-model sweeps are latency-bound)
             const int64_t row_cap = d.row_len < 32 ? kWave : kMaxRows;
-            const int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(row_cap, kChunk / d.row_len));
+            int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(row_cap, kChunk / d.row_len));
+            if (packed && (d.row_len & 1) && rpt > 1) rpt &= ~int64_t(1);   // even task starts
             for (int64_t r = 0; r < d.rows; r += rpt) {
                 const int64_t nr = std::min<int64_t>(rpt, d.rows - r);
                 DevTask k{};

@@ -58,10 +58,11 @@ def _layout(spec: Dict) -> List[tuple]:
 
 
 def output_spec(weight: torch.Tensor, per_channel: bool, bits: int, symmetric: bool, khw: int,
-                want_esum: bool) -> Dict:
+                want_esum: bool, pack_int4: bool = False) -> Dict:
     rows = weight.shape[0] if per_channel else 1
     cdt = (torch.int8 if symmetric else torch.uint8) if bits <= 8 else torch.int16
-    spec = {"dq": (tuple(weight.shape), torch.float32), "codes": (tuple(weight.shape), cdt),
+    cshape = ((weight.numel() + 1) // 2,) if pack_int4 else tuple(weight.shape)
+    spec = {"dq": (tuple(weight.shape), torch.float32), "codes": (cshape, torch.uint8 if pack_int4 else cdt),
             "scale": ((rows,), torch.float32), "zero": ((rows,), torch.float32)}
     if want_esum:
         spec["esum"] = ((weight.numel() // khw,), torch.float32)
@@ -154,7 +155,7 @@ def max_over_ranks(value: float, device=None, group=None) -> float:
 
 
 def gpu_sweep(weights: Sequence[torch.Tensor], bits=8, per_channel=True, symmetric=True, want_esum=True,
-              clip=None, reuse: bool = False) -> Callable[[List[int]], List[LayerOut]]:
+              clip=None, reuse: bool = False, pack_int4: bool = False) -> Callable[[List[int]], List[LayerOut]]:
     """The product compute for ``sharded_sweep``: one grouped HIP sweep over the
     rank's layers (SweepPlan).  ``reuse``: keep the plan and its output buffers
     for the next call with the same layers (repeated passes overwrite them)."""
@@ -167,7 +168,8 @@ def gpu_sweep(weights: Sequence[torch.Tensor], bits=8, per_channel=True, symmetr
             plan, items = cache[key]
         else:
             items = [allocate(weights[i], bits=bits, per_channel=per_channel, symmetric=symmetric,
-                              khw=khw_of(weights[i]), want_esum=want_esum, clip=clip) for i in indices]
+                              khw=khw_of(weights[i]), want_esum=want_esum, clip=clip, pack_int4=pack_int4)
+                     for i in indices]
             plan = SweepPlan(items) if items else None
             if reuse:
                 cache[key] = (plan, items)

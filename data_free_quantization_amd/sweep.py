@@ -30,6 +30,7 @@ class SweepItem:
     khw: int = 1
     clip: Optional[Sequence[float]] = None
     rows: Optional[int] = None
+    pack_int4: bool = False                  # codes as packed nibbles (bits <= 4; n/2 bytes)
 
     def mode(self) -> int:
         if self.per_channel:
@@ -44,15 +45,22 @@ def code_dtype(bits: int, symmetric: bool) -> torch.dtype:
 
 
 def allocate(src: torch.Tensor, bits=8, per_channel=True, symmetric=True, khw=1, in_place=False,
-             want_codes=True, want_esum=False, clip=None) -> SweepItem:
-    """A SweepItem with freshly allocated outputs on src's device."""
+             want_codes=True, want_esum=False, clip=None, pack_int4=False) -> SweepItem:
+    """A SweepItem with freshly allocated outputs on src's device.  ``pack_int4``:
+    codes as nibbles, two per byte (element 2k low, 2k+1 high; DFQ_PACK_INT4)."""
     rows = src.shape[0] if (per_channel and src.dim() > 0) else 1
     npar = rows if per_channel else 1
     dev = src.device
+    if pack_int4 and bits > 4:
+        raise ValueError("packed codes need bits <= 4")
+    if pack_int4:
+        codes = torch.empty((src.numel() + 1) // 2, dtype=torch.uint8, device=dev) if want_codes else None
+    else:
+        codes = torch.empty(src.shape, dtype=code_dtype(bits, symmetric), device=dev) if want_codes else None
     return SweepItem(
         src=src, bits=bits, per_channel=per_channel, symmetric=symmetric,
         dst=src if in_place else torch.empty_like(src),
-        codes=torch.empty(src.shape, dtype=code_dtype(bits, symmetric), device=dev) if want_codes else None,
+        codes=codes, pack_int4=pack_int4,
         scale=torch.empty(npar, dtype=torch.float32, device=dev),
         zero=torch.empty(npar, dtype=torch.float32, device=dev),
         esum=torch.empty(src.numel() // khw, dtype=torch.float32, device=dev) if want_esum else None,
@@ -81,7 +89,7 @@ class SweepPlan:
             d.khw = it.khw
             d.bits = it.bits
             d.mode = it.mode()
-            d.flags = _lib.DFQ_CLIP if it.clip is not None else 0
+            d.flags = (_lib.DFQ_CLIP if it.clip is not None else 0) | (_lib.DFQ_PACK_INT4 if it.pack_int4 else 0)
             if it.clip is not None:
                 d.clip_lo, d.clip_hi = float(it.clip[0]), float(it.clip[1])
         self._plan = C.c_void_p()

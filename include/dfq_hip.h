@@ -53,12 +53,17 @@ extern "C" {
 #define DFQ_SCALE_F32     0x4  /* scale arithmetic in fp32 (quantize() called with min/max=None,
                                   utils/quantize.py:26-37: 0-d fp32 tensors) instead of fp64;
                                   with DFQ_GIVEN_RANGE the given values are fp32 tensor values */
+#define DFQ_PACK_INT4     0x8  /* bits <= 4: codes packed two per byte, element 2k in the low nibble and
+                                  2k+1 in the high nibble (two's-complement nibbles when symmetric);
+                                  codes holds rows*row_len/2 bytes.  Needs the 16-B layout (numel and,
+                                  per channel, row_len multiples of 4; src/dst 16-B aligned), else
+                                  DFQ_ERR_UNSUPPORTED */
 
 /* One fp32 tensor viewed as [rows, row_len], row_len = I*KH*KW (KCRS) or I (Linear).
  * Outputs are written only where the pointer is non-NULL:
  *   dst    fp32 dequantized values (may alias src: in-place, like weight.data.copy_)
  *   codes  integer grid indices: uint8 (asym, bits<=8), int8 (sym, bits<=8),
- *          uint16/int16 for 8<bits<=16
+ *          uint16/int16 for 8<bits<=16, or packed nibbles (DFQ_PACK_INT4)
  *   scale  fp32 step, [rows] in CHANNEL modes, [1] in TENSOR modes
  *   zero   fp32 value added back after scaling (the range min for asym, +0 for sym)
  *   esum   fp32 bias-correction error sums E[o,i] = sum_k (y - x)[o, i*khw + k],
@@ -76,7 +81,7 @@ typedef struct dfq_tensor_desc {
     int32_t      khw;       /* spatial size for esum (1 for Linear / 1x1) */
     int32_t      bits;      /* 2..16 */
     int32_t      mode;      /* DFQ_TENSOR_ASYM ... DFQ_CHANNEL_SYM */
-    int32_t      flags;     /* DFQ_CLIP | DFQ_GIVEN_RANGE | DFQ_SCALE_F32 */
+    int32_t      flags;     /* DFQ_CLIP | DFQ_GIVEN_RANGE | DFQ_SCALE_F32 | DFQ_PACK_INT4 */
     float        clip_lo;
     float        clip_hi;
     double       given_min;
