@@ -357,3 +357,40 @@ def test_packed_int4_codes_vs_oracle():
     bad = allocate(torch.randn(3, 1025, device=DEV), bits=4, per_channel=True, pack_int4=True)
     with pytest.raises(NotImplementedError):
         SweepPlan([bad])
+
+
+def test_tensor_past_int32_elements():
+    """Maximum sizes: one tensor of 2^31 + 36 elements (64-bit element offsets in
+    the task table, 1M+ tasks, two-launch per-tensor range) and per-channel rows
+    of 2^20 elements; checked with oracle-free properties on the device and the
+    oracle on slices (the per-tensor range taken from torch's min/max)."""
+    from data_free_quantization_amd.sweep import allocate, SweepPlan
+    n = (1 << 31) + 36
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.empty(n, device=DEV).normal_(0, 1, generator=g)
+    x[n - 1] = 9.0   # the range's max sits past 2^31
+    it = allocate(x, bits=8, per_channel=False, symmetric=False)
+    plan = SweepPlan([it])
+    plan.execute()
+    torch.cuda.synchronize()
+    mn, mx = float(x.min()), float(x.max())
+    assert mx == 9.0
+    for lo in (0, (1 << 31) - 1000, n - 2048):
+        xs = x[lo:lo + 2048].cpu().numpy()
+        o = O.quantize(xs, 8, O.TENSOR_ASYM, rows=1, flags=O.F_GIVEN, given=(mn, mx))
+        assert np.array_equal(it.dst[lo:lo + 2048].cpu().numpy(), o["dq"])
+        assert np.array_equal(it.codes[lo:lo + 2048].cpu().numpy(), o["codes"])
+    assert float(it.zero[0]) == mn
+    regen = it.codes.float() * it.scale[0] + it.zero[0]
+    assert torch.equal(regen, it.dst)
+    plan.destroy()
+    del x, it, regen
+    torch.cuda.empty_cache()
+    w = torch.empty(8, 1 << 20, device=DEV).normal_(0, 1, generator=g)
+    it = allocate(w, bits=4, per_channel=True, symmetric=True, want_esum=True)
+    plan = SweepPlan([it])
+    plan.execute()
+    torch.cuda.synchronize()
+    o = O.quantize(w.cpu().numpy(), 4, O.CHANNEL_SYM, rows=8, want_esum=True)
+    assert np.array_equal(it.dst.cpu().numpy(), o["dq"]) and np.array_equal(it.esum.cpu().numpy(), o["esum"])
+    plan.destroy()
