@@ -394,3 +394,88 @@ def test_tensor_past_int32_elements():
     o = O.quantize(w.cpu().numpy(), 4, O.CHANNEL_SYM, rows=8, want_esum=True)
     assert np.array_equal(it.dst.cpu().numpy(), o["dq"]) and np.array_equal(it.esum.cpu().numpy(), o["esum"])
     plan.destroy()
+
+
+_FUZZ_SEEDS = [int(v) for v in __import__("os").environ.get("DFQ_FUZZ_SEEDS", "1,2,3").split(",")]
+
+
+@pytest.mark.parametrize("seed", _FUZZ_SEEDS)
+def test_random_mixed_plans_vs_oracle(seed):
+    """Fuzz: one plan of 40 random tensors -- rows 1..300, odd and even row lengths,
+    KH*KW in {1, 4, 9, 25, 49}, all four modes, 2..16 bits, clip, given per-tensor
+    ranges (Python doubles and fp32 bounds), E sums, packed nibbles, unaligned
+    views -- every output bit-exact with the oracle."""
+    from data_free_quantization_amd import _lib
+    from data_free_quantization_amd.sweep import SweepItem, SweepPlan, code_dtype
+    rng = np.random.default_rng(seed)
+    items, refs = [], []
+    for _ in range(40):
+        khw = int(rng.choice([1, 1, 4, 9, 25, 49]))
+        rows = int(rng.integers(1, 300))
+        row_len = khw * int(rng.choice([1, 3, 7, 16, 32, 100, 257, 512])) + (0 if khw > 1 else int(rng.integers(0, 3)))
+        mode = int(rng.integers(0, 4))
+        bits = int(rng.choice([2, 3, 4, 5, 8, 8, 8, 12, 16]))
+        sym = mode in (1, 3)
+        x = (rng.standard_normal((rows, row_len)) * rng.choice([1e-3, 0.1, 1.0, 30.0])).astype(np.float32)
+        offset = int(rng.integers(0, 2))   # an unaligned view (scalar path) now and then
+        base = torch.from_numpy(np.concatenate([np.zeros(offset, np.float32), x.reshape(-1)])).to(DEV)
+        src = base[offset:].view(rows, row_len)
+        flags, given = 0, (0.0, 0.0)
+        clip = None
+        if rng.random() < 0.3:
+            clip = tuple(sorted(float(v) for v in rng.normal(0, np.abs(x).max() / 2 + 1e-6, 2)))
+            flags |= O.F_CLIP
+        if mode < 2 and rng.random() < 0.3:
+            flags |= O.F_GIVEN | (O.F_F32 if rng.random() < 0.5 else 0)
+            given = (float(x.min()) * 0.8, float(x.max()) * 0.9)
+        esum = rng.random() < 0.5
+        pack = bits <= 4 and rng.random() < 0.5 and not (mode >= 2 and row_len % 2 and 2 * row_len > 2048 and rows > 1)
+        npar = rows if mode >= 2 else 1
+        it = SweepItem(src=src, bits=bits, per_channel=mode >= 2, symmetric=sym, dst=torch.empty_like(src),
+                       codes=(torch.empty((rows * row_len + 1) // 2, dtype=torch.uint8, device=DEV) if pack else
+                              torch.empty(src.shape, dtype=code_dtype(bits, sym), device=DEV)),
+                       scale=torch.empty(npar, device=DEV), zero=torch.empty(npar, device=DEV),
+                       esum=torch.empty(rows * row_len // khw, device=DEV) if esum else None, khw=khw, clip=clip,
+                       rows=rows if mode >= 2 else 1, pack_int4=pack)
+        items.append(it)
+        refs.append((x, mode, bits, khw, flags, clip, given, esum, pack))
+    plan = SweepPlan(items)
+    # given ranges go through the descriptor (SweepItem has no field for them)
+    L = _lib.load()
+    descs = (_lib.TensorDesc * len(items))()
+    for i, (it, r) in enumerate(zip(items, refs)):
+        x, mode, bits, khw, flags, clip, given, esum, pack = r
+        d = descs[i]
+        d.src, d.dst = it.src.data_ptr(), it.dst.data_ptr()
+        d.codes, d.scale, d.zero = it.codes.data_ptr(), it.scale.data_ptr(), it.zero.data_ptr()
+        d.esum = it.esum.data_ptr() if esum else None
+        d.rows = x.shape[0] if mode >= 2 else 1
+        d.row_len = x.size // d.rows
+        d.khw, d.bits, d.mode = khw, bits, mode
+        d.flags = (flags & 7) | (_lib.DFQ_PACK_INT4 if pack else 0)
+        if clip is not None:
+            d.clip_lo, d.clip_hi = clip
+        d.given_min, d.given_max = given
+    plan.destroy()
+    import ctypes as C
+    p = C.c_void_p()
+    _lib.check(L.dfq_sweep_plan_create(descs, len(items), C.byref(p)), "create")
+    _lib.check(L.dfq_sweep_plan_execute(p, C.c_void_p(torch.cuda.current_stream().cuda_stream)), "execute")
+    torch.cuda.synchronize()
+    for it, (x, mode, bits, khw, flags, clip, given, esum, pack) in zip(items, refs):
+        o = O.quantize(x, bits, mode, rows=x.shape[0] if mode >= 2 else 1, khw=khw, flags=flags,
+                       clip=clip or (0.0, 0.0), given=given, want_esum=esum)
+        tag = (x.shape, mode, bits, khw, flags, pack)
+        assert np.array_equal(it.dst.cpu().numpy(), o["dq"]), tag
+        if pack:
+            c = o["codes"].reshape(-1).astype(np.uint8) & 0xF
+            c = np.append(c, np.zeros(c.size % 2, np.uint8))
+            assert np.array_equal(it.codes.cpu().numpy(), c[0::2] | (c[1::2] << 4)), tag
+        else:
+            assert np.array_equal(it.codes.cpu().numpy().view(o["codes"].dtype).reshape(x.shape),
+                                  o["codes"].reshape(x.shape)), tag
+        assert np.array_equal(it.scale.cpu().numpy(), o["scale"]), tag
+        assert np.array_equal(it.zero.cpu().numpy() + np.float32(0), o["zero"] + np.float32(0)), tag
+        if esum:
+            assert np.array_equal(it.esum.cpu().numpy(), o["esum"]), tag
+    L.dfq_sweep_plan_destroy(p)
