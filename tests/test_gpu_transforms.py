@@ -138,3 +138,61 @@ def test_clip_weight():
     ref = conv.weight.detach().clamp(-15, 15)
     clip_weight({1: conv}, [-15, 15], [nn.Conv2d, nn.Linear])
     assert torch.equal(conv.weight.detach(), ref)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_cle_relation_and_bn_fold_fuzz(seed):
+    """Random relations (dense, depthwise pairs, grouped W2, Linear W2, signed, dead
+    channels, huge/tiny ranges hitting the s clamps) and random BN folds: the HIP
+    kernels bit-exact with the oracle (pinned to the reference by the golden cases)."""
+    from oracle import oracle as O
+    from data_free_quantization_amd.Cross_layer_equal import _layer_equalization
+    from data_free_quantization_amd.utils.layer_transform import merge_batchnorm
+    rng = np.random.default_rng(seed)
+    for _ in range(12):
+        c1 = int(rng.choice([1, 3, 16, 96, 160, 257]))
+        kind = rng.choice(["dense", "dw", "grouped", "linear"])
+        k1 = int(rng.choice([1, 3]))
+        w1 = (rng.standard_normal((c1, int(rng.integers(1, 40)), k1, k1)) *
+              rng.choice([1e-4, 0.1, 3.0])).astype(np.float32)
+        if kind == "dw":
+            w2 = rng.standard_normal((c1, 1, 3, 3)).astype(np.float32)
+        elif kind == "grouped":
+            g = 1 if c1 % 2 else 2
+            w2 = rng.standard_normal((4 * g, c1 // g, 3, 3)).astype(np.float32)
+        elif kind == "linear":
+            w2 = rng.standard_normal((int(rng.integers(1, 50)), c1)).astype(np.float32)
+        else:
+            w2 = rng.standard_normal((int(rng.integers(1, 70)), c1, 1, 1)).astype(np.float32)
+        if rng.random() < 0.3:
+            w1[int(rng.integers(0, c1))] = 0.0   # dead channel: s -> 1e8
+        b1 = rng.standard_normal(c1).astype(np.float32)
+        bnw = rng.uniform(0.5, 1.5, c1).astype(np.float32)
+        bnb = rng.normal(0, 0.5, c1).astype(np.float32)
+        signed = bool(rng.random() < 0.3)
+        ref = O.cle_relation(w1, w2, b1, bnw, bnb, signed=signed)
+        tw1, tw2, tb1, tbw, tbb = T(w1), T(w2), T(b1), T(bnw), T(bnb)
+        W1, W2, B1, S = _layer_equalization(tw1, tw2, tb1, tbw, tbb, s_min_max=[1e-8, 1e8], signed=signed)
+        for got, want, name in ((W1, ref[0], "w1"), (W2, ref[1], "w2"), (B1, ref[2], "b1"), (tbw, ref[3], "bnw"),
+                                (tbb, ref[4], "bnb"), (S, ref[5], "S")):
+            assert np.array_equal(got.cpu().numpy(), want), (name, kind, c1, w2.shape, signed)
+    for _ in range(6):
+        o, i, k = int(rng.integers(1, 300)), int(rng.integers(1, 64)), int(rng.choice([1, 3, 5]))
+        w = rng.standard_normal((o, i, k, k)).astype(np.float32)
+        b = rng.standard_normal(o).astype(np.float32)
+        g, beta = rng.uniform(-1.5, 1.5, o).astype(np.float32), rng.normal(0, 1, o).astype(np.float32)
+        m, v = rng.normal(0, 0.3, o).astype(np.float32), rng.uniform(1e-3, 3, o).astype(np.float32)
+        eps = float(rng.choice([1e-5, 1e-3, 0.0]))
+        ref = O.bn_fold(w, b, g, beta, m, v, eps)
+        conv = nn.Conv2d(i, o, k, bias=True).to(DEV)
+        bn = nn.BatchNorm2d(o, eps=eps).to(DEV)
+        with torch.no_grad():
+            conv.weight.copy_(T(w)); conv.bias.copy_(T(b))
+            bn.weight.copy_(T(g)); bn.bias.copy_(T(beta)); bn.running_mean.copy_(T(m)); bn.running_var.copy_(T(v))
+        graph = OrderedDict([("Data", "Data"), (1, conv), (2, bn)])
+        bottoms = OrderedDict([("Data", None), (1, ["Data"]), (2, [1])])
+        merge_batchnorm(None, graph, bottoms, (nn.Conv2d, nn.Linear))
+        assert np.array_equal(conv.weight.detach().cpu().numpy(), ref[0])
+        assert np.array_equal(conv.bias.detach().cpu().numpy(), ref[1])
+        assert np.array_equal(bn.fake_weight.cpu().numpy(), ref[6]) and np.array_equal(bn.fake_bias.cpu().numpy(),
+                                                                                       ref[7])
