@@ -62,6 +62,8 @@ def get_argument(argv=None):
     p.add_argument("--bc_mode", default="literal", choices=["literal", "reference", "fused"])
     p.add_argument("--val", default="./val")
     p.add_argument("--device", default="cuda:0")
+    p.add_argument("--export", default=None,
+                   help="write the integer weights (codes, scale, zero, bias) to this safetensors file")
     return p.parse_args(argv)
 
 
@@ -138,7 +140,7 @@ def main(argv=None):
         cross_layer_equalization(graph, res, targ_layer, Save_state=False, Treshhold=2e-7)
     if args.absorption:
         bias_absorption(graph, res, bottoms, N=3, visualize=args.visualize)
-    state = {} if args.bc_mode == "fused" else None
+    state = {} if (args.bc_mode == "fused" or args.export) else None
     if args.quantize:
         set_layer_bits(graph, args.bits_weight, args.bits_activation, args.bits_bias, targ_layer)
         model = merge_batchnorm(model, graph, bottoms, targ_layer)
@@ -152,11 +154,17 @@ def main(argv=None):
     if args.correction:
         # main_dfq.py:231 passes visualize= to a signature without it (TypeError in the
         # reference); this driver calls the documented signature.
-        err = {k: v["esum"] for k, v in state.items()} if state else None
+        err = {k: v["esum"] for k, v in state.items()} if (state and args.bc_mode == "fused") else None
         bias_correction(graph, bottoms, targ_layer, bits_weight=args.bits_weight, signed=args.symmetric,
                         error_sums=err)
     torch.cuda.synchronize()
     print(f"DFQ weight transforms took {time.perf_counter() - t0:.3f} s on {args.device}")
+    if args.export and args.quantize and state:
+        from . import export
+        clip = [-15, 15] if args.clip_weight else None   # fused in the sweep or clip_weight after it: same clamp
+        export.save(args.export, graph, state, bits=args.bits_weight, granularity=args.granularity,
+                    symmetric=args.symmetric, clip=clip)
+        print(f"Exported {len(state)} quantized layers to {args.export}")
 
     if args.quantize:
         replace_op()
