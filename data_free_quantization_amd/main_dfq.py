@@ -75,12 +75,36 @@ def _model_name(args):
     return "resnet50" if args.resnet else "mobilenetv2"
 
 
+def canonical_state_dict(state):
+    """A reference checkpoint's state_dict in this package's module names.  The
+    reference's DeepLab backbone exposes features[0:4] / features[4:] a second
+    time as low_level_features / high_level_features
+    (modeling/segmentation/backbone/mobilenet.py:115-116), so its checkpoints hold
+    every backbone tensor twice; a slice of an nn.Sequential keeps the original
+    child names, so ``low_level_features.N`` / ``high_level_features.N`` map back
+    to ``backbone.features.N`` (and must agree with it)."""
+    out = {}
+    alias = ("backbone.low_level_features.", "backbone.high_level_features.")
+    for k, v in state.items():
+        for pre in alias:
+            if k.startswith(pre):
+                canon = "backbone.features." + k[len(pre):]
+                if canon in state and not torch.equal(state[canon], v):
+                    raise ValueError(f"checkpoint alias {k} disagrees with {canon}")
+                out.setdefault(canon, v)
+                break
+        else:
+            out[k] = v
+    return out
+
+
 def build_model(args):
     name = _model_name(args)
     model = zoo.build(name, seed=args.seed)
     if args.weights:
         state = torch.load(args.weights, map_location="cpu", weights_only=True)
-        model.load_state_dict(state.get("state_dict", state) if isinstance(state, dict) else state)
+        state = state.get("state_dict", state) if isinstance(state, dict) else state
+        model.load_state_dict(canonical_state_dict(state))
     return model, name
 
 

@@ -494,6 +494,19 @@ def literal_bc(name="mobilenetv2"):
     return same
 
 
+def state_dict_keys():
+    """The reference models' state_dict key names and shapes (checkpoint format),
+    so tests can check that reference checkpoints load into the zoo models."""
+    from modeling.classification.MobileNetV2 import MobileNetV2 as RefMBv2
+    from modeling.segmentation.deeplab import DeepLab as RefDeepLab
+    from modeling.segmentation.backbone.resnet import ResNet as RefResNet, Bottleneck
+    out = {"mobilenetv2": RefMBv2(), "deeplab": RefDeepLab(sync_bn=False),
+           "resnet50_backbone": RefResNet(Bottleneck, [3, 4, 6, 3], 16, nn.BatchNorm2d, pretrained=False)}
+    res = {k: [[n, list(t.shape)] for n, t in m.state_dict().items()] for k, m in out.items()}
+    (HERE / "state_dict_keys.json").write_text(json.dumps(res))
+    print("state_dict keys:", {k: len(v) for k, v in res.items()})
+
+
 if __name__ == "__main__":
     _check_ieee_sqrt()
     which = sys.argv[1:] or ["quant", "transform", "mobilenetv2", "resnet50", "deeplab"]
@@ -509,5 +522,7 @@ if __name__ == "__main__":
     for m in ("mobilenetv2", "resnet50", "deeplab"):
         if "act" in which or f"act_{m}" in which:
             act_ranges(m)
+    if "keys" in which:
+        state_dict_keys()
     if "literal" in which:
         print("literal bias_correction is a no-op:", literal_bc())

@@ -125,3 +125,46 @@ def test_transformer_swaps_layers():
     assert len(graph) == 152
     assert np.array_equal(model.features[0][0].weight.detach().numpy(), w0.numpy())
     assert len(create_relation(graph, t.log.getBottoms(), (QuantConv2d, QuantLinear))) == 37
+
+
+def test_reference_checkpoint_keys_load(tmp_path):
+    """A checkpoint with the reference's module names loads into the zoo models:
+    MobileNetV2 keys are identical; the reference DeepLab's aliased backbone keys
+    (low_level_features / high_level_features) map back to backbone.features."""
+    import torch
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd.main_dfq import canonical_state_dict
+    m = zoo.build("deeplab", seed=1)
+    sd = dict(m.state_dict())
+    ref_style = dict(sd)
+    for k, v in sd.items():   # what the reference's DeepLab state_dict looks like
+        if k.startswith("backbone.features."):   # Sequential slices keep the child names
+            i = int(k[len("backbone.features."):].split(".", 1)[0])
+            pre = "backbone.low_level_features." if i < 4 else "backbone.high_level_features."
+            ref_style[pre + k[len("backbone.features."):]] = v.clone()
+    m2 = zoo.build("deeplab", seed=2)
+    m2.load_state_dict(canonical_state_dict(ref_style))
+    for k, v in m2.state_dict().items():
+        assert torch.equal(v, sd[k])
+    bad = dict(ref_style)
+    first_alias = next(k for k in bad if k.startswith("backbone.low_level_features."))
+    bad[first_alias] = bad[first_alias] + 1
+    with pytest.raises(ValueError):
+        canonical_state_dict(bad)
+
+
+def test_zoo_matches_reference_checkpoint_format():
+    """tests/golden/state_dict_keys.json (the reference models' state_dict names and
+    shapes): MobileNetV2 identical, DeepLab identical after canonical_state_dict,
+    ResNet-50 = the reference backbone + the fc head."""
+    import json
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd.main_dfq import canonical_state_dict
+    from tests.helpers import GOLDEN
+    ref = json.loads((GOLDEN / "state_dict_keys.json").read_text())
+    shapes = lambda m: {k: list(v.shape) for k, v in m.state_dict().items()}   # noqa: E731
+    assert shapes(zoo.build("mobilenetv2", seed=0)) == {k: s for k, s in ref["mobilenetv2"]}
+    fake = {k: __import__("torch").zeros(s) for k, s in ref["deeplab"]}
+    assert {k: list(v.shape) for k, v in canonical_state_dict(fake).items()} == shapes(zoo.build("deeplab", seed=0))
+    r50 = shapes(zoo.build("resnet50", seed=0))
+    assert {k: s for k, s in r50.items() if not k.startswith("fc.")} == {k: s for k, s in ref["resnet50_backbone"]}
