@@ -159,11 +159,13 @@ class UniformQuantize(InplaceFunction):
             out = input
         else:
             out = torch.empty_like(input)
-        if rng is None:   # 0-d fp32 range of the whole tensor, reduced in the kernel
-            fake_quant(input.detach(), num_bits, symmetric=symmetric, out=out, want_codes=False, scale_f32=True)
+        # async: one elementwise launch (plus the range reduction), no task table,
+        # no host synchronisation
+        x = input.detach()
+        if rng is None:   # 0-d fp32 range of the whole tensor, reduced on the device
+            fake_quant_given(x, num_bits, symmetric, range_enc=device_range(x), scale_f32=True, out=out)
         else:
-            fake_quant(input.detach(), num_bits, symmetric=symmetric, min_value=rng[0], max_value=rng[1], out=out,
-                       want_codes=False, scale_f32=rng[2])
+            fake_quant_given(x, num_bits, symmetric, min_value=rng[0], max_value=rng[1], scale_f32=rng[2], out=out)
         return out
 
     @staticmethod
