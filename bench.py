@@ -284,30 +284,41 @@ def pipeline_timing(dev, model="mobilenetv2"):
 
 
 def same_mix_probe(n, dev, stream, reps=10):
-    """Achievable-ceiling probe: a grid-stride stream with the sweep's 1x1-layer
-    traffic mix (read 4 B, write 4 + 1 + 4 B per element) and no arithmetic."""
+    """Achievable-ceiling probes with the sweep's 1x1-layer traffic mix (read 4 B,
+    write 4 + 1 + 4 B per element) and no arithmetic: a grid-stride VGPR stream,
+    and the sweep's own memory pattern (2048-element wave tasks through LDS-DMA,
+    non-temporal stores).  Returns (stream GB/s, LDS-DMA GB/s)."""
     import ctypes as C
     from data_free_quantization_amd import _lib
-    n = n // 16 * 16
+    n = n // 2048 * 2048
     x = torch.randn(n, device=dev)
     y = torch.empty_like(x)
     cds = torch.empty(n, dtype=torch.uint8, device=dev)
     e = torch.empty_like(x)
     L = _lib.load()
-    best = None
-    for blocks in (2048, 8192, -4096):
+    s = C.c_void_p(stream.cuda_stream)
+
+    def best_of(fn):
+        best = None
         for _ in range(2):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(reps):
-                _lib.check(L.dfq_probe_stream(_lib.ptr(x), _lib.ptr(y), C.c_void_p(cds.data_ptr()), _lib.ptr(e), n,
-                                              blocks, C.c_void_p(stream.cuda_stream)), "dfq_probe_stream")
+                fn()
             e1.record(stream)
             torch.cuda.synchronize(dev)
             ms = e0.elapsed_time(e1) / reps
             best = ms if best is None else min(best, ms)
+        return best
+
+    stream_ms = min(best_of(lambda b=b: _lib.check(L.dfq_probe_stream(_lib.ptr(x), _lib.ptr(y),
+                                                                      C.c_void_p(cds.data_ptr()), _lib.ptr(e), n,
+                                                                      b, s), "dfq_probe_stream"))
+                    for b in (2048, 8192, -4096))
+    lds_ms = best_of(lambda: _lib.check(L.dfq_probe_lds(_lib.ptr(x), _lib.ptr(y), C.c_void_p(cds.data_ptr()),
+                                                        _lib.ptr(e), n, 0, 16384, s), "dfq_probe_lds"))
     del x, y, cds, e
-    return round(13 * n / (best / 1e3) / 1e9, 1)
+    return round(13 * n / (stream_ms / 1e3) / 1e9, 1), round(13 * n / (lds_ms / 1e3) / 1e9, 1)
 
 
 def main():
@@ -358,7 +369,7 @@ def main():
     sharded = sharded_single_model(dev, stream, world) if world > 1 and not args.no_secondary else None
     res = None
     if rank == 0:
-        probe = same_mix_probe(per_copy * copies, dev, stream)
+        probe_stream, probe_lds = same_mix_probe(per_copy * copies, dev, stream)
         second = None if args.no_secondary else secondary_configs(dev, stream)
         single = None if args.no_secondary else single_model_latency(dev, stream)
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
@@ -403,7 +414,10 @@ def main():
                 "tasks": st["n_tasks_main"],
                 "grid_blocks": st["grid_blocks"],
                 "variant": st["variant"],
-                "same_mix_probe_GBs": probe,
+                "same_mix_probe_GBs": probe_lds,
+                "same_mix_probe_note": "the sweep's memory pattern (LDS-DMA wave tasks, nt stores) without "
+                                       "arithmetic: the ceiling this mix reaches on this box; a VGPR "
+                                       f"grid-stride stream of the same mix: {probe_stream} GB/s",
             },
             "cpu_baseline": cpu,
             "secondary_configs": second,

@@ -28,6 +28,9 @@ FAMILIES = {
     "fc_256x1152(row1152)": (256, 1152),
     "fc_256x2304(row2304)": (256, 2304),
     "fc_256x576(row576)": (256, 576),
+    "fc_1000x1280(row1280)": (1000, 1280),
+    "1x1_960x160": (960, 160, 1, 1),
+    "1x1_160x960": (160, 960, 1, 1),
 }
 
 
