@@ -12,7 +12,9 @@ shapes, already resident in HBM).  The batch defeats the 256 MB Infinity Cache
 
 Rank 0 prints ONE JSON line (contract in the task statement); ``roofline``
 times the sweep kernel with HIP events on the stream it is launched on;
-``cpu_baseline`` times the CPU port (oracle/, 1 thread) on a bounded sample.
+``cpu_baseline`` times the reference's torch CPU ops as restated in
+oracle/torch_port.py (all host threads; the 1-thread C oracle beside it) on a
+bounded sample.
 """
 from __future__ import annotations
 
@@ -416,8 +418,9 @@ def main():
                 "variant": st["variant"],
                 "same_mix_probe_GBs": probe_lds,
                 "same_mix_probe_note": "the sweep's memory pattern (LDS-DMA wave tasks, nt stores) without "
-                                       "arithmetic: the ceiling this mix reaches on this box; a VGPR "
-                                       f"grid-stride stream of the same mix: {probe_stream} GB/s",
+                                       "arithmetic, measured on this box after the timed steps (box to box "
+                                       "5.2-6.5 TB/s, the sweep 5.9-6.3); a VGPR grid-stride stream of the "
+                                       f"same mix: {probe_stream} GB/s",
             },
             "cpu_baseline": cpu,
             "secondary_configs": second,
