@@ -1480,7 +1480,9 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_means = T.add<double>(n_targets);
     const int64_t o_state = T.add<CleState>(1);
     const int64_t o_hist = T.add<double>(kCleHistCap);
+    const double tm0 = now_us();
     if ((e = hipMalloc(&p->d_tables, T.total)) != hipSuccess) return fail(e);
+    const double tm1 = now_us();
     char* base = static_cast<char*>(p->d_tables);
     std::vector<char> blob(host_bytes, 0);
     auto put = [&](int64_t off, const auto& v) {
@@ -1489,6 +1491,9 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     put(o_rels, R); put(o_rt, rt); put(o_at, at); put(o_layers, layers); put(o_chunks, chunks); put(o_units, units);
     put(o_b1off, b1off);
     if ((e = hipMemcpy(base, blob.data(), host_bytes, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    if (cle_timing())
+        fprintf(stderr, "DFQ_CLE_TIMING create: hipMalloc %lld B %.1f us, copy %lld B %.1f us\n", (long long)T.total,
+                tm1 - tm0, (long long)host_bytes, now_us() - tm1);
     p->d_rels = reinterpret_cast<CleRel*>(base + o_rels);
     p->d_rtasks = reinterpret_cast<CleTask*>(base + o_rt);
     p->d_atasks = reinterpret_cast<CleTask*>(base + o_at);
@@ -1510,17 +1515,19 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
 
 // One CLE iteration's launches (steps, metric, stop rule) on stream s.
 static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
+    // grid caps: 2,048 / 4,096 blocks (caps of 128-1,024 measured 4-150 % slower on MobileNetV2)
+    constexpr int64_t kStepGrid = 2048, kTileGrid = 4096;
     for (int32_t k = 0; k < p->steps; ++k) {
         const int64_t r0 = p->fused ? (k == 0 ? p->rstep[0] : 0) : p->rstep[k];
         const int64_t r1 = p->fused ? (k == 0 ? p->rstep[1] : 0) : p->rstep[k + 1];
         const int64_t a0 = p->astep[k], a1 = p->astep[k + 1];
         if (r1 > r0) {
-            hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(r1 - r0, 2048)), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(r1 - r0, kStepGrid)), dim3(kThreads), 0, s,
                                p->d_rels, p->d_rtasks, r0, r1, p->d_rng, p->M, p->d_state);
             DFQ_LAUNCH_CHECK();
         }
         if (a1 > a0) {
-            hipLaunchKernelGGL(cle_loop_apply_kernel, dim3((int)std::min<int64_t>(a1 - a0, 2048)), dim3(kThreads), 0, s,
+            hipLaunchKernelGGL(cle_loop_apply_kernel, dim3((int)std::min<int64_t>(a1 - a0, kStepGrid)), dim3(kThreads), 0, s,
                                p->d_rels, p->d_atasks, a0, a1, p->d_rng, p->M, p->d_state, p->is_signed, p->eps,
                                p->smin, p->smax);
             DFQ_LAUNCH_CHECK();
@@ -1528,7 +1535,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
     }
     if (p->nchunks > 0) {
         if (p->nunits > 0) {
-            hipLaunchKernelGGL(cle_loop_diff_tiles_kernel, dim3((int)std::min<int64_t>(p->nunits, 4096)), dim3(kThreads),
+            hipLaunchKernelGGL(cle_loop_diff_tiles_kernel, dim3((int)std::min<int64_t>(p->nunits, kTileGrid)), dim3(kThreads),
                                0, s, p->d_layers, p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail,
                                p->d_state);
             DFQ_LAUNCH_CHECK();
