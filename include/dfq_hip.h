@@ -55,9 +55,10 @@ extern "C" {
                                   with DFQ_GIVEN_RANGE the given values are fp32 tensor values */
 #define DFQ_PACK_INT4     0x8  /* bits <= 4: codes packed two per byte, element 2k in the low nibble and
                                   2k+1 in the high nibble (two's-complement nibbles when symmetric);
-                                  codes holds rows*row_len/2 bytes.  Needs the 16-B layout (numel and,
-                                  per channel, row_len multiples of 4; src/dst 16-B aligned), else
-                                  DFQ_ERR_UNSUPPORTED */
+                                  codes holds ceil(rows*row_len/2) bytes.  bits > 4: DFQ_ERR_INVALID.
+                                  Every task starts at an even element, so per channel an odd row_len
+                                  above half a task (1024 elements by default) with rows > 1 is
+                                  DFQ_ERR_UNSUPPORTED (two rows' tasks would share a byte) */
 
 /* One fp32 tensor viewed as [rows, row_len], row_len = I*KH*KW (KCRS) or I (Linear).
  * Outputs are written only where the pointer is non-NULL:
