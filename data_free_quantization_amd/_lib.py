@@ -31,7 +31,7 @@ EXPORTS = [
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
     "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
-    "dfq_bias_absorb", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate",
+    "dfq_bias_absorb", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate", "dfq_bc_chain",
     "dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline",
     "dfq_act_moments", "dfq_act_minmax", "dfq_act_affine",
 ]
@@ -69,6 +69,15 @@ class CleRel(C.Structure):
         ("khw2", C.c_int64), ("s_acc_init", C.c_int32), ("reserved", C.c_int32),
     ]
 
+
+class BcOp(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("flag", C.c_int32), ("a", C.c_void_p), ("b", C.c_void_p), ("out", C.c_void_p),
+        ("out2", C.c_void_p), ("n", C.c_int64), ("i2", C.c_int64), ("f", C.c_int64),
+    ]
+
+
+DFQ_BC_OP_EXPECT, DFQ_BC_OP_APPLY, DFQ_BC_OP_PROPAGATE = 0, 1, 2
 
 _LIB: Optional[C.CDLL] = None
 
@@ -125,6 +134,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_bc_expect": ([P, P, I64, I32, I32, P, P], C.c_int),
         "dfq_bc_apply": ([P, I64, I64, P, I64, P, P, C.POINTER(I64), P], C.c_int),
         "dfq_bc_propagate": ([P, I64, P, I64, I32, P], C.c_int),
+        "dfq_bc_chain": ([C.POINTER(BcOp), I32, C.POINTER(I32), P], C.c_int),
         "dfq_probe_stream": ([P, P, P, P, I64, I32, P], C.c_int),
         "dfq_debug_timeline": ([P, I64], C.c_int),
         "dfq_probe_lds": ([P, P, P, P, I64, I32, I32, P], C.c_int),

@@ -164,6 +164,113 @@ def _snapshot(tensors):
     return out
 
 
+class _BcChain:
+    """The walk's device work recorded in graph order and enqueued by ONE
+    ``dfq_bc_chain`` call (instead of a Python call per expect / apply /
+    propagate).  Expectations and bias vectors live in one scratch buffer:
+    refs are ``(None, float offset)`` there, or ``(tensor, 0)`` for a live
+    tensor.  ``flush()`` runs what was recorded; the walk flushes before it
+    raises, so the ops before an error take effect, as in the reference."""
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.ops = []
+        self.top = 0            # scratch floats allocated
+        self.keep = []          # tensors the recorded ops point into
+
+    def alloc(self, n):
+        off = self.top
+        self.top += -(-n // 64) * 64   # 256-B aligned slots
+        return off
+
+    def extend_last(self, off, size, n):
+        """grow the most recent slot [off, off + size) to size + n (torch.cat)"""
+        assert self.top == off + -(-size // 64) * 64, "cat target is not the last scratch slot"
+        self.top = off + -(-(size + n) // 64) * 64
+
+    def _ptr(self, ref, base):
+        t, off = ref
+        return (t.data_ptr() if t is not None else base) + 4 * off
+
+    def expect(self, bn, relu, dst, accumulate):
+        w, b = bn.fake_weight, bn.fake_bias
+        _lib.require_device(w, b)
+        self.keep += [w, b]
+        self.ops.append((_lib.DFQ_BC_OP_EXPECT, int(bool(relu)) | (int(accumulate) << 1), (w, 0), (b, 0), dst, None,
+                         b.numel(), 0, 0))
+
+    def apply(self, E, o, i2, expect, f, bias, vec):
+        self.keep += [E, bias]
+        self.ops.append((_lib.DFQ_BC_OP_APPLY, 0, (E, 0), expect, (bias, 0), vec, o, i2, f))
+
+    def propagate(self, vec, numel, fake_b, f):
+        _lib.require_device(fake_b)
+        self.keep.append(fake_b)
+        self.ops.append((_lib.DFQ_BC_OP_PROPAGATE, _lib.REF_THREADS, vec, None, (fake_b, 0), None, numel, 0, f))
+
+    def flush(self, stream):
+        if not self.ops:
+            return
+        scratch = torch.empty(max(self.top, 1), dtype=torch.float32, device=self.dev)
+        base = scratch.data_ptr()
+        arr = (_lib.BcOp * len(self.ops))()
+        for k, (kind, flag, a, b, out, out2, n, i2, f) in enumerate(self.ops):
+            op = arr[k]
+            op.kind, op.flag, op.n, op.i2, op.f = kind, flag, n, i2, f
+            op.a = self._ptr(a, base)
+            op.b = self._ptr(b, base) if b is not None else None
+            op.out = self._ptr(out, base)
+            op.out2 = self._ptr(out2, base) if out2 is not None else None
+        failed = C.c_int32(-1)
+        rc = _lib.load().dfq_bc_chain(arr, len(self.ops), C.byref(failed), stream)
+        _lib.check(rc, f"dfq_bc_chain (op {failed.value})", RuntimeError)
+        # the ops run asynchronously: keep the scratch alive until they are done
+        scratch.record_stream(torch.cuda.current_stream(self.dev))
+        self.ops, self.keep, self.top = [], [], 0
+
+
+def _record_branches(chain, bn_branch):
+    """_calculate_bias_correction_for_branches (bias_correction.py:15-58) as chain
+    ops: {key: (connect_type, expect ref, numel)}."""
+    res = {}
+    for key, branch in bn_branch.items():
+        off, size, connect_type = None, 0, None
+        for layer, relu_attached, connect_type in branch:
+            n = layer.fake_bias.numel()
+            if off is None:
+                off, size = chain.alloc(n), n
+                chain.expect(layer, relu_attached, (None, off), False)
+            elif connect_type == "cat":   # torch.cat([cum, e]): e lands right after cum
+                chain.extend_last(off, size, n)
+                chain.expect(layer, relu_attached, (None, off + size), False)
+                size += n
+            else:                          # cum += e (in place)
+                if n != size:
+                    raise RuntimeError(f"output with shape [{size}] doesn't match the broadcast shape [{n}]"
+                                       if n != 1 else "a one-channel BN expectation broadcast is not supported")
+                chain.expect(layer, relu_attached, (None, off), True)
+        res[key] = (connect_type, (None, off), size)
+    return res
+
+
+def _record_apply(chain, layer, E, o, i2, connect_type, expect, f):
+    """_apply_bias_correction_E's checks, then one chain op; returns the bias_vec
+    ref and its numel (kept for the next BN)."""
+    if connect_type == "cat":
+        raise RuntimeError("Tensors must have same number of dimensions: got 2 and 1")
+    if layer.bias is None:   # :89-90 references an undefined `nn`
+        raise NameError("name 'nn' is not defined")
+    bcols = _broadcast_cols(i2, f)
+    if o * bcols <= o:
+        logger.error("Error in applying bias correction: Bias correction shape mismatch that cannot be handled "
+                     "automatically.")
+        raise ValueError("Bias correction shape mismatch that cannot be handled automatically.")
+    _lib.require_device(E, layer.bias.data)
+    vec = (None, chain.alloc(o * bcols))
+    chain.apply(E.reshape(-1), o, i2, expect, f, layer.bias.data, vec)
+    return vec, o * bcols
+
+
 def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.BatchNorm2d, signed=False, *,
                     error_sums=None):
     """Returns (bias_before_correction, bias_after_correction) keyed "layer_<idx>".
@@ -186,49 +293,58 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
         # clone per layer (and likewise for "after", at the end).
         before = _snapshot({f"layer_{i}": l.bias.data for i, l in enumerate(graph.values())
                             if i in bottoms and isinstance(l, targ_type) and getattr(l, "bias", None) is not None})
-        for idx_layer, layer in enumerate(graph.values()):
-            layer_name = f"layer_{idx_layer}"
-            if idx_layer not in bottoms:
-                logger.warning(f"Layer index {idx_layer} not found in bottoms")
-                continue
-            bot = bottoms[idx_layer]
-            if bot is None or bot[0] == "Data":
-                continue
-            node = graph[idx_layer]
-            if isinstance(node, bn_type):
-                bn_module[idx_layer] = node
-                relu_attached[idx_layer] = False
-                if bias_prev is not None:
-                    f = node.fake_bias.size(0)
-                    if bias_prev.numel() == f:
-                        # fake_bias.add_(bias_prev) with a 2-D bias_prev cannot broadcast in place
-                        raise RuntimeError("output with shape [{}] doesn't match the broadcast shape".format(f))
-                    rc = _lib.load().dfq_bc_propagate(_lib.ptr(bias_prev), bias_prev.numel(),
-                                                      _lib.ptr(node.fake_bias), f, _lib.REF_THREADS,
-                                                      _lib.stream_of(bias_prev))
-                    _lib.check(rc, "dfq_bc_propagate", RuntimeError)
-                    bias_prev = None
-                continue
-            if isinstance(node, torch.nn.ReLU) and bot[0] in bn_module:
-                relu_attached[bot[0]] = True
-            if isinstance(node, targ_type):
-                bn_list, relu_list, type_list, _ = find_prev_bn(bn_module, relu_attached, graph, bottoms, bot[:])
-                pre = None if error_sums is None else error_sums.get(keys[idx_layer])
-                E, o, i2 = _error_sums(node.weight.data, bits_weight, signed, pre)
-                branches = {}
-                for j, (bn_layer, bid) in enumerate(bn_list):
-                    branches.setdefault(bid[0], []).append((bn_layer, relu_list[j], type_list[j]))
-                for connect_type, expect in _calculate_bias_correction_for_branches(branches).values():
-                    try:
-                        bias = _apply_bias_correction_E(node, E, o, i2, connect_type, expect)
-                    except ValueError as e:
-                        logger.error(f"Error in applying bias correction: {e}")
-                        raise
-                if bias is None:
-                    raise UnboundLocalError("local variable 'bias' referenced before assignment")
-                bias_prev = bias
-                if getattr(layer, "bias", None) is not None:
-                    after_src[layer_name] = layer.bias.data
+        chain = _BcChain(next(iter(before.values())).device if before else torch.device("cuda"))
+        stream = None
+        try:
+            for idx_layer, layer in enumerate(graph.values()):
+                layer_name = f"layer_{idx_layer}"
+                if idx_layer not in bottoms:
+                    logger.warning(f"Layer index {idx_layer} not found in bottoms")
+                    continue
+                bot = bottoms[idx_layer]
+                if bot is None or bot[0] == "Data":
+                    continue
+                node = graph[idx_layer]
+                if isinstance(node, bn_type):
+                    bn_module[idx_layer] = node
+                    relu_attached[idx_layer] = False
+                    if bias_prev is not None:
+                        vec, numel = bias_prev
+                        f = node.fake_bias.size(0)
+                        if numel == f:
+                            # fake_bias.add_(bias_prev) with a 2-D bias_prev cannot broadcast in place
+                            raise RuntimeError("output with shape [{}] doesn't match the broadcast shape".format(f))
+                        if numel % f:
+                            raise RuntimeError(f"shape '[-1, {f}]' is invalid for input of size {numel}")
+                        chain.propagate(vec, numel, node.fake_bias, f)
+                        bias_prev = None
+                    continue
+                if isinstance(node, torch.nn.ReLU) and bot[0] in bn_module:
+                    relu_attached[bot[0]] = True
+                if isinstance(node, targ_type):
+                    bn_list, relu_list, type_list, _ = find_prev_bn(bn_module, relu_attached, graph, bottoms, bot[:])
+                    pre = None if error_sums is None else error_sums.get(keys[idx_layer])
+                    E, o, i2 = _error_sums(node.weight.data, bits_weight, signed, pre)
+                    if stream is None:
+                        stream = _lib.stream_of(E)
+                        chain.dev = E.device
+                    branches = {}
+                    for j, (bn_layer, bid) in enumerate(bn_list):
+                        branches.setdefault(bid[0], []).append((bn_layer, relu_list[j], type_list[j]))
+                    for connect_type, expect, f in _record_branches(chain, branches).values():
+                        try:
+                            bias = _record_apply(chain, node, E, o, i2, connect_type, expect, f)
+                        except ValueError as e:
+                            logger.error(f"Error in applying bias correction: {e}")
+                            raise
+                    if bias is None:
+                        raise UnboundLocalError("local variable 'bias' referenced before assignment")
+                    bias_prev = bias
+                    if getattr(layer, "bias", None) is not None:
+                        after_src[layer_name] = layer.bias.data
+        finally:   # the ops recorded before an error still take effect, as in the reference
+            if chain.ops:
+                chain.flush(stream)
         after = _snapshot(after_src)
     logger.info("Bias correction completed.")
     return before, after

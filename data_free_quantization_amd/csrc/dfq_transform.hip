@@ -538,6 +538,49 @@ extern "C" int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fak
     return DFQ_OK;
 }
 
+extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed_op, void* stream) {
+    if (failed_op) *failed_op = -1;
+    if (n_ops < 0 || (n_ops > 0 && !ops)) return DFQ_ERR_INVALID;
+    auto fail = [&](int32_t k, int rc) {
+        if (failed_op) *failed_op = k;
+        return rc;
+    };
+    // validate everything first: a rejected op enqueues nothing
+    for (int32_t k = 0; k < n_ops; ++k) {
+        const dfq_bc_op& op = ops[k];
+        switch (op.kind) {
+            case DFQ_BC_OP_EXPECT:
+                if (!op.a || !op.b || !op.out || op.n < 0) return fail(k, DFQ_ERR_INVALID);
+                break;
+            case DFQ_BC_OP_APPLY: {
+                if (!op.a || !op.b || !op.out || op.n <= 0 || op.i2 <= 0 || op.f <= 0) return fail(k, DFQ_ERR_INVALID);
+                const bool bcast = op.i2 == op.f || op.f == 1 || op.i2 == 1;
+                const int64_t bcols = (op.i2 == op.f || op.f == 1) ? op.i2 : op.f;
+                if (!bcast || op.n * bcols <= op.n) return fail(k, DFQ_ERR_SHAPE);
+                break;
+            }
+            case DFQ_BC_OP_PROPAGATE:
+                if (!op.a || !op.out || op.n <= 0 || op.f <= 0 || op.flag < 1) return fail(k, DFQ_ERR_INVALID);
+                if (op.n % op.f != 0) return fail(k, DFQ_ERR_SHAPE);
+                break;
+            default:
+                return fail(k, DFQ_ERR_INVALID);
+        }
+    }
+    for (int32_t k = 0; k < n_ops; ++k) {
+        const dfq_bc_op& op = ops[k];
+        int rc = DFQ_OK;
+        if (op.kind == DFQ_BC_OP_EXPECT)
+            rc = dfq_bc_expect(op.a, op.b, op.n, op.flag & 1, (op.flag >> 1) & 1, op.out, stream);
+        else if (op.kind == DFQ_BC_OP_APPLY)
+            rc = dfq_bc_apply(op.a, op.n, op.i2, op.b, op.f, op.out, op.out2, nullptr, stream);
+        else
+            rc = dfq_bc_propagate(op.a, op.n, op.out, op.f, op.flag, stream);
+        if (rc != DFQ_OK) return fail(k, rc);
+    }
+    return DFQ_OK;
+}
+
 extern "C" int dfq_act_moments(const float* w, const float* b, int64_t n, int32_t kind, int32_t sqrt_w, float eps,
                                int32_t accumulate, float* mean, float* var, void* stream) {
     if (!w || !b || !mean || !var || n < 0 || kind < 0 || kind > 2) return DFQ_ERR_INVALID;

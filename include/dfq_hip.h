@@ -274,6 +274,25 @@ int dfq_bc_apply(const float* E, int64_t o, int64_t i2, const float* expect, int
 int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_t f,
                      int32_t ref_threads, void* stream);
 
+/* dfq_bc_chain: a whole bias_correction walk's device work in one call -- the
+ * ops above, recorded by the host walk in graph order and enqueued back to back
+ * on `stream` (bias_correction.py:147-258 issues them one Python call each).
+ * Every op is validated before the first launch; a bad op returns its error code
+ * and `*failed_op` = its index, with nothing enqueued. */
+enum { DFQ_BC_OP_EXPECT = 0, DFQ_BC_OP_APPLY = 1, DFQ_BC_OP_PROPAGATE = 2 };
+typedef struct dfq_bc_op {
+    int32_t      kind;      /* DFQ_BC_OP_* */
+    int32_t      flag;      /* EXPECT: relu | (accumulate << 1); PROPAGATE: ref_threads */
+    const float* a;         /* EXPECT: fake_w  APPLY: E       PROPAGATE: bias_vec */
+    const float* b;         /* EXPECT: fake_b  APPLY: expect */
+    float*       out;       /* EXPECT: out     APPLY: bias    PROPAGATE: fake_b */
+    float*       out2;      /* APPLY: bias_vec (may be NULL) */
+    int64_t      n;         /* EXPECT: n       APPLY: o       PROPAGATE: numel */
+    int64_t      i2;        /* APPLY: i2 */
+    int64_t      f;         /* APPLY: expect numel  PROPAGATE: F */
+} dfq_bc_op;
+int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed_op, void* stream);
+
 /* ---- measurement --------------------------------------------------------
  * Same-mix streaming probe (no arithmetic): y = x, codes = bits of x, esum = x,
  * n elements (multiple of 4); blocks < 0 selects a 4-deep variant with -blocks

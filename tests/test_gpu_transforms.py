@@ -106,6 +106,42 @@ def test_bias_correction_helpers():
         bc._apply_bias_correction_E(layer, E, 32, 64, "cat", T(z["bc_expect_relu"]))
 
 
+def test_bc_chain_matches_single_ops():
+    """dfq_bc_chain (the walk's ops in one call) == the same fixtures as the
+    per-op entry points; a bad op is reported by index with nothing enqueued."""
+    import ctypes as C
+    from data_free_quantization_amd import _lib
+    z, _ = transform_cases()
+    L = _lib.load()
+    w, b = T(z["bc_w"]), T(z["bc_b"])
+    ex = torch.empty_like(b)
+    bias = T(z["bc_bias"]).clone()
+    E = T(z["bc_E"])
+    vec = torch.empty(32 * 64, device=DEV)
+    fb = T(z["bc_fb"]).clone()
+    ops = (_lib.BcOp * 3)()
+    ops[0].kind, ops[0].flag, ops[0].a, ops[0].b, ops[0].out, ops[0].n = (
+        _lib.DFQ_BC_OP_EXPECT, 1, w.data_ptr(), b.data_ptr(), ex.data_ptr(), b.numel())
+    ops[1].kind, ops[1].a, ops[1].b, ops[1].out, ops[1].out2, ops[1].n, ops[1].i2, ops[1].f = (
+        _lib.DFQ_BC_OP_APPLY, E.data_ptr(), ex.data_ptr(), bias.data_ptr(), vec.data_ptr(), 32, 64, ex.numel())
+    ops[2].kind, ops[2].flag, ops[2].a, ops[2].out, ops[2].n, ops[2].f = (
+        _lib.DFQ_BC_OP_PROPAGATE, 8, vec.data_ptr(), fb.data_ptr(), vec.numel(), 32)
+    failed = C.c_int32(0)
+    _lib.check(L.dfq_bc_chain(ops, 3, C.byref(failed), _lib.stream_of(fb)), "dfq_bc_chain")
+    assert failed.value == -1
+    assert np.array_equal(ex.cpu().numpy(), z["bc_expect_relu"])
+    assert np.array_equal(bias.cpu().numpy(), z["bc_bias_out"])
+    assert np.array_equal(vec.cpu().numpy(), z["bc_vec"])
+    assert np.array_equal(fb.cpu().numpy(), z["bc_fb_out"])
+    before = fb.clone()
+    ops[0].out = fb.data_ptr()          # would overwrite fb if anything ran
+    ops[2].f = 30                       # 2048 % 30 != 0: .view(-1, F) fails
+    assert L.dfq_bc_chain(ops, 3, C.byref(failed), _lib.stream_of(fb)) == _lib.DFQ_ERR_SHAPE
+    assert failed.value == 2
+    torch.cuda.synchronize()
+    assert torch.equal(fb, before)
+
+
 def test_bc_reference_named_helpers():
     """_compute_final_bias_correction + _apply_bias_correction (bias_correction.py:61-106)
     called by their reference names: same fixtures as the fused path."""
