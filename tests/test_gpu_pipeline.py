@@ -102,3 +102,31 @@ def test_per_channel_extension_matches_reference_slices():
         for i, k in enumerate(tkeys):
             r = fake_quant(graph[k].weight.detach(), 8, per_channel=True, symmetric=sym)
             assert hb(r.dq.cpu().numpy()) == bytes(P[f"{tag}_wh"][i]), (tag, k)
+
+
+def test_reference_bc_crash_keeps_earlier_corrections():
+    """DeepLab's reference-mode bias correction raises at its first 'cat' branch
+    (bias_correction.py:74-75).  The layers corrected before that point keep their
+    corrections, as in the reference's eager walk: the recorded device ops are
+    flushed before the error propagates, and nothing after the crash changes."""
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd.pipeline import run_dfq
+    from data_free_quantization_amd.utils.tracer import build_graph
+    model = zoo.build("deeplab", seed=0, relu=True).cuda()
+    g = build_graph(model, "positional")
+    graph, bottoms = g.getGraph(), g.getBottoms()
+    before = {}
+
+    def hook(stage):   # target biases as bias correction starts (graph order)
+        if stage == "clip":
+            before.update({k: graph[k].bias.detach().clone() for k in graph
+                           if type(graph[k]) in TARG and graph[k].bias is not None})
+
+    with pytest.raises(RuntimeError):
+        run_dfq(model, graph, bottoms, TARG, bc_mode="reference", stage_hook=hook)
+    assert before
+    changed = [not torch.equal(graph[k].bias.detach(), b) for k, b in before.items()]
+    assert any(changed)
+    last = max(i for i, c in enumerate(changed) if c)
+    assert not any(changed[last + 1:])
+    assert sum(changed) >= last // 2   # corrections run over the prefix, not one stray layer
