@@ -613,19 +613,18 @@ __device__ void tile_range_by_position(const CleRel& R, const CleTask& tk, uint3
     __syncthreads();   // tl is reused by the next task
 }
 
-__global__ void __launch_bounds__(kThreads)
-cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
-                      uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st) {
-    __shared__ float tl[2 * kThreads * kTileMaxKhw];
-    if (st->done) return;
-    const int par = st->iters & 1;
+// Range tasks [t0, t1) for parity `par`, taken by blocks blk, blk + nblk, ...
+// (tl: 2 * kThreads * kTileMaxKhw floats of LDS).
+__device__ __forceinline__ void cle_range_body(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks,
+                                               int64_t t0, int64_t t1, uint32_t* __restrict__ rng, int64_t M, int par,
+                                               int64_t blk, int64_t nblk, float* tl) {
     uint32_t* mins = rng + (int64_t)par * 2 * M;
     uint32_t* maxs = mins + M;
     uint32_t* omins = rng + (int64_t)(par ^ 1) * 2 * M;
     uint32_t* omaxs = omins + M;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    for (int64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
+    for (int64_t t = t0 + blk; t < t1; t += nblk) {
         const CleTask tk = tasks[t];
         const CleRel& R = rels[tk.rel];
         uint32_t* mn = mins + R.moff;
@@ -703,6 +702,16 @@ cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
             }
         }
     }
+}
+
+// `next` = 1: the ranges of the NEXT iteration (launched after this iteration's
+// last rescale, fused into the metric-tile launch; see cle_loop_tiles_range_kernel)
+__global__ void __launch_bounds__(kThreads)
+cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
+                      uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int next) {
+    __shared__ float tl[2 * kThreads * kTileMaxKhw];
+    if (st->done) return;
+    cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + next) & 1, blockIdx.x, gridDim.x, tl);
 }
 
 __global__ void __launch_bounds__(kThreads)
@@ -949,15 +958,14 @@ __global__ void cle_loop_snap_kernel(const CleLayer* __restrict__ layers, const 
 }
 
 
-__global__ void __launch_bounds__(kThreads)
-cle_loop_diff_tiles_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
-                           const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t nunits,
-                           float* __restrict__ b1buf, float* __restrict__ tailbuf, const CleState* __restrict__ st) {
-    __shared__ float d[kCleTile + kCleTailWords];
-    __shared__ float b0[512];
-    if (st->done) return;
+// Metric tiles taken by blocks blk, blk + nblk, ... (d: kCleTile + kCleTailWords
+// floats of LDS, b0: 512).
+__device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
+                                               const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units,
+                                               int64_t nunits, float* __restrict__ b1buf, float* __restrict__ tailbuf,
+                                               int64_t blk, int64_t nblk, float* d, float* b0) {
     const int tid = threadIdx.x;
-    for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+    for (int64_t u = blk; u < nunits; u += nblk) {
         const CleUnit un = units[u];
         const CleChunk ch = chunks[un.chunk];
         const CleLayer Ly = layers[ch.layer];
@@ -1024,6 +1032,38 @@ cle_loop_diff_tiles_kernel(const CleLayer* __restrict__ layers, const CleChunk* 
         }
         __syncthreads();   // LDS reused by the next unit
     }
+}
+
+constexpr int kCleTilesLds = kCleTile + kCleTailWords + 512;
+constexpr int kCleRangeLds = 2 * kThreads * kTileMaxKhw;
+
+__global__ void __launch_bounds__(kThreads)
+cle_loop_diff_tiles_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
+                           const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t nunits,
+                           float* __restrict__ b1buf, float* __restrict__ tailbuf, const CleState* __restrict__ st) {
+    __shared__ float lds[kCleTilesLds];
+    if (st->done) return;
+    cle_tiles_body(layers, chunks, b1off, units, nunits, b1buf, tailbuf, blockIdx.x, gridDim.x, lds,
+                   lds + kCleTile + kCleTailWords);
+}
+
+// The metric tiles of this iteration and the range launch of the next one in ONE
+// launch (fused schedule): both only read the weights the iteration's last rescale
+// wrote.  Blocks [0, ntb) take tiles, the rest the range tasks (parity iters + 1;
+// its resets clear this iteration's words, no longer read).
+__global__ void __launch_bounds__(kThreads)
+cle_loop_tiles_range_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
+                            const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t nunits,
+                            float* __restrict__ b1buf, float* __restrict__ tailbuf, int64_t ntb,
+                            const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
+                            uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st) {
+    __shared__ float lds[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
+    if (st->done) return;
+    if ((int64_t)blockIdx.x < ntb)
+        cle_tiles_body(layers, chunks, b1off, units, nunits, b1buf, tailbuf, blockIdx.x, ntb, lds,
+                       lds + kCleTile + kCleTailWords);
+    else
+        cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + 1) & 1, blockIdx.x - ntb, gridDim.x - ntb, lds);
 }
 
 // One wave per chunk: the rest of the cascade, the ILP and lane combines and
@@ -1517,13 +1557,15 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
 static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
     // grid caps: 2,048 / 4,096 blocks (caps of 128-1,024 measured 4-150 % slower on MobileNetV2)
     constexpr int64_t kStepGrid = 2048, kTileGrid = 4096;
+    // fused schedule: this iteration's ranges were taken at the end of the previous
+    // one (or by plan_run before the first); the next iteration's ride with the tiles
     for (int32_t k = 0; k < p->steps; ++k) {
-        const int64_t r0 = p->fused ? (k == 0 ? p->rstep[0] : 0) : p->rstep[k];
-        const int64_t r1 = p->fused ? (k == 0 ? p->rstep[1] : 0) : p->rstep[k + 1];
+        const int64_t r0 = p->fused ? 0 : p->rstep[k];
+        const int64_t r1 = p->fused ? 0 : p->rstep[k + 1];
         const int64_t a0 = p->astep[k], a1 = p->astep[k + 1];
         if (r1 > r0) {
             hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(r1 - r0, kStepGrid)), dim3(kThreads), 0, s,
-                               p->d_rels, p->d_rtasks, r0, r1, p->d_rng, p->M, p->d_state);
+                               p->d_rels, p->d_rtasks, r0, r1, p->d_rng, p->M, p->d_state, 0);
             DFQ_LAUNCH_CHECK();
         }
         if (a1 > a0) {
@@ -1533,9 +1575,21 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
             DFQ_LAUNCH_CHECK();
         }
     }
+    const int64_t nr = p->fused ? p->rstep[1] - p->rstep[0] : 0;   // next iteration's range tasks
+    const int64_t ntb = std::min<int64_t>(p->nunits, kTileGrid), nrb = std::min<int64_t>(nr, kStepGrid);
+    if (p->nchunks > 0 && ntb > 0 && nrb > 0) {
+        hipLaunchKernelGGL(cle_loop_tiles_range_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
+                           p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
+                           p->d_rtasks, p->rstep[0], p->rstep[1], p->d_rng, p->M, p->d_state);
+        DFQ_LAUNCH_CHECK();
+    } else if (nrb > 0) {
+        hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)nrb), dim3(kThreads), 0, s, p->d_rels, p->d_rtasks,
+                           p->rstep[0], p->rstep[1], p->d_rng, p->M, p->d_state, 1);
+        DFQ_LAUNCH_CHECK();
+    }
     if (p->nchunks > 0) {
-        if (p->nunits > 0) {
-            hipLaunchKernelGGL(cle_loop_diff_tiles_kernel, dim3((int)std::min<int64_t>(p->nunits, kTileGrid)), dim3(kThreads),
+        if (ntb > 0 && nrb == 0) {
+            hipLaunchKernelGGL(cle_loop_diff_tiles_kernel, dim3((int)ntb), dim3(kThreads),
                                0, s, p->d_layers, p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail,
                                p->d_state);
             DFQ_LAUNCH_CHECK();
@@ -1604,6 +1658,13 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
                            dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_units, p->nunits);
         DFQ_LAUNCH_CHECK();
     }
+    // fused schedule: the first iteration's ranges (later ones ride with the tiles)
+    if (p->fused && p->rstep[1] > p->rstep[0]) {
+        hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(p->rstep[1] - p->rstep[0], 2048)),
+                           dim3(kThreads), 0, s, p->d_rels, p->d_rtasks, p->rstep[0], p->rstep[1], p->d_rng, p->M,
+                           p->d_state, 0);
+        DFQ_LAUNCH_CHECK();
+    }
     // kCleBatch iterations as one HIP graph (kernels of finished runs return at
     // once: the stop rule lives in d_state); DFQ_CLE_GRAPH=0: eager launches.
     const char* ge = getenv("DFQ_CLE_GRAPH");
@@ -1666,7 +1727,8 @@ extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t
     if (chains) *chains = p->chains;
     if (steps) *steps = p->steps;
     if (launches)   // per iteration: range + rescale launches, then the metric (2) and the stop rule
-        *launches = (p->fused ? 1 + p->steps : 2 * p->steps) + (p->nunits > 0 ? 1 : 0) + (p->nchunks > 0 ? 1 : 0) + 1;
+        *launches = (p->fused ? p->steps + ((p->nunits > 0 && p->nchunks > 0) ? 0 : 1) : 2 * p->steps) +
+                    (p->nunits > 0 ? 1 : 0) + (p->nchunks > 0 ? 1 : 0) + 1;
     return DFQ_OK;
 }
 
