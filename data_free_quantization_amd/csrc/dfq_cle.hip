@@ -1133,9 +1133,30 @@ cle_loop_diff_combine_kernel(const CleLayer* __restrict__ layers, const CleChunk
 }
 
 // numpy pairwise float64 sum (identity 0 + pairwise_sum), as np.sum(diff_list).
+// numpy's pairwise leaf: n <= 128 values, 8 accumulators.
+__device__ __forceinline__ double np_pairwise_leaf(const double* x, int64_t n) {
+    if (n < 8) {
+        double res = 0.;
+        for (int64_t i = 0; i < n; ++i) res += x[i];
+        return res;
+    }
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = x[j];
+    int64_t i;
+    for (i = 8; i < n - (n % 8); i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += x[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += x[i];
+    return res;
+}
+
 __device__ double np_pairwise(const double* a, int64_t n) {
     // numpy's recursion (blocks of <= 128 with 8 accumulators; split at n/2
-    // rounded down to a multiple of 8) as an explicit post-order walk.
+    // rounded down to a multiple of 8) as an explicit post-order walk; a single
+    // leaf (every model here: <= 128 target layers) skips the frame stack.
+    if (n <= 128) return 0. + np_pairwise_leaf(a, n);
     struct Frame {
         int64_t o, n;
         int state;
@@ -1147,21 +1168,7 @@ __device__ double np_pairwise(const double* a, int64_t n) {
     while (fp > 0) {
         Frame& f = fr[fp - 1];
         if (f.n <= 128) {
-            const double* x = a + f.o;
-            double res;
-            if (f.n < 8) {
-                res = 0.;
-                for (int64_t i = 0; i < f.n; ++i) res += x[i];
-            } else {
-                double r[8];
-                for (int j = 0; j < 8; ++j) r[j] = x[j];
-                int64_t i;
-                for (i = 8; i < f.n - (f.n % 8); i += 8)
-                    for (int j = 0; j < 8; ++j) r[j] += x[i + j];
-                res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-                for (; i < f.n; ++i) res += x[i];
-            }
-            acc[ap++] = res;
+            acc[ap++] = np_pairwise_leaf(a + f.o, f.n);
             --fp;
         } else if (f.state == 0) {
             int64_t n2 = f.n / 2;
@@ -1184,16 +1191,18 @@ __device__ double np_pairwise(const double* a, int64_t n) {
 // then / n), np.sum over layers, history and the stop rule.  One block.
 __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32_t nl, const float* __restrict__ part,
                                       double* __restrict__ means, double* __restrict__ hist, CleState* __restrict__ st) {
+    __shared__ double sm[1024];   // the per-layer means, read back by one thread
     if (st->done) return;
+    double* m = nl <= 1024 ? sm : means;
     for (int l = threadIdx.x; l < nl; l += blockDim.x) {
         float acc = 0.f;
         for (int t = 0; t < 8; ++t) acc += part[(int64_t)l * 8 + t];
         const float sum = 0.f + acc;
-        means[l] = (double)(sum / (float)layers[l].n);
+        m[l] = (double)(sum / (float)layers[l].n);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const double dt = nl > 0 ? np_pairwise(means, nl) : 0.0;
+        const double dt = nl > 0 ? np_pairwise(m, nl) : 0.0;
         const int it = st->iters;
         hist[it] = dt;
         st->iters = it + 1;
