@@ -2,13 +2,21 @@
 
 One STEP = one pass of the fused DFQ sweep (per-channel symmetric INT8
 quantize-dequantize + integer codes + clip_weight + bias-correction error sums
-E[o,i]) over a batch of ``--copies`` independent MobileNetV2 weight sets
+E[o,i]) over ONE layer list: ``--copies`` MobileNetV2 weight sets back to back
 (BASELINE.json configs[1]; synthetic random-init weights of the reference's
-shapes, already resident in HBM).  The batch defeats the 256 MB Infinity Cache
+shapes, already resident in HBM).  The list defeats the 256 MB Infinity Cache
 (SURVEY.md 8d), so the number is an HBM number.
 
+At N GPUs the SAME layer list is LPT-sharded over the ranks (strong scaling,
+data_free_quantization_amd/distributed.py): rank 0 holds every weight and
+scatters each rank its slab once before timing; a step is every rank sweeping
+its share with outputs left sharded.  Also reported (``sharded_modes``): the
+step with a gather of every output slab to rank 0, rank 0 -> ranks scatter +
+sweep + gather (rank 0 holds everything, end to end), the in-place all-gather,
+and the replicated form (every rank sweeps the whole list; weak scaling).
+
   python bench.py [--gpus N --steps K --warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N     (one process per GPU; weak scaling)
+  torchrun --nproc-per-node N bench.py --gpus N     (one process per GPU, RCCL)
 
 Rank 0 prints ONE JSON line (contract in the task statement); ``roofline``
 times the sweep kernel with HIP events on the stream it is launched on;
@@ -40,7 +48,7 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--model", default="mobilenetv2", choices=["mobilenetv2", "resnet50", "deeplab"])
-    p.add_argument("--copies", type=int, default=0, help="weight sets per GPU (0: enough for >= 2 GiB)")
+    p.add_argument("--copies", type=int, default=0, help="weight sets in the layer list (0: enough for >= 2 GiB)")
     p.add_argument("--bits", type=int, default=8)
     p.add_argument("--granularity", default="channel", choices=["channel", "tensor"])
     p.add_argument("--asym", action="store_true", help="asymmetric (reference default) instead of symmetric")
@@ -51,27 +59,6 @@ def parse():
                    help="skip the other BASELINE configs (ResNet-50, DeepLab, INT4, per-tensor; sharded single model)")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r01.json"))
     return p.parse_args()
-
-
-def setup_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        # DFQ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
-        # cards round-robin); the default is RCCL, one rank per GPU.
-        backend = os.environ.get("DFQ_DIST_BACKEND", "nccl")
-        local = local % torch.cuda.device_count() if backend == "gloo" else local
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:
-            dist.init_process_group(backend)
-    else:
-        local = 0
-        torch.cuda.set_device(0)
-    return world, rank, torch.device(f"cuda:{local}")
 
 
 def model_shapes(name):
@@ -165,46 +152,111 @@ def single_model_latency(dev, stream, reps=200):
     return out
 
 
-def sharded_single_model(dev, stream, world, reps=20):
-    """BASELINE configs[4]: ONE ResNet-50 weight set (INT4 per-channel asym +
-    clip), its layer list LPT-sharded over the ranks; ms per pass with the
-    outputs left sharded and with a packed all-gather to every rank."""
+def _timed_steps(fn, dev, reps, warmup=3):
+    """Wall seconds per call of ``fn`` (collectives inside), barrier-bracketed and
+    max over ranks."""
     import torch.distributed as dist
+    from data_free_quantization_amd.distributed import max_over_ranks
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    if dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize(dev)
+    if dist.is_initialized():
+        dist.barrier()
+    return max_over_ranks(time.perf_counter() - t0, dev) / reps
+
+
+def sharded_modes(sw, dev, stream, reps=10):
+    """The layer-sharded sweep's collective forms (N > 1), ms per step:
+    sweep + gather of every output slab to rank 0; rank 0 -> ranks scatter of the
+    input slabs + sweep + gather (rank 0 holds the whole list, end to end);
+    sweep + in-place all_gather_into_tensor; and the replicated form (every rank
+    sweeps the WHOLE list after a broadcast: weak scaling, weight-GB/s summed)."""
+    from data_free_quantization_amd.sweep import SweepItem, SweepPlan
+    world = sw.world
+    wbytes = 4 * sum(s.numel for s in sw.specs)
+    out = {}
+
+    def step_root():
+        sw.run(stream)
+        sw.gather("root")
+
+    def step_e2e():
+        sw.scatter()
+        sw.run(stream)
+        sw.gather("root")
+
+    def step_all():
+        sw.run(stream)
+        sw.gather("all")
+
+    for name, fn in (("sweep_gather_root", step_root), ("scatter_sweep_gather_root", step_e2e),
+                     ("sweep_allgather", step_all)):
+        t = _timed_steps(fn, dev, reps)
+        out[f"{name}_ms"] = round(t * 1e3, 4)
+        out[f"{name}_weight_GBs"] = round(wbytes / t / 1e9, 1)
+    # replicas: every rank holds (broadcast) and sweeps the whole list
+    sw.broadcast()
+    items = []
+    for i, s in enumerate(sw.specs):
+        o = sw.outputs(i)
+        items.append(SweepItem(src=sw.weight(i), dst=o.dq, codes=o.codes, scale=o.scale, zero=o.zero, esum=o.esum,
+                               bits=s.bits, per_channel=s.per_channel, symmetric=s.symmetric, khw=s.khw,
+                               clip=s.clip, rows=s.rows, pack_int4=s.pack_int4))
+    plan = SweepPlan(items)
+    t = _timed_steps(lambda: plan.execute(stream), dev, reps)
+    plan.destroy()
+    out["replicas_ms"] = round(t * 1e3, 4)
+    out["replicas_weight_GBs"] = round(world * wbytes / t / 1e9, 1)
+    out["note"] = ("host-timed, barrier-bracketed, max over ranks; gather/scatter = one grouped send/recv per "
+                   "rank of exactly its slab (RCCL over xGMI), all-gather = one in-place "
+                   "all_gather_into_tensor of the slab-strided arena; replicas = every rank sweeps the whole "
+                   f"list (weight-GB/s summed over {world} ranks)")
+    return out
+
+
+def sharded_single_model(dev, stream, reps=20):
+    """BASELINE configs[4]: ONE ResNet-50 weight set (INT4 per-channel asym +
+    clip, packed codes), its layer list LPT-sharded over the ranks; ms per pass
+    with outputs left sharded, gathered to rank 0, and all-gathered."""
     from data_free_quantization_amd import distributed as D
-    from data_free_quantization_amd.sweep import khw_of
-    gen = torch.Generator(device=dev).manual_seed(7)            # same weights on every rank
-    ws = [synth_weight(s, dev, gen) for s in model_shapes("resnet50")]
-    specs = [D.output_spec(w, True, 4, False, khw_of(w), False, pack_int4=True) for w in ws]
-    compute = D.gpu_sweep(ws, bits=4, per_channel=True, symmetric=False, want_esum=False, clip=(-15.0, 15.0),
-                          reuse=True, pack_int4=True)
+    specs = D.uniform_specs(model_shapes("resnet50"), bits=4, per_channel=True, symmetric=False, want_esum=False,
+                            clip=(-15.0, 15.0), pack_int4=True)
+    sw = D.ShardedSweep(specs, replicate=True, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(7)
+    if sw.rank == 0:
+        for i, s in enumerate(specs):
+            sw.weight(i).copy_(synth_weight(s.shape, dev, gen))
+    sw.broadcast()
     res = {}
-    for gather in ("none", "all"):
-        for _ in range(3):
-            D.sharded_sweep(ws, compute, specs, gather=gather)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            D.sharded_sweep(ws, compute, specs, gather=gather)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        t = D.max_over_ranks(time.perf_counter() - t0, dev) / reps
-        res[f"ms_gather_{gather}"] = round(t * 1e3, 4)
-    res["weights"] = sum(w.numel() for w in ws)
-    res["note"] = "host-timed per pass (sweep launch + packing + all_gather_into_tensor); single-model sizes " \
-                  "are latency bound"
+    for name, fn in (("none", lambda: sw.run(stream)),
+                     ("root", lambda: (sw.run(stream), sw.gather("root"))),
+                     ("all", lambda: (sw.run(stream), sw.gather("all")))):
+        res[f"ms_gather_{name}"] = round(_timed_steps(fn, dev, reps) * 1e3, 4)
+    sw.destroy()
+    res["weights"] = sum(s.numel for s in specs)
+    res["note"] = "host-timed per pass; single-model sizes are latency bound (one 102 MB weight set)"
     return res
 
 
 def cpu_baseline(args, shapes, seconds):
     """The reference's CPU arithmetic on the GPU box's host cores, on a bounded
-    sample of the same workload (whole weight sets of the model):
+    sample of the same workload (one whole weight set of the model), BASELINE.md
+    section 2's protocol: best of 5 passes with all of this process's host threads and
+    best of 5 (3 when a pass is long) on 1 thread.
 
-    * value: oracle/torch_port.py -- the reference's own torch CPU op sequence
-      (UniformQuantize.forward per output channel, clip_weight's clamp, the BC
-      error sums), torch.get_num_threads() intra-op threads;
-    * per_tensor_GBs: quantize_targ_layer's per-tensor sweep, same threads;
-    * oracle_c_1thread_GBs: the scalar C port (oracle/dfq_oracle.c), 1 thread."""
+    * value: oracle/torch_port.py -- a PORT of the reference's own torch CPU op
+      sequence (UniformQuantize.forward per output channel, clip_weight's clamp,
+      the BC error sums; the per-channel composition SURVEY.md 8a row a3 defines),
+      ``cores`` intra-op threads;
+    * per_tensor_*: quantize_targ_layer's per-tensor sweep (the reference's own
+      mode), same protocol;
+    * oracle_c_1thread_GBs: the scalar C restatement (oracle/dfq_oracle.c)."""
     import numpy as np
     from oracle import oracle as O
     from oracle import torch_port as TP
@@ -217,14 +269,17 @@ def cpu_baseline(args, shapes, seconds):
     elems = sum(w.size for w in ws)
     sym = not args.asym
 
-    def timed(fn, budget):
-        passes, t0 = 0, time.perf_counter()
-        while True:
+    def best_of(fn, reps, budget):
+        """Best single-pass seconds over up to ``reps`` passes within ``budget`` s."""
+        best, t_all = None, time.perf_counter()
+        for _ in range(reps):
+            t0 = time.perf_counter()
             fn()
-            passes += 1
             el = time.perf_counter() - t0
-            if el >= budget:
-                return passes, el
+            best = el if best is None else min(best, el)
+            if time.perf_counter() - t_all > budget:
+                break
+        return best
 
     def port_pass():
         for w in tw:
@@ -245,16 +300,30 @@ def cpu_baseline(args, shapes, seconds):
                        want_esum=not args.no_esum)
 
     threads = torch.get_num_threads()
-    p1, e1 = timed(port_pass, seconds)
-    p2, e2 = timed(per_tensor_pass, max(1.0, seconds / 5))
-    p3, e3 = timed(c_pass, max(1.0, seconds / 5))
-    gbs = lambda p, e: round(4.0 * elems * p / e / 1e9, 4)
-    return {"value": gbs(p1, e1), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"{args.model} x1 weight set ({len(ws)} layers, {elems} weights) x {p1} passes in {e1:.1f} s: "
-                      f"the reference's torch CPU ops (oracle/torch_port.py: quantize() per output channel + "
-                      f"clamp + BC error sums), {threads} intra-op threads",
-            "per_tensor_GBs": gbs(p2, e2), "per_tensor_sample": f"{p2} passes, quantize_targ_layer arithmetic",
-            "oracle_c_1thread_GBs": gbs(p3, e3)}
+    gbs = lambda t: round(4.0 * elems / t / 1e9, 4)    # noqa: E731
+    t_port = best_of(port_pass, 5, seconds * 0.4)
+    t_tensor = best_of(per_tensor_pass, 5, seconds * 0.05)
+    torch.set_num_threads(1)
+    try:
+        t_port1 = best_of(port_pass, 5, seconds * 0.4)
+        t_tensor1 = best_of(per_tensor_pass, 5, seconds * 0.05)
+    finally:
+        torch.set_num_threads(threads)
+    t_c = best_of(c_pass, 3, seconds * 0.1)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
+    return {"value": gbs(t_port), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{args.model} x1 weight set ({len(ws)} layers, {elems} weights), best of 5 passes: a port "
+                      f"of the reference's torch CPU ops (oracle/torch_port.py: quantize() per output channel + "
+                      f"clamp + BC error sums) on {threads} intra-op threads (this process's host-CPU share: "
+                      f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, os.cpu_count()={os.cpu_count()}, "
+                      f"affinity {affinity})",
+            "value_1thread": gbs(t_port1),
+            "per_tensor_GBs": gbs(t_tensor), "per_tensor_1thread_GBs": gbs(t_tensor1),
+            "per_tensor_sample": "quantize_targ_layer's arithmetic (one range per tensor), best of 5",
+            "oracle_c_1thread_GBs": gbs(t_c)}
 
 
 def pipeline_timing(dev, model="mobilenetv2"):
@@ -329,18 +398,27 @@ def same_mix_probe(n, dev, stream, reps=10):
 
 def main():
     args = parse()
-    world, rank, dev = setup_dist(args)
-    from data_free_quantization_amd.sweep import SweepPlan
-    from data_free_quantization_amd.distributed import max_over_ranks
-    items, shapes, per_copy, copies = build_batch(args.model, dev, args.copies, args.bits,
-                                                  args.granularity == "channel", not args.asym, not args.no_esum)
-    plan = SweepPlan(items)
-    st = plan.stats
+    from data_free_quantization_amd import distributed as D
+    world, rank, dev = D.init_from_env()
+    shapes = model_shapes(args.model)
+    per_copy = sum(int(torch.Size(s).numel()) for s in shapes)
+    copies = args.copies or max(1, -(-(2 << 30) // (4 * per_copy)))   # >= 2 GiB of fp32 weights in the list
+    specs = D.uniform_specs(shapes * copies, bits=args.bits, per_channel=args.granularity == "channel",
+                            symmetric=not args.asym, want_esum=not args.no_esum, clip=(-15.0, 15.0))
+    # rank 0 holds the whole layer list and scatters each rank its slab (untimed)
+    sw = D.ShardedSweep(specs, replicate=world > 1, device=dev)
+    if rank == 0:
+        gen = torch.Generator(device=dev).manual_seed(1234)
+        for i, s in enumerate(specs):
+            std = (2.0 / (s.shape[2] * s.shape[3] * s.shape[0])) ** 0.5 if len(s.shape) == 4 else 0.01
+            sw.weight(i).normal_(0.0, std, generator=gen)
+    sw.scatter()
+    st = sw.plan_stats
     stream = torch.cuda.current_stream(dev)
     if world > 1:
         import torch.distributed as dist
     for _ in range(args.warmup):
-        plan.execute(stream)
+        sw.run(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -349,21 +427,22 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        plan.execute(stream)
+        sw.run(stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    dev_ms = ev0.elapsed_time(ev1)          # device time of the K launches on this stream
-    t_step = max_over_ranks(wall, dev) / args.steps
-    weight_bytes = 4 * per_copy * copies * world
+    dev_ms = ev0.elapsed_time(ev1)          # device time of this rank's K launches on this stream
+    t_step = D.max_over_ranks(wall, dev) / args.steps
+    weight_bytes = 4 * per_copy * copies    # the whole list, swept once per step by all ranks together
     value = weight_bytes / t_step / 1e9
     launch_ms = dev_ms / args.steps          # device time of one execute() (st["launches"] kernels)
     achieved = st["algo_bytes"] / (launch_ms / 1e3) / 1e9
-    plan.destroy()
-    del plan, items
+    modes = sharded_modes(sw, dev, stream) if world > 1 else None
+    sw.destroy()
+    del sw
     torch.cuda.empty_cache()
     traffic = None
     tj = Path(args.traffic_json)
@@ -372,10 +451,10 @@ def main():
             traffic = json.loads(tj.read_text()).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    sharded = sharded_single_model(dev, stream, world) if world > 1 and not args.no_secondary else None
+    sharded = sharded_single_model(dev, stream) if world > 1 and not args.no_secondary else None
     res = None
     if rank == 0:
-        probe_stream, probe_lds = same_mix_probe(per_copy * copies, dev, stream)
+        probe_stream, probe_lds = same_mix_probe(per_copy * copies // world, dev, stream)
         second = None if args.no_secondary else secondary_configs(dev, stream)
         single = None if args.no_secondary else single_model_latency(dev, stream)
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
@@ -389,22 +468,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "codes": f"{args.bits}-bit grid indices stored as "
                      f"{'int16' if args.bits > 8 else ('uint8' if args.asym else 'int8')}",
             "data": "synthetic random-init weights of the reference shapes (no checkpoints offline)",
             "config": {
-                "workload": f"{args.model} x{copies} weight sets per GPU: {args.granularity} "
+                "workload": f"{args.model} x{copies} weight sets in one layer list: {args.granularity} "
                             f"{'asym' if args.asym else 'sym'} INT{args.bits} quantize-dequantize + codes + "
                             f"clip[-15,15]" + ("" if args.no_esum else " + bias-correction error sums"),
                 "weight_shapes": f"{args.model} target layers (SURVEY.md 8, synthetic init)",
-                "copies_per_gpu": copies,
+                "copies": copies,
+                "layers": len(specs),
                 "layers_per_copy": len(shapes),
                 "weights_per_copy": per_copy,
-                "parallelism": f"{world} rank(s), one process per GPU, independent weight sets per rank "
-                               "(no data-path collective)",
+                "parallelism": f"{world} rank(s), one process per GPU: the layer list LPT-sharded over the ranks "
+                               "(rank 0 scatters the input slabs before timing), outputs left sharded "
+                               "(no collective in the timed step); gathered forms in sharded_modes",
             },
             "roofline": {
                 "bound": "hbm",
@@ -412,7 +493,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
+                "traffic": traffic if world == 1 else None,
                 "algo_bytes_per_launch": st["algo_bytes"],
                 "launch_ms": round(launch_ms, 4),
                 "launches": st["launches"],
@@ -420,12 +501,14 @@ def main():
                 "tasks": st["n_tasks_main"],
                 "grid_blocks": st["grid_blocks"],
                 "variant": st["variant"],
+                "rank": 0,
                 "same_mix_probe_GBs": probe_lds,
                 "same_mix_probe_note": "the sweep's memory pattern (LDS-DMA wave tasks, nt stores) without "
                                        "arithmetic, measured on this box after the timed steps (box to box "
                                        "5.2-6.5 TB/s, the sweep 5.9-6.3); a VGPR grid-stride stream of the "
                                        f"same mix: {probe_stream} GB/s",
             },
+            "sharded_modes": modes,
             "cpu_baseline": cpu,
             "secondary_configs": second,
             "single_model_latency": single,

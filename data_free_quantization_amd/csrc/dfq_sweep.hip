@@ -636,6 +636,25 @@ static void push_reduce(std::vector<DevTask>& R, const DevTask& k, int64_t span)
     R.push_back(k);
 }
 
+// DFQ_SWEEP_SHUFFLE=<seed> (A/B): visit the main list's 4-task units (one
+// workgroup's grid-stride step; block-row groups stay whole) in a seeded random
+// order instead of list order.  Only for single-slab plans (slab ranges index
+// the list).
+static void shuffle_quads(Built& B) {
+    const char* e = getenv("DFQ_SWEEP_SHUFFLE");
+    if (!e || !*e || B.mslab.size() > 2) return;
+    const int64_t units = (int64_t)B.main.size() / kWavesPerBlock;
+    if (units < 2) return;
+    uint64_t x = (uint64_t)atoll(e) * 0x9E3779B97F4A7C15ull + 1;
+    auto next = [&x]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (int64_t u = units - 1; u > 0; --u) {
+        const int64_t v = (int64_t)(next() % (uint64_t)(u + 1));
+        if (v != u)
+            std::swap_ranges(B.main.begin() + u * kWavesPerBlock, B.main.begin() + (u + 1) * kWavesPerBlock,
+                             B.main.begin() + v * kWavesPerBlock);
+    }
+}
+
 static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Variant& V) {
     const int64_t rspan = reduce_span();
     const bool use_blockrow = blockrow_enabled();
@@ -761,6 +780,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
     const int64_t base = (int64_t)B.main.size();   // slot pieces follow the single-pass tasks
     for (auto& m : B.mslab) m += base;
     B.main.insert(B.main.end(), B.slotted.begin(), B.slotted.end());
+    shuffle_quads(B);
     return DFQ_OK;
 }
 

@@ -4,8 +4,9 @@ fake-quantized fp32 weights).
 
 ``save(path, graph, state, ...)`` writes one safetensors file with, per target
 layer key ``k``: ``k.codes`` (the grid indices as the sweep wrote them: int8 /
-uint8 / int16, or packed nibbles), ``k.scale``, ``k.zero`` ([rows] per channel,
-[1] per tensor) and ``k.bias`` (the final fp32 bias after bias correction), plus
+uint8 / int16, or packed nibbles; asymmetric codes above 8 bits are unsigned
+16-bit patterns held in int16, recorded as ``code_storage: "u16_in_i16"``),
+``k.scale``, ``k.zero`` ([rows] per channel, [1] per tensor) and ``k.bias`` (the final fp32 bias after bias correction), plus
 metadata (bits, granularity, symmetric, clip, shapes).  ``load(path)`` returns
 the tensors; ``dequantize(entry)`` rebuilds the fp32 weight exactly as the sweep
 did: ``clamp(fl(fl(q * s) + zero), clip)``.
@@ -33,8 +34,11 @@ def save(path, graph, state: Dict, *, bits: int, granularity: str, symmetric: bo
         if layer.bias is not None:
             tensors[f"{k}.bias"] = layer.bias.detach().contiguous()
         layers[k] = {"shape": list(w.shape), "type": type(layer).__name__}
+    storage = "nibbles" if packed else ("i8" if symmetric else "u8") if bits <= 8 else \
+        ("i16" if symmetric else "u16_in_i16")
     meta = {"format": "dfq-mi355x/1", "bits": bits, "granularity": granularity, "symmetric": symmetric,
-            "clip": list(clip) if clip is not None else None, "packed_int4": packed, "layers": layers}
+            "clip": list(clip) if clip is not None else None, "packed_int4": packed, "code_storage": storage,
+            "layers": layers}
     save_file({n: t.cpu() for n, t in tensors.items()}, str(path), metadata={"dfq": json.dumps(meta)})
     return layers
 
@@ -64,6 +68,10 @@ def dequantize(meta: dict, key: str, entry: Dict[str, torch.Tensor]) -> torch.Te
         q = torch.stack([c & 0xF, c >> 4], 1).view(-1)[:n]
         if meta["symmetric"]:
             q = torch.where(q >= 8, q - 16, q)
+    elif not meta["symmetric"] and meta["bits"] > 8:
+        # asymmetric codes 0 .. 2^b - 1 > 32767 are uint16 bit patterns in an int16
+        # tensor (the sweep's (int16_t)(int)q): reinterpret, do not sign-extend
+        q = q.to(torch.int32) & 0xFFFF
     rows = entry["scale"].numel()
     qf = q.reshape(rows, -1).to(torch.float32)
     y = qf * entry["scale"].view(-1, 1)      # fl(q * s)

@@ -9,6 +9,9 @@ Same flags and stage order; the transforms run on the GPU.  Additive flags:
   --bc_mode {literal,reference,fused}          see pipeline.py (default literal = the
                        reference's effective behaviour)
   --val PATH           ImageNet-val folder for --task cls evaluation
+  --world_size N       shard quantize_targ_layer's layer list over N ranks (one
+                       process per GPU under torchrun, RCCL all-gather of the
+                       results; distributed.py); rank 0 evaluates / logs / exports
 
 Example (README.md:137 of the reference):
   python -m data_free_quantization_amd.main_dfq --task cls --relu --equalize --absorption \
@@ -64,6 +67,8 @@ def get_argument(argv=None):
     p.add_argument("--device", default="cuda:0")
     p.add_argument("--export", default=None,
                    help="write the integer weights (codes, scale, zero, bias) to this safetensors file")
+    p.add_argument("--world_size", type=int, default=1,
+                   help="ranks sharing quantize_targ_layer's layer list (launch with torchrun --nproc-per-node N)")
     return p.parse_args(argv)
 
 
@@ -137,6 +142,14 @@ def main(argv=None):
     args = get_argument(argv)
     assert args.relu or args.relu == args.equalize, "must replace relu6 to relu while equalization"
     assert args.equalize or args.absorption == args.equalize, "must use absorption with equalize"
+    rank = 0
+    if args.world_size > 1:
+        from . import distributed as D
+        world, rank, dev = D.init_from_env()
+        if world != args.world_size:
+            raise ValueError(f"--world_size {args.world_size} but WORLD_SIZE={world} (launch with torchrun "
+                             f"--nproc-per-node {args.world_size})")
+        args.device = str(dev)
     model, name = build_model(args)
     if args.sizedisp:
         print("param size:", sum(p.numel() for p in model.parameters()) * 4 / 2 ** 20, "MB")
@@ -171,7 +184,7 @@ def main(argv=None):
         fused_clip = [-15, 15] if (args.clip_weight and args.bc_mode == "fused") else None
         graph = quantize_targ_layer(graph, args.bits_weight, args.bits_bias, targ_layer,
                                     granularity=args.granularity, symmetric=args.symmetric, clip=fused_clip,
-                                    state=state)
+                                    state=state, shard=args.world_size > 1)
         set_quant_minmax(graph, bottoms)   # main_dfq.py:217
     if args.clip_weight and not (args.quantize and args.bc_mode == "fused"):
         clip_weight(graph, range_clip=[-15, 15], targ_type=targ_layer)
@@ -183,21 +196,26 @@ def main(argv=None):
                         error_sums=err)
     torch.cuda.synchronize()
     print(f"DFQ weight transforms took {time.perf_counter() - t0:.3f} s on {args.device}")
-    if args.export and args.quantize and state:
+    if args.export and args.quantize and state and rank == 0:
         from . import export
         clip = [-15, 15] if args.clip_weight else None   # fused in the sweep or clip_weight after it: same clamp
         export.save(args.export, graph, state, bits=args.bits_weight, granularity=args.granularity,
                     symmetric=args.symmetric, clip=clip)
         print(f"Exported {len(state)} quantized layers to {args.export}")
 
-    if args.quantize:
-        replace_op()
-    start = time.time()
-    accuracy = inference_all(model, args.task, args)
-    print(f"Inference time is {time.time() - start} seconds")
-    if args.quantize:
-        restore_op()
-    if args.log:
+    accuracy = None
+    if rank == 0:
+        if args.quantize:
+            replace_op()
+        start = time.time()
+        accuracy = inference_all(model, args.task, args)
+        print(f"Inference time is {time.time() - start} seconds")
+        if args.quantize:
+            restore_op()
+    if args.world_size > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    if args.log and rank == 0:
         with open("dfq_result.txt", "a+") as ww:
             ww.write("task: {}, resnet: {}, relu: {}, equalize: {}, absorption: {}, quantize: {}, correction: {}, "
                      "clip: {}, bits_weight: {}, bits_activation: {}, bits_bias: {}\n".format(

@@ -129,7 +129,8 @@ def _identity_forward_hooks(bn):
 
 
 def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, granularity="tensor",
-                        symmetric=False, clip=None, state: Optional[Dict] = None):
+                        symmetric=False, clip=None, state: Optional[Dict] = None, shard: bool = False,
+                        group=None):
     """Fake-quantize every target layer's weight (and bias when bits_bias < 32) in
     place, all layers in one grouped launch.
 
@@ -138,7 +139,16 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
     ``symmetric=True``, ``clip=(lo, hi)`` fused (the clip_weight clamp), and
     ``state`` -- a dict filled with per-layer codes/scale/zero and the BC error
     sums E[o,i] of this quantization.
+
+    ``shard=True`` with torch.distributed initialised (main_dfq --world_size N,
+    every rank holding the model): each rank sweeps its LPT share of the tensors
+    into its slab of an output arena, one in-place all-gather (RCCL) gives every
+    rank every result, and each rank writes them back into its parameters
+    (distributed.ShardedSweep).  Results are identical to the unsharded call.
     """
+    if shard and torch.distributed.is_initialized():
+        return _quantize_targ_layer_sharded(graph, bit_weight, bits_bias, targ_type, granularity=granularity,
+                                            symmetric=symmetric, clip=clip, state=state, group=group)
     print("Quantizing Layer parameters")
     if bits_bias == 32:
         print("Skipping bias quantization (32 bits)")
@@ -190,6 +200,51 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
         for k, it in zip(keys, items):
             if k is not None:
                 state[k] = dict(codes=it.codes, scale=it.scale, zero=it.zero, esum=it.esum, khw=it.khw)
+    return graph
+
+
+def _quantize_targ_layer_sharded(graph, bit_weight, bits_bias, targ_type, *, granularity, symmetric, clip, state,
+                                 group):
+    """quantize_targ_layer's layer list sharded over the process group (see above)."""
+    from .. import distributed as D
+    print("Quantizing Layer parameters")
+    if bits_bias == 32:
+        print("Skipping bias quantization (32 bits)")
+    assert targ_type is not None, "targ_type cannot be None!"
+    if granularity not in ("tensor", "channel"):
+        raise ValueError("granularity must be 'tensor' or 'channel'")
+    per_channel = granularity == "channel"
+    want = state is not None
+    specs, srcs, keys = [], [], []
+    for layer_idx in graph:
+        layer = graph[layer_idx]
+        if type(layer) not in targ_type:
+            continue
+        w = layer.weight.data
+        _lib.require_device(w)
+        specs.append(D.LayerSpec(shape=tuple(w.shape), bits=bit_weight, per_channel=per_channel,
+                                 symmetric=symmetric, want_codes=want, want_esum=want,
+                                 clip=tuple(clip) if clip is not None else None))
+        srcs.append(w)
+        keys.append(layer_idx)
+        if layer.bias is not None and bits_bias < 32:
+            b = layer.bias.data
+            specs.append(D.LayerSpec(shape=tuple(b.shape), bits=bits_bias, per_channel=False, symmetric=False,
+                                     want_codes=False))
+            srcs.append(b)
+            keys.append(None)
+    if not specs:
+        return graph
+    sw = D.ShardedSweep(specs, sources=srcs, replicate=True, group=group)
+    sw.run()
+    sw.gather("all")
+    outs = [sw.outputs(i) for i in range(len(specs))]
+    torch._foreach_copy_(srcs, [o.dq for o in outs])        # back into the parameters, in place
+    sw.destroy()
+    if state is not None:
+        for k, sp, o in zip(keys, specs, outs):
+            if k is not None:
+                state[k] = dict(codes=o.codes, scale=o.scale, zero=o.zero, esum=o.esum, khw=sp.khw)
     return graph
 
 

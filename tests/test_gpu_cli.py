@@ -33,7 +33,8 @@ def test_main_dfq_full_flags(extra, tmp_path, monkeypatch):
     assert sum(float(q.running_min) == 0.0 and float(q.running_max) == 6.0 for q in qs) > 30
 
 
-@pytest.mark.parametrize("extra", [[], ["--granularity", "channel", "--symmetric", "--bc_mode", "fused"]])
+@pytest.mark.parametrize("extra", [[], ["--granularity", "channel", "--symmetric", "--bc_mode", "fused"],
+                                   ["--bits_weight", "16"], ["--bits_weight", "16", "--granularity", "channel"]])
 def test_main_dfq_export_roundtrip(extra, tmp_path, monkeypatch):
     """--export writes the integer grid (codes, scale, zero) and final biases; the
     exported layers dequantize to the model's weights bit for bit."""
@@ -44,12 +45,86 @@ def test_main_dfq_export_roundtrip(extra, tmp_path, monkeypatch):
             "--export", str(out)] + extra
     model, graph, _ = main_dfq.main(argv)
     meta, layers = export.load(out, device="cuda:0")
-    assert meta["bits"] == 8 and len(layers) == 53
+    assert meta["bits"] == (16 if "16" in extra else 8) and len(layers) == 53
     by_name = {str(k): k for k in graph}
     for key, entry in layers.items():
         layer = graph[by_name[key]]
         w = export.dequantize(meta, key, entry)
         assert torch.equal(w, layer.weight.detach()), key
         assert torch.equal(entry["bias"], layer.bias.detach()), key
-        if "--symmetric" not in extra:
+        if "--symmetric" not in extra and "16" not in extra:
             assert entry["codes"].dtype == torch.uint8 and entry["scale"].numel() == 1
+    if "16" in extra:   # the unsigned 16-bit grid really uses codes >= 32768
+        assert meta["code_storage"] == "u16_in_i16"
+        assert any(int((e["codes"] < 0).sum()) > 0 for e in layers.values())
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("gran", ["tensor", "channel"])
+def test_quantize_targ_layer_sharded_rccl_world1(gran, monkeypatch):
+    """quantize_targ_layer(shard=True) under an RCCL ("nccl") process group: the
+    same weights, biases, codes, scales and E as the unsharded call."""
+    import os
+    import torch.distributed as dist
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd.utils.layer_transform import quantize_targ_layer
+    from data_free_quantization_amd.utils.tracer import build_graph
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(_free_port()))
+    dev = torch.device("cuda:0")
+    models, states = [], []
+    for shard in (False, True):
+        m = zoo.build("resnet50", seed=3).to(dev)
+        g = build_graph(m, "positional").getGraph()
+        st = {}
+        if shard:
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        try:
+            quantize_targ_layer(g, 8, 8, (nn.Conv2d, nn.Linear), granularity=gran, symmetric=gran == "channel",
+                                clip=(-0.3, 0.3), state=st, shard=shard)
+            torch.cuda.synchronize()
+        finally:
+            if shard:
+                dist.destroy_process_group()
+        models.append(m)
+        states.append(st)
+    for (n, a), (_, b) in zip(models[0].state_dict().items(), models[1].state_dict().items()):
+        assert torch.equal(a, b), n
+    assert states[0].keys() == states[1].keys() and len(states[0]) == 54
+    for k in states[0]:
+        for f in ("codes", "scale", "zero", "esum"):
+            assert torch.equal(states[0][k][f], states[1][k][f]), (k, f)
+
+
+def test_main_dfq_world2_one_gpu(tmp_path, monkeypatch):
+    """main_dfq --world_size 2 under torchrun (two ranks on the one GPU, gloo
+    between them): rank 0's export equals a single-process run's, tensor for
+    tensor."""
+    import os
+    import subprocess
+    import sys
+    from safetensors.torch import load_file
+    from data_free_quantization_amd import main_dfq
+    flags = ["--task", "cls", "--relu", "--equalize", "--absorption", "--quantize", "--correction", "--clip_weight",
+             "--granularity", "channel", "--symmetric", "--bc_mode", "fused"]
+    monkeypatch.chdir(tmp_path)
+    one = tmp_path / "one.safetensors"
+    main_dfq.main(flags + ["--export", str(one)])
+    two = tmp_path / "two.safetensors"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DFQ_DIST_BACKEND="gloo", PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "data_free_quantization_amd.main_dfq", "--world_size", "2"] + flags + ["--export", str(two)]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    a, b = load_file(str(one)), load_file(str(two))
+    assert a.keys() == b.keys() and len(a) > 0
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
