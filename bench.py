@@ -370,7 +370,7 @@ def same_mix_probe(n, dev, stream, reps=10):
     y = torch.empty_like(x)
     cds = torch.empty(n, dtype=torch.uint8, device=dev)
     e = torch.empty_like(x)
-    L = _lib.load()
+    L = _lib.load_diag()   # the probes live in the diagnostics library (include/dfq_diag.h)
     s = C.c_void_p(stream.cuda_stream)
 
     def best_of(fn):
@@ -405,20 +405,37 @@ def main():
     copies = args.copies or max(1, -(-(2 << 30) // (4 * per_copy)))   # >= 2 GiB of fp32 weights in the list
     specs = D.uniform_specs(shapes * copies, bits=args.bits, per_channel=args.granularity == "channel",
                             symmetric=not args.asym, want_esum=not args.no_esum, clip=(-15.0, 15.0))
-    # rank 0 holds the whole layer list and scatters each rank its slab (untimed)
-    sw = D.ShardedSweep(specs, replicate=world > 1, device=dev)
-    if rank == 0:
-        gen = torch.Generator(device=dev).manual_seed(1234)
-        for i, s in enumerate(specs):
-            std = (2.0 / (s.shape[2] * s.shape[3] * s.shape[0])) ** 0.5 if len(s.shape) == 4 else 0.01
-            sw.weight(i).normal_(0.0, std, generator=gen)
-    sw.scatter()
-    st = sw.plan_stats
     stream = torch.cuda.current_stream(dev)
+    std_of = lambda shp: (2.0 / (shp[2] * shp[3] * shp[0])) ** 0.5 if len(shp) == 4 else 0.01   # noqa: E731
+    sw = plan = None
     if world > 1:
         import torch.distributed as dist
+        # rank 0 holds the whole layer list and scatters each rank its slab (untimed)
+        sw = D.ShardedSweep(specs, replicate=True, device=dev)
+        if rank == 0:
+            gen = torch.Generator(device=dev).manual_seed(1234)
+            for i, s in enumerate(specs):
+                sw.weight(i).normal_(0.0, std_of(s.shape), generator=gen)
+        sw.scatter()
+        st = sw.plan_stats
+        run = lambda: sw.run(stream)   # noqa: E731
+    else:
+        # one rank: no exchange, so no slabs -- every tensor is its own allocation, in
+        # the order eager code makes them (input, then its outputs).  One arena per
+        # field measured bimodal from box to box (1.08 or 1.31-1.37 ms per step,
+        # profiles/r02/ab_arena.md), per-tensor allocations 1.09-1.14.
+        from data_free_quantization_amd.sweep import SweepPlan, allocate
+        gen = torch.Generator(device=dev).manual_seed(1234)
+        items = []
+        for s in specs:
+            w = torch.empty(s.shape, device=dev).normal_(0.0, std_of(s.shape), generator=gen)
+            items.append(allocate(w, bits=s.bits, per_channel=s.per_channel, symmetric=s.symmetric, khw=s.khw,
+                                  want_esum=s.want_esum, clip=s.clip, pack_int4=s.pack_int4))
+        plan = SweepPlan(items)
+        st = plan.stats
+        run = lambda: plan.execute(stream)   # noqa: E731
     for _ in range(args.warmup):
-        sw.run(stream)
+        run()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -427,7 +444,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        sw.run(stream)
+        run()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -441,8 +458,10 @@ def main():
     launch_ms = dev_ms / args.steps          # device time of one execute() (st["launches"] kernels)
     achieved = st["algo_bytes"] / (launch_ms / 1e3) / 1e9
     modes = sharded_modes(sw, dev, stream) if world > 1 else None
-    sw.destroy()
-    del sw
+    for obj in (sw, plan):
+        if obj is not None:
+            obj.destroy()
+    del sw, plan, run
     torch.cuda.empty_cache()
     traffic = None
     tj = Path(args.traffic_json)
@@ -483,9 +502,10 @@ def main():
                 "layers": len(specs),
                 "layers_per_copy": len(shapes),
                 "weights_per_copy": per_copy,
-                "parallelism": f"{world} rank(s), one process per GPU: the layer list LPT-sharded over the ranks "
-                               "(rank 0 scatters the input slabs before timing), outputs left sharded "
-                               "(no collective in the timed step); gathered forms in sharded_modes",
+                "parallelism": (f"{world} ranks, one process per GPU: the layer list LPT-sharded over the ranks "
+                                "(rank 0 scatters the input slabs before timing), outputs left sharded "
+                                "(no collective in the timed step); gathered forms in sharded_modes")
+                if world > 1 else "1 rank: the whole layer list on one GPU (per-tensor allocations, no exchange)",
             },
             "roofline": {
                 "bound": "hbm",

@@ -32,9 +32,11 @@ EXPORTS = [
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
     "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
     "dfq_bias_absorb", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate", "dfq_bc_chain",
-    "dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline",
     "dfq_act_moments", "dfq_act_minmax", "dfq_act_affine",
 ]
+#: entry points only the diagnostics library exports (include/dfq_diag.h)
+DIAG_EXPORTS = ["dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline"]
+DIAG_LIB_PATH = PKG / "libdfq_diag.so"
 
 
 class TensorDesc(C.Structure):
@@ -87,10 +89,15 @@ class DFQLibraryError(RuntimeError):
 
 
 def load(path: Optional[os.PathLike] = None) -> C.CDLL:
-    """Load (once) and type the library.  Raises if it is not built."""
+    """Load (once) and type the library.  Raises if it is not built.
+    ``DFQ_LIB=diag`` makes the diagnostics build (libdfq_diag.so: the same entry
+    points plus A/B variants, environment switches and probes) the library of this
+    process -- for scripts/ A/B runs only."""
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
+    if path is None and os.environ.get("DFQ_LIB") == "diag":
+        path = DIAG_LIB_PATH
     p = Path(path) if path else LIB_PATH
     if not p.exists():
         raise DFQLibraryError(
@@ -135,22 +142,40 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_bc_apply": ([P, I64, I64, P, I64, P, P, C.POINTER(I64), P], C.c_int),
         "dfq_bc_propagate": ([P, I64, P, I64, I32, P], C.c_int),
         "dfq_bc_chain": ([C.POINTER(BcOp), I32, C.POINTER(I32), P], C.c_int),
-        "dfq_probe_stream": ([P, P, P, P, I64, I32, P], C.c_int),
-        "dfq_debug_timeline": ([P, I64], C.c_int),
-        "dfq_probe_lds": ([P, P, P, P, I64, I32, I32, P], C.c_int),
         "dfq_act_moments": ([P, P, I64, I32, I32, F32, I32, P, P, P], C.c_int),
         "dfq_act_minmax": ([P, P, I64, I32, F32, F32, P, P], C.c_int),
         "dfq_act_affine": ([P, P, P, I64, I64, I64, I64, P, P], C.c_int),
+    }
+    diag = {
+        "dfq_probe_stream": ([P, P, P, P, I64, I32, P], C.c_int),
+        "dfq_debug_timeline": ([P, I64], C.c_int),
+        "dfq_probe_lds": ([P, P, P, P, I64, I32, I32, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    for name, (args, res) in diag.items():
+        if hasattr(L, name):
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
     if L.dfq_abi_version() != 1:
         raise DFQLibraryError("libdfq_hip.so ABI version mismatch")
     if path is None:
         _LIB = L
     return L
+
+
+_DIAG: Optional[C.CDLL] = None
+
+
+def load_diag() -> C.CDLL:
+    """The diagnostics library (include/dfq_diag.h): bench.py's ceiling probes."""
+    global _DIAG
+    if _DIAG is None:
+        _DIAG = load(DIAG_LIB_PATH)
+    return _DIAG
 
 
 def check(rc: int, what: str, shape_error=RuntimeError):

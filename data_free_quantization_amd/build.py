@@ -15,7 +15,12 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libdfq_hip.so"
-SOURCES = ["dfq_lib.hip", "dfq_sweep.hip", "dfq_transform.hip", "dfq_cle.hip", "dfq_probe.hip"]
+SOURCES = ["dfq_lib.hip", "dfq_sweep.hip", "dfq_transform.hip", "dfq_cle.hip"]
+# Diagnostics build (bench.py's ceiling probes, scripts/ A/B runs): the same
+# sources with -DDFQ_DIAGNOSTICS (the sweep's A/B variants and environment
+# switches) plus the probes (include/dfq_diag.h).  Never loaded by the product path.
+DIAG_LIB = PKG / "libdfq_diag.so"
+DIAG_SOURCES = SOURCES + ["dfq_probe.hip"]
 ARCH = os.environ.get("DFQ_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: no FMA contraction (bit parity with torch CPU eager ops).
@@ -41,24 +46,35 @@ def _stale(out: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    deps = [CSRC / s for s in SOURCES] + [CSRC / "dfq_common.h", ROOT / "include" / "dfq_hip.h", Path(__file__)]
-    if not force and not _stale(LIB, deps):
-        return LIB
+def _build_one(out: Path, sources, defines, force: bool, verbose: bool) -> Path:
+    deps = [CSRC / s for s in sources] + [CSRC / "dfq_common.h", ROOT / "include" / "dfq_hip.h",
+                                          ROOT / "include" / "dfq_diag.h", Path(__file__)]
+    if not force and not _stale(out, deps):
+        return out
     objs = []
-    for s in SOURCES:
-        obj = CSRC / (Path(s).stem + ".o")
-        cmd = [hipcc(), *FLAGS, "-I", str(ROOT / "include"), "-I", str(CSRC), "-c", str(CSRC / s), "-o", str(obj)]
+    tag = out.stem
+    for s in sources:
+        obj = CSRC / f"{Path(s).stem}.{tag}.o"
+        cmd = [hipcc(), *FLAGS, *defines, "-I", str(ROOT / "include"), "-I", str(CSRC), "-c", str(CSRC / s),
+               "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(str(obj))
-    tmp = LIB.with_suffix(".so.tmp")
+    tmp = out.with_suffix(".so.tmp")
     cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *objs]
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, out)
     for o in objs:
         os.remove(o)
+    return out
+
+
+def build(force: bool = False, verbose: bool = False, diagnostics: bool = True) -> Path:
+    """Build libdfq_hip.so (the product) and, by default, libdfq_diag.so."""
+    _build_one(LIB, SOURCES, [], force, verbose)
+    if diagnostics:
+        _build_one(DIAG_LIB, DIAG_SOURCES, ["-DDFQ_DIAGNOSTICS"], force, verbose)
     return LIB
 
 

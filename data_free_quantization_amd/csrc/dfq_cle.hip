@@ -1255,7 +1255,7 @@ struct dfq_cle_plan {
 
 // DFQ_CLE_TIMING: host-side phase times of create / run / destroy on stderr.
 static bool cle_timing() {
-    static const bool on = getenv("DFQ_CLE_TIMING") != nullptr;
+    static const bool on = ab_env("DFQ_CLE_TIMING") != nullptr;
     return on;
 }
 static double now_us() {
@@ -1676,7 +1676,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     }
     // kCleBatch iterations as one HIP graph (kernels of finished runs return at
     // once: the stop rule lives in d_state); DFQ_CLE_GRAPH=0: eager launches.
-    const char* ge = getenv("DFQ_CLE_GRAPH");
+    const char* ge = ab_env("DFQ_CLE_GRAPH");
     const bool use_graph = !(ge && ge[0] == '0');
     const double tc0 = now_us();
     if (use_graph && !p->gexec && !init.done) {
@@ -1716,7 +1716,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         fprintf(stderr, "DFQ_CLE_TIMING run: capture+instantiate %.1f us, loop %.1f us (%d iterations launched)\n",
                 tc1 - tc0, now_us() - tc1, launched);
     const CleState fin = *p->h_state;
-    if (getenv("DFQ_CLE_DEBUG")) {   // per-layer chunk sums of the last iteration run
+    if (ab_env("DFQ_CLE_DEBUG")) {   // per-layer chunk sums of the last iteration run
         std::vector<float> part(8 * std::max(p->nl, 1));
         DFQ_HIP_CHECK(hipMemcpy(part.data(), p->d_part, sizeof(float) * part.size(), hipMemcpyDeviceToHost));
         for (int32_t l = 0; l < p->nl; ++l) {

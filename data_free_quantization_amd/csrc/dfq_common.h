@@ -6,6 +6,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "dfq_hip.h"
 
 namespace dfq {
@@ -361,6 +362,23 @@ __host__ __device__ inline float aten_outer_col_sum(const float* a, int64_t R, i
 // Host-side error plumbing shared by the translation units.
 namespace dfq {
 void set_last_hip_error(hipError_t e);
+// Stream-ordered host -> device upload of a host-built table (task lists, fold
+// jobs): `bytes` are copied into a pinned staging slot at once, the DMA is
+// enqueued on `s`, and the slot is reused only after an event recorded behind
+// that DMA has completed.  The caller's buffer may die at return; nothing
+// synchronises the stream.
+hipError_t stage_h2d(void* dst, const void* src, size_t bytes, hipStream_t s);
+// Environment switches for A/B runs and diagnostics: read only by the diagnostics
+// library (libdfq_diag.so, built with -DDFQ_DIAGNOSTICS); the product library
+// runs its measured defaults whatever the environment says.
+inline const char* ab_env(const char* name) {
+#ifdef DFQ_DIAGNOSTICS
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 }
 #define DFQ_HIP_CHECK(expr)                                   \
     do {                                                      \

@@ -4,6 +4,7 @@
 // bench.py times it next to the sweep so the roofline fraction can be read
 // against an achievable same-mix ceiling as well as against the 8 TB/s spec.
 #include "dfq_common.h"
+#include "dfq_diag.h"
 
 namespace dfq {
 __global__ void __launch_bounds__(256) probe_stream_kernel(const float4* __restrict__ x, float4* __restrict__ y,

@@ -23,6 +23,9 @@
 // per-row reductions and the KHW error sums, and writes dq (16 B/lane), codes
 // (4 B/lane) and E.  Waves walk the task table grid-stride (persistent grid).
 #include "dfq_common.h"
+#ifdef DFQ_DIAGNOSTICS
+#include "dfq_diag.h"
+#endif
 
 #include <algorithm>
 #include <cstring>
@@ -603,7 +606,13 @@ static int piece_len(int khw, bool vec4, int chunk, bool packed = false) {
     return p > 0 ? p : -1;
 }
 
-// DFQ_SWEEP_BLOCKROW=0: long rows through the reduce launch instead (A/B switch).
+// A/B and diagnostics switches (DFQ_SWEEP_VARIANT / _SLAB_MB / _REDUCE_SPAN /
+// _SHUFFLE / _BLOCKS_PER_CU) are read only by the diagnostics library
+// (libdfq_diag.so, -DDFQ_DIAGNOSTICS); the product library runs the measured
+// defaults whatever the environment says.
+
+// DFQ_SWEEP_BLOCKROW=0: long rows through the reduce launch instead (a supported
+// alternative schedule, parity-tested against the default).
 static bool blockrow_enabled() {
     const char* e = getenv("DFQ_SWEEP_BLOCKROW");
     return !(e && e[0] == '0');
@@ -613,7 +622,7 @@ static bool blockrow_enabled() {
 // about this many MB, each reduced and quantized back to back, so the second read
 // of a slab can still hit the 256 MB Infinity Cache (0: one slab).
 static int64_t slab_bytes() {
-    const char* e = getenv("DFQ_SWEEP_SLAB_MB");
+    const char* e = ab_env("DFQ_SWEEP_SLAB_MB");
     return (e && *e) ? (int64_t)atoll(e) << 20 : 0;
 }
 
@@ -621,7 +630,7 @@ static int64_t slab_bytes() {
 // elements per wave task (fewer same-address atomics, longer read streams).
 // DFQ_SWEEP_REDUCE_SPAN overrides (A/B).
 static int64_t reduce_span() {
-    const char* e = getenv("DFQ_SWEEP_REDUCE_SPAN");
+    const char* e = ab_env("DFQ_SWEEP_REDUCE_SPAN");
     return (e && *e) ? std::max<int64_t>(1, atoll(e)) : 16384;
 }
 static void push_reduce(std::vector<DevTask>& R, const DevTask& k, int64_t span) {
@@ -641,7 +650,7 @@ static void push_reduce(std::vector<DevTask>& R, const DevTask& k, int64_t span)
 // order instead of list order.  Only for single-slab plans (slab ranges index
 // the list).
 static void shuffle_quads(Built& B) {
-    const char* e = getenv("DFQ_SWEEP_SHUFFLE");
+    const char* e = ab_env("DFQ_SWEEP_SHUFFLE");
     if (!e || !*e || B.mslab.size() > 2) return;
     const int64_t units = (int64_t)B.main.size() / kWavesPerBlock;
     if (units < 2) return;
@@ -785,7 +794,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
 }
 
 static int variant_from_env() {
-    const char* e = getenv("DFQ_SWEEP_VARIANT");
+    const char* e = ab_env("DFQ_SWEEP_VARIANT");
     if (!e || !*e) return kDefaultVariant;
     const int v = atoi(e);
     return (v >= 0 && v < kNumVariants) ? v : kDefaultVariant;
@@ -800,6 +809,10 @@ using MainKernel = void (*)(const DevTensor*, const DevTask*, int64_t, const uin
 
 static MainKernel main_kernel(int variant) {
 #define DFQ_V(i) kVariants[i].chunk, kVariants[i].max_rows, kVariants[i].prefetch
+#ifndef DFQ_DIAGNOSTICS
+    (void)variant;   // the product library carries the default variant only
+    return sweep_main_kernel<DFQ_V(kDefaultVariant), true, 1>;
+#else
     switch (variant) {
         case 1: return sweep_main_kernel<DFQ_V(1)>;
         case 2: return sweep_main_kernel<DFQ_V(2)>;
@@ -816,6 +829,7 @@ static MainKernel main_kernel(int variant) {
         case 13: return sweep_main_kernel<DFQ_V(13), true, 1, true>;
         default: return sweep_main_kernel<DFQ_V(0)>;
     }
+#endif
 #undef DFQ_V
 }
 
@@ -829,7 +843,7 @@ static MainKernel main_kernel(int variant) {
 constexpr int kBlocksPerCu = 64;
 static int blocks_per_cu() {
     static const int v = [] {
-        const char* e = getenv("DFQ_SWEEP_BLOCKS_PER_CU");
+        const char* e = ab_env("DFQ_SWEEP_BLOCKS_PER_CU");
         return e && *e ? std::max(1, std::min(1024, atoi(e))) : kBlocksPerCu;
     }();
     return v;
@@ -925,9 +939,8 @@ static int sweep_plan_create_impl(const dfq_tensor_desc* descs, int32_t n, void*
         if (!B.reduce.empty())
             std::memcpy(blob.data() + Lo.o_reduce, B.reduce.data(), sizeof(DevTask) * B.reduce.size());
         if (!B.main.empty()) std::memcpy(blob.data() + Lo.o_main, B.main.data(), sizeof(DevTask) * B.main.size());
-        if (ws) {
-            e = hipMemcpyAsync(base, blob.data(), Lo.o_slots, hipMemcpyHostToDevice, stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        if (ws) {   // stream-ordered: pinned staging, no host synchronisation
+            e = stage_h2d(base, blob.data(), Lo.o_slots, stream);
         } else {
             e = hipMemcpy(base, blob.data(), Lo.o_slots, hipMemcpyHostToDevice);
         }
@@ -1021,11 +1034,9 @@ extern "C" int dfq_sweep_plan_destroy(dfq_sweep_plan* p) {
 }
 
 // ---------------------------------------------------------------------------
-// Single-tensor path: tasks are uploaded into the caller's workspace with
-// hipMemcpyAsync from a per-call host staging vector kept alive by a stream
-// callback-free scheme: the workspace carries [slots | tensor | tasks] and the
-// host copy is made from pinned-agnostic memory, so we synchronise the copy
-// only (hipMemcpyAsync on pageable memory stages synchronously).
+// Single-tensor path: the workspace carries [slots | tensor | tasks]; the host-built
+// tables go up through the pinned staging ring (stage_h2d), so a call is
+// asynchronous on the caller's stream like every other entry point.
 // ---------------------------------------------------------------------------
 namespace dfq {
 static size_t single_ws_layout(const Built& B, size_t* off_tensor, size_t* off_reduce, size_t* off_main) {
@@ -1065,13 +1076,16 @@ extern "C" int dfq_quantize_tensor(const dfq_tensor_desc* d, void* ws, size_t ws
     DevTensor* dt = reinterpret_cast<DevTensor*>(base + ot);
     DevTask* dr = reinterpret_cast<DevTask*>(base + orr);
     DevTask* dm = reinterpret_cast<DevTask*>(base + om);
-    // Pageable host->device async copies are staged before hipMemcpyAsync returns,
-    // so the local vectors may be released afterwards.
-    DFQ_HIP_CHECK(hipMemcpyAsync(dt, B.tensors.data(), sizeof(DevTensor), hipMemcpyHostToDevice, s));
-    if (!B.reduce.empty())
-        DFQ_HIP_CHECK(hipMemcpyAsync(dr, B.reduce.data(), sizeof(DevTask) * B.reduce.size(), hipMemcpyHostToDevice, s));
-    if (!B.main.empty())
-        DFQ_HIP_CHECK(hipMemcpyAsync(dm, B.main.data(), sizeof(DevTask) * B.main.size(), hipMemcpyHostToDevice, s));
+    // one table blob [tensor | reduce tasks | main tasks] through the pinned staging
+    // ring: stream-ordered, no host synchronisation
+    {
+        const size_t tb = om + sizeof(DevTask) * B.main.size() - ot;
+        std::vector<char> blob(tb, 0);
+        std::memcpy(blob.data(), B.tensors.data(), sizeof(DevTensor));
+        if (!B.reduce.empty()) std::memcpy(blob.data() + (orr - ot), B.reduce.data(), sizeof(DevTask) * B.reduce.size());
+        if (!B.main.empty()) std::memcpy(blob.data() + (om - ot), B.main.data(), sizeof(DevTask) * B.main.size());
+        DFQ_HIP_CHECK(stage_h2d(dt, blob.data(), tb, s));
+    }
     if (!B.reduce.empty()) {
         DFQ_HIP_CHECK(hipMemsetAsync(slots, 0xFF, sizeof(uint32_t) * B.slots, s));
         DFQ_HIP_CHECK(hipMemsetAsync(slots + B.slots, 0x00, sizeof(uint32_t) * B.slots, s));
@@ -1085,13 +1099,10 @@ extern "C" int dfq_quantize_tensor(const dfq_tensor_desc* d, void* ws, size_t ws
                     slots + B.slots);
         DFQ_LAUNCH_CHECK();
     }
-    // The staging copies above read host vectors that die at return: make sure the
-    // runtime has consumed them (pageable memcpy is host-synchronous on ROCm, but
-    // do not rely on it for correctness).
-    DFQ_HIP_CHECK(hipStreamSynchronize(s));
     return DFQ_OK;
 }
 
+#ifdef DFQ_DIAGNOSTICS
 // Diagnostics: point variant 13's timeline at `buf` (4 uint64 per main-list task,
 // `cap` tasks); NULL/0 disables.  Not part of the reference interface.
 extern "C" int dfq_debug_timeline(void* buf, int64_t cap) {
@@ -1100,3 +1111,4 @@ extern "C" int dfq_debug_timeline(void* buf, int64_t cap) {
     DFQ_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_timeline_cap), &cap, sizeof(cap)));
     return DFQ_OK;
 }
+#endif  // DFQ_DIAGNOSTICS

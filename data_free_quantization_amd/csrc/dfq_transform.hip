@@ -662,7 +662,8 @@ extern "C" int dfq_bn_fold_batch(const dfq_bn_fold_desc* d, int32_t n, void* ws,
     std::vector<char> blob(need, 0);
     std::memcpy(blob.data(), jobs.data(), sizeof(BnFoldJob) * n);
     if (!chunks.empty()) std::memcpy(blob.data() + jb, chunks.data(), sizeof(BnFoldChunk) * chunks.size());
-    hipError_t e = hipMemcpyAsync(base, blob.data(), need, hipMemcpyHostToDevice, s);
+    hipError_t e = own ? hipMemcpyAsync(base, blob.data(), need, hipMemcpyHostToDevice, s)
+                       : stage_h2d(base, blob.data(), need, s);
     if (e == hipSuccess && !chunks.empty()) {
         hipLaunchKernelGGL(bn_fold_weight_batch_kernel, dim3((int)std::min<size_t>(chunks.size(), 4096)),
                            dim3(kThreads), 0, s, dj, dc, (int64_t)chunks.size());
@@ -672,9 +673,9 @@ extern "C" int dfq_bn_fold_batch(const dfq_bn_fold_desc* d, int32_t n, void* ws,
         hipLaunchKernelGGL(bn_fold_channel_batch_kernel, dim3(std::min(n, 2048)), dim3(kThreads), 0, s, dj, n);
         e = hipGetLastError();
     }
-    // The staging blob dies with this call (and private tables with it): wait for
-    // the stream rather than lean on pageable-copy staging semantics.
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    // Caller workspace: stream-ordered (pinned staging).  Private tables die with
+    // this call: wait for the stream then.
+    if (e == hipSuccess && own) e = hipStreamSynchronize(s);
     if (own) (void)hipFree(own);
     if (e != hipSuccess) {
         set_last_hip_error(e);

@@ -1,14 +1,17 @@
 """The reference CLI driver (main_dfq.py:36-267) on the MI355X DFQ path.
 
 Same flags and stage order; the transforms run on the GPU.  Additive flags:
-  --model {mobilenetv2,resnet50,deeplab}   (default: from --task/--resnet)
+  --model {mobilenetv2,resnet50,deeplab,resnet18}   (default: from --task/--resnet:
+                       --resnet = ResNet-18 as in the reference, torchvision layout)
   --weights PATH       state_dict to load (torch.load(weights_only=True)); synthetic
                        random-init weights otherwise (the reference checkpoints are
                        not shipped, .MISSING_LARGE_BLOBS)
   --granularity {tensor,channel}, --symmetric   weight quantizer (reference: tensor, asym)
   --bc_mode {literal,reference,fused}          see pipeline.py (default literal = the
                        reference's effective behaviour)
-  --val PATH           ImageNet-val folder for --task cls evaluation
+  --val PATH           ImageNet-val folder (ImageFolder layout) for --task cls evaluation
+  --voc PATH           VOCdevkit/VOC2012 for --task seg evaluation (mIoU)
+  --batch_size, --workers   evaluation DataLoader (reference: 256 / 4 cls, 32 / 2 seg)
   --world_size N       shard quantize_targ_layer's layer list over N ranks (one
                        process per GPU under torchrun, RCCL all-gather of the
                        results; distributed.py); rank 0 evaluates / logs / exports
@@ -64,6 +67,9 @@ def get_argument(argv=None):
     p.add_argument("--symmetric", action="store_true")
     p.add_argument("--bc_mode", default="literal", choices=["literal", "reference", "fused"])
     p.add_argument("--val", default="./val")
+    p.add_argument("--voc", default="./VOCdevkit/VOC2012/")
+    p.add_argument("--batch_size", type=int, default=256)
+    p.add_argument("--workers", type=int, default=4)
     p.add_argument("--device", default="cuda:0")
     p.add_argument("--export", default=None,
                    help="write the integer weights (codes, scale, zero, bias) to this safetensors file")
@@ -77,7 +83,7 @@ def _model_name(args):
         return args.model
     if args.task == "seg":
         return "deeplab"
-    return "resnet50" if args.resnet else "mobilenetv2"
+    return "resnet18" if args.resnet else "mobilenetv2"   # main_dfq.py:126-131
 
 
 def canonical_state_dict(state):
@@ -114,28 +120,28 @@ def build_model(args):
 
 
 def inference_all(model, task, args):
-    """Evaluation needs ImageNet-val (./val) + torchvision, or VOC for seg; neither
-    ships with the reference nor with this image.  Returns None when unavailable."""
-    if task != "cls" or not os.path.isdir(args.val):
-        print(f"Evaluation skipped: no dataset at {args.val}")
+    """main_dfq.py:66-113 on the GPU: ImageNet-val top-1 (``--val``, ImageFolder
+    layout) for cls, PASCAL VOC 2012 val mIoU (``--voc``) for seg, through the
+    torchvision-free harness in evaluate.py.  Returns None (with a message) when
+    the dataset is not there -- neither ships with the reference or this image."""
+    from . import evaluate
+    if task == "cls":
+        if not os.path.isdir(args.val):
+            print(f"Evaluation skipped: no ImageFolder at {args.val}")
+            return None
+        print("Start inference")
+        acc = evaluate.inference_cls(model, args.val, args.device, batch_size=args.batch_size,
+                                     workers=args.workers)
+        print(f"Final Accuracy: {acc * 100:.2f}%")
+        return acc
+    if not os.path.isdir(args.voc):
+        print(f"Evaluation skipped: no VOC 2012 tree at {args.voc}")
         return None
-    try:
-        from torchvision import datasets, transforms  # noqa: F401
-    except ImportError:
-        print("Evaluation skipped: torchvision is not installed")
-        return None
-    from torch.utils.data import DataLoader
-    ds = datasets.ImageFolder(args.val, transforms.Compose([
-        transforms.Resize(256), transforms.CenterCrop(224), transforms.ToTensor(),
-        transforms.Normalize(mean=[0.485, 0.456, 0.406], std=[0.229, 0.224, 0.225])]))
-    dl = DataLoader(ds, batch_size=256, shuffle=False, num_workers=4, pin_memory=True)
-    correct = total = 0
-    with torch.no_grad():
-        for image, label in dl:
-            pred = model(image.to(args.device)).argmax(1).cpu()
-            correct += int((pred == label).sum())
-            total += image.shape[0]
-    return correct / max(total, 1)
+    print("Start inference")
+    miou = evaluate.inference_seg(model, args.voc, args.device, batch_size=min(args.batch_size, 32),
+                                  workers=args.workers)
+    print(f"mIoU: {miou * 100:.2f}%")
+    return miou
 
 
 def main(argv=None):
@@ -203,6 +209,9 @@ def main(argv=None):
                     symmetric=args.symmetric, clip=clip)
         print(f"Exported {len(state)} quantized layers to {args.export}")
 
+    # main_dfq.py:237-240: inference in eval mode -- also the observers set_layer_bits
+    # created (new modules start in training mode)
+    model.eval()
     accuracy = None
     if rank == 0:
         if args.quantize:

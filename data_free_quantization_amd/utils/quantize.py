@@ -10,6 +10,7 @@ Tensors must live on a ROCm device; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import struct
 from dataclasses import dataclass
 from typing import Optional
 
@@ -173,12 +174,16 @@ class UniformQuantize(InplaceFunction):
         return grad_output, None, None, None, None, None, None
 
 
+def _dec_ord(e: int) -> float:
+    """Inverse of the library's order-preserving float encoding (dfq_common.h enc_ord)."""
+    u = (e & 0x7FFFFFFF) if (e & 0x80000000) else (~e & 0xFFFFFFFF)
+    return struct.unpack("<f", struct.pack("<I", u))[0]
+
+
 def _data_range(x: torch.Tensor):
-    """fp32 (min, max) of x via the device sweep (asym zero == min; max from the
-    negated tensor's min)."""
-    r1 = fake_quant(x.detach().contiguous(), 8, want_codes=False)
-    r2 = fake_quant((-x.detach()).contiguous(), 8, want_codes=False)
-    return r1.zero[0].item(), -r2.zero[0].item()
+    """fp32 (min, max) of x: one dfq_range launch and one 8-byte read back."""
+    a, b = (v & 0xFFFFFFFF for v in device_range(x).tolist())
+    return _dec_ord(~a & 0xFFFFFFFF), _dec_ord(b)
 
 
 def _no_autograd(*tensors) -> bool:

@@ -305,8 +305,66 @@ def relu6_to_relu(model: nn.Module) -> nn.Module:
     return model
 
 
-MODELS = {"mobilenetv2": MobileNetV2, "resnet50": ResNet50, "deeplab": DeepLab}
-INPUT_SHAPES = {"mobilenetv2": (4, 3, 224, 224), "resnet50": (4, 3, 224, 224), "deeplab": (4, 3, 513, 513)}
+# --------------------------------------------------------------------------
+# ResNet-18: the reference's --resnet model (main_dfq.py:126-128 loads
+# torchvision.models.resnet18, absent here).  Module names, shapes and forward
+# follow torchvision's ResNet(BasicBlock, [2, 2, 2, 2]) so its checkpoints load
+# into it: conv1/bn1/relu/maxpool, layer1..4 of BasicBlocks (downsample.0/.1),
+# avgpool, flatten, fc.
+# --------------------------------------------------------------------------
+class _BasicBlock(nn.Module):
+    def __init__(self, cin, planes, stride=1, down=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = down
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        out += identity
+        return self.relu(out)
+
+
+class ResNet18(nn.Module):
+    def __init__(self, n_class=1000):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self._cin = 64
+        self.layer1 = self._stage(64, 1)
+        self.layer2 = self._stage(128, 2)
+        self.layer3 = self._stage(256, 2)
+        self.layer4 = self._stage(512, 2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512, n_class)
+
+    def _stage(self, planes, stride):
+        down = None
+        if stride != 1 or self._cin != planes:
+            down = nn.Sequential(nn.Conv2d(self._cin, planes, 1, stride, bias=False), nn.BatchNorm2d(planes))
+        blocks = [_BasicBlock(self._cin, planes, stride, down), _BasicBlock(planes, planes)]
+        self._cin = planes
+        return nn.Sequential(*blocks)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(self.avgpool(x), 1)
+        return self.fc(x)
+
+
+MODELS = {"mobilenetv2": MobileNetV2, "resnet50": ResNet50, "deeplab": DeepLab, "resnet18": ResNet18}
+INPUT_SHAPES = {"mobilenetv2": (4, 3, 224, 224), "resnet50": (4, 3, 224, 224), "deeplab": (4, 3, 513, 513),
+                "resnet18": (4, 3, 224, 224)}
 
 
 def build(name: str, seed: int = 0, relu: bool = False) -> nn.Module:

@@ -1,0 +1,39 @@
+/*
+ * dfq_diag.h -- diagnostics entry points of libdfq_diag.so (NOT the product).
+ *
+ * libdfq_diag.so is the product library (every dfq_hip.h entry point) built with
+ * -DDFQ_DIAGNOSTICS: it also carries the sweep's A/B kernel variants and
+ * environment switches (DFQ_SWEEP_VARIANT, DFQ_SWEEP_SLAB_MB, DFQ_CLE_GRAPH, ...)
+ * and the probes below, which bench.py and scripts/ use to measure the ceiling
+ * of the sweep's memory pattern.  None of this is part of the reference
+ * interface; libdfq_hip.so exports none of it.
+ */
+#ifndef DFQ_DIAG_H_
+#define DFQ_DIAG_H_
+
+#include "dfq_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- measurement --------------------------------------------------------
+ * Same-mix streaming probe (no arithmetic): y = x, codes = bits of x, esum = x,
+ * n elements (multiple of 4); blocks < 0 selects a 4-deep variant with -blocks
+ * blocks (n multiple of 16).  Used by bench.py as the achievable ceiling for
+ * the sweep's traffic mix; not part of the reference interface. */
+int dfq_probe_stream(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t blocks,
+                     void* stream);
+/* Per-task timeline of sweep variant 13 (DFQ_SWEEP_VARIANT=13): 4 uint64 per
+ * main-list task {start, data landed, done (s_memrealtime, 100 MHz), xcc<<32|hw_id};
+ * buf NULL / cap 0 disables. */
+int dfq_debug_timeline(void* buf, int64_t cap);
+/* The sweep's memory pattern without arithmetic: 2048-element wave tasks through
+ * LDS-DMA, non-temporal dq / codes / E stores (copy_only: dq only).  n % 2048 == 0. */
+int dfq_probe_lds(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t copy_only,
+                  int32_t blocks, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFQ_DIAG_H_ */

@@ -293,22 +293,6 @@ typedef struct dfq_bc_op {
 } dfq_bc_op;
 int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed_op, void* stream);
 
-/* ---- measurement --------------------------------------------------------
- * Same-mix streaming probe (no arithmetic): y = x, codes = bits of x, esum = x,
- * n elements (multiple of 4); blocks < 0 selects a 4-deep variant with -blocks
- * blocks (n multiple of 16).  Used by bench.py as the achievable ceiling for
- * the sweep's traffic mix; not part of the reference interface. */
-int dfq_probe_stream(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t blocks,
-                     void* stream);
-/* Per-task timeline of sweep variant 13 (DFQ_SWEEP_VARIANT=13): 4 uint64 per
- * main-list task {start, data landed, done (s_memrealtime, 100 MHz), xcc<<32|hw_id};
- * buf NULL / cap 0 disables. */
-int dfq_debug_timeline(void* buf, int64_t cap);
-/* The sweep's memory pattern without arithmetic: 2048-element wave tasks through
- * LDS-DMA, non-temporal dq / codes / E stores (copy_only: dq only).  n % 2048 == 0. */
-int dfq_probe_lds(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t copy_only,
-                  int32_t blocks, void* stream);
-
 /* ---- activation ranges from BN statistics (set_quant_minmax,
  *      utils/layer_transform.py:356-618) ---------------------------------------
  * Per channel j, with w = sqrt_w ? sqrt(w[j] + eps) : w[j], b = b[j]:

@@ -1,4 +1,5 @@
 #!/bin/bash
+export DFQ_LIB=diag   # A/B variants and switches live in libdfq_diag.so
 # A/B of the long-row strategies on ResNet-50 and DeepLab (block-row pieces vs reduce launch).
 set -u
 mkdir -p gpurun_out

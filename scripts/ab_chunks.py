@@ -6,6 +6,8 @@ allocations) of each layout on one box, device ms per step of the bench list.
   interC<M>     per-layer interleaved fields (dq, codes, E, scale, zero), chunks of M MB
   <layout>+shuf the same with DFQ_SWEEP_SHUFFLE=1 (workgroup quads in random order)
 Inputs: one packed 4 KB arena (measured neutral)."""
+import os
+os.environ.setdefault("DFQ_LIB", "diag")   # A/B variants, switches and probes: libdfq_diag.so
 import gc
 import json
 import sys

@@ -1,4 +1,5 @@
 #!/bin/bash
+export DFQ_LIB=diag   # A/B variants and switches live in libdfq_diag.so
 # A/B an environment knob on the bench's sweep: ENVS="label:VAR=v,VAR2=w label2:..." BENCH_ARGS="..." REPS=n
 # Each configuration runs REPS times, interleaved; one JSON line per run into gpurun_out/ab_env.jsonl.
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export DFQ_LIB=diag   # A/B variants and switches live in libdfq_diag.so
 # Whole-bench A/B (primary + secondary configs + single-model latency) across env
 # configurations, interleaved: ENVS="label:VAR=v ..." REPS=n -> gpurun_out/ab_full.jsonl
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export DFQ_LIB=diag   # A/B variants and switches live in libdfq_diag.so
 # A/B of persistent-grid sizes (blocks per CU) for sweep variants, one process per setting.
 set -u
 mkdir -p gpurun_out

@@ -1,3 +1,4 @@
+export DFQ_LIB=diag   # A/B variants and switches live in libdfq_diag.so
 set -u
 mkdir -p gpurun_out
 for v in 6 1 2 11; do

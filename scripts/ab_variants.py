@@ -1,5 +1,7 @@
 """A/B the sweep kernel variants in ONE process on the same data (interleaved
 rounds, median and min per variant; cdna_hip_programming.md 5.4 rule 24)."""
+import os
+os.environ.setdefault("DFQ_LIB", "diag")   # A/B variants, switches and probes: libdfq_diag.so
 import json
 import os
 import statistics

@@ -1,5 +1,7 @@
 """Host-side breakdown of one device CLE call (plan create / run / destroy) on a
 model after BN folding: where the non-kernel time of the CLE stage goes."""
+import os
+os.environ.setdefault("DFQ_LIB", "diag")   # A/B variants, switches and probes: libdfq_diag.so
 import contextlib
 import io
 import sys

@@ -3,6 +3,8 @@
 Prints algorithmic GB/s for: the sweep (MobileNetV2 x155 batch), the flat
 same-mix stream (bench.py's probe), the sweep's own memory pattern without
 arithmetic (LDS-DMA in, non-temporal out), and plain copies."""
+import os
+os.environ.setdefault("DFQ_LIB", "diag")   # A/B variants, switches and probes: libdfq_diag.so
 import ctypes as C
 import json
 import sys

@@ -4,6 +4,8 @@ Each family is a >= 1 GiB batch of identical conv/linear weights; per-channel sy
 INT8 + codes + clip, with and without the BC error sums.  Prints one JSON line
 per (family, esum): algorithmic GB/s of one execute() and the plan's task mix.
 """
+import os
+os.environ.setdefault("DFQ_LIB", "diag")   # A/B variants, switches and probes: libdfq_diag.so
 import json
 import os
 import sys

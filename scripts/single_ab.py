@@ -1,6 +1,8 @@
 """Single-model sweep latency per kernel variant: one weight set,
 per-channel sym INT8 + codes + clip + BC sums, device us per execute (diagnostic).
 usage: python scripts/single_ab.py [variants...]   (env DFQ_SWEEP_BLOCKS_PER_CU applies)"""
+import os
+os.environ.setdefault("DFQ_LIB", "diag")   # A/B variants, switches and probes: libdfq_diag.so
 import json
 import os
 import sys

@@ -1,3 +1,4 @@
+export DFQ_LIB=diag   # A/B variants and switches live in libdfq_diag.so
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out/slab

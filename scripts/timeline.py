@@ -4,6 +4,8 @@ usage: python scripts/timeline.py [model] [copies]
 Prints the kernel span and, per phase, when tasks started / had their data /
 finished (us from the first task start), plus latency percentiles.  Timestamps
 are s_memrealtime (100 MHz, 10 ns resolution)."""
+import os
+os.environ.setdefault("DFQ_LIB", "diag")   # A/B variants, switches and probes: libdfq_diag.so
 import json
 import os
 import sys

@@ -128,3 +128,23 @@ def test_main_dfq_world2_one_gpu(tmp_path, monkeypatch):
     assert a.keys() == b.keys() and len(a) > 0
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+def test_main_dfq_evaluates_an_image_folder(tmp_path, monkeypatch):
+    """inference_all (main_dfq.py:66-113) through the torchvision-free harness: a
+    synthetic ImageFolder, the quantized MobileNetV2 with the tensor ops quantized
+    (replace_op), an accuracy in [0, 1] written to dfq_result.txt."""
+    from PIL import Image
+    from data_free_quantization_amd import main_dfq
+    rng = np.random.default_rng(0)
+    for c in range(3):
+        d = tmp_path / "val" / f"n{c:08d}"
+        d.mkdir(parents=True)
+        for k in range(3):
+            Image.fromarray(rng.integers(0, 256, (240, 300, 3), dtype=np.uint8)).save(d / f"{k}.png")
+    monkeypatch.chdir(tmp_path)
+    argv = ["--task", "cls", "--relu", "--equalize", "--absorption", "--quantize", "--correction", "--clip_weight",
+            "--val", str(tmp_path / "val"), "--batch_size", "4", "--workers", "0", "--log"]
+    model, graph, acc = main_dfq.main(argv)
+    assert acc is not None and 0.0 <= acc <= 1.0
+    assert "Accuracy: " in (tmp_path / "dfq_result.txt").read_text()

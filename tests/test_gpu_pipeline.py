@@ -18,7 +18,7 @@ TARG = (nn.Conv2d, nn.Linear)
 
 
 @pytest.mark.parametrize("cle_mode", ["device", "host"])
-@pytest.mark.parametrize("name", ["mobilenetv2", "resnet50", "deeplab"])
+@pytest.mark.parametrize("name", ["mobilenetv2", "resnet50", "deeplab", "resnet18"])
 def test_pipeline_matches_reference(name, cle_mode, monkeypatch):
     monkeypatch.setenv("DFQ_CLE_MODE", cle_mode)
     from data_free_quantization_amd import zoo

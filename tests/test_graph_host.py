@@ -19,6 +19,7 @@ EXPECT = {
     "mobilenetv2": (152, 53, 3_469_760, 37),
     "resnet50": (175, 54, 25_502_912, 32),
     "deeplab": (201, 61, 5_780_288, 35),
+    "resnet18": (69, 21, 11_678_912, 8),    # torchvision resnet18 (the reference's --resnet)
 }
 
 

@@ -12,8 +12,12 @@ HEADER = ROOT / "include" / "dfq_hip.h"
 LIB = ROOT / "data_free_quantization_amd" / "libdfq_hip.so"
 
 
-def declared():
-    text = HEADER.read_text()
+DIAG_HEADER = ROOT / "include" / "dfq_diag.h"
+DIAG_LIB = ROOT / "data_free_quantization_amd" / "libdfq_diag.so"
+
+
+def declared(header=HEADER):
+    text = header.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(dfq_[a-z0-9_]+)\s*\(", text)))
 
@@ -43,6 +47,23 @@ def test_library_exports_every_declared_symbol(lib):
 def test_python_binding_covers_header():
     from data_free_quantization_amd import _lib
     assert sorted(_lib.EXPORTS) == declared()
+    assert sorted(_lib.DIAG_EXPORTS) == [n for n in declared(DIAG_HEADER) if n not in declared()]
+
+
+def _exports(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(path)], capture_output=True, text=True, check=True).stdout
+    return set(re.findall(r" T (dfq_[a-z0-9_]+)", out))
+
+
+def test_product_library_carries_no_diagnostics():
+    """The probes, the timeline and the A/B variants live in libdfq_diag.so only."""
+    if not LIB.exists() or not DIAG_LIB.exists():
+        pytest.skip("libraries not built (run __graft_entry__.build())")
+    prod, diag = _exports(LIB), _exports(DIAG_LIB)
+    diag_only = [n for n in declared(DIAG_HEADER) if n not in declared()]
+    assert diag_only and not (set(diag_only) & prod)
+    assert set(declared(DIAG_HEADER)) <= diag
+    assert LIB.stat().st_size < DIAG_LIB.stat().st_size
 
 
 def test_version_and_errors(lib):

@@ -20,7 +20,7 @@ def _bias_hashes(R):
                      for k in R.tkeys])
 
 
-@pytest.mark.parametrize("name", ["mobilenetv2", "resnet50", "deeplab"])
+@pytest.mark.parametrize("name", ["mobilenetv2", "resnet50", "deeplab", "resnet18"])
 def test_oracle_pipeline_matches_reference(name):
     P = pipeline(name)
     m = zoo.build(name, seed=0, relu=True)
