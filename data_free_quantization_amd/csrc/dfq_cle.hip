@@ -439,7 +439,7 @@ struct CleState {
     int32_t done;
     int32_t count;       // Count
     int32_t max_iters;
-    int32_t pad;
+    int32_t error;       // persistent loop: a grid barrier timed out (never expected)
 };
 
 constexpr int kCleW1RowsPerTask = 4;       // one wave per row
@@ -714,21 +714,26 @@ cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
     cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + next) & 1, blockIdx.x, gridDim.x, tl);
 }
 
-__global__ void __launch_bounds__(kThreads)
-cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
-                      uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
-                      float eps, double smin, double smax) {
-    __shared__ float red[2][kThreads / 64][kColTileRows];
-    __shared__ float inv_s[kThreads];
-    __shared__ float inv_pos[kThreads * kTileMaxKhw];
-    if (st->done) return;
-    const int par = st->iters & 1;
-    const bool first_iter = st->iters == 0;
+// LDS of one rescale task (the position-parallel and fused tiles)
+struct CleApplyLds {
+    float red[2][kThreads / 64][kColTileRows];
+    float inv_s[kThreads];
+    float inv_pos[kThreads * kTileMaxKhw];
+};
+
+// Rescale tasks [t0, t1) of iteration parity `par`, taken by blocks blk, blk + nblk, ...
+__device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks,
+                                               int64_t t0, int64_t t1, uint32_t* __restrict__ rng, int64_t M,
+                                               int par, bool first_iter, int is_signed, float eps, double smin,
+                                               double smax, int64_t blk, int64_t nblk, CleApplyLds& A) {
+    auto& red = A.red;
+    float* inv_s = A.inv_s;
+    float* inv_pos = A.inv_pos;
     uint32_t* mins = rng + (int64_t)par * 2 * M;
     uint32_t* maxs = mins + M;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    for (int64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
+    for (int64_t t = t0 + blk; t < t1; t += nblk) {
         const CleTask tk = tasks[t];
         const CleRel& R = rels[tk.rel];
         const uint32_t* mn = mins + R.moff;
@@ -916,6 +921,16 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
     }
 }
 
+__global__ void __launch_bounds__(kThreads)
+cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
+                      uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
+                      float eps, double smin, double smax) {
+    __shared__ CleApplyLds A;
+    if (st->done) return;
+    cle_apply_body(rels, tasks, t0, t1, rng, M, st->iters & 1, st->iters == 0, is_signed, eps, smin, smax,
+                   blockIdx.x, gridDim.x, A);
+}
+
 // The metric's fp32 sums (torch.mean's vectorized_inner_sum over one chunk) as a
 // fixed tree.  A chunk of len elements is 32 streams (s = 8k + l: 8 vector lanes x
 // ILP 4; stream element i is chunk element 32i + s) of sz = len/32 elements, each
@@ -1068,15 +1083,14 @@ cle_loop_tiles_range_kernel(const CleLayer* __restrict__ layers, const CleChunk*
 
 // One wave per chunk: the rest of the cascade, the ILP and lane combines and
 // the scalar tail, in ATen's order; part[layer][t] = 0 + sum.
-__global__ void __launch_bounds__(kThreads)
-cle_loop_diff_combine_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks, int64_t nchunks,
-                             const int64_t* __restrict__ b1off, const float* __restrict__ b1buf,
-                             const float* __restrict__ tailbuf, float* __restrict__ part,
-                             const CleState* __restrict__ st) {
-    if (st->done) return;
+__device__ __forceinline__ void cle_combine_body(const CleLayer* __restrict__ layers,
+                                                 const CleChunk* __restrict__ chunks, int64_t nchunks,
+                                                 const int64_t* __restrict__ b1off, const float* __restrict__ b1buf,
+                                                 const float* __restrict__ tailbuf, float* __restrict__ part,
+                                                 int64_t blk, int64_t nblk) {
     const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+    const int64_t wave = blk * (kThreads / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = nblk * (kThreads / 64);
     for (int64_t k = wave; k < nchunks; k += nwaves) {
         const CleChunk ch = chunks[k];
         const int64_t len = ch.len;
@@ -1130,6 +1144,15 @@ cle_loop_diff_combine_kernel(const CleLayer* __restrict__ layers, const CleChunk
         }
         if (lane == 0) part[(int64_t)ch.layer * 8 + ch.t] = 0.f + fa;   // buffer[t] starts at 0
     }
+}
+
+__global__ void __launch_bounds__(kThreads)
+cle_loop_diff_combine_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks, int64_t nchunks,
+                             const int64_t* __restrict__ b1off, const float* __restrict__ b1buf,
+                             const float* __restrict__ tailbuf, float* __restrict__ part,
+                             const CleState* __restrict__ st) {
+    if (st->done) return;
+    cle_combine_body(layers, chunks, nchunks, b1off, b1buf, tailbuf, part, blockIdx.x, gridDim.x);
 }
 
 // numpy pairwise float64 sum (identity 0 + pairwise_sum), as np.sum(diff_list).
@@ -1189,10 +1212,12 @@ __device__ double np_pairwise(const double* a, int64_t n) {
 
 // Per-layer fp32 mean from the chunk sums (final_reduce over the 8-slot buffer,
 // then / n), np.sum over layers, history and the stop rule.  One block.
-__global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32_t nl, const float* __restrict__ part,
-                                      double* __restrict__ means, double* __restrict__ hist, CleState* __restrict__ st) {
-    __shared__ double sm[1024];   // the per-layer means, read back by one thread
-    if (st->done) return;
+// kLeafOnly: nl <= 128 (numpy's pairwise sum is one leaf) -- no frame stack, so
+// no scratch in the persistent kernel
+template <bool kLeafOnly = false>
+__device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ layers, int32_t nl,
+                                               const float* __restrict__ part, double* __restrict__ means,
+                                               double* __restrict__ hist, CleState* __restrict__ st, double* sm) {
     double* m = nl <= 1024 ? sm : means;
     for (int l = threadIdx.x; l < nl; l += blockDim.x) {
         float acc = 0.f;
@@ -1202,7 +1227,12 @@ __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const double dt = nl > 0 ? np_pairwise(m, nl) : 0.0;
+        double dt = 0.0;
+        if constexpr (kLeafOnly) {
+            dt = nl > 0 ? 0. + np_pairwise_leaf(m, nl) : 0.0;
+        } else {
+            dt = nl > 0 ? np_pairwise(m, nl) : 0.0;
+        }
         const int it = st->iters;
         hist[it] = dt;
         st->iters = it + 1;
@@ -1216,6 +1246,242 @@ __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32
         st->done = (!cont || st->iters >= st->max_iters) ? 1 : 0;
     }
 }
+
+__global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32_t nl, const float* __restrict__ part,
+                                      double* __restrict__ means, double* __restrict__ hist, CleState* __restrict__ st) {
+    __shared__ double sm[1024];   // the per-layer means, read back by one thread
+    if (st->done) return;
+    cle_final_body(layers, nl, part, means, hist, st, sm);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent loop (fused schedule): ONE cooperative launch runs up to `batch`
+// whole iterations -- every chain step's rescale, the metric tiles with the next
+// iteration's ranges, the chunk combine and the stop rule -- separated by grid
+// barriers instead of kernel boundaries, and leaves as soon as the stop rule
+// says so.  The grid is co-resident (hipLaunchCooperativeKernel), so the barrier
+// cannot deadlock; a barrier that still waits ~1 s flags st->error and every
+// block leaves (the host turns that into an error), so a fault cannot hang.
+// ---------------------------------------------------------------------------
+constexpr int kClePersistMaxSteps = 32;
+
+struct ClePersist {
+    const CleRel* rels;
+    const CleTask* rtasks;
+    const CleTask* atasks;
+    const CleLayer* layers;
+    const CleChunk* chunks;
+    const int64_t* b1off;
+    const CleUnit* units;
+    float* b1;
+    float* tail;
+    uint32_t* rng;
+    float* part;
+    double* means;
+    double* hist;
+    CleState* st;
+    uint32_t* bar;       // {arrivals, generation}
+    int64_t M, nchunks, nunits, r0, r1;
+    int64_t astep[kClePersistMaxSteps + 1];
+    int32_t steps, nl, is_signed, batch;
+    float eps;
+    double smin, smax;
+};
+
+constexpr uint32_t kCleBarrierSpins = 1u << 20;
+
+// Sense-reversing grid barrier: agent-scope release (this block's writes, the
+// XCD's L2 written back) before arriving, acquire after leaving.
+__device__ __forceinline__ bool cle_grid_sync(uint32_t* bar, uint32_t nblk, CleState* st) {
+    __shared__ int ok;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int good = 1;
+        // one release (L2 write-back) per block: the arrival RMW; the generation is
+        // read before it (no later block can bump it until this one has arrived)
+        const uint32_t gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t arrived = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (arrived == nblk - 1) {
+            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(bar + 1, gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            uint32_t spins = 0;
+            // relaxed polls: an acquire load would invalidate the XCD's L2 on every
+            // poll under the blocks still working; one acquire fence after the wait
+            while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > kCleBarrierSpins) {
+                    __hip_atomic_store(&st->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    good = 0;
+                    break;
+                }
+            }
+        }
+        if (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other blocks' writes
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
+// Two-level barrier: one L2 write-back and one L2 invalidate per XCD per barrier
+// (what a kernel boundary costs), instead of one per block.  The blocks of an
+// XCD meet at that XCD's counter (their stores are in its L2 once vmcnt drains);
+// the last one to arrive writes the XCD's L2 back (agent release), meets the
+// other XCDs' last arrivals at the global counter, invalidates the XCD's L2
+// (agent acquire) and releases its XCD's blocks, which then acquire too (their
+// CU's L1; the L2 has no stale lines left by then).
+// Counters only grow (arrival k of barrier b is the last one iff it equals
+// (b + 1) * members - 1), so nothing is reset between barriers.
+// Words (uint32, one 128-B line each): [0] global arrivals, [32] global
+// generation, [64 + 32 x] XCD x arrivals, [64 + 32 (16 + x)] XCD x generation,
+// [64 + 32 (32 + x)] XCD x block count (registration), [kCleRegBar] the
+// registration barrier.
+constexpr int kCleMaxXcd = 16;
+constexpr int kCleRegBar = 64 + 32 * 3 * kCleMaxXcd;   // the registration barrier's two words
+constexpr int kCleBarWords = kCleRegBar + 64;
+
+struct CleXcdSync {
+    uint32_t* bar;
+    uint32_t xcc;        // this block's XCD
+    uint32_t members;    // blocks on this XCD
+    uint32_t nxcd;       // XCDs holding blocks
+    uint32_t count;      // barriers passed by this block
+};
+
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & (kCleMaxXcd - 1);
+}
+
+__device__ __forceinline__ bool cle_spin_until(const uint32_t* w, uint32_t target, CleState* st) {
+    uint32_t spins = 0;
+    while ((int32_t)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kCleBarrierSpins) {
+            __hip_atomic_store(&st->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ bool cle_grid_sync_xcd(CleXcdSync& S, CleState* st) {
+    __shared__ int ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores are in the XCD's L2
+    __syncthreads();
+    const uint32_t b = ++S.count;
+    if (threadIdx.x == 0) {
+        int good = 1;
+        uint32_t* xa = S.bar + 64 + 32 * S.xcc;
+        uint32_t* xg = S.bar + 64 + 32 * (kCleMaxXcd + S.xcc);
+        const uint32_t a = __hip_atomic_fetch_add(xa, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a == b * S.members - 1) {   // the XCD's last arrival
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");      // this XCD's L2 -> memory
+            const uint32_t ga = __hip_atomic_fetch_add(S.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ga == b * S.nxcd - 1)
+                __hip_atomic_store(S.bar + 32, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                good = cle_spin_until(S.bar + 32, b, st);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");      // drop this XCD's stale L2 lines
+            __hip_atomic_store(xg, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            good = cle_spin_until(xg, b, st);
+            // this CU's L1 (a workgroup-scope invalidate is a no-op outside
+            // threadgroup-split mode, so the agent-scope acquire)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        if (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
+union ClePersistLds {
+    float tiles[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
+    CleApplyLds apply;
+    double fin[1024];
+};
+
+__global__ void __launch_bounds__(kThreads) cle_persist_kernel(ClePersist P) {
+    __shared__ ClePersistLds L;
+    __shared__ uint32_t reg[2];
+    const int64_t blk = blockIdx.x, nblk = gridDim.x;
+    // registration: which XCD this block runs on, and how many blocks each XCD
+    // holds (one plain barrier; the bar words are zeroed before the launch)
+    CleXcdSync S{P.bar, xcc_id(), 0, 0, 0};
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(P.bar + 64 + 32 * (2 * kCleMaxXcd + S.xcc), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    if (!cle_grid_sync(P.bar + kCleRegBar, (uint32_t)nblk, P.st)) return;
+    if (threadIdx.x == 0) {
+        uint32_t nx = 0;
+        for (int x = 0; x < kCleMaxXcd; ++x)
+            nx += __hip_atomic_load(P.bar + 64 + 32 * (2 * kCleMaxXcd + x), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) ? 1 : 0;
+        reg[0] = __hip_atomic_load(P.bar + 64 + 32 * (2 * kCleMaxXcd + S.xcc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        reg[1] = nx;
+    }
+    __syncthreads();
+    S.members = reg[0];
+    S.nxcd = reg[1];
+    for (int32_t it = 0; it < P.batch; ++it) {
+        // read after the last barrier (or before the launch): the same values in every block
+        const int32_t done = __hip_atomic_load(&P.st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int32_t iters = __hip_atomic_load(&P.st->iters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done) return;
+        const int par = iters & 1;
+        for (int32_t k = 0; k < P.steps; ++k) {
+            cle_apply_body(P.rels, P.atasks, P.astep[k], P.astep[k + 1], P.rng, P.M, par, iters == 0, P.is_signed,
+                           P.eps, P.smin, P.smax, blk, nblk, L.apply);
+            if (!cle_grid_sync_xcd(S, P.st)) return;
+        }
+        // the metric tiles and the next iteration's ranges: both only read what the
+        // last rescale wrote
+        if (P.nchunks > 0)
+            cle_tiles_body(P.layers, P.chunks, P.b1off, P.units, P.nunits, P.b1, P.tail, blk, nblk, L.tiles,
+                           L.tiles + kCleTile + kCleTailWords);
+        cle_range_body(P.rels, P.rtasks, P.r0, P.r1, P.rng, P.M, par ^ 1, blk, nblk, L.tiles);
+        if (!cle_grid_sync_xcd(S, P.st)) return;
+        if (P.nchunks > 0) {
+            cle_combine_body(P.layers, P.chunks, P.nchunks, P.b1off, P.b1, P.tail, P.part, blk, nblk);
+            if (!cle_grid_sync_xcd(S, P.st)) return;
+        }
+        if (blk == 0) cle_final_body<true>(P.layers, P.nl, P.part, P.means, P.hist, P.st, L.fin);
+        if (!cle_grid_sync_xcd(S, P.st)) return;
+    }
+}
+
+#ifdef DFQ_DIAGNOSTICS
+// Diagnostics: the persistent loop's grid barrier alone (nbar barriers, no work).
+// mode 0: the two-level XCD barrier; 1: the flat barrier (every block releases).
+__global__ void __launch_bounds__(kThreads) cle_barrier_probe_kernel(uint32_t* bar, CleState* st, int32_t nbar,
+                                                                     int32_t mode) {
+    __shared__ uint32_t reg[2];
+    CleXcdSync S{bar, xcc_id(), 0, 0, 0};
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(bar + 64 + 32 * (2 * kCleMaxXcd + S.xcc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!cle_grid_sync(bar + kCleRegBar, gridDim.x, st)) return;
+    if (threadIdx.x == 0) {
+        uint32_t nx = 0;
+        for (int x = 0; x < kCleMaxXcd; ++x)
+            nx += __hip_atomic_load(bar + 64 + 32 * (2 * kCleMaxXcd + x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1 : 0;
+        reg[0] = __hip_atomic_load(bar + 64 + 32 * (2 * kCleMaxXcd + S.xcc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        reg[1] = nx;
+    }
+    __syncthreads();
+    S.members = reg[0];
+    S.nxcd = reg[1];
+    for (int32_t i = 0; i < nbar; ++i) {
+        const bool ok = mode == 0 ? cle_grid_sync_xcd(S, st) : cle_grid_sync(bar + kCleRegBar + 32, gridDim.x, st);
+        if (!ok) return;
+    }
+}
+#endif
 
 }  // namespace dfq
 
@@ -1251,6 +1517,8 @@ struct dfq_cle_plan {
     void* d_tables = nullptr;       // every device table above but d_hist: ONE allocation
     void* d_snap_owned = nullptr;   // snapshots when the caller passed no workspace
     double* d_hist_owned = nullptr; // history beyond kCleHistCap iterations
+    uint32_t* d_bar = nullptr;      // persistent loop's grid barrier words
+    int32_t persist_grid = -1;      // cooperative grid of the persistent loop (0: not usable; -1: not sized)
 };
 
 // DFQ_CLE_TIMING: host-side phase times of create / run / destroy on stderr.
@@ -1529,6 +1797,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_means = T.add<double>(n_targets);
     const int64_t o_state = T.add<CleState>(1);
     const int64_t o_hist = T.add<double>(kCleHistCap);
+    const int64_t o_bar = T.add<uint32_t>(kCleBarWords);
     const double tm0 = now_us();
     if ((e = hipMalloc(&p->d_tables, T.total)) != hipSuccess) return fail(e);
     const double tm1 = now_us();
@@ -1557,6 +1826,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->d_means = reinterpret_cast<double*>(base + o_means);
     p->d_state = reinterpret_cast<CleState*>(base + o_state);
     p->d_hist = reinterpret_cast<double*>(base + o_hist);
+    p->d_bar = reinterpret_cast<uint32_t*>(base + o_bar);
     p->hist_cap = kCleHistCap;
     *out = p;
     return DFQ_OK;
@@ -1615,6 +1885,30 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
 }
 
 constexpr int32_t kCleBatch = 8;   // iterations enqueued between state read-backs
+constexpr int32_t kClePersistBatch = 256;   // persistent loop: iterations per cooperative launch
+
+// The persistent loop's co-resident grid (0 = use the graph path).  Measured
+// slower than the graph path (profiles/r02/cle_persistent.md: MobileNetV2 CLE
+// 7.7-8.7 ms against 4.8; an empty grid barrier costs 4.4-6.5 us, no less than a
+// kernel boundary inside a graph, and the fused kernel holds 177 VGPRs, 2 waves
+// per SIMD), so it is a diagnostics-library A/B only: DFQ_CLE_PERSIST_BPC=<blocks
+// per CU> turns it on there; the product library never takes it.
+static int32_t cle_persist_grid(dfq_cle_plan* p) {
+    if (p->persist_grid >= 0) return p->persist_grid;
+    p->persist_grid = 0;
+    int bpc = 0;
+    if (const char* e = ab_env("DFQ_CLE_PERSIST_BPC")) bpc = atoi(e);
+    if (bpc <= 0 || !p->fused || p->nchunks <= 0 || p->steps > kClePersistMaxSteps || p->nl > 128) return 0;
+    int dev = 0, cus = 0, coop = 0, occ = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess || !coop) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(cle_persist_kernel),
+                                                     kThreads, 0) != hipSuccess || occ <= 0)
+        return 0;
+    p->persist_grid = cus * std::min(bpc, occ);
+    return p->persist_grid;
+}
 
 extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count, int32_t max_iters,
                                 int32_t* iterations, double* diffs, void* stream) {
@@ -1673,6 +1967,44 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
                            dim3(kThreads), 0, s, p->d_rels, p->d_rtasks, p->rstep[0], p->rstep[1], p->d_rng, p->M,
                            p->d_state, 0);
         DFQ_LAUNCH_CHECK();
+    }
+    // Persistent loop (fused schedule): one cooperative launch per kClePersistBatch
+    // iterations, the stop rule read back once per launch.
+    if (!init.done && cle_persist_grid(p) > 0) {
+        (void)0;
+        ClePersist P{};
+        P.rels = p->d_rels; P.rtasks = p->d_rtasks; P.atasks = p->d_atasks; P.layers = p->d_layers;
+        P.chunks = p->d_chunks; P.b1off = p->d_b1off; P.units = p->d_units; P.b1 = p->d_b1; P.tail = p->d_tail;
+        P.rng = p->d_rng; P.part = p->d_part; P.means = p->d_means; P.hist = p->d_hist; P.st = p->d_state;
+        P.bar = p->d_bar;
+        P.M = p->M; P.nchunks = p->nchunks; P.nunits = p->nunits; P.r0 = p->rstep[0]; P.r1 = p->rstep[1];
+        for (int32_t k = 0; k <= p->steps; ++k) P.astep[k] = p->astep[k];
+        P.steps = p->steps; P.nl = p->nl; P.is_signed = p->is_signed; P.eps = p->eps;
+        P.smin = p->smin; P.smax = p->smax;
+        const double tl0 = now_us();
+        int32_t launched = 0;
+        while (!init.done && launched < max_iters) {
+            P.batch = std::min<int32_t>(kClePersistBatch, max_iters - launched);
+            DFQ_HIP_CHECK(hipMemsetAsync(p->d_bar, 0, sizeof(uint32_t) * kCleBarWords, s));
+            void* args[] = {&P};
+            DFQ_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(cle_persist_kernel),
+                                                     dim3(p->persist_grid), dim3(kThreads), args, 0, s));
+            launched += P.batch;
+            DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
+            DFQ_HIP_CHECK(hipStreamSynchronize(s));
+            init = *p->h_state;
+            if (init.error) {
+                set_last_hip_error(hipErrorLaunchTimeOut);
+                return DFQ_ERR_HIP;
+            }
+        }
+        if (cle_timing())
+            fprintf(stderr, "DFQ_CLE_TIMING run: persistent grid %d, loop %.1f us (%d iterations)\n",
+                    p->persist_grid, now_us() - tl0, init.iters);
+        if (iterations) *iterations = init.iters;
+        if (diffs && init.iters > 0)
+            DFQ_HIP_CHECK(hipMemcpy(diffs, p->d_hist, sizeof(double) * init.iters, hipMemcpyDeviceToHost));
+        return DFQ_OK;
     }
     // kCleBatch iterations as one HIP graph (kernels of finished runs return at
     // once: the stop rule lives in d_state); DFQ_CLE_GRAPH=0: eager launches.
@@ -1746,3 +2078,23 @@ extern "C" int dfq_cle_plan_destroy(dfq_cle_plan* p) {
     cle_plan_free(p);
     return DFQ_OK;
 }
+
+#ifdef DFQ_DIAGNOSTICS
+#include "dfq_diag.h"
+extern "C" int dfq_probe_grid_barrier(int32_t nbar, int32_t blocks_per_cu, int32_t mode, void* ws, void* stream) {
+    if (!ws || nbar < 0 || blocks_per_cu < 1) return DFQ_ERR_INVALID;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int dev = 0, cus = 0, occ = 0;
+    DFQ_HIP_CHECK(hipGetDevice(&dev));
+    DFQ_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    DFQ_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(cle_barrier_probe_kernel),
+                                                               kThreads, 0));
+    uint32_t* bar = static_cast<uint32_t*>(ws);
+    CleState* st = reinterpret_cast<CleState*>(bar + kCleBarWords + 64);
+    DFQ_HIP_CHECK(hipMemsetAsync(ws, 0, sizeof(uint32_t) * (kCleBarWords + 64) + sizeof(CleState), s));
+    void* args[] = {&bar, &st, &nbar, &mode};
+    DFQ_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(cle_barrier_probe_kernel),
+                                             dim3(cus * std::min(blocks_per_cu, occ)), dim3(kThreads), args, 0, s));
+    return DFQ_OK;
+}
+#endif

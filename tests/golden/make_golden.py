@@ -38,7 +38,8 @@ import torch.nn as nn
 # 1 ulp below the IEEE value, on the AVX2 path they are IEEE-exact.  Pin MKL's
 # conditional-numerical-reproducibility mode to AVX2 so the fixtures are the
 # reference's arithmetic with IEEE sqrt (checked below).
-os.environ.setdefault("MKL_CBWR", "AVX2")
+if not os.environ.get("DFQ_MKL_DEFAULT"):
+    os.environ.setdefault("MKL_CBWR", "AVX2")
 REF = Path(os.environ.get("DFQ_REFERENCE", "/root/reference"))
 HERE = Path(__file__).resolve().parent
 ROOT = HERE.parent.parent
@@ -363,8 +364,14 @@ class _NpSpy:
         return getattr(np, name)
 
 
-def pipeline(name: str, seed: int = 0, per_channel: bool = False):
+def pipeline(name: str, seed: int = 0, per_channel: bool = False, threads: int = 8, out: Path = None):
+    """``threads``: torch's intra-op thread count for the run.  ATen splits two of the
+    reference's fp32 reductions by it -- the CLE metric's torch.mean
+    (Cross_layer_equal.py:107) and bias correction's view(-1, F).mean(0)
+    (bias_correction.py:98-104,206-213) -- so the results depend on it;
+    pipeline_<name>.npz is the 8-thread run, pipeline_<name>_t<T>.npz the others."""
     t0 = time.time()
+    torch.set_num_threads(threads)
     model = zoo.build(name, seed=seed, relu=True)
     g = build_graph(model, "positional")
     graph, bottoms = g.getGraph(), g.getBottoms()
@@ -436,9 +443,33 @@ def pipeline(name: str, seed: int = 0, per_channel: bool = False):
         P["bc_error"] = np.array(f"{type(e).__name__}")
     snap("bc", full_bias=True); snap_bn("bc", full=True)
     stats["seconds"] = time.time() - t0
+    stats["threads"] = threads
     P["stats"] = np.array(json.dumps(stats))
-    np.savez_compressed(HERE / f"pipeline_{name}.npz", **P)
+    if out is None:
+        out = HERE / (f"pipeline_{name}.npz" if threads == 8 else f"pipeline_{name}_t{threads}.npz")
+    np.savez_compressed(out, **P)
+    torch.set_num_threads(8)
     print(name, "relations", len(res), "cle iters", len(spy.diffs), "bc", str(P["bc_error"]), stats)
+
+
+def mkl_gap(name: str):
+    """How much the reference itself moves when MKL is NOT pinned to its AVX2 code
+    path (run with MKL_CBWR unset: torch.sqrt is then MKL VML's HA path, 1 ulp low
+    on 0.65 % of inputs on AVX-512 hosts).  Compares a fresh run against the
+    committed (pinned) pipeline_<name>.npz stage by stage; prints a JSON line."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        out = Path(d) / "p.npz"
+        pipeline(name, out=out)
+        A, B = np.load(out), np.load(HERE / f"pipeline_{name}.npz")
+        rep = {"model": name, "MKL_CBWR": os.environ.get("MKL_CBWR"),
+               "cle_iterations": [int(len(A["cle_diffs"])), int(len(B["cle_diffs"]))]}
+        for st in ("bn1", "cle", "absorb", "bn2", "quant", "clip", "bc"):
+            rep[f"{st}_weight_layers_differ"] = int((A[f"{st}_wh"] != B[f"{st}_wh"]).any(1).sum())
+            if f"{st}_bias" in A.files and A[f"{st}_bias"].shape == B[f"{st}_bias"].shape:
+                rep[f"{st}_bias_elems_differ"] = int((A[f"{st}_bias"] != B[f"{st}_bias"]).sum())
+        rep["layers"] = int(len(B["targets"]))
+        print("MKLGAP", json.dumps(rep))
 
 
 def act_ranges(name: str, seed: int = 0):
@@ -664,8 +695,14 @@ def state_dict_keys():
 
 
 if __name__ == "__main__":
-    _check_ieee_sqrt()
     which = sys.argv[1:] or ["quant", "transform", "mobilenetv2", "resnet50", "deeplab"]
+    if any(w.startswith("mklgap_") for w in which):
+        # run as: env -u MKL_CBWR DFQ_MKL_DEFAULT=1 python make_golden.py mklgap_<model>
+        for w in which:
+            if w.startswith("mklgap_"):
+                mkl_gap(w[len("mklgap_"):])
+        sys.exit(0)
+    _check_ieee_sqrt()
     if "quant" in which:
         quant_cases()
     if "quant" in which or "chunks" in which:
@@ -675,6 +712,9 @@ if __name__ == "__main__":
     for m in ("mobilenetv2", "resnet50", "deeplab", "resnet18"):
         if m in which:
             pipeline(m, per_channel=(m == "mobilenetv2"))
+        for t in (1, 16):
+            if f"{m}_t{t}" in which:
+                pipeline(m, threads=t)
     for m in ("mobilenetv2", "resnet50", "deeplab"):
         if "act" in which or f"act_{m}" in which:
             act_ranges(m)

@@ -156,3 +156,37 @@ def test_device_cle_no_relations(monkeypatch):
     assert cle.LAST_RUN["iterations"] == 1 and cle.LAST_RUN["diffs"] == [0.0]
     for k, w in before.items():
         assert torch.equal(g[k].weight, w)
+
+
+@pytest.mark.parametrize("name", ["mobilenetv2", "resnet50"])
+def test_persistent_loop_equals_graph_loop(name, monkeypatch):
+    """The graph-batched multi-launch loop (the product) and the persistent
+    cooperative loop (one launch, two-level grid barriers between chain steps;
+    diagnostics library, DFQ_CLE_PERSIST_BPC=2 -- an A/B that measured slower)
+    give the same weights, biases, scales, iteration count and diffs, bit for
+    bit, on a whole model."""
+    from data_free_quantization_amd import _lib, zoo
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    from data_free_quantization_amd.utils.layer_transform import merge_batchnorm
+    from data_free_quantization_amd.utils.relation import create_relation
+    from data_free_quantization_amd.utils.tracer import build_graph
+    monkeypatch.setenv("DFQ_CLE_MODE", "device")
+    runs = []
+    for lib in ("product", "persistent"):
+        if lib == "persistent":
+            monkeypatch.setattr(_lib, "_LIB", _lib.load_diag())
+            monkeypatch.setenv("DFQ_CLE_PERSIST_BPC", "2")
+        m = zoo.build(name, seed=4, relu=True).cuda()
+        g = build_graph(m, "positional")
+        G, B = g.getGraph(), g.getBottoms()
+        merge_batchnorm(m, G, B, [nn.Conv2d, nn.Linear])
+        rels = create_relation(G, B, [nn.Conv2d, nn.Linear])
+        cle.cross_layer_equalization(G, rels, [nn.Conv2d, nn.Linear], Save_state=False, Treshhold=2e-7)
+        torch.cuda.synchronize()
+        runs.append((m, [r.S.clone() for r in rels], dict(cle.LAST_RUN)))
+    (m0, s0, r0), (m1, s1, r1) = runs
+    assert r0["iterations"] == r1["iterations"] and r0["diffs"] == r1["diffs"]
+    for (k, a), (_, b) in zip(m0.state_dict().items(), m1.state_dict().items()):
+        assert torch.equal(a, b), k
+    for a, b in zip(s0, s1):
+        assert torch.equal(a, b)
