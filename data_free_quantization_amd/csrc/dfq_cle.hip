@@ -420,6 +420,7 @@ struct CleLayer {
     float* w;
     float* snap;
     int64_t n;
+    int64_t nt;   // torch.mean's chunks (1: serial sum)
 };
 
 // One fp32 torch.mean chunk (a thread's share of at::parallel_for in
@@ -1087,7 +1088,7 @@ __device__ __forceinline__ void cle_combine_body(const CleLayer* __restrict__ la
                                                  const CleChunk* __restrict__ chunks, int64_t nchunks,
                                                  const int64_t* __restrict__ b1off, const float* __restrict__ b1buf,
                                                  const float* __restrict__ tailbuf, float* __restrict__ part,
-                                                 int64_t blk, int64_t nblk) {
+                                                 int32_t S, int64_t blk, int64_t nblk) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = blk * (kThreads / 64) + (threadIdx.x >> 6);
     const int64_t nwaves = nblk * (kThreads / 64);
@@ -1142,17 +1143,17 @@ __device__ __forceinline__ void cle_combine_body(const CleLayer* __restrict__ la
                 }
             }
         }
-        if (lane == 0) part[(int64_t)ch.layer * 8 + ch.t] = 0.f + fa;   // buffer[t] starts at 0
+        if (lane == 0) part[(int64_t)ch.layer * S + ch.t] = 0.f + fa;   // buffer[t] starts at 0
     }
 }
 
 __global__ void __launch_bounds__(kThreads)
 cle_loop_diff_combine_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks, int64_t nchunks,
                              const int64_t* __restrict__ b1off, const float* __restrict__ b1buf,
-                             const float* __restrict__ tailbuf, float* __restrict__ part,
+                             const float* __restrict__ tailbuf, float* __restrict__ part, int32_t S,
                              const CleState* __restrict__ st) {
     if (st->done) return;
-    cle_combine_body(layers, chunks, nchunks, b1off, b1buf, tailbuf, part, blockIdx.x, gridDim.x);
+    cle_combine_body(layers, chunks, nchunks, b1off, b1buf, tailbuf, part, S, blockIdx.x, gridDim.x);
 }
 
 // numpy pairwise float64 sum (identity 0 + pairwise_sum), as np.sum(diff_list).
@@ -1216,13 +1217,15 @@ __device__ double np_pairwise(const double* a, int64_t n) {
 // no scratch in the persistent kernel
 template <bool kLeafOnly = false>
 __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ layers, int32_t nl,
-                                               const float* __restrict__ part, double* __restrict__ means,
+                                               const float* __restrict__ part, int32_t S, double* __restrict__ means,
                                                double* __restrict__ hist, CleState* __restrict__ st, double* sm) {
     double* m = nl <= 1024 ? sm : means;
     for (int l = threadIdx.x; l < nl; l += blockDim.x) {
-        float acc = 0.f;
-        for (int t = 0; t < 8; ++t) acc += part[(int64_t)l * 8 + t];
-        const float sum = 0.f + acc;
+        // serial: sum = 0 + (0 + slot); two_pass_reduction: its S-slot buffer
+        // (at::get_num_threads()) summed as a contiguous reduction
+        const float* pl = part + (int64_t)l * S;
+        const float sum = layers[l].nt == 1 ? 0.f + (0.f + pl[0])
+                                            : 0.f + aten_inner_sum([&](int64_t e) { return pl[e]; }, S);
         m[l] = (double)(sum / (float)layers[l].n);
     }
     __syncthreads();
@@ -1248,10 +1251,11 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
 }
 
 __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32_t nl, const float* __restrict__ part,
-                                      double* __restrict__ means, double* __restrict__ hist, CleState* __restrict__ st) {
+                                      int32_t S, double* __restrict__ means, double* __restrict__ hist,
+                                      CleState* __restrict__ st) {
     __shared__ double sm[1024];   // the per-layer means, read back by one thread
     if (st->done) return;
-    cle_final_body(layers, nl, part, means, hist, st, sm);
+    cle_final_body(layers, nl, part, S, means, hist, st, sm);
 }
 
 // ---------------------------------------------------------------------------
@@ -1283,7 +1287,7 @@ struct ClePersist {
     uint32_t* bar;       // {arrivals, generation}
     int64_t M, nchunks, nunits, r0, r1;
     int64_t astep[kClePersistMaxSteps + 1];
-    int32_t steps, nl, is_signed, batch;
+    int32_t steps, nl, is_signed, batch, slots;
     float eps;
     double smin, smax;
 };
@@ -1448,10 +1452,10 @@ __global__ void __launch_bounds__(kThreads) cle_persist_kernel(ClePersist P) {
         cle_range_body(P.rels, P.rtasks, P.r0, P.r1, P.rng, P.M, par ^ 1, blk, nblk, L.tiles);
         if (!cle_grid_sync_xcd(S, P.st)) return;
         if (P.nchunks > 0) {
-            cle_combine_body(P.layers, P.chunks, P.nchunks, P.b1off, P.b1, P.tail, P.part, blk, nblk);
+            cle_combine_body(P.layers, P.chunks, P.nchunks, P.b1off, P.b1, P.tail, P.part, P.slots, blk, nblk);
             if (!cle_grid_sync_xcd(S, P.st)) return;
         }
-        if (blk == 0) cle_final_body<true>(P.layers, P.nl, P.part, P.means, P.hist, P.st, L.fin);
+        if (blk == 0) cle_final_body<true>(P.layers, P.nl, P.part, P.slots, P.means, P.hist, P.st, L.fin);
         if (!cle_grid_sync_xcd(S, P.st)) return;
     }
 }
@@ -1494,7 +1498,8 @@ struct dfq_cle_plan {
     CleLayer* d_layers = nullptr;
     CleChunk* d_chunks = nullptr;
     uint32_t* d_rng = nullptr;      // [2 parities][mins M | maxs M]
-    float* d_part = nullptr;        // [layers][8]
+    float* d_part = nullptr;        // [layers][slots]
+    int32_t slots = 8;              // torch.mean's thread buffer (the reference run's thread count)
     double* d_means = nullptr;
     double* d_hist = nullptr;
     int32_t hist_cap = 0;
@@ -1748,10 +1753,10 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         if (!targets[l] || n <= 0) { cle_plan_free(p); return DFQ_ERR_INVALID; }
         float* snap = reinterpret_cast<float*>(snap_base + snap_off);
         snap_off += snap_bytes(n);
-        layers[l] = CleLayer{targets[l], snap, n};
+        layers[l] = CleLayer{targets[l], snap, n, 1};
         int64_t nt = 1;
         if (n >= 32768 && ref_threads > 1) nt = std::min<int64_t>(ref_threads, ceil_div(n, (int64_t)32768));
-        if (nt > 8) nt = 8;
+        layers[l].nt = nt;
         const int64_t chunk = ceil_div(n, nt);
         for (int64_t t = 0; t < nt; ++t) {
             const int64_t b = t * chunk;
@@ -1793,7 +1798,8 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_b1 = T.add<float>(32 * nb1_total);
     const int64_t o_tail = T.add<float>(kCleTailWords * (int64_t)chunks.size());
     const int64_t o_rng = T.add<uint32_t>(4 * M);
-    const int64_t o_part = T.add<float>(8 * (int64_t)n_targets);
+    p->slots = std::max<int32_t>(ref_threads, 1);
+    const int64_t o_part = T.add<float>((int64_t)p->slots * n_targets);
     const int64_t o_means = T.add<double>(n_targets);
     const int64_t o_state = T.add<CleState>(1);
     const int64_t o_hist = T.add<double>(kCleHistCap);
@@ -1875,11 +1881,11 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
         }
         hipLaunchKernelGGL(cle_loop_diff_combine_kernel, dim3((int)ceil_div(p->nchunks, (int64_t)(kThreads / 64))),
                            dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_b1off, p->d_b1, p->d_tail,
-                           p->d_part, p->d_state);
+                           p->d_part, p->slots, p->d_state);
         DFQ_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(cle_loop_final_kernel, dim3(1), dim3(kThreads), 0, s, p->d_layers, p->nl, p->d_part, p->d_means,
-                       p->d_hist, p->d_state);
+    hipLaunchKernelGGL(cle_loop_final_kernel, dim3(1), dim3(kThreads), 0, s, p->d_layers, p->nl, p->d_part, p->slots,
+                       p->d_means, p->d_hist, p->d_state);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }
@@ -1955,7 +1961,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         DFQ_HIP_CHECK(hipMemsetAsync(p->d_rng + (int64_t)par * 2 * p->M, 0xFF, sizeof(uint32_t) * p->M, s));
         DFQ_HIP_CHECK(hipMemsetAsync(p->d_rng + (int64_t)par * 2 * p->M + p->M, 0x00, sizeof(uint32_t) * p->M, s));
     }
-    DFQ_HIP_CHECK(hipMemsetAsync(p->d_part, 0, sizeof(float) * 8 * std::max(p->nl, 1), s));
+    DFQ_HIP_CHECK(hipMemsetAsync(p->d_part, 0, sizeof(float) * p->slots * std::max(p->nl, 1), s));
     if (p->nchunks > 0) {
         hipLaunchKernelGGL(cle_loop_snap_kernel, dim3((int)std::min<int64_t>(std::max<int64_t>(p->nunits, 1), 4096)),
                            dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_units, p->nunits);
@@ -1979,7 +1985,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         P.bar = p->d_bar;
         P.M = p->M; P.nchunks = p->nchunks; P.nunits = p->nunits; P.r0 = p->rstep[0]; P.r1 = p->rstep[1];
         for (int32_t k = 0; k <= p->steps; ++k) P.astep[k] = p->astep[k];
-        P.steps = p->steps; P.nl = p->nl; P.is_signed = p->is_signed; P.eps = p->eps;
+        P.steps = p->steps; P.nl = p->nl; P.is_signed = p->is_signed; P.eps = p->eps; P.slots = p->slots;
         P.smin = p->smin; P.smax = p->smax;
         const double tl0 = now_us();
         int32_t launched = 0;
@@ -2049,11 +2055,11 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
                 tc1 - tc0, now_us() - tc1, launched);
     const CleState fin = *p->h_state;
     if (ab_env("DFQ_CLE_DEBUG")) {   // per-layer chunk sums of the last iteration run
-        std::vector<float> part(8 * std::max(p->nl, 1));
+        std::vector<float> part((size_t)p->slots * std::max(p->nl, 1));
         DFQ_HIP_CHECK(hipMemcpy(part.data(), p->d_part, sizeof(float) * part.size(), hipMemcpyDeviceToHost));
         for (int32_t l = 0; l < p->nl; ++l) {
             fprintf(stderr, "DFQ_CLE_DEBUG layer %d:", l);
-            for (int t = 0; t < 8; ++t) fprintf(stderr, " %.9g", part[8 * l + t]);
+            for (int t = 0; t < p->slots; ++t) fprintf(stderr, " %.9g", part[(size_t)p->slots * l + t]);
             fprintf(stderr, "\n");
         }
     }

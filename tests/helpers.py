@@ -57,8 +57,11 @@ def transform_cases():
     return z, json.loads(str(z["meta"]))
 
 
-def pipeline(name):
-    return np.load(GOLDEN / f"pipeline_{name}.npz", allow_pickle=False)
+def pipeline(name, threads=8):
+    """The reference's main_dfq stage order on the synthetic model, run with
+    ``threads`` torch intra-op threads (tests/golden/make_golden.py:pipeline)."""
+    f = f"pipeline_{name}.npz" if threads == 8 else f"pipeline_{name}_t{threads}.npz"
+    return np.load(GOLDEN / f, allow_pickle=False)
 
 
 def recover_codes_consistent(dq, codes, scale, zero):

@@ -104,7 +104,7 @@ class OracleDFQ:
         for k in self.tkeys:
             self.W[k] = np.clip(self.W[k], np.float32(lo), np.float32(hi)).astype(np.float32)
 
-    def bias_correction(self, bits=8, signed=False):
+    def bias_correction(self, bits=8, signed=False, threads=8):
         """The reference's BC walk (positional keys) with the oracle's arithmetic."""
         g, bottoms = self.graph, self.bottoms
         bn_module, relu_attached = {}, {}
@@ -125,7 +125,7 @@ class OracleDFQ:
                 bn_module[idx] = _BN(idx)
                 relu_attached[idx] = False
                 if bias_prev is not None:
-                    fake[idx]["fb"] = O.bc_propagate(bias_prev, fake[idx]["fb"])
+                    fake[idx]["fb"] = O.bc_propagate(bias_prev, fake[idx]["fb"], threads)
                     bias_prev = None
                 continue
             if isinstance(g[idx], nn.ReLU) and bot[0] in bn_module:

@@ -17,15 +17,23 @@ pytestmark = pytest.mark.gpu
 TARG = (nn.Conv2d, nn.Linear)
 
 
+@pytest.mark.parametrize("threads", [8, 1, 16])
 @pytest.mark.parametrize("cle_mode", ["device", "host"])
 @pytest.mark.parametrize("name", ["mobilenetv2", "resnet50", "deeplab", "resnet18"])
-def test_pipeline_matches_reference(name, cle_mode, monkeypatch):
+def test_pipeline_matches_reference(name, cle_mode, threads, monkeypatch):
+    """``threads``: the reference run's torch intra-op thread count, which splits
+    the CLE metric's mean and bias correction's view(-1, F).mean(0)
+    (DFQ_REF_THREADS; fixtures at 1, 8 and 16 threads)."""
+    if cle_mode == "host" and threads != 8:
+        pytest.skip("the host-loop mode's fp64 metric does not depend on the thread count")
     monkeypatch.setenv("DFQ_CLE_MODE", cle_mode)
+    from data_free_quantization_amd import _lib
+    monkeypatch.setattr(_lib, "REF_THREADS", threads)
     from data_free_quantization_amd import zoo
     from data_free_quantization_amd import Cross_layer_equal as cle
     from data_free_quantization_amd.pipeline import run_dfq
     from data_free_quantization_amd.utils.tracer import build_graph
-    P = pipeline(name)
+    P = pipeline(name, threads)
     model = zoo.build(name, seed=0, relu=True).cuda()
     g = build_graph(model, "positional")
     graph, bottoms = g.getGraph(), g.getBottoms()

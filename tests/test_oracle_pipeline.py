@@ -20,16 +20,19 @@ def _bias_hashes(R):
                      for k in R.tkeys])
 
 
+@pytest.mark.parametrize("threads", [8, 1, 16])
 @pytest.mark.parametrize("name", ["mobilenetv2", "resnet50", "deeplab", "resnet18"])
-def test_oracle_pipeline_matches_reference(name):
-    P = pipeline(name)
+def test_oracle_pipeline_matches_reference(name, threads):
+    """At 1, 8 and 16 torch threads: ATen splits the CLE metric's mean and bias
+    correction's view(-1, F).mean(0) by the thread count."""
+    P = pipeline(name, threads)
     m = zoo.build(name, seed=0, relu=True)
     g = build_graph(m, "positional")
     R = OracleDFQ(g.getGraph(), g.getBottoms())
     R.merge_bn()
     assert np.array_equal(_stage_hashes(R), P["bn1_wh"])
     assert np.array_equal(_bias_hashes(R), P["bn1_bh"])
-    R.cle()
+    R.cle(threads=threads)
     assert len(R.cle_diffs) == len(P["cle_diffs"])
     assert R.cle_diffs == list(P["cle_diffs"])   # fp32 torch.mean order + numpy pairwise sum, bit-exact
     assert np.array_equal(_stage_hashes(R), P["cle_wh"])
@@ -51,6 +54,6 @@ def test_oracle_pipeline_matches_reference(name):
         with pytest.raises(RuntimeError):
             R.bias_correction(8)
     else:
-        R.bias_correction(8)
+        R.bias_correction(8, threads=threads)
         got = np.concatenate([R.B[k] for k in R.tkeys])
         assert np.array_equal(got, P["bc_bias"])   # ATen reduction order reproduced
