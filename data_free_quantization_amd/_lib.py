@@ -31,7 +31,7 @@ EXPORTS = [
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
     "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
-    "dfq_bias_absorb", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate", "dfq_bc_chain",
+    "dfq_bias_absorb", "dfq_bias_absorb_ws_bytes", "dfq_bias_absorb_batch", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate", "dfq_bc_chain",
     "dfq_act_moments", "dfq_act_minmax", "dfq_act_affine",
 ]
 #: entry points only the diagnostics library exports (include/dfq_diag.h)
@@ -69,6 +69,13 @@ class CleRel(C.Structure):
         ("w1", C.c_void_p), ("w2", C.c_void_p), ("b1", C.c_void_p), ("bn_w", C.c_void_p), ("bn_b", C.c_void_p),
         ("s_acc", C.c_void_p), ("c1", C.c_int64), ("len1", C.c_int64), ("o2", C.c_int64), ("i2", C.c_int64),
         ("khw2", C.c_int64), ("s_acc_init", C.c_int32), ("reserved", C.c_int32),
+    ]
+
+
+class AbsorbDesc(C.Structure):
+    _fields_ = [
+        ("w2", C.c_void_p), ("b1", C.c_void_p), ("b2", C.c_void_p), ("bn_w", C.c_void_p), ("bn_b", C.c_void_p),
+        ("c1", C.c_int64), ("o2", C.c_int64), ("i2", C.c_int64), ("khw2", C.c_int64),
     ]
 
 
@@ -138,6 +145,8 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_cle_plan_info": ([P, C.POINTER(I32), C.POINTER(I32), C.POINTER(I32)], C.c_int),
         "dfq_cle_plan_destroy": ([P], C.c_int),
         "dfq_bias_absorb": ([P, P, P, P, P, I64, I64, I64, I64, F32, P], C.c_int),
+        "dfq_bias_absorb_ws_bytes": ([C.POINTER(AbsorbDesc), I32], C.c_int64),
+        "dfq_bias_absorb_batch": ([C.POINTER(AbsorbDesc), I32, F32, P, I64, C.POINTER(I32), P], C.c_int),
         "dfq_bc_expect": ([P, P, I64, I32, I32, P, P], C.c_int),
         "dfq_bc_apply": ([P, I64, I64, P, I64, P, P, C.POINTER(I64), P], C.c_int),
         "dfq_bc_propagate": ([P, I64, P, I64, I32, P], C.c_int),

@@ -16,6 +16,7 @@ from __future__ import annotations
 import ctypes as C
 import logging
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -164,6 +165,11 @@ def _snapshot(tensors):
     return out
 
 
+_BC_OP = np.dtype([("kind", "<i4"), ("flag", "<i4"), ("a", "<u8"), ("b", "<u8"), ("out", "<u8"), ("out2", "<u8"),
+                   ("n", "<i8"), ("i2", "<i8"), ("f", "<i8")])
+assert _BC_OP.itemsize == C.sizeof(_lib.BcOp)
+
+
 class _BcChain:
     """The walk's device work recorded in graph order and enqueued by ONE
     ``dfq_bc_chain`` call (instead of a Python call per expect / apply /
@@ -213,16 +219,14 @@ class _BcChain:
             return
         scratch = torch.empty(max(self.top, 1), dtype=torch.float32, device=self.dev)
         base = scratch.data_ptr()
-        arr = (_lib.BcOp * len(self.ops))()
-        for k, (kind, flag, a, b, out, out2, n, i2, f) in enumerate(self.ops):
-            op = arr[k]
-            op.kind, op.flag, op.n, op.i2, op.f = kind, flag, n, i2, f
-            op.a = self._ptr(a, base)
-            op.b = self._ptr(b, base) if b is not None else None
-            op.out = self._ptr(out, base)
-            op.out2 = self._ptr(out2, base) if out2 is not None else None
+        # the op table as a numpy record array (layout of _lib.BcOp), filled row-wise
+        # from plain tuples instead of ctypes field by field
+        ptr = lambda ref: 0 if ref is None else self._ptr(ref, base)   # noqa: E731
+        arr = np.array([(kind, flag, ptr(a), ptr(b), ptr(out), ptr(out2), n, i2, f)
+                        for (kind, flag, a, b, out, out2, n, i2, f) in self.ops], dtype=_BC_OP)
         failed = C.c_int32(-1)
-        rc = _lib.load().dfq_bc_chain(arr, len(self.ops), C.byref(failed), stream)
+        rc = _lib.load().dfq_bc_chain(arr.ctypes.data_as(C.POINTER(_lib.BcOp)), len(self.ops), C.byref(failed),
+                                      stream)
         _lib.check(rc, f"dfq_bc_chain (op {failed.value})", RuntimeError)
         # the ops run asynchronously: keep the scratch alive until they are done
         scratch.record_stream(torch.cuda.current_stream(self.dev))

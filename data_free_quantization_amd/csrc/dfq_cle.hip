@@ -974,12 +974,30 @@ __global__ void cle_loop_snap_kernel(const CleLayer* __restrict__ layers, const 
 }
 
 
+// Agent-coherent fp32 store / load (sc1: no stale copy in another XCD's L2), for
+// the few words one block hands to another inside a launch (level-1 sums, chunk
+// tails, chunk sums) without an L2 write-back.
+__device__ __forceinline__ void st_coh(float* p, float v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_coh(const float* p) {
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Metric tiles taken by blocks blk, blk + nblk, ... (d: kCleTile + kCleTailWords
 // floats of LDS, b0: 512).
+struct CleNoUnitHook {
+    __device__ void operator()(const CleUnit&, const CleChunk&, int64_t) const {}
+};
+
+// hook(unit, chunk, nb1) runs after each unit (LDS free again)
+template <class Hook = CleNoUnitHook>
 __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
                                                const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units,
                                                int64_t nunits, float* __restrict__ b1buf, float* __restrict__ tailbuf,
-                                               int64_t blk, int64_t nblk, float* d, float* b0) {
+                                               int64_t blk, int64_t nblk, float* d, float* b0, Hook hook = Hook()) {
     const int tid = threadIdx.x;
     for (int64_t u = blk; u < nunits; u += nblk) {
         const CleUnit un = units[u];
@@ -992,38 +1010,59 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
         const bool full = un.tile < nb1;
         const int64_t e0 = (int64_t)un.tile * kCleTile;
         const int64_t cnt = full ? kCleTile : len - e0;
-        for (int64_t e = tid; e < cnt; e += 8 * kThreads) {   // |W - W_prev|, snap := W; 8 loads in flight
-            float x[8], y[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (e + u * kThreads < cnt) {
-                    x[u] = w[e0 + e + u * kThreads];
-                    y[u] = sn[e0 + e + u * kThreads];
-                }
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (e + u * kThreads < cnt) {
-                    d[e + u * kThreads] = fabsf(x[u] - y[u]);
-                    sn[e0 + e + u * kThreads] = x[u];
-                }
-        }
-        __syncthreads();
         if (full) {
-            for (int q = tid; q < 512; q += kThreads) {   // level 0: 16 blocks x 32 streams
-                const int s = q & 31, m = q >> 5;
+            // level 0 straight from the loads: thread t owns (block m, stream s) for
+            // q = t and t + 256; its 16 elements 32 (16 m + j) + s sit at stride 32,
+            // so each load instruction covers whole 128-B lines across the lanes,
+            // and the 16-term sum runs in ATen's order in registers (32 loads in
+            // flight per thread, no LDS staging of |W - W_prev|)
+            float xs[2][16], ys[2][16];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int q = tid + h * kThreads;
+                const int64_t base = e0 + 32 * (16 * (q >> 5)) + (q & 31);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    xs[h][j] = w[base + 32 * j];
+                    ys[h][j] = sn[base + 32 * j];
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int q = tid + h * kThreads;
+                const int64_t base = e0 + 32 * (16 * (q >> 5)) + (q & 31);
                 float a = 0.f;
 #pragma unroll
-                for (int j = 0; j < 16; ++j) a += d[32 * (16 * m + j) + s];
-                b0[m * 32 + s] = a;
+                for (int j = 0; j < 16; ++j) {
+                    a += fabsf(xs[h][j] - ys[h][j]);
+                    sn[base + 32 * j] = xs[h][j];
+                }
+                b0[q] = a;   // b0[m * 32 + s]
             }
             __syncthreads();
             if (tid < 32) {   // level 1
                 float a = 0.f;
 #pragma unroll
                 for (int m = 0; m < 16; ++m) a += b0[m * 32 + tid];
-                b1buf[b1off[un.chunk] + (int64_t)un.tile * 32 + tid] = a;
+                st_coh(b1buf + b1off[un.chunk] + (int64_t)un.tile * 32 + tid, a);
             }
         } else {
+            for (int64_t e = tid; e < cnt; e += 8 * kThreads) {   // |W - W_prev|, snap := W; 8 loads in flight
+                float x[8], y[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (e + u * kThreads < cnt) {
+                        x[u] = w[e0 + e + u * kThreads];
+                        y[u] = sn[e0 + e + u * kThreads];
+                    }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (e + u * kThreads < cnt) {
+                        d[e + u * kThreads] = fabsf(x[u] - y[u]);
+                        sn[e0 + e + u * kThreads] = x[u];
+                    }
+            }
+            __syncthreads();
             const int64_t ni = sz - nb1 * 256;   // stream elements left: rem_b0 blocks + tail0
             const int64_t rem_b0 = ni / 16, tail0 = ni % 16;
             float* tb = tailbuf + (int64_t)un.chunk * kCleTailWords;
@@ -1038,15 +1077,16 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
                 for (int64_t j = 0; j < tail0; ++j) a0t += d[32 * (16 * rem_b0 + j) + tid];
                 float p = a0t;   // a0 += a1 (a2 and a3 follow in the combine)
                 p += a1p;
-                tb[tid] = p;
+                st_coh(tb + tid, p);
             } else if (tid < 64) {   // raw row_sum-tail vectors (v in [4sz, vs)) and scalar tail
                 const int t = tid - 32;
                 const int64_t nv = vs - 4 * sz;
-                if (t < 24 && t < nv * 8) tb[32 + t] = d[8 * (4 * sz) + t - e0];
-                if (t < 8 && t < len - 8 * vs) tb[56 + t] = d[8 * vs + t - e0];
+                if (t < 24 && t < nv * 8) st_coh(tb + 32 + t, d[8 * (4 * sz) + t - e0]);
+                if (t < 8 && t < len - 8 * vs) st_coh(tb + 56 + t, d[8 * vs + t - e0]);
             }
         }
         __syncthreads();   // LDS reused by the next unit
+        hook(un, ch, nb1);
     }
 }
 
@@ -1082,8 +1122,66 @@ cle_loop_tiles_range_kernel(const CleLayer* __restrict__ layers, const CleChunk*
         cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + 1) & 1, blockIdx.x - ntb, gridDim.x - ntb, lds);
 }
 
-// One wave per chunk: the rest of the cascade, the ILP and lane combines and
-// the scalar tail, in ATen's order; part[layer][t] = 0 + sum.
+// One chunk's sum from its tiles' level-1 sums and tail words (one wave; the
+// result on lane 0): the rest of the cascade, the ILP and lane combines and the
+// scalar tail, in ATen's order.  Coherent loads: other blocks wrote b1 / tb.
+template <class LdB1, class LdTb>
+__device__ __forceinline__ float cle_chunk_sum_with(const CleChunk& ch, LdB1&& b1, LdTb&& tb, int lane) {
+    const int64_t len = ch.len;
+    const int64_t sz = len / 32, vs = len / 8;
+    const int64_t nb1 = sz / 256, nb2 = nb1 / 16, rem_b1 = nb1 % 16;
+    float fa = 0.f;
+    float p = 0.f;
+    if (lane < 32) {
+        float a3 = 0.f;
+        for (int64_t r = 0; r < nb2; ++r) {
+            float b2 = 0.f;
+            for (int q = 0; q < 16; ++q) b2 += b1((r * 16 + q) * 32 + lane);
+            a3 += b2;
+        }
+        float a2p = 0.f;
+        for (int64_t q = 0; q < rem_b1; ++q) a2p += b1((nb2 * 16 + q) * 32 + lane);
+        p = tb(lane);   // a0 + a1
+        p += a2p;
+        p += a3;
+    }
+    float ps[32];
+#pragma unroll
+    for (int s = 0; s < 32; ++s) ps[s] = __shfl(p, s, 64);
+    if (lane == 0) {
+        for (int64_t e = 0; e < len - 8 * vs; ++e) fa += tb(56 + e);   // scalar tail first
+        const int64_t nv = vs - 4 * sz;
+        for (int l = 0; l < 8; ++l) {
+            float p0 = ps[l];
+            for (int64_t v = 0; v < nv; ++v) p0 += tb(32 + v * 8 + l);   // row_sum tail into p0
+            p0 += ps[l + 8];
+            p0 += ps[l + 16];
+            p0 += ps[l + 24];
+            fa += p0;
+        }
+    }
+    return fa;
+}
+
+__device__ __forceinline__ float cle_chunk_sum(const CleChunk& ch, const float* b1, const float* tb, int lane) {
+    return cle_chunk_sum_with(ch, [&](int64_t i) { return ld_coh(b1 + i); }, [&](int64_t i) { return ld_coh(tb + i); },
+                              lane);
+}
+
+// Tiny chunk (< 8 elements, no tiles): scalar row_sum of |W - snap| on lane 0, snap := W.
+__device__ __forceinline__ float cle_tiny_chunk_sum(const CleLayer* __restrict__ layers, const CleChunk& ch) {
+    const CleLayer Ly = layers[ch.layer];
+    float* w = Ly.w + ch.c0;
+    float* sn = Ly.snap + ch.c0;
+    return aten_inner_sum([&](int64_t e) {
+        const float x = w[e];
+        const float dd = fabsf(x - sn[e]);
+        sn[e] = x;
+        return dd;
+    }, ch.len);
+}
+
+// One wave per chunk: part[layer][t] = 0 + the chunk's sum.
 __device__ __forceinline__ void cle_combine_body(const CleLayer* __restrict__ layers,
                                                  const CleChunk* __restrict__ chunks, int64_t nchunks,
                                                  const int64_t* __restrict__ b1off, const float* __restrict__ b1buf,
@@ -1097,51 +1195,11 @@ __device__ __forceinline__ void cle_combine_body(const CleLayer* __restrict__ la
         const int64_t len = ch.len;
         float fa = 0.f;
         if (len < 8) {   // tiny chunk: scalar row_sum (no tiles ran for it)
-            if (lane == 0) {
-                const CleLayer Ly = layers[ch.layer];
-                float* w = Ly.w + ch.c0;
-                float* sn = Ly.snap + ch.c0;
-                fa = aten_inner_sum([&](int64_t e) {
-                    const float x = w[e];
-                    const float dd = fabsf(x - sn[e]);
-                    sn[e] = x;
-                    return dd;
-                }, len);
-            }
-        } else {
-            const int64_t sz = len / 32, vs = len / 8;
-            const int64_t nb1 = sz / 256, nb2 = nb1 / 16, rem_b1 = nb1 % 16;
+            if (lane == 0) fa = cle_tiny_chunk_sum(layers, ch);
+        } else {   // a later launch than the tiles: plain loads see their stores
             const float* b1 = b1buf + b1off[k];
             const float* tb = tailbuf + k * kCleTailWords;
-            float p = 0.f;
-            if (lane < 32) {
-                float a3 = 0.f;
-                for (int64_t r = 0; r < nb2; ++r) {
-                    float b2 = 0.f;
-                    for (int q = 0; q < 16; ++q) b2 += b1[(r * 16 + q) * 32 + lane];
-                    a3 += b2;
-                }
-                float a2p = 0.f;
-                for (int64_t q = 0; q < rem_b1; ++q) a2p += b1[(nb2 * 16 + q) * 32 + lane];
-                p = tb[lane];   // a0 + a1
-                p += a2p;
-                p += a3;
-            }
-            float ps[32];
-#pragma unroll
-            for (int s = 0; s < 32; ++s) ps[s] = __shfl(p, s, 64);
-            if (lane == 0) {
-                for (int64_t e = 0; e < len - 8 * vs; ++e) fa += tb[56 + e];   // scalar tail first
-                const int64_t nv = vs - 4 * sz;
-                for (int l = 0; l < 8; ++l) {
-                    float p0 = ps[l];
-                    for (int64_t v = 0; v < nv; ++v) p0 += tb[32 + v * 8 + l];   // row_sum tail into p0
-                    p0 += ps[l + 8];
-                    p0 += ps[l + 16];
-                    p0 += ps[l + 24];
-                    fa += p0;
-                }
-            }
+            fa = cle_chunk_sum_with(ch, [&](int64_t i) { return b1[i]; }, [&](int64_t i) { return tb[i]; }, lane);
         }
         if (lane == 0) part[(int64_t)ch.layer * S + ch.t] = 0.f + fa;   // buffer[t] starts at 0
     }
@@ -1215,17 +1273,27 @@ __device__ double np_pairwise(const double* a, int64_t n) {
 // then / n), np.sum over layers, history and the stop rule.  One block.
 // kLeafOnly: nl <= 128 (numpy's pairwise sum is one leaf) -- no frame stack, so
 // no scratch in the persistent kernel
-template <bool kLeafOnly = false>
+// kCoherent: the chunk sums come from other blocks of the same launch (agent-
+// coherent loads); else from an earlier launch (plain loads).
+template <bool kLeafOnly = false, bool kCoherent = false>
 __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ layers, int32_t nl,
                                                const float* __restrict__ part, int32_t S, double* __restrict__ means,
-                                               double* __restrict__ hist, CleState* __restrict__ st, double* sm) {
+                                               double* __restrict__ hist, CleState* __restrict__ st, double* sm,
+                                               float* part_lds = nullptr) {
+    if (part_lds) {   // every chunk sum in one parallel pass of coherent loads
+        for (int64_t i = threadIdx.x; i < (int64_t)nl * S; i += blockDim.x)
+            part_lds[i] = kCoherent ? ld_coh(part + i) : part[i];
+        __syncthreads();
+        part = part_lds;
+    }
     double* m = nl <= 1024 ? sm : means;
     for (int l = threadIdx.x; l < nl; l += blockDim.x) {
         // serial: sum = 0 + (0 + slot); two_pass_reduction: its S-slot buffer
         // (at::get_num_threads()) summed as a contiguous reduction
         const float* pl = part + (int64_t)l * S;
-        const float sum = layers[l].nt == 1 ? 0.f + (0.f + pl[0])
-                                            : 0.f + aten_inner_sum([&](int64_t e) { return pl[e]; }, S);
+        auto ld = [&](int64_t e) { return (part_lds || !kCoherent) ? pl[e] : ld_coh(pl + e); };
+        const float sum = layers[l].nt == 1 ? 0.f + (0.f + ld(0))
+                                            : 0.f + aten_inner_sum([&](int64_t e) { return ld(e); }, S);
         m[l] = (double)(sum / (float)layers[l].n);
     }
     __syncthreads();
@@ -1256,6 +1324,88 @@ __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32
     __shared__ double sm[1024];   // the per-layer means, read back by one thread
     if (st->done) return;
     cle_final_body(layers, nl, part, S, means, hist, st, sm);
+}
+
+// The metric tiles (+ the next iteration's ranges) with the chunk combine and the
+// stop rule folded in: the block that finishes a chunk's last tile sums that
+// chunk, and the block that finishes the last chunk runs the stop rule -- two
+// launches fewer per iteration.  Hand-offs between blocks go through
+// agent-coherent stores / loads and monotone arrival counters (cnt: one per
+// chunk, then one for the chunks; zeroed by plan_run, iteration i's target is
+// (i + 1) x members), so no L2 write-back is needed inside the launch.
+struct CleFin {
+    uint32_t* cnt;
+    float* part;
+    double* means;
+    double* hist;
+    int64_t nchunks, nbig;   // all chunks / chunks with tiles (len >= 8)
+    int32_t S, nl;
+};
+
+__global__ void __launch_bounds__(kThreads)
+cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
+                          const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t nunits,
+                          float* __restrict__ b1buf, float* __restrict__ tailbuf, int64_t ntb,
+                          const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
+                          uint32_t* __restrict__ rng, int64_t M, CleFin F, CleState* __restrict__ st) {
+    __shared__ float lds[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
+    __shared__ int flag;
+    if (st->done) return;
+    const uint32_t round = (uint32_t)st->iters + 1u;
+    if ((int64_t)blockIdx.x >= ntb) {
+        cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + 1) & 1, blockIdx.x - ntb, gridDim.x - ntb, lds);
+        return;
+    }
+    auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this unit's coherent stores are done
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t a = __hip_atomic_fetch_add(F.cnt + un.chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            flag = a == round * (uint32_t)(nb1 + 1) - 1u;
+        }
+        __syncthreads();
+        if (!flag) return;   // not the chunk's last tile
+        {
+            // the chunk's level-1 sums and tail words in one parallel pass of coherent
+            // loads into LDS (free again: the unit is done), then one wave sums them
+            const float* gb1 = b1buf + b1off[un.chunk];
+            const float* gtb = tailbuf + (int64_t)un.chunk * kCleTailWords;
+            const int64_t nw = 32 * nb1;
+            const bool staged = nw + kCleTailWords <= kCleTile;
+            if (staged) {
+                for (int64_t i = threadIdx.x; i < nw; i += kThreads) lds[i] = ld_coh(gb1 + i);
+                if (threadIdx.x < kCleTailWords) lds[nw + threadIdx.x] = ld_coh(gtb + threadIdx.x);
+            }
+            __syncthreads();
+            if (threadIdx.x < 64) {
+                const float fa = staged ? cle_chunk_sum_with(ch, [&](int64_t i) { return lds[i]; },
+                                                             [&](int64_t i) { return lds[nw + i]; }, threadIdx.x)
+                                        : cle_chunk_sum(ch, gb1, gtb, threadIdx.x);
+                if (threadIdx.x == 0) st_coh(F.part + (int64_t)ch.layer * F.S + ch.t, 0.f + fa);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t a = __hip_atomic_fetch_add(F.cnt + F.nchunks, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            flag = a == round * (uint32_t)F.nbig - 1u;
+        }
+        __syncthreads();
+        if (!flag) return;   // not the last chunk
+        if (threadIdx.x == 0)
+            for (int64_t k = 0; k < F.nchunks; ++k) {
+                const CleChunk c2 = chunks[k];
+                if (c2.len < 8) st_coh(F.part + (int64_t)c2.layer * F.S + c2.t, 0.f + cle_tiny_chunk_sum(layers, c2));
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
+        cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
+                                   stage_part ? lds + 2048 : nullptr);
+    };
+    cle_tiles_body(layers, chunks, b1off, units, nunits, b1buf, tailbuf, blockIdx.x, ntb, lds,
+                   lds + kCleTile + kCleTailWords, hook);
 }
 
 // ---------------------------------------------------------------------------
@@ -1523,6 +1673,9 @@ struct dfq_cle_plan {
     void* d_snap_owned = nullptr;   // snapshots when the caller passed no workspace
     double* d_hist_owned = nullptr; // history beyond kCleHistCap iterations
     uint32_t* d_bar = nullptr;      // persistent loop's grid barrier words
+    uint32_t* d_cnt = nullptr;      // tiles_fin arrival counters [nchunks + 1]
+    bool fin_fused = false;         // combine + stop rule folded into the tiles launch
+    int64_t nbig = 0;               // chunks with tiles
     int32_t persist_grid = -1;      // cooperative grid of the persistent loop (0: not usable; -1: not sized)
 };
 
@@ -1804,6 +1957,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_state = T.add<CleState>(1);
     const int64_t o_hist = T.add<double>(kCleHistCap);
     const int64_t o_bar = T.add<uint32_t>(kCleBarWords);
+    const int64_t o_cnt = T.add<uint32_t>((int64_t)chunks.size() + 1);
     const double tm0 = now_us();
     if ((e = hipMalloc(&p->d_tables, T.total)) != hipSuccess) return fail(e);
     const double tm1 = now_us();
@@ -1833,6 +1987,9 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->d_state = reinterpret_cast<CleState*>(base + o_state);
     p->d_hist = reinterpret_cast<double*>(base + o_hist);
     p->d_bar = reinterpret_cast<uint32_t*>(base + o_bar);
+    p->d_cnt = reinterpret_cast<uint32_t*>(base + o_cnt);
+    for (const auto& c : chunks) p->nbig += c.len >= 8 ? 1 : 0;
+    p->fin_fused = p->nunits > 0 && p->nbig > 0 && n_targets <= 128 && !ab_env("DFQ_CLE_UNFUSED_FIN");
     p->hist_cap = kCleHistCap;
     *out = p;
     return DFQ_OK;
@@ -1862,6 +2019,15 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
     }
     const int64_t nr = p->fused ? p->rstep[1] - p->rstep[0] : 0;   // next iteration's range tasks
     const int64_t ntb = std::min<int64_t>(p->nunits, kTileGrid), nrb = std::min<int64_t>(nr, kStepGrid);
+    if (p->fin_fused) {   // tiles (+ ranges) + chunk combine + stop rule: one launch
+        CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl};
+        hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
+                           p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
+                           p->d_rtasks, p->rstep[0], p->fused ? p->rstep[1] : p->rstep[0], p->d_rng, p->M, F,
+                           p->d_state);
+        DFQ_LAUNCH_CHECK();
+        return DFQ_OK;
+    }
     if (p->nchunks > 0 && ntb > 0 && nrb > 0) {
         hipLaunchKernelGGL(cle_loop_tiles_range_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
                            p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
@@ -1962,6 +2128,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         DFQ_HIP_CHECK(hipMemsetAsync(p->d_rng + (int64_t)par * 2 * p->M + p->M, 0x00, sizeof(uint32_t) * p->M, s));
     }
     DFQ_HIP_CHECK(hipMemsetAsync(p->d_part, 0, sizeof(float) * p->slots * std::max(p->nl, 1), s));
+    DFQ_HIP_CHECK(hipMemsetAsync(p->d_cnt, 0, sizeof(uint32_t) * (p->nchunks + 1), s));
     if (p->nchunks > 0) {
         hipLaunchKernelGGL(cle_loop_snap_kernel, dim3((int)std::min<int64_t>(std::max<int64_t>(p->nunits, 1), 4096)),
                            dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_units, p->nunits);
@@ -2073,9 +2240,13 @@ extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t
     if (!p) return DFQ_ERR_INVALID;
     if (chains) *chains = p->chains;
     if (steps) *steps = p->steps;
-    if (launches)   // per iteration: range + rescale launches, then the metric (2) and the stop rule
-        *launches = (p->fused ? p->steps + ((p->nunits > 0 && p->nchunks > 0) ? 0 : 1) : 2 * p->steps) +
-                    (p->nunits > 0 ? 1 : 0) + (p->nchunks > 0 ? 1 : 0) + 1;
+    if (launches) {   // per iteration: range + rescale launches, then the metric (2) and the stop rule
+        if (p->fin_fused)   // rescales (+ per-step ranges), then tiles + ranges + combine + stop rule
+            *launches = (p->fused ? p->steps : 2 * p->steps) + 1;
+        else
+            *launches = (p->fused ? p->steps + ((p->nunits > 0 && p->nchunks > 0) ? 0 : 1) : 2 * p->steps) +
+                        (p->nunits > 0 ? 1 : 0) + (p->nchunks > 0 ? 1 : 0) + 1;
+    }
     return DFQ_OK;
 }
 

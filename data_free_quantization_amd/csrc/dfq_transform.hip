@@ -499,6 +499,196 @@ extern "C" int dfq_bias_absorb(const float* w2, float* b1, float* b2, float* bn_
     return DFQ_OK;
 }
 
+// ---- batched absorption ---------------------------------------------------
+namespace dfq {
+struct AbsRel {
+    const float* w2;
+    const float* bn_w;
+    float* bn_b;
+    int64_t o2, i2, khw2, o2g;
+    int64_t wc;    // float offset of this relation's W2sum @ c in the scratch
+};
+struct AbsRows {   // GEMV task: rows [o0, o1) of relation r, one wave per row
+    int32_t r;
+    int32_t pad;
+    int64_t o0, o1;
+};
+struct AbsVec {    // a bias vector and its update list
+    float* b;
+    int64_t n;
+    int32_t op0, nops;
+};
+struct AbsOp {     // kind 0: b += wc[r]; kind 1: b -= c[r] and beta[r] -= c[r]
+    int32_t kind;
+    int32_t r;
+};
+struct AbsElems {  // bias walk task: elements [e0, e1) of vector v
+    int32_t v;
+    int32_t pad;
+    int64_t e0, e1;
+};
+
+__global__ void absorb_batch_gemv_kernel(const AbsRel* __restrict__ rels, const AbsRows* __restrict__ tasks,
+                                         int64_t ntasks, float* __restrict__ wc, float n_sigma) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t t = wave; t < ntasks; t += nwaves) {
+        const AbsRows tk = tasks[t];
+        const AbsRel R = rels[tk.r];
+        for (int64_t o = tk.o0; o < tk.o1; ++o) {
+            const int64_t g = o / R.o2g;
+            const float* row = R.w2 + o * R.i2 * R.khw2;
+            float acc = 0.f;
+            for (int64_t i = lane; i < R.i2; i += 64) {
+                float ssum = 0.f;
+                for (int64_t k = 0; k < R.khw2; ++k) ssum += row[i * R.khw2 + k];
+                const int64_t ch = g * R.i2 + i;
+                acc += ssum * absorb_c(R.bn_b[ch], R.bn_w[ch], n_sigma);
+            }
+            acc = wave_sum_f(acc);
+            if (lane == 0) wc[R.wc + o] = acc;
+        }
+    }
+}
+
+__global__ void absorb_batch_bias_kernel(const AbsRel* __restrict__ rels, const AbsVec* __restrict__ vecs,
+                                         const AbsOp* __restrict__ ops, const AbsElems* __restrict__ tasks,
+                                         int64_t ntasks, const float* __restrict__ wc, float n_sigma) {
+    for (int64_t t = blockIdx.x; t < ntasks; t += gridDim.x) {
+        const AbsElems tk = tasks[t];
+        const AbsVec V = vecs[tk.v];
+        for (int64_t e = tk.e0 + threadIdx.x; e < tk.e1; e += blockDim.x) {
+            float b = V.b[e];
+            for (int32_t q = 0; q < V.nops; ++q) {
+                const AbsOp op = ops[V.op0 + q];
+                const AbsRel& R = rels[op.r];
+                if (op.kind == 0) {
+                    b = b + wc[R.wc + e];
+                } else {
+                    const float cc = absorb_c(R.bn_b[e], R.bn_w[e], n_sigma);
+                    b = b + (-cc);
+                    R.bn_b[e] = R.bn_b[e] + (-cc);
+                }
+            }
+            V.b[e] = b;
+        }
+    }
+}
+
+struct AbsTables {
+    std::vector<AbsRel> rels;
+    std::vector<AbsRows> rows;
+    std::vector<AbsVec> vecs;
+    std::vector<AbsOp> ops;
+    std::vector<AbsElems> elems;
+    int64_t wc_floats = 0;
+};
+
+static int absorb_tables(const dfq_absorb_desc* d, int32_t n, AbsTables& T, int32_t* failed) {
+    // per bias vector, its updates in relation order
+    std::vector<std::pair<float*, int64_t>> vlist;
+    std::vector<std::vector<AbsOp>> vops;
+    auto vec_of = [&](float* b, int64_t len) {
+        for (size_t k = 0; k < vlist.size(); ++k)
+            if (vlist[k].first == b) return (int32_t)k;
+        vlist.push_back({b, len});
+        vops.emplace_back();
+        return (int32_t)vlist.size() - 1;
+    };
+    for (int32_t r = 0; r < n; ++r) {
+        const dfq_absorb_desc& x = d[r];
+        if (failed) *failed = r;
+        if (!x.w2 || !x.b1 || !x.b2 || !x.bn_w || !x.bn_b || x.c1 <= 0 || x.o2 <= 0 || x.i2 <= 0 || x.khw2 <= 0)
+            return DFQ_ERR_INVALID;
+        const int64_t groups = x.c1 / x.i2;   // bias_absorption.py:159
+        if (groups <= 0 || x.o2 % groups != 0 || groups * x.i2 > x.c1) return DFQ_ERR_SHAPE;
+        if (x.b1 == x.b2) return DFQ_ERR_SHAPE;
+        for (int32_t q = 0; q < r; ++q)   // a BN shared by two relations: the per-relation call keeps its order
+            if (d[q].bn_b == x.bn_b) return DFQ_ERR_UNSUPPORTED;
+        AbsRel R{x.w2, x.bn_w, x.bn_b, x.o2, x.i2, x.khw2, x.o2 / groups, T.wc_floats};
+        T.wc_floats += ceil_div(x.o2, (int64_t)64) * 64;
+        T.rels.push_back(R);
+        for (int64_t o = 0; o < x.o2; o += 4) T.rows.push_back(AbsRows{r, 0, o, std::min<int64_t>(o + 4, x.o2)});
+        // reference order inside a relation: b1 -= c (and beta), then b2 += wc
+        const int32_t v1 = vec_of(x.b1, x.c1);
+        if (vlist[v1].second != x.c1) return DFQ_ERR_SHAPE;
+        vops[v1].push_back(AbsOp{1, r});
+        const int32_t v2 = vec_of(x.b2, x.o2);
+        if (vlist[v2].second != x.o2) return DFQ_ERR_SHAPE;
+        vops[v2].push_back(AbsOp{0, r});
+    }
+    if (failed) *failed = -1;
+    for (size_t k = 0; k < vlist.size(); ++k) {
+        T.vecs.push_back(AbsVec{vlist[k].first, vlist[k].second, (int32_t)T.ops.size(), (int32_t)vops[k].size()});
+        T.ops.insert(T.ops.end(), vops[k].begin(), vops[k].end());
+        for (int64_t e = 0; e < vlist[k].second; e += 1024)
+            T.elems.push_back(AbsElems{(int32_t)k, 0, e, std::min<int64_t>(e + 1024, vlist[k].second)});
+    }
+    return DFQ_OK;
+}
+
+struct AbsLayout {
+    int64_t o_rels, o_rows, o_vecs, o_ops, o_elems, host, o_wc, total;
+};
+static AbsLayout absorb_layout(const AbsTables& T) {
+    AbsLayout L{};
+    int64_t o = 0;
+    auto add = [&](int64_t bytes) {
+        const int64_t at = o;
+        o += ceil_div(std::max<int64_t>(bytes, 1), (int64_t)256) * 256;
+        return at;
+    };
+    L.o_rels = add(sizeof(AbsRel) * T.rels.size());
+    L.o_rows = add(sizeof(AbsRows) * T.rows.size());
+    L.o_vecs = add(sizeof(AbsVec) * T.vecs.size());
+    L.o_ops = add(sizeof(AbsOp) * T.ops.size());
+    L.o_elems = add(sizeof(AbsElems) * T.elems.size());
+    L.host = o;
+    L.o_wc = add(sizeof(float) * T.wc_floats);
+    L.total = o;
+    return L;
+}
+}  // namespace dfq
+
+extern "C" int64_t dfq_bias_absorb_ws_bytes(const dfq_absorb_desc* d, int32_t n) {
+    if (n < 0 || (n > 0 && !d)) return -1;
+    AbsTables T;
+    if (absorb_tables(d, n, T, nullptr) != DFQ_OK) return -1;
+    return absorb_layout(T).total;
+}
+
+extern "C" int dfq_bias_absorb_batch(const dfq_absorb_desc* d, int32_t n, float n_sigma, void* ws, int64_t ws_bytes,
+                                     int32_t* failed, void* stream) {
+    if (failed) *failed = -1;
+    if (n < 0 || (n > 0 && !d)) return DFQ_ERR_INVALID;
+    if (n == 0) return DFQ_OK;
+    AbsTables T;
+    const int rc = absorb_tables(d, n, T, failed);
+    if (rc != DFQ_OK) return rc;
+    const AbsLayout L = absorb_layout(T);
+    if (!ws || ws_bytes < L.total || reinterpret_cast<uintptr_t>(ws) % 256 != 0) return DFQ_ERR_WORKSPACE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    char* base = static_cast<char*>(ws);
+    std::vector<char> blob(L.host, 0);
+    auto put = [&](int64_t off, const auto& v) {
+        if (!v.empty()) std::memcpy(blob.data() + off, v.data(), sizeof(v[0]) * v.size());
+    };
+    put(L.o_rels, T.rels); put(L.o_rows, T.rows); put(L.o_vecs, T.vecs); put(L.o_ops, T.ops); put(L.o_elems, T.elems);
+    DFQ_HIP_CHECK(stage_h2d(base, blob.data(), L.host, s));
+    const AbsRel* dr = reinterpret_cast<const AbsRel*>(base + L.o_rels);
+    float* wc = reinterpret_cast<float*>(base + L.o_wc);
+    const int64_t nrow = (int64_t)T.rows.size(), nel = (int64_t)T.elems.size();
+    hipLaunchKernelGGL(absorb_batch_gemv_kernel, dim3((int)std::min<int64_t>(ceil_div(nrow, kThreads / 64), 4096)),
+                       dim3(kThreads), 0, s, dr, reinterpret_cast<const AbsRows*>(base + L.o_rows), nrow, wc, n_sigma);
+    DFQ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(absorb_batch_bias_kernel, dim3((int)std::min<int64_t>(nel, 4096)), dim3(kThreads), 0, s, dr,
+                       reinterpret_cast<const AbsVec*>(base + L.o_vecs), reinterpret_cast<const AbsOp*>(base + L.o_ops),
+                       reinterpret_cast<const AbsElems*>(base + L.o_elems), nel, wc, n_sigma);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
 extern "C" int dfq_bc_expect(const float* fake_w, const float* fake_b, int64_t n, int32_t relu, int32_t accumulate,
                              float* out, void* stream) {
     if (!fake_w || !fake_b || !out || n < 0) return DFQ_ERR_INVALID;

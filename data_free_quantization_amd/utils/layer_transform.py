@@ -13,7 +13,10 @@ Graph/bottoms follow SURVEY.md 8b.  Target tensors must be on a ROCm device.
 from __future__ import annotations
 
 import ctypes as C
+import types
 from typing import Dict, Optional
+
+import numpy as np
 
 import torch
 import torch.nn as nn
@@ -57,75 +60,75 @@ def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d]):
 
 def _carve(total_sizes, fill_zero, device):
     """Views of ONE allocation, one per size (a model's worth of small vectors in a
-    single allocator call instead of one each)."""
-    n = sum(total_sizes)
-    flat = (torch.zeros if fill_zero else torch.empty)(max(n, 1), dtype=torch.float32, device=device)
-    out, off = [], 0
-    for k in total_sizes:
-        out.append(flat[off:off + k])
-        off += k
-    return out
+    single allocator call and one split instead of one each)."""
+    flat = (torch.zeros if fill_zero else torch.empty)(max(sum(total_sizes), 1), dtype=torch.float32,
+                                                       device=device)
+    return list(torch.split(flat[:sum(total_sizes)], list(total_sizes))) if total_sizes else []
+
+
+# dfq_bn_fold_desc as a numpy record (same layout as _lib.BnFoldDesc): the table
+# of a model's folds is filled column-wise instead of field by field
+_BN_DESC = np.dtype([("ptr", "<u8", (8,)), ("eps", "<f4"), ("reserved", "<i4"), ("rows", "<i8"),
+                     ("row_len", "<i8")])
+assert _BN_DESC.itemsize == C.sizeof(_lib.BnFoldDesc)
 
 
 def _fold_batch(pairs):
     with torch.no_grad():
-        descs = (_lib.BnFoldDesc * len(pairs))()
         dev = pairs[0][1].weight.device
         for bn, layer in pairs:
             _lib.require_device(layer.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var)
         need_bias = [layer for _, layer in pairs if layer.bias is None]
         for layer, z in zip(need_bias, _carve([l.weight.size(0) for l in need_bias], True, dev)):   # :262-263
             layer.bias = nn.Parameter(z, requires_grad=False)
-        fakes = _carve([bn.weight.numel() for bn, _ in pairs] * 2, False, dev)
+        nc = [bn.weight.numel() for bn, _ in pairs]
+        fakes = _carve(nc * 2, False, dev)
+        n = len(pairs)
+        tab = np.zeros(n, dtype=_BN_DESC)
+        ptrs = tab["ptr"]
         for j, (bn, layer) in enumerate(pairs):
             w = layer.weight
-            bn.register_buffer("fake_weight", fakes[j].view_as(bn.weight))
-            bn.register_buffer("fake_bias", fakes[len(pairs) + j].view_as(bn.bias))
-            d = descs[j]
-            d.w, d.bias = w.data_ptr(), layer.bias.data_ptr()
-            d.bn_w, d.bn_b = bn.weight.data_ptr(), bn.bias.data_ptr()
-            d.bn_mean, d.bn_var = bn.running_mean.data_ptr(), bn.running_var.data_ptr()
-            d.fake_w, d.fake_b = bn.fake_weight.data_ptr(), bn.fake_bias.data_ptr()
-            d.eps = float(bn.eps)
-            d.rows = w.size(0)
-            d.row_len = w.numel() // w.size(0)
+            fw, fb = fakes[j], fakes[n + j]
+            buf = bn._buffers   # register_buffer("fake_weight" / "fake_bias") without the per-call checks
+            buf["fake_weight"], buf["fake_bias"] = fw, fb
+            ptrs[j] = (w.data_ptr(), layer.bias.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(),
+                       bn.running_mean.data_ptr(), bn.running_var.data_ptr(), fw.data_ptr(), fb.data_ptr())
+        tab["eps"] = [float(bn.eps) for bn, _ in pairs]
+        tab["rows"] = [layer.weight.size(0) for _, layer in pairs]
+        tab["row_len"] = [layer.weight.numel() // layer.weight.size(0) for _, layer in pairs]
+        descs = tab.ctypes.data_as(C.POINTER(_lib.BnFoldDesc))
         L = _lib.load()
-        nb = int(L.dfq_bn_fold_ws_bytes(descs, len(pairs)))
+        nb = int(L.dfq_bn_fold_ws_bytes(descs, n))
         if nb < 0:
             raise RuntimeError("dfq_bn_fold_ws_bytes: invalid layer shapes")
-        dev = pairs[0][1].weight.device
         ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=dev)   # stream-ordered (caching allocator)
-        rc = L.dfq_bn_fold_batch(descs, len(pairs), ws.data_ptr(), ws.numel(), _lib.stream_of(pairs[0][1].weight))
+        rc = L.dfq_bn_fold_batch(descs, n, ws.data_ptr(), ws.numel(), _lib.stream_of(pairs[0][1].weight))
         _lib.check(rc, "dfq_bn_fold_batch")
         for bn, _ in pairs:
             bn.eps = 0
-            _identity_forward_hooks(bn)
+            _identity_forward(bn)
 
 
 _TINY = float(torch.finfo(torch.float32).tiny)
 
 
-def _identity_forward_hooks(bn):
+def _folded_bn_forward(self, input):
     """The folded BN (weight 1, bias 0, mean 0, var 1, eps 0 -- the reference's
-    state) is an identity, but torch >= 2 rejects eps == 0 in F.batch_norm.  Run
-    its forward with the smallest normal fp32 eps (1 + eps == 1 in fp32, so the
+    state) is an identity, but torch >= 2 rejects eps == 0 in F.batch_norm: run
+    the forward with the smallest normal fp32 eps (1 + eps == 1 in fp32, so the
     result is unchanged) and put eps = 0 back afterwards."""
-    if getattr(bn, "_dfq_identity_hooks", False):
-        return
+    if self.eps != 0:
+        return nn.BatchNorm2d.forward(self, input)
+    self.eps = _TINY
+    try:
+        return nn.BatchNorm2d.forward(self, input)
+    finally:
+        self.eps = 0
 
-    def pre(mod, args):
-        if mod.eps == 0:
-            mod.eps = _TINY
-            mod._dfq_eps_swapped = True
 
-    def post(mod, args, out):
-        if getattr(mod, "_dfq_eps_swapped", False):
-            mod.eps = 0
-            mod._dfq_eps_swapped = False
-
-    bn.register_forward_pre_hook(pre)
-    bn.register_forward_hook(post)
-    bn._dfq_identity_hooks = True
+def _identity_forward(bn):
+    if "forward" not in bn.__dict__:   # one instance attribute (no per-BN hook objects)
+        bn.forward = types.MethodType(_folded_bn_forward, bn)
 
 
 def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, granularity="tensor",

@@ -254,6 +254,25 @@ int dfq_cle_plan_destroy(dfq_cle_plan* plan);
 int dfq_bias_absorb(const float* w2, float* b1, float* b2, float* bn_w, float* bn_b,
                     int64_t c1, int64_t o2, int64_t i2, int64_t khw2, float n_sigma,
                     void* stream);
+/* Every absorption of a model in two launches (bias_absorption.py:9-121, the
+ * relations in the reference's order): all c = clamp(beta - N*gamma, 0) and
+ * W2-sum GEMVs first (into the workspace), then one pass per bias element that
+ * applies that vector's updates in relation order (b -= c as a layer_first,
+ * b += W2sum @ c as a layer_second) and beta -= c -- the same fp32 operations in
+ * the same per-element order as one dfq_bias_absorb call per relation.
+ * `*failed` = the index of a relation whose shapes are invalid (nothing is
+ * enqueued then). */
+typedef struct dfq_absorb_desc {
+    const float* w2;
+    float*       b1;
+    float*       b2;
+    float*       bn_w;    /* fake_weight of the BN between the layers */
+    float*       bn_b;    /* fake_bias (updated) */
+    int64_t      c1, o2, i2, khw2;
+} dfq_absorb_desc;
+int64_t dfq_bias_absorb_ws_bytes(const dfq_absorb_desc* descs, int32_t n);
+int dfq_bias_absorb_batch(const dfq_absorb_desc* descs, int32_t n, float n_sigma, void* ws, int64_t ws_bytes,
+                          int32_t* failed, void* stream);
 
 /* ---- bias correction (bias_correction.py) -------------------------------
  * dfq_bc_expect: out[j] (+)= relu ? max(0, w*phi(-b/w) + b*(1-Phi(-b/w))) : b

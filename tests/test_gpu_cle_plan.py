@@ -111,9 +111,12 @@ def test_device_cle_matches_oracle(signed, eps, smm, thr, count, monkeypatch):
                                  signed=signed, eps=eps, Save_state=False)
     torch.cuda.synchronize()
     assert cle.LAST_RUN["chains"] == 3 and cle.LAST_RUN["steps"] == 2
-    # fused schedule: 2 rescale steps + metric tiles (with the next iteration's
-    # ranges) + combine + stop rule; else 2 x (range + rescale) + metric (2) + stop rule
-    expect = 5 if os.environ.get("DFQ_CLE_FUSED", "1") != "0" else 7
+    # fused schedule: 2 rescale steps + ONE launch of metric tiles with the next
+    # iteration's ranges, the chunk combine and the stop rule folded in; else
+    # 2 x (range + rescale) + that launch
+    expect = 3 if os.environ.get("DFQ_CLE_FUSED", "1") != "0" else 5
+    if os.environ.get("DFQ_LIB") == "diag" and os.environ.get("DFQ_CLE_UNFUSED_FIN"):
+        expect += 2   # A/B: the chunk combine and the stop rule as launches of their own
     assert cle.LAST_RUN["launches_per_iteration"] == expect
     assert cle.LAST_RUN["diffs"] == diffs
     for k in W:
