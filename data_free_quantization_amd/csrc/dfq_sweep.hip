@@ -621,9 +621,16 @@ static bool blockrow_enabled() {
 // DFQ_SWEEP_SLAB_MB: split the two-pass (reduce -> quantize) tensors into slabs of
 // about this many MB, each reduced and quantized back to back, so the second read
 // of a slab can still hit the 256 MB Infinity Cache (0: one slab).
+// Two-pass ranges can be pipelined in slabs of this many bytes of inputs (see
+// dfq_sweep_plan_execute): the quantize pass of slab k re-reads its inputs while
+// they are still in the 256 MB Infinity Cache.  Measured slower at every slab
+// size (profiles/r02/ab_slab.json: 16-256 MB slabs on two streams 1.34-3.9 ms per
+// step against 1.11 for the two passes back to back), so the product runs one
+// slab; DFQ_SWEEP_SLAB_MB sets the size in the diagnostics library.
+constexpr int64_t kSlabBytes = 0;
 static int64_t slab_bytes() {
     const char* e = ab_env("DFQ_SWEEP_SLAB_MB");
-    return (e && *e) ? (int64_t)atoll(e) << 20 : 0;
+    return (e && *e) ? (int64_t)atoll(e) << 20 : kSlabBytes;
 }
 
 // Reduce-launch tasks: consecutive pieces of one range merged up to `span`
@@ -872,6 +879,13 @@ struct dfq_sweep_plan {
     void* d_owned = nullptr;       // the tables' allocation when no workspace was given
     int64_t n_reduce = 0, n_main = 0, n_slots = 0, n_tensors = 0, n_elems = 0, algo_bytes = 0;
     std::vector<int64_t> rslab, mslab;   // slab boundaries (Built)
+    // slab pipeline: reduce launches on `aux`, quantize launches on the caller's
+    // stream, each quantize slab waiting for its reduce (ev_r) and each reduce
+    // waiting for the quantize two slabs back (ev_m: the reduce stream stays at
+    // most two slabs ahead, so the re-reads hit the Infinity Cache)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr;
+    std::vector<hipEvent_t> ev_r, ev_m;
 };
 
 namespace dfq {
@@ -986,21 +1000,50 @@ extern "C" int dfq_sweep_plan_execute(dfq_sweep_plan* p, void* stream) {
         }
         return DFQ_OK;
     }
-    // slabs: reduce(k), then quantize slab k (the first main launch also takes the
-    // single-pass tasks)
+    // slabs, two streams: the single-pass tasks, then quantize slab k as soon as
+    // reduce slab k (running ahead on the plan's aux stream) has its ranges
+    if (!p->aux) {
+        int dev = 0;
+        DFQ_HIP_CHECK(hipStreamGetDevice(s, &dev));
+        int cur = 0;
+        DFQ_HIP_CHECK(hipGetDevice(&cur));
+        if (cur != dev) DFQ_HIP_CHECK(hipSetDevice(dev));
+        hipError_t e = hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming);
+        p->ev_r.assign(nslab, nullptr);
+        p->ev_m.assign(nslab, nullptr);
+        for (size_t k = 0; k < nslab && e == hipSuccess; ++k) {
+            e = hipEventCreateWithFlags(&p->ev_r[k], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_m[k], hipEventDisableTiming);
+        }
+        if (cur != dev) (void)hipSetDevice(cur);
+        DFQ_HIP_CHECK(e);
+    }
+    DFQ_HIP_CHECK(hipEventRecord(p->ev_fork, s));   // after the slot initialisation
+    DFQ_HIP_CHECK(hipStreamWaitEvent(p->aux, p->ev_fork, 0));
+    const int64_t single = p->mslab[0];   // blockrow + whole-row tasks: no range needed
+    if (single > 0) {
+        launch_main(p->variant, grid_for_variant(single, p->variant), s, p->d_tensors, p->d_main, single, p->d_slots,
+                    p->d_slots + p->n_slots);
+        DFQ_LAUNCH_CHECK();
+    }
     for (size_t k = 0; k < nslab; ++k) {
         const int64_t r0 = p->rslab[k], r1 = p->rslab[k + 1];
+        if (k >= 2) DFQ_HIP_CHECK(hipStreamWaitEvent(p->aux, p->ev_m[k - 2], 0));
         if (r1 > r0) {
-            hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for(r1 - r0)), dim3(kBlockThreads), 0, s, p->d_tensors,
-                               p->d_reduce + r0, r1 - r0, p->d_slots, p->d_slots + p->n_slots);
+            hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for(r1 - r0)), dim3(kBlockThreads), 0, p->aux,
+                               p->d_tensors, p->d_reduce + r0, r1 - r0, p->d_slots, p->d_slots + p->n_slots);
             DFQ_LAUNCH_CHECK();
         }
-        const int64_t m0 = k == 0 ? 0 : p->mslab[k], m1 = p->mslab[k + 1];
+        DFQ_HIP_CHECK(hipEventRecord(p->ev_r[k], p->aux));
+        DFQ_HIP_CHECK(hipStreamWaitEvent(s, p->ev_r[k], 0));
+        const int64_t m0 = p->mslab[k], m1 = p->mslab[k + 1];
         if (m1 > m0) {
             launch_main(p->variant, grid_for_variant(m1 - m0, p->variant), s, p->d_tensors, p->d_main + m0, m1 - m0,
                         p->d_slots, p->d_slots + p->n_slots);
             DFQ_LAUNCH_CHECK();
         }
+        DFQ_HIP_CHECK(hipEventRecord(p->ev_m[k], s));
     }
     return DFQ_OK;
 }
@@ -1014,9 +1057,9 @@ extern "C" int dfq_sweep_plan_stats(const dfq_sweep_plan* p, dfq_sweep_stats* st
     st->algo_bytes = p->algo_bytes;
     if (p->rslab.size() > 2) {
         int32_t l = 0;
+        l = p->mslab[0] > 0 ? 1 : 0;
         for (size_t k = 0; k + 1 < p->rslab.size(); ++k)
-            l += (p->rslab[k + 1] > p->rslab[k] ? 1 : 0) +
-                 ((p->mslab[k + 1] > (k == 0 ? 0 : p->mslab[k])) ? 1 : 0);
+            l += (p->rslab[k + 1] > p->rslab[k] ? 1 : 0) + ((p->mslab[k + 1] > p->mslab[k]) ? 1 : 0);
         st->launches = l;
     } else {
         st->launches = (p->n_reduce > 0 ? 1 : 0) + (p->n_main > 0 ? 1 : 0);
@@ -1028,6 +1071,13 @@ extern "C" int dfq_sweep_plan_stats(const dfq_sweep_plan* p, dfq_sweep_stats* st
 
 extern "C" int dfq_sweep_plan_destroy(dfq_sweep_plan* p) {
     if (!p) return DFQ_OK;
+    if (p->aux) {
+        (void)hipStreamSynchronize(p->aux);
+        for (auto e : p->ev_r) (void)hipEventDestroy(e);
+        for (auto e : p->ev_m) (void)hipEventDestroy(e);
+        (void)hipEventDestroy(p->ev_fork);
+        (void)hipStreamDestroy(p->aux);
+    }
     (void)hipFree(p->d_owned);   // NULL for workspace-backed plans
     delete p;
     return DFQ_OK;

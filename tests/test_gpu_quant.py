@@ -266,7 +266,8 @@ def test_large_ranges_vs_oracle(monkeypatch):
 
 def test_many_models_per_tensor():
     """quantize_targ_layer's mode over 24 MobileNetV2 weight sets in one plan
-    (reduce launch + quantize launch); every layer bit-exact with the oracle."""
+    (reduce launch + quantize launch); every layer bit-exact with the oracle.  The
+    two-stream slab pipeline (diagnostics A/B) is covered below."""
     from data_free_quantization_amd import zoo
     from data_free_quantization_amd.sweep import allocate, SweepPlan, khw_of
     m = zoo.build("mobilenetv2", seed=9)
@@ -280,9 +281,10 @@ def test_many_models_per_tensor():
             items.append(allocate(wd, bits=8, per_channel=False, symmetric=False, khw=khw_of(wd), want_esum=True,
                                   clip=(-0.3, 0.3)))
     plan = SweepPlan(items)
-    plan.execute()
+    for _ in range(2):   # replay: the range slots are re-armed
+        plan.execute()
     torch.cuda.synchronize()
-    assert plan.stats["launches"] == 2
+    assert plan.stats["launches"] == 2   # one reduce launch, one quantize launch
     for i, it in enumerate(items):
         o = ref[i % len(layers)]
         assert np.array_equal(it.dst.cpu().numpy(), o["dq"])
@@ -479,3 +481,29 @@ def test_random_mixed_plans_vs_oracle(seed):
         if esum:
             assert np.array_equal(it.esum.cpu().numpy(), o["esum"]), tag
     L.dfq_sweep_plan_destroy(p)
+
+
+def test_slab_pipeline_equals_two_passes(monkeypatch):
+    """The two-stream slab pipeline of two-pass ranges (diagnostics library,
+    DFQ_SWEEP_SLAB_MB: reduce slab k on the plan's second stream, quantize slab k on
+    the caller's, 3 slabs here) gives the same bytes as the product's two passes."""
+    from data_free_quantization_amd import _lib
+    from data_free_quantization_amd.sweep import allocate, SweepPlan
+    rng = np.random.default_rng(31)
+    xs = [rng.normal(0, 1, (1 << 20) + 4 * k).astype(np.float32) for k in range(12)]
+    outs = []
+    for lib, mb in (("product", None), ("diag", "8")):
+        if lib == "diag":
+            monkeypatch.setattr(_lib, "_LIB", _lib.load_diag())
+            monkeypatch.setenv("DFQ_SWEEP_SLAB_MB", mb)
+        items = [allocate(torch.from_numpy(x).to(DEV), bits=8, per_channel=False, symmetric=False, clip=(-2.0, 2.0))
+                 for x in xs]
+        plan = SweepPlan(items)
+        for _ in range(2):
+            plan.execute()
+        torch.cuda.synchronize()
+        outs.append((plan.stats["launches"], items))
+        plan.destroy()
+    assert outs[0][0] == 2 and outs[1][0] > 2
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert torch.equal(a.dst, b.dst) and torch.equal(a.codes, b.codes) and torch.equal(a.scale, b.scale)
