@@ -67,6 +67,9 @@ constexpr Variant kVariants[] = {
     {2048, 64, false},    // 13: variant 6 + per-task timestamps (diagnostics: dfq_debug_timeline)
 };
 constexpr int kNumVariants = 14;
+// DevTask.nrows <= kGroupTag: a row-group piece of R = kGroupTag - nrows + 1 rows
+constexpr int kGroupTag = -64;
+constexpr int kGroupMaxRows = 16;
 constexpr int kDefaultVariant = 6;   // = 5 with 87 instead of 105 VGPRs (profiles/r01/ab_*_v568.json)
 
 struct alignas(16) DevTensor {
@@ -97,7 +100,7 @@ struct alignas(16) DevTask {
     int32_t tensor;
     int32_t n;           // elements in the task
     int32_t row0;        // first row of a whole-row task / the row of a long-row piece
-    int32_t nrows;       // > 0: whole rows; 0: slot piece; -1: block-row piece
+    int32_t nrows;       // > 0: whole rows; 0: slot piece; -1/-2/-4: block-row piece; <= kGroupTag: row group
     int32_t slot;        // workspace (min,max) slot for pieces, -1 = given range
     int32_t first;       // this piece writes scale/zero for its slot
 };
@@ -227,19 +230,26 @@ __device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTas
 
 // Steps 2-4 on a chunk that has landed in ``data``.
 // ESPEC: compile-time KH*KW error sums -- 2: 3x3/5x5/7x7/2x2, 1: 3x3, 0: none
+// goff >= 0: a row-group piece whose per-row parameters are already in ls / lmn
+// (local row 0 = the row holding the piece's first element, goff = that element's
+// offset inside it).
 template <int MAXROWS, bool VEC, bool NT = false, int ESPEC = 2>
 __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& task, float* data, float* ls,
                                              float* lmn, const uint32_t* __restrict__ slot_min,
                                              const uint32_t* __restrict__ slot_max, int lane, float bmn = 0.f,
-                                             float bmx = 0.f) {
+                                             float bmx = 0.f, int goff = -1) {
     const int n = task.n;
     const bool sym = is_sym(T.mode);
     const int len = (int)T.row_len;
 
     // 2. per-row parameters (whole-row tasks) or the slot's parameters (pieces)
     QParams pc{};
-    const bool whole = task.nrows > 0;
-    if (whole) {
+    const bool group = goff >= 0;
+    const bool whole = task.nrows > 0 || group;
+    const int eoff = group ? goff : 0;
+    if (group) {
+        // parameters set by the caller
+    } else if (whole) {
         // G lanes per row (G * next_pow2(nrows) = 64): every row of the task is
         // reduced at once; shuffles stay inside a G-lane group and every group
         // leader builds its row's parameters concurrently.
@@ -309,7 +319,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         if (!whole) return pc;
         // row = floor(e / len): (e + 0.5)/len is >= 0.5/len from an integer and
         // e < 2048, so this fp32 estimate is exact.
-        int r = (int)(((float)e + 0.5f) * T.inv_len);
+        int r = (int)(((float)(e + eoff) + 0.5f) * T.inv_len);
         r = min(r, MAXROWS - 1);
         QParams p;
         p.s = ls[r];
@@ -330,7 +340,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
 #pragma unroll 2
         for (int j = lane; j < nj; j += kWave) {
             const float4 xv = reinterpret_cast<const float4*>(data)[j];
-            const QParams p = params_for(4 * j);   // 4 | len: one row per float4
+            const QParams p = params_for(4 * j);   // 4 | len, 4 | goff: one row per float4
             float q0, q1, q2, q3;
             const float y0 = one(xv.x, p, q0);
             const float y1 = one(xv.y, p, q1);
@@ -467,7 +477,68 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
             if constexpr (TL) tl1 = wall_clock64();
             wave_lds_sync();
             float bmn = 0.f, bmx = 0.f;
-            if (task.nrows < 0) {   // block-row piece: all 4 waves of this block are here
+            int goff = -1;
+            if (task.nrows <= kGroupTag) {
+                // row-group piece: the 4 waves of this block hold 4 pieces of R complete
+                // rows.  Per-row partial (min, max) of this piece's row segments into
+                // this wave's ls (max) / lmn (min) slots, one barrier, each wave combines
+                // the rows its piece touches, a second barrier, then its row parameters.
+                const int R = kGroupTag - task.nrows + 1;
+                const int len = (int)T.row_len;
+                const int g0 = (int)(task.elem_start - (int64_t)task.row0 * len);   // piece offset in the group
+                const int rf = g0 / len;
+                const int rl = task.n > 0 ? (g0 + task.n - 1) / len : rf - 1;
+                for (int r = 0; r < R; ++r) {
+                    float vmin = INFINITY, vmax = -INFINITY;
+                    if (r >= rf && r <= rl) {
+                        const int a = max(r * len, g0) - g0, b = min((r + 1) * len, g0 + task.n) - g0;
+                        if (T.vec4) {
+                            for (int j = (a >> 2) + lane; j < (b >> 2); j += kWave) {
+                                const float4 v = reinterpret_cast<const float4*>(wl)[j];
+                                vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+                                vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+                            }
+                        } else {
+                            for (int e = a + lane; e < b; e += kWave) {
+                                vmin = fminf(vmin, wl[e]);
+                                vmax = fmaxf(vmax, wl[e]);
+                            }
+                        }
+                        vmin = wave_min(vmin);
+                        vmax = wave_max(vmax);
+                    }
+                    if (lane == 0) {
+                        lmn[r] = vmin;
+                        ls[r] = vmax;
+                    }
+                }
+                block_lds_sync();
+                constexpr int P = Lay::kPerWave;
+                const int rr = rf + lane;   // one lane per row this piece touches
+                float gmn = INFINITY, gmx = -INFINITY;
+                if (rr <= rl) {
+                    const float* b0 = lds + NB * CHUNK;   // wave 0's ls; lmn = ls + MAXROWS
+#pragma unroll
+                    for (int q = 0; q < kWavesPerBlock; ++q) {
+                        gmx = fmaxf(gmx, b0[q * P + rr]);
+                        gmn = fminf(gmn, b0[q * P + MAXROWS + rr]);
+                    }
+                }
+                block_lds_sync();   // every wave has read the partials
+                if (rr <= rl) {
+                    const QParams p = make_qparams(gmn, gmx, T.bits, is_sym(T.mode), T.flags, T.given_min,
+                                                   T.given_max);
+                    ls[lane] = p.s;
+                    lmn[lane] = p.mn;
+                    if (rr * len >= g0) {   // the row starts in this piece: its parameters are stored once
+                        const int64_t row_g = task.row0 + rr;
+                        if (T.scale) st<false>(T.scale + row_g, p.s);
+                        if (T.zero) st<false>(T.zero + row_g, p.mn);
+                    }
+                }
+                wave_lds_sync();
+                goff = g0 - rf * len;
+            } else if (task.nrows < 0) {   // block-row piece: all 4 waves of this block are here
                 float vmin = INFINITY, vmax = -INFINITY;
                 if (T.vec4) {
                     for (int j = lane; j < (task.n >> 2); j += kWave) {
@@ -503,9 +574,11 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                 block_lds_sync();   // the slots are rewritten by the next task
             }
             if (T.vec4)
-                compute_task<MAXROWS, true, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
+                compute_task<MAXROWS, true, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx,
+                                                       goff);
             else
-                compute_task<MAXROWS, false, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx);
+                compute_task<MAXROWS, false, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx,
+                                                        goff);
             if constexpr (TL) {
                 if (lane == 0 && t < g_timeline_cap) {
                     uint32_t hw;
@@ -610,6 +683,16 @@ static int piece_len(int khw, bool vec4, int chunk, bool packed = false) {
 // _SHUFFLE / _BLOCKS_PER_CU) are read only by the diagnostics library
 // (libdfq_diag.so, -DDFQ_DIAGNOSTICS); the product library runs the measured
 // defaults whatever the environment says.
+
+// DFQ_SWEEP_GROUP_ROWS=1 (diagnostics): per-channel rows of kChunk/2 .. 4 kChunk
+// elements as row groups instead of whole-row tasks / block-row pieces.  Bit-exact
+// and neutral (-1.4 .. +1.4 % on the five replicated configs interleaved on one box,
+// profiles/r02/ab_group_rows.json: task fill is not what limits the 3x3 families),
+// so the product keeps the simpler tasks.
+static bool group_rows_enabled() {
+    const char* e = ab_env("DFQ_SWEEP_GROUP_ROWS");
+    return e && e[0] == '1';
+}
 
 // DFQ_SWEEP_BLOCKROW=0: long rows through the reduce launch instead (a supported
 // alternative schedule, parity-tested against the default).
@@ -716,6 +799,44 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
         if (plen <= 0) return DFQ_ERR_UNSUPPORTED;   // khw > kChunk
         const bool given = (d.flags & DFQ_GIVEN_RANGE) != 0;
         const int64_t blen = channel ? d.row_len : total;   // the range's extent
+        // Row groups (per-channel rows of kChunk/2 .. 4 kChunk elements): R whole rows
+        // split into 4 balanced pieces, one per wave of a block, the rows' ranges
+        // combined through LDS -- tasks hold ~R len / 4 elements instead of one row
+        // (1,152-element 3x3 rows: 56 % of a task) or half a row.
+        int64_t grp_rows = 0, grp_unit = 0;
+        if (channel && use_blockrow && !V.prefetch && !given && d.row_len > kChunk / 2 &&
+            d.row_len <= (int64_t)kWavesPerBlock * kChunk && group_rows_enabled()) {
+            grp_unit = T.vec4 ? std::lcm<int64_t>(4, d.khw) : (packed ? std::lcm<int64_t>(2, d.khw) : d.khw);
+            for (int64_t R = std::min<int64_t>(kGroupMaxRows, (int64_t)kWavesPerBlock * kChunk / d.row_len); R >= 1;
+                 --R) {
+                const int64_t piece = ceil_div(ceil_div(R * d.row_len, grp_unit), (int64_t)kWavesPerBlock) * grp_unit;
+                if (piece <= kChunk) {
+                    grp_rows = R;
+                    break;
+                }
+            }
+            // whole-row tasks already fill >= 85 % of a task: keep them
+            if (grp_rows > 0 && d.row_len <= kChunk && (kChunk / d.row_len) * d.row_len * 100 >= 85 * kChunk)
+                grp_rows = 0;
+        }
+        if (grp_rows > 0) {
+            for (int64_t r0 = 0; r0 < d.rows; r0 += grp_rows) {
+                const int64_t R = std::min<int64_t>(grp_rows, d.rows - r0);
+                const int64_t tot = R * d.row_len;
+                const int64_t piece = ceil_div(ceil_div(tot, grp_unit), (int64_t)kWavesPerBlock) * grp_unit;
+                for (int i = 0; i < kWavesPerBlock; ++i) {
+                    const int64_t off = std::min<int64_t>((int64_t)i * piece, tot);
+                    DevTask k{};
+                    k.tensor = ti; k.slot = -1; k.first = 0;
+                    k.nrows = kGroupTag - (int32_t)(R - 1);
+                    k.row0 = (int32_t)r0;
+                    k.elem_start = r0 * d.row_len + off;
+                    k.n = (int32_t)std::min<int64_t>(piece, tot - off);
+                    B.blockrow.push_back(k);
+                }
+            }
+            continue;
+        }
         const bool block_row = use_blockrow && !V.prefetch && !given && blen <= (int64_t)kWavesPerBlock * plen &&
                                (!channel || d.row_len > kChunk);
         if (block_row) {

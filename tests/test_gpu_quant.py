@@ -507,3 +507,35 @@ def test_slab_pipeline_equals_two_passes(monkeypatch):
     assert outs[0][0] == 2 and outs[1][0] > 2
     for a, b in zip(outs[0][1], outs[1][1]):
         assert torch.equal(a.dst, b.dst) and torch.equal(a.codes, b.codes) and torch.equal(a.scale, b.scale)
+
+
+@pytest.mark.parametrize("pack", [False, True])
+def test_row_groups_equal_default_tasks(pack, monkeypatch):
+    """Row groups (diagnostics library, DFQ_SWEEP_GROUP_ROWS=1: R whole rows of
+    1,025-8,192 elements split over the 4 waves of a block, row ranges combined
+    through LDS) give the same bytes as the product's whole-row tasks and
+    block-row pieces, including the KH*KW error sums and packed INT4 codes."""
+    from data_free_quantization_amd import _lib
+    from data_free_quantization_amd.sweep import allocate, SweepPlan, khw_of
+    rng = np.random.default_rng(41)
+    shapes = [(37, 128, 3, 3), (21, 256, 3, 3), (9, 320, 3, 3), (40, 1280), (13, 1100), (5, 512, 3, 3), (7, 2048)]
+    xs = [rng.normal(0, 1, s).astype(np.float32) for s in shapes]
+    outs = []
+    for lib in ("product", "groups"):
+        if lib == "groups":
+            monkeypatch.setattr(_lib, "_LIB", _lib.load_diag())
+            monkeypatch.setenv("DFQ_SWEEP_GROUP_ROWS", "1")
+        items = []
+        for x in xs:
+            t = torch.from_numpy(x).to(DEV)
+            items.append(allocate(t, bits=4 if pack else 8, per_channel=True, symmetric=not pack, khw=khw_of(t),
+                                  want_esum=True, clip=(-1.5, 1.5), pack_int4=pack))
+        plan = SweepPlan(items)
+        plan.execute()
+        torch.cuda.synchronize()
+        outs.append((plan.stats["n_tasks_main"], items))
+        plan.destroy()
+    assert outs[0][0] != outs[1][0]   # the group layout really was used
+    for a, b in zip(outs[0][1], outs[1][1]):
+        for f in ("dst", "codes", "scale", "zero", "esum"):
+            assert torch.equal(getattr(a, f), getattr(b, f)), f
