@@ -23,7 +23,7 @@ DFQ_OK, DFQ_ERR_INVALID, DFQ_ERR_HIP, DFQ_ERR_UNSUPPORTED = 0, -1, -2, -3
 DFQ_ERR_NOMEM, DFQ_ERR_SHAPE, DFQ_ERR_WORKSPACE = -4, -5, -6
 
 EXPORTS = [
-    "dfq_abi_version", "dfq_error_string", "dfq_last_hip_error",
+    "dfq_abi_version", "dfq_preload", "dfq_error_string", "dfq_last_hip_error",
     "dfq_quantize_ws_bytes", "dfq_quantize_tensor", "dfq_chunk_range", "dfq_range", "dfq_fake_quant_given",
     "dfq_sweep_plan_create", "dfq_sweep_plan_ws_bytes", "dfq_sweep_plan_create_ws", "dfq_sweep_plan_execute",
     "dfq_sweep_plan_stats", "dfq_sweep_plan_destroy",
@@ -60,7 +60,7 @@ class BnFoldDesc(C.Structure):
     _fields_ = [
         ("w", C.c_void_p), ("bias", C.c_void_p), ("bn_w", C.c_void_p), ("bn_b", C.c_void_p),
         ("bn_mean", C.c_void_p), ("bn_var", C.c_void_p), ("fake_w", C.c_void_p), ("fake_b", C.c_void_p),
-        ("eps", C.c_float), ("reserved", C.c_int32), ("rows", C.c_int64), ("row_len", C.c_int64),
+        ("eps", C.c_float), ("flags", C.c_int32), ("rows", C.c_int64), ("row_len", C.c_int64),
     ]
 
 
@@ -86,7 +86,8 @@ class BcOp(C.Structure):
     ]
 
 
-DFQ_BC_OP_EXPECT, DFQ_BC_OP_APPLY, DFQ_BC_OP_PROPAGATE = 0, 1, 2
+DFQ_BC_OP_EXPECT, DFQ_BC_OP_APPLY, DFQ_BC_OP_PROPAGATE, DFQ_BC_OP_COPY = 0, 1, 2, 3
+DFQ_BN_FOLD_ZERO_BIAS = 1
 
 _LIB: Optional[C.CDLL] = None
 
@@ -114,6 +115,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
     P, I32, I64, F32, F64, SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double, C.c_size_t
     sig = {
         "dfq_abi_version": ([], C.c_int),
+        "dfq_preload": ([], C.c_int),
         "dfq_error_string": ([C.c_int], C.c_char_p),
         "dfq_last_hip_error": ([], C.c_char_p),
         "dfq_quantize_ws_bytes": ([C.POINTER(TensorDesc), C.POINTER(SZ)], C.c_int),
@@ -174,6 +176,20 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         raise DFQLibraryError("libdfq_hip.so ABI version mismatch")
     if path is None:
         _LIB = L
+    return L
+
+
+_PRELOADED = False
+
+
+def preload() -> C.CDLL:
+    """Load the library and every kernel's code object on the current device
+    (dfq_preload) so the first DFQ stage does not pay for it.  Needs a GPU."""
+    global _PRELOADED
+    L = load()
+    if not _PRELOADED:
+        check(L.dfq_preload(), "dfq_preload")
+        _PRELOADED = True
     return L
 
 

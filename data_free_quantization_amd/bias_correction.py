@@ -152,14 +152,17 @@ def _error_sums(weight, bits, signed, precomputed=None):
     return r.esum.view(o, i2), o, i2
 
 
-def _snapshot(tensors):
-    """{name: t.clone()} as views of ONE buffer filled by one concatenation."""
+def _snapshot(chain, tensors):
+    """{name: t.clone()} as views of ONE buffer, filled by COPY ops recorded in the
+    chain (bias_correction.py:196,255 clone each bias), so the copies run in walk
+    order with the rest of the chain's work."""
     if not tensors:
         return {}
     vals = list(tensors.values())
-    flat = torch.cat([t.reshape(-1) for t in vals])
+    flat = torch.empty(sum(t.numel() for t in vals), dtype=torch.float32, device=vals[0].device)
     out, off = {}, 0
     for name, t in tensors.items():
+        chain.copy(t, flat, off)
         out[name] = flat[off:off + t.numel()].view(t.shape)
         off += t.numel()
     return out
@@ -213,6 +216,12 @@ class _BcChain:
         _lib.require_device(fake_b)
         self.keep.append(fake_b)
         self.ops.append((_lib.DFQ_BC_OP_PROPAGATE, _lib.REF_THREADS, vec, None, (fake_b, 0), None, numel, 0, f))
+
+    def copy(self, src, dst, off):
+        _lib.require_device(src, dst)
+        assert src.dtype == torch.float32 and src.is_contiguous()
+        self.keep += [src, dst]
+        self.ops.append((_lib.DFQ_BC_OP_COPY, 0, (src, 0), None, (dst, off), None, src.numel(), 0, 0))
 
     def flush(self, stream):
         if not self.ops:
@@ -295,9 +304,10 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
         # The walk only writes the bias of the layer it is on, after recording it, so
         # every "before" value is the bias at entry: one batched copy instead of a
         # clone per layer (and likewise for "after", at the end).
-        before = _snapshot({f"layer_{i}": l.bias.data for i, l in enumerate(graph.values())
-                            if i in bottoms and isinstance(l, targ_type) and getattr(l, "bias", None) is not None})
-        chain = _BcChain(next(iter(before.values())).device if before else torch.device("cuda"))
+        biases = {f"layer_{i}": l.bias.data for i, l in enumerate(graph.values())
+                  if i in bottoms and isinstance(l, targ_type) and getattr(l, "bias", None) is not None}
+        chain = _BcChain(next(iter(biases.values())).device if biases else torch.device("cuda"))
+        before = _snapshot(chain, biases)
         stream = None
         try:
             for idx_layer, layer in enumerate(graph.values()):
@@ -346,9 +356,9 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                     bias_prev = bias
                     if getattr(layer, "bias", None) is not None:
                         after_src[layer_name] = layer.bias.data
+            after = _snapshot(chain, after_src)
         finally:   # the ops recorded before an error still take effect, as in the reference
             if chain.ops:
-                chain.flush(stream)
-        after = _snapshot(after_src)
+                chain.flush(stream if stream is not None else _lib.stream_of(next(iter(biases.values()))))
     logger.info("Bias correction completed.")
     return before, after

@@ -1700,6 +1700,14 @@ static CleDeviceCtx& cle_device_ctx(int dev) {
     static CleDeviceCtx ctx[64];
     return ctx[dev & 63];
 }
+// The loop stream and the pinned state word (caller holds ctx.mu).  Creating a
+// stream can take milliseconds the first time, so dfq_preload does it up front.
+static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
+    hipError_t e = hipSuccess;
+    if (!ctx.st) e = hipStreamCreateWithFlags(&ctx.st, hipStreamNonBlocking);
+    if (e == hipSuccess && !ctx.h_state) e = hipHostMalloc(&ctx.h_state, sizeof(CleState));
+    return e;
+}
 
 static void cle_plan_free(dfq_cle_plan* p) {
     const double t0 = now_us();
@@ -2087,13 +2095,16 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     if (!p || max_iters < 0) return DFQ_ERR_INVALID;
     // The loop runs on the plan's own stream (graph capture needs a non-default
     // stream): wait for the caller's producers first; the call is blocking.
+    const double ts0 = now_us();
     DFQ_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    const double ts1 = now_us();
     int dev = 0;
     DFQ_HIP_CHECK(hipGetDevice(&dev));
     CleDeviceCtx& ctx = cle_device_ctx(dev);
     std::lock_guard<std::mutex> lock(ctx.mu);
-    if (!ctx.st) DFQ_HIP_CHECK(hipStreamCreateWithFlags(&ctx.st, hipStreamNonBlocking));
-    if (!ctx.h_state) DFQ_HIP_CHECK(hipHostMalloc(&ctx.h_state, sizeof(CleState)));
+    DFQ_HIP_CHECK(cle_ctx_ready(ctx));
+    if (cle_timing()) fprintf(stderr, "DFQ_CLE_TIMING run: caller sync %.1f us, context %.1f us\n", ts1 - ts0,
+                              now_us() - ts1);
     if (p->st && p->st != ctx.st && p->gexec) {   // captured on another device's stream: recapture
         (void)hipGraphExecDestroy(p->gexec);
         p->gexec = nullptr;
@@ -2275,3 +2286,20 @@ extern "C" int dfq_probe_grid_barrier(int32_t nbar, int32_t blocks_per_cu, int32
     return DFQ_OK;
 }
 #endif
+
+namespace dfq {
+hipError_t preload_cle() {   // see dfq_preload
+    int dev = 0;
+    hipError_t e0 = hipGetDevice(&dev);
+    if (e0 != hipSuccess) return e0;
+    {
+        CleDeviceCtx& ctx = cle_device_ctx(dev);
+        std::lock_guard<std::mutex> lock(ctx.mu);
+        if ((e0 = cle_ctx_ready(ctx)) != hipSuccess) return e0;
+    }
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_apply_kernel));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_tiles_fin_kernel));
+    return e;
+}
+}  // namespace dfq

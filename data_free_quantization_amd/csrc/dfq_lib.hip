@@ -86,6 +86,19 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
 }
 }  // namespace dfq
 
+namespace dfq {
+hipError_t preload_sweep();
+hipError_t preload_transform();
+hipError_t preload_cle();
+}  // namespace dfq
+
+extern "C" int dfq_preload(void) {
+    DFQ_HIP_CHECK(dfq::preload_sweep());
+    DFQ_HIP_CHECK(dfq::preload_transform());
+    DFQ_HIP_CHECK(dfq::preload_cle());
+    return DFQ_OK;
+}
+
 extern "C" int dfq_abi_version(void) { return DFQ_ABI_VERSION; }
 
 extern "C" const char* dfq_last_hip_error(void) { return dfq::g_last_hip; }

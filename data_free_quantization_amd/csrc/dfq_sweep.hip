@@ -1283,3 +1283,14 @@ extern "C" int dfq_debug_timeline(void* buf, int64_t cap) {
     return DFQ_OK;
 }
 #endif  // DFQ_DIAGNOSTICS
+
+// Code-object loading at library initialisation (dfq_preload): the first launch of
+// a kernel otherwise pays for loading its translation unit's code object.
+namespace dfq {
+hipError_t preload_sweep() {
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(main_kernel(kDefaultVariant)));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(sweep_reduce_kernel));
+    return e;
+}
+}  // namespace dfq

@@ -297,7 +297,7 @@ struct BnFoldJob {
     float* fake_w;
     float* fake_b;
     float eps;
-    int32_t pad;
+    int32_t flags;    // DFQ_BN_FOLD_ZERO_BIAS
     int64_t rows, row_len;
 };
 struct BnFoldChunk {
@@ -327,7 +327,9 @@ __global__ void bn_fold_channel_batch_kernel(const BnFoldJob* __restrict__ jobs,
             const float go = J.g[o], bo = J.b[o], mo = J.m[o], vo = J.v[o];
             const float f = bn_factor(go, vo, J.eps);
             const float shift = bo - (go * mo) / sqrtf(vo + J.eps);
-            J.bias[o] = J.bias[o] * f + shift;
+            // a layer without a bias gets torch.zeros first (layer_transform.py:262-263)
+            const float b0 = (J.flags & DFQ_BN_FOLD_ZERO_BIAS) ? 0.0f : J.bias[o];
+            J.bias[o] = b0 * f + shift;
             if (J.fake_w) J.fake_w[o] = fabsf(go);
             if (J.fake_b) J.fake_b[o] = bo;
             J.g[o] = 1.0f;
@@ -728,6 +730,24 @@ extern "C" int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fak
     return DFQ_OK;
 }
 
+// Up to kCopyBatch consecutive DFQ_BC_OP_COPY ops of a chain in one launch: the
+// batch rides in the kernel arguments, blockIdx.y picks the copy.
+constexpr int kCopyBatch = 64;   // 1.5 KB of kernel arguments
+struct CopyBatch {
+    const float* src[kCopyBatch];
+    float*       dst[kCopyBatch];
+    int64_t      n[kCopyBatch];
+};
+
+__global__ void __launch_bounds__(256) copy_batch_kernel(CopyBatch b) {
+    const int k = blockIdx.y;
+    const float* __restrict__ src = b.src[k];
+    float* __restrict__ dst = b.dst[k];
+    const int64_t n = b.n[k];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed_op, void* stream) {
     if (failed_op) *failed_op = -1;
     if (n_ops < 0 || (n_ops > 0 && !ops)) return DFQ_ERR_INVALID;
@@ -753,6 +773,9 @@ extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed
                 if (!op.a || !op.out || op.n <= 0 || op.f <= 0 || op.flag < 1) return fail(k, DFQ_ERR_INVALID);
                 if (op.n % op.f != 0) return fail(k, DFQ_ERR_SHAPE);
                 break;
+            case DFQ_BC_OP_COPY:
+                if (!op.a || !op.out || op.n < 0) return fail(k, DFQ_ERR_INVALID);
+                break;
             default:
                 return fail(k, DFQ_ERR_INVALID);
         }
@@ -760,6 +783,31 @@ extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed
     for (int32_t k = 0; k < n_ops; ++k) {
         const dfq_bc_op& op = ops[k];
         int rc = DFQ_OK;
+        if (op.kind == DFQ_BC_OP_COPY) {   // this copy and the ones right after it: one launch
+            CopyBatch b{};
+            int cnt = 0;
+            int64_t most = 0;
+            int32_t j = k;
+            for (; j < n_ops && ops[j].kind == DFQ_BC_OP_COPY && cnt < kCopyBatch; ++j) {
+                if (ops[j].n == 0) continue;
+                b.src[cnt] = ops[j].a;
+                b.dst[cnt] = ops[j].out;
+                b.n[cnt] = ops[j].n;
+                most = std::max(most, ops[j].n);
+                ++cnt;
+            }
+            if (cnt > 0) {
+                hipLaunchKernelGGL(copy_batch_kernel, dim3(blocks_for(most), cnt), dim3(256), 0,
+                                   static_cast<hipStream_t>(stream), b);
+                const hipError_t e = hipGetLastError();
+                if (e != hipSuccess) {
+                    dfq::set_last_hip_error(e);
+                    return fail(k, DFQ_ERR_HIP);
+                }
+            }
+            k = j - 1;
+            continue;
+        }
         if (op.kind == DFQ_BC_OP_EXPECT)
             rc = dfq_bc_expect(op.a, op.b, op.n, op.flag & 1, (op.flag >> 1) & 1, op.out, stream);
         else if (op.kind == DFQ_BC_OP_APPLY)
@@ -809,7 +857,7 @@ static int bn_fold_tables(const dfq_bn_fold_desc* d, int32_t n, std::vector<BnFo
             return DFQ_ERR_INVALID;
         for (int32_t k = 0; k < j; ++k)   // each weight folded once per call (sequential semantics otherwise)
             if (d[k].w == x.w) return DFQ_ERR_INVALID;
-        jobs[j] = BnFoldJob{x.w, x.bias, x.bn_w, x.bn_b, x.bn_mean, x.bn_var, x.fake_w, x.fake_b, x.eps, 0, x.rows,
+        jobs[j] = BnFoldJob{x.w, x.bias, x.bn_w, x.bn_b, x.bn_mean, x.bn_var, x.fake_w, x.fake_b, x.eps, x.flags, x.rows,
                             x.row_len};
         const int64_t ne = x.rows * x.row_len;
         for (int64_t e = 0; e < ne; e += 8192) chunks.push_back(BnFoldChunk{j, 0, e, std::min<int64_t>(e + 8192, ne)});
@@ -913,3 +961,12 @@ extern "C" int dfq_fake_quant_given(const float* x, float* y, int64_t n, int32_t
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }
+
+namespace dfq {
+hipError_t preload_transform() {   // see dfq_preload
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(bn_fold_weight_batch_kernel));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(absorb_batch_gemv_kernel));
+    return e;
+}
+}  // namespace dfq

@@ -68,7 +68,7 @@ def _carve(total_sizes, fill_zero, device):
 
 # dfq_bn_fold_desc as a numpy record (same layout as _lib.BnFoldDesc): the table
 # of a model's folds is filled column-wise instead of field by field
-_BN_DESC = np.dtype([("ptr", "<u8", (8,)), ("eps", "<f4"), ("reserved", "<i4"), ("rows", "<i8"),
+_BN_DESC = np.dtype([("ptr", "<u8", (8,)), ("eps", "<f4"), ("flags", "<i4"), ("rows", "<i8"),
                      ("row_len", "<i8")])
 assert _BN_DESC.itemsize == C.sizeof(_lib.BnFoldDesc)
 
@@ -78,9 +78,12 @@ def _fold_batch(pairs):
         dev = pairs[0][1].weight.device
         for bn, layer in pairs:
             _lib.require_device(layer.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var)
+        # :262-263 give a bias-less layer torch.zeros; here the fold reads such a
+        # bias as 0 (DFQ_BN_FOLD_ZERO_BIAS) and writes every element of it
         need_bias = [layer for _, layer in pairs if layer.bias is None]
-        for layer, z in zip(need_bias, _carve([l.weight.size(0) for l in need_bias], True, dev)):   # :262-263
+        for layer, z in zip(need_bias, _carve([l.weight.size(0) for l in need_bias], False, dev)):
             layer.bias = nn.Parameter(z, requires_grad=False)
+        fresh = {id(layer) for layer in need_bias}
         nc = [bn.weight.numel() for bn, _ in pairs]
         fakes = _carve(nc * 2, False, dev)
         n = len(pairs)
@@ -94,6 +97,7 @@ def _fold_batch(pairs):
             ptrs[j] = (w.data_ptr(), layer.bias.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(),
                        bn.running_mean.data_ptr(), bn.running_var.data_ptr(), fw.data_ptr(), fb.data_ptr())
         tab["eps"] = [float(bn.eps) for bn, _ in pairs]
+        tab["flags"] = [_lib.DFQ_BN_FOLD_ZERO_BIAS if id(layer) in fresh else 0 for _, layer in pairs]
         tab["rows"] = [layer.weight.size(0) for _, layer in pairs]
         tab["row_len"] = [layer.weight.numel() // layer.weight.size(0) for _, layer in pairs]
         descs = tab.ctypes.data_as(C.POINTER(_lib.BnFoldDesc))
@@ -426,6 +430,38 @@ def _through_layer(vec, layer_type, layer):
     return out
 
 
+class _RangeWrites:
+    """The walk's ``running_min/max.fill_(v)`` calls, kept on the host and written
+    at the end in one H2D copy plus one ``dfq_bc_chain`` COPY launch per 64
+    buffers (instead of a torch fill kernel per buffer).  Last write wins, as with
+    sequential fills; ``flush`` runs in a ``finally``, so the writes made before an
+    error take effect, as in the reference."""
+
+    def __init__(self):
+        self.dst = {}
+
+    def fill(self, buf, value):
+        if buf.numel() != 1 or buf.dtype != torch.float32 or not buf.is_cuda:
+            buf.fill_(value)   # not a QuantMeasure scalar: the plain op
+            return
+        self.dst[buf.data_ptr()] = (buf, float(value))
+
+    def flush(self):
+        if not self.dst:
+            return
+        bufs = [b for b, _ in self.dst.values()]
+        dev = bufs[0].device
+        src = torch.tensor([v for _, v in self.dst.values()], dtype=torch.float32).to(dev)
+        ops = (_lib.BcOp * len(bufs))()
+        for k, b in enumerate(bufs):
+            ops[k].kind, ops[k].a, ops[k].out, ops[k].n = _lib.DFQ_BC_OP_COPY, src.data_ptr() + 4 * k, b.data_ptr(), 1
+        failed = C.c_int32(-1)
+        rc = _lib.load().dfq_bc_chain(ops, len(bufs), C.byref(failed), _lib.stream_of(src))
+        _lib.check(rc, f"dfq_bc_chain (range write {failed.value})", RuntimeError)
+        src.record_stream(torch.cuda.current_stream(dev))
+        self.dst.clear()
+
+
 def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchNorm2d, N=6, verbose=True):
     """Set every QuantMeasure's running_min / running_max from the statistics of
     the BatchNorms feeding it (utils/layer_transform.py:356-618): 1-to-1, 1-to-many
@@ -448,127 +484,131 @@ def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchN
         return 1 if use_relu == "relu" else 2 if use_relu == "relu6" else 0
 
     bn_module, relu_attached = {}, {}
-    for idx_layer in graph:
-        bot = bottoms[idx_layer]
-        if bot is None:
-            continue
-        node = graph[idx_layer]
-        if type(node) == bn_type:
-            bn_module[idx_layer] = node
-            relu_attached[idx_layer] = "none"
-            continue
-        if type(node) == torch.nn.ReLU:
-            relu_attached[bot[0]] = "relu"
-        elif type(node) == torch.nn.ReLU6:
-            relu_attached[bot[0]] = "relu6"
-        quant_module = get_quant_module(node, idx_layer)
-        if len(bot) == 1 and bot[0] == "Data":
-            if is_detection:
-                quant_module[0].running_max.fill_(1)
-                quant_module[0].running_min.fill_(-1)
-            else:   # (1 - mean) / std and (0 - mean) / std of the data preprocessing
-                quant_module[0].running_max.fill_(2.64)
-                quant_module[0].running_min.fill_(-2.11790393)
-        elif quant_module is not None:
-            bn_list, relu_attach_list, connect_type_list, targ_without_bn = find_prev_bn(
-                bn_module, relu_attached, graph, bottoms, bot[:])
-            if len(quant_module) == len(bn_list):   # 1 to 1
-                for idx in range(len(bn_list)):
-                    bias = getattr(bn_list[idx][0], "fake_bias").view(-1)
-                    weight = getattr(bn_list[idx][0], "fake_weight").view(-1)
-                    if bn_list[idx][1][0] in targ_without_bn:   # case (d.)
-                        CASE_D.append(quant_module[idx])
-                        layer_type, obj_layer = targ_without_bn[bn_list[idx][1][0]]
-                        bias = _through_layer(bias, layer_type, obj_layer)
-                        weight = _through_layer(weight, layer_type, obj_layer)
-                        value_max = _get_max_value(bias, weight, N)
-                        value_min = _get_min_value(bias, weight, N)
-                    else:
-                        lo, hi = _minmax(bias, weight, N)
-                        value_min = max(0., lo) if "relu" in relu_attach_list[idx] else lo
-                        value_max = min(6., hi) if "relu6" in relu_attach_list[idx] else hi
-                    quant_module[idx].running_max.fill_(value_max)
-                    quant_module[idx].running_min.fill_(value_min)
-            else:   # 1 to many or many to many
-                bn_branch = {}
-                for idx, tmp in enumerate(bn_list):
-                    _, bid = tmp
-                    bn_branch.setdefault(bid[0], []).append((tmp, relu_attach_list[idx], connect_type_list[idx]))
-                bn_res = {}
-                for key in bn_branch:
-                    tmp_list = sorted(bn_branch[key], key=lambda x: len(x[0][1]), reverse=True)
-                    node_cur, use_relu, connect_type = tmp_list[0]
-                    layer_cur, bid = node_cur
-                    depth = len(bid)
-                    tmp_list.pop(0)
-                    bias = layer_cur.fake_bias.detach().clone()
-                    weight = layer_cur.fake_weight.detach().clone()
-                    mean = var = None
-                    value_min = value_max = None
-                    if "add" in connect_type:
-                        mean, var = _moments(weight, bias, kind_of(use_relu))
-                    else:
-                        lo, hi = _minmax(bias, weight, N)
-                        value_min = max(0., lo) if "relu" in use_relu else lo
-                        value_max = min(6., hi) if "relu6" in use_relu else hi
-                    while len(tmp_list) > 0:
-                        idx_bound = 0
-                        while idx_bound < len(tmp_list) and len(tmp_list[idx_bound][0][1]) == depth:
-                            idx_bound += 1
-                        if idx_bound == 0 and len(tmp_list) > 0:   # cut depth
-                            depth = len(tmp_list[idx_bound][0][1])
+    writes = _RangeWrites()
+    try:
+        for idx_layer in graph:
+            bot = bottoms[idx_layer]
+            if bot is None:
+                continue
+            node = graph[idx_layer]
+            if type(node) == bn_type:
+                bn_module[idx_layer] = node
+                relu_attached[idx_layer] = "none"
+                continue
+            if type(node) == torch.nn.ReLU:
+                relu_attached[bot[0]] = "relu"
+            elif type(node) == torch.nn.ReLU6:
+                relu_attached[bot[0]] = "relu6"
+            quant_module = get_quant_module(node, idx_layer)
+            if len(bot) == 1 and bot[0] == "Data":
+                if is_detection:
+                    writes.fill(quant_module[0].running_max, 1)
+                    writes.fill(quant_module[0].running_min, -1)
+                else:   # (1 - mean) / std and (0 - mean) / std of the data preprocessing
+                    writes.fill(quant_module[0].running_max, 2.64)
+                    writes.fill(quant_module[0].running_min, -2.11790393)
+            elif quant_module is not None:
+                bn_list, relu_attach_list, connect_type_list, targ_without_bn = find_prev_bn(
+                    bn_module, relu_attached, graph, bottoms, bot[:])
+                if len(quant_module) == len(bn_list):   # 1 to 1
+                    for idx in range(len(bn_list)):
+                        bias = getattr(bn_list[idx][0], "fake_bias").view(-1)
+                        weight = getattr(bn_list[idx][0], "fake_weight").view(-1)
+                        if bn_list[idx][1][0] in targ_without_bn:   # case (d.)
+                            CASE_D.append(quant_module[idx])
+                            layer_type, obj_layer = targ_without_bn[bn_list[idx][1][0]]
+                            bias = _through_layer(bias, layer_type, obj_layer)
+                            weight = _through_layer(weight, layer_type, obj_layer)
+                            value_max = _get_max_value(bias, weight, N)
+                            value_min = _get_min_value(bias, weight, N)
                         else:
-                            for idx in range(idx_bound):
-                                node_tmp, use_relu_tmp, connect_type = tmp_list[idx]
-                                bias = node_tmp[0].fake_bias.detach().clone()
-                                weight = node_tmp[0].fake_weight.detach().clone()
-                                if "add" in connect_type:
-                                    _moments(weight, bias, kind_of(use_relu_tmp), into=(mean, var))
-                                    if "relu6" in connect_type:
-                                        _moments_inplace(mean, var, 2)
-                                    elif "relu" in connect_type:
-                                        _moments_inplace(mean, var, 1)
-                                else:
-                                    lo, hi = _minmax(bias, weight, N)
-                                    if "cat" == connect_type:
-                                        value_min = min(value_min, max(0., lo) if "relu" in use_relu_tmp else lo)
-                                        value_max = max(value_max, min(6., hi) if "relu6" in use_relu_tmp else hi)
+                            lo, hi = _minmax(bias, weight, N)
+                            value_min = max(0., lo) if "relu" in relu_attach_list[idx] else lo
+                            value_max = min(6., hi) if "relu6" in relu_attach_list[idx] else hi
+                        writes.fill(quant_module[idx].running_max, value_max)
+                        writes.fill(quant_module[idx].running_min, value_min)
+                else:   # 1 to many or many to many
+                    bn_branch = {}
+                    for idx, tmp in enumerate(bn_list):
+                        _, bid = tmp
+                        bn_branch.setdefault(bid[0], []).append((tmp, relu_attach_list[idx], connect_type_list[idx]))
+                    bn_res = {}
+                    for key in bn_branch:
+                        tmp_list = sorted(bn_branch[key], key=lambda x: len(x[0][1]), reverse=True)
+                        node_cur, use_relu, connect_type = tmp_list[0]
+                        layer_cur, bid = node_cur
+                        depth = len(bid)
+                        tmp_list.pop(0)
+                        bias = layer_cur.fake_bias.detach().clone()
+                        weight = layer_cur.fake_weight.detach().clone()
+                        mean = var = None
+                        value_min = value_max = None
+                        if "add" in connect_type:
+                            mean, var = _moments(weight, bias, kind_of(use_relu))
+                        else:
+                            lo, hi = _minmax(bias, weight, N)
+                            value_min = max(0., lo) if "relu" in use_relu else lo
+                            value_max = min(6., hi) if "relu6" in use_relu else hi
+                        while len(tmp_list) > 0:
+                            idx_bound = 0
+                            while idx_bound < len(tmp_list) and len(tmp_list[idx_bound][0][1]) == depth:
+                                idx_bound += 1
+                            if idx_bound == 0 and len(tmp_list) > 0:   # cut depth
+                                depth = len(tmp_list[idx_bound][0][1])
+                            else:
+                                for idx in range(idx_bound):
+                                    node_tmp, use_relu_tmp, connect_type = tmp_list[idx]
+                                    bias = node_tmp[0].fake_bias.detach().clone()
+                                    weight = node_tmp[0].fake_weight.detach().clone()
+                                    if "add" in connect_type:
+                                        _moments(weight, bias, kind_of(use_relu_tmp), into=(mean, var))
+                                        if "relu6" in connect_type:
+                                            _moments_inplace(mean, var, 2)
+                                        elif "relu" in connect_type:
+                                            _moments_inplace(mean, var, 1)
                                     else:
-                                        value_min += max(0., lo) if use_relu_tmp else lo
-                                        value_max += hi
-                            tmp_list = tmp_list[idx_bound:]
-                            if "one" == connect_type:
-                                value_min /= (idx_bound + 1)
-                                value_max /= (idx_bound + 1)
-                    if "add" in connect_type:
-                        bn_res[key] = (connect_type, mean, var)
-                    else:
-                        bn_res[key] = (connect_type, value_min, value_max)
+                                        lo, hi = _minmax(bias, weight, N)
+                                        if "cat" == connect_type:
+                                            value_min = min(value_min, max(0., lo) if "relu" in use_relu_tmp else lo)
+                                            value_max = max(value_max, min(6., hi) if "relu6" in use_relu_tmp else hi)
+                                        else:
+                                            value_min += max(0., lo) if use_relu_tmp else lo
+                                            value_max += hi
+                                tmp_list = tmp_list[idx_bound:]
+                                if "one" == connect_type:
+                                    value_min /= (idx_bound + 1)
+                                    value_max /= (idx_bound + 1)
+                        if "add" in connect_type:
+                            bn_res[key] = (connect_type, mean, var)
+                        else:
+                            bn_res[key] = (connect_type, value_min, value_max)
 
-                if len(quant_module) == 1 and len(quant_module) < len(bn_list):   # 1 to many
-                    assert len(list(bn_res.keys())) == 1, "Error occurs when setting min/max, should be 1 to many"
-                    first = list(bn_res.values())[0]
-                    if "add" in first[0]:
-                        _, mean, var = first
-                        value_min, value_max = _minmax(mean, var, N, w_is_var=True)
-                    else:
-                        _, value_min, value_max = first
-                    quant_module[0].running_max.fill_(value_max)
-                    quant_module[0].running_min.fill_(value_min)
-                elif len(quant_module) < len(bn_list):   # many to many
-                    assert len(bn_res) == len(quant_module), "LENGTH NOT EQUAL {} vs {}".format(
-                        len(bn_res), len(quant_module))
-                    for idx in range(len(bn_res)):
-                        entry = bn_res[str(idx)]
-                        if "add" in entry[0]:
-                            _, mean, var = entry
+                    if len(quant_module) == 1 and len(quant_module) < len(bn_list):   # 1 to many
+                        assert len(list(bn_res.keys())) == 1, "Error occurs when setting min/max, should be 1 to many"
+                        first = list(bn_res.values())[0]
+                        if "add" in first[0]:
+                            _, mean, var = first
                             value_min, value_max = _minmax(mean, var, N, w_is_var=True)
                         else:
-                            _, value_min, value_max = entry
-                        quant_module[idx].running_max.fill_(value_max)
-                        quant_module[idx].running_min.fill_(value_min)
-                else:
-                    assert False, "Unknown error occured while setting min/max"
+                            _, value_min, value_max = first
+                        writes.fill(quant_module[0].running_max, value_max)
+                        writes.fill(quant_module[0].running_min, value_min)
+                    elif len(quant_module) < len(bn_list):   # many to many
+                        assert len(bn_res) == len(quant_module), "LENGTH NOT EQUAL {} vs {}".format(
+                            len(bn_res), len(quant_module))
+                        for idx in range(len(bn_res)):
+                            entry = bn_res[str(idx)]
+                            if "add" in entry[0]:
+                                _, mean, var = entry
+                                value_min, value_max = _minmax(mean, var, N, w_is_var=True)
+                            else:
+                                _, value_min, value_max = entry
+                            writes.fill(quant_module[idx].running_max, value_max)
+                            writes.fill(quant_module[idx].running_min, value_min)
+                    else:
+                        assert False, "Unknown error occured while setting min/max"
+    finally:
+        writes.flush()
 
 
 _RAW_OPS = {}

@@ -28,6 +28,11 @@ extern "C" {
 
 #define DFQ_ABI_VERSION 1
 
+/* Load every kernel's code object on the current device now (otherwise the first
+ * launch from each translation unit pays for it, ~ms): the Python layer calls it
+ * once when it loads the library.  Blocking; 0 or DFQ_ERR_HIP. */
+int dfq_preload(void);
+
 /* ---- error codes ------------------------------------------------------- */
 #define DFQ_OK              0
 #define DFQ_ERR_INVALID    -1   /* bad argument (null pointer, bits out of range, ...) */
@@ -160,6 +165,7 @@ int dfq_bn_fold(float* w, float* bias, float* bn_w, float* bn_b, float* bn_mean,
 
 /* All BN folds of a model in two launches (blocking): one descriptor per
  * (BN, producer layer) pair, each weight at most once per call; eps per BN. */
+enum { DFQ_BN_FOLD_ZERO_BIAS = 1 };
 typedef struct dfq_bn_fold_desc {
     float* w;
     float* bias;
@@ -170,7 +176,8 @@ typedef struct dfq_bn_fold_desc {
     float* fake_w;      /* may be NULL */
     float* fake_b;      /* may be NULL */
     float  eps;
-    int32_t reserved;
+    int32_t flags;      /* DFQ_BN_FOLD_ZERO_BIAS: `bias` holds no value yet and is read as 0
+                         * (the zeros the reference gives a bias-less layer) */
     int64_t rows;
     int64_t row_len;
 } dfq_bn_fold_desc;
@@ -296,17 +303,19 @@ int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_
 /* dfq_bc_chain: a whole bias_correction walk's device work in one call -- the
  * ops above, recorded by the host walk in graph order and enqueued back to back
  * on `stream` (bias_correction.py:147-258 issues them one Python call each).
+ * COPY ops (the walk's before/after bias snapshots, bias_correction.py:196,255)
+ * copy n floats; consecutive ones share a launch.
  * Every op is validated before the first launch; a bad op returns its error code
  * and `*failed_op` = its index, with nothing enqueued. */
-enum { DFQ_BC_OP_EXPECT = 0, DFQ_BC_OP_APPLY = 1, DFQ_BC_OP_PROPAGATE = 2 };
+enum { DFQ_BC_OP_EXPECT = 0, DFQ_BC_OP_APPLY = 1, DFQ_BC_OP_PROPAGATE = 2, DFQ_BC_OP_COPY = 3 };
 typedef struct dfq_bc_op {
     int32_t      kind;      /* DFQ_BC_OP_* */
     int32_t      flag;      /* EXPECT: relu | (accumulate << 1); PROPAGATE: ref_threads */
-    const float* a;         /* EXPECT: fake_w  APPLY: E       PROPAGATE: bias_vec */
+    const float* a;         /* EXPECT: fake_w  APPLY: E       PROPAGATE: bias_vec  COPY: src */
     const float* b;         /* EXPECT: fake_b  APPLY: expect */
-    float*       out;       /* EXPECT: out     APPLY: bias    PROPAGATE: fake_b */
+    float*       out;       /* EXPECT: out     APPLY: bias    PROPAGATE: fake_b    COPY: dst */
     float*       out2;      /* APPLY: bias_vec (may be NULL) */
-    int64_t      n;         /* EXPECT: n       APPLY: o       PROPAGATE: numel */
+    int64_t      n;         /* EXPECT: n       APPLY: o       PROPAGATE: numel     COPY: floats */
     int64_t      i2;        /* APPLY: i2 */
     int64_t      f;         /* APPLY: expect numel  PROPAGATE: F */
 } dfq_bc_op;
