@@ -136,6 +136,91 @@ def secondary_configs(dev, stream, steps=20):
     return out
 
 
+def fold_quant_pair(dev, stream, steps=20):
+    """main_dfq's merge_batchnorm #2 + quantize_targ_layer pair (main_dfq.py:211-214)
+    in the reference's per-tensor mode, MobileNetV2 x155 (per-tensor asym INT8 +
+    clip): the second fold's BatchNorms are the identity the first fold left, so it
+    reads each weight (factor exactly 1: nothing rewritten) and leaves the
+    weight's (min, max) on the device; the quantize sweep then runs in ONE pass
+    (DFQ_DEVICE_RANGE) instead of reduce + quantize.  Algorithmic bytes: the
+    fold's read (4 B/element) + the sweep's 9 B/element (+ scale, zero)."""
+    import ctypes as C
+    import numpy as np
+    from data_free_quantization_amd import _lib
+    from data_free_quantization_amd.sweep import SweepPlan
+    from data_free_quantization_amd.utils.layer_transform import _BN_DESC
+    L = _lib.load()
+    items, _, per_copy, copies = build_batch("mobilenetv2", dev, bits=8, channel=False, sym=False, esum=False,
+                                             seed=99)
+    n = len(items)
+    rows = np.array([it.src.shape[0] for it in items], dtype=np.int64)
+    off = np.concatenate([[0], np.cumsum(rows)[:-1]]).astype(np.uint64)
+    tot = int(rows.sum())
+    ones = torch.ones(2 * tot, device=dev)           # bn weight, bn var
+    zeros = torch.zeros(3 * tot, device=dev)         # bn bias, bn mean, conv bias
+    rbuf = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+    tab = np.zeros(n, dtype=_BN_DESC)
+    p1, p0 = np.uint64(ones.data_ptr()), np.uint64(zeros.data_ptr())
+    t4 = np.uint64(4 * tot)
+    ptr = tab["ptr"]
+    ptr[:, 0] = [it.src.data_ptr() for it in items]
+    ptr[:, 1] = p0 + 2 * t4 + 4 * off                # conv bias
+    ptr[:, 2] = p1 + 4 * off                         # bn weight
+    ptr[:, 3] = p0 + 4 * off                         # bn bias
+    ptr[:, 4] = p0 + t4 + 4 * off                    # bn mean
+    ptr[:, 5] = p1 + t4 + 4 * off                    # bn var
+    tab["rows"] = rows
+    tab["row_len"] = [it.src.numel() // it.src.shape[0] for it in items]
+    tab["range_enc"] = np.uint64(rbuf.data_ptr()) + 8 * np.arange(n, dtype=np.uint64)
+    descs = tab.ctypes.data_as(C.POINTER(_lib.BnFoldDesc))
+    ws = torch.empty(max(int(L.dfq_bn_fold_ws_bytes(descs, n)), 256), dtype=torch.uint8, device=dev)
+    sp = C.c_void_p(stream.cuda_stream)
+
+    def fold():
+        _lib.check(L.dfq_bn_fold_batch(descs, n, ws.data_ptr(), ws.numel(), sp), "dfq_bn_fold_batch")
+
+    two_pass = SweepPlan(items)                      # the range from a reduce pass
+    for j, it in enumerate(items):
+        it.range_enc = rbuf[2 * j:2 * j + 2]
+    one_pass = SweepPlan(items)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / steps
+
+    def pair():
+        fold()
+        one_pass.execute(stream)
+
+    def old_pair():
+        fold()
+        two_pass.execute(stream)
+
+    ms_pair, ms_fold = timed(pair), timed(fold)
+    ms_old = timed(old_pair)
+    elems = per_copy * copies
+    algo = 4 * elems + one_pass.stats["algo_bytes"]
+    out = {"config": "mobilenetv2 bn2 fold + per-tensor asym INT8 + clip (main_dfq order, fold ranges -> "
+                     "one-pass sweep)", "copies": copies,
+           "algo_GBs": round(algo / ms_pair / 1e6, 1), "frac": round(algo / ms_pair / 1e6 / HBM_PEAK_GBS, 4),
+           "weight_GBs": round(4 * elems / ms_pair / 1e6, 1), "step_ms": round(ms_pair, 4),
+           "fold_ms": round(ms_fold, 4), "sweep_launches": one_pass.stats["launches"],
+           "with_reduce_pass_ms": round(ms_old, 4)}
+    two_pass.destroy()
+    one_pass.destroy()
+    del items, ws, ones, zeros
+    torch.cuda.empty_cache()
+    return out
+
+
 def single_model_latency(dev, stream, reps=200):
     """ONE weight set per model (cache-resident: MobileNetV2
     45 MB algorithmic), per-channel sym INT8 + codes + clip + BC sums; device
@@ -475,6 +560,8 @@ def main():
     if rank == 0:
         probe_stream, probe_lds = same_mix_probe(per_copy * copies // world, dev, stream)
         second = None if args.no_secondary else secondary_configs(dev, stream)
+        if second is not None:
+            second.append(fold_quant_pair(dev, stream))
         single = None if args.no_secondary else single_model_latency(dev, stream)
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
         pipe = None if args.no_pipeline else {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")}

@@ -18,7 +18,7 @@ PKG = Path(__file__).resolve().parent
 LIB_PATH = PKG / "libdfq_hip.so"
 
 DFQ_TENSOR_ASYM, DFQ_TENSOR_SYM, DFQ_CHANNEL_ASYM, DFQ_CHANNEL_SYM = 0, 1, 2, 3
-DFQ_CLIP, DFQ_GIVEN_RANGE, DFQ_SCALE_F32, DFQ_PACK_INT4 = 0x1, 0x2, 0x4, 0x8
+DFQ_CLIP, DFQ_GIVEN_RANGE, DFQ_SCALE_F32, DFQ_PACK_INT4, DFQ_DEVICE_RANGE = 0x1, 0x2, 0x4, 0x8, 0x10
 DFQ_OK, DFQ_ERR_INVALID, DFQ_ERR_HIP, DFQ_ERR_UNSUPPORTED = 0, -1, -2, -3
 DFQ_ERR_NOMEM, DFQ_ERR_SHAPE, DFQ_ERR_WORKSPACE = -4, -5, -6
 
@@ -45,6 +45,7 @@ class TensorDesc(C.Structure):
         ("zero", C.c_void_p), ("esum", C.c_void_p), ("rows", C.c_int64), ("row_len", C.c_int64),
         ("khw", C.c_int32), ("bits", C.c_int32), ("mode", C.c_int32), ("flags", C.c_int32),
         ("clip_lo", C.c_float), ("clip_hi", C.c_float), ("given_min", C.c_double), ("given_max", C.c_double),
+        ("range_enc", C.c_void_p),
     ]
 
 
@@ -61,6 +62,7 @@ class BnFoldDesc(C.Structure):
         ("w", C.c_void_p), ("bias", C.c_void_p), ("bn_w", C.c_void_p), ("bn_b", C.c_void_p),
         ("bn_mean", C.c_void_p), ("bn_var", C.c_void_p), ("fake_w", C.c_void_p), ("fake_b", C.c_void_p),
         ("eps", C.c_float), ("flags", C.c_int32), ("rows", C.c_int64), ("row_len", C.c_int64),
+        ("range_enc", C.c_void_p),
     ]
 
 

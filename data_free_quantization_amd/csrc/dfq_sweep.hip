@@ -93,6 +93,7 @@ struct alignas(16) DevTensor {
     int32_t vec4;      // 16-B loads / stores legal
     int32_t code_bytes;
     int32_t pad;
+    const uint32_t* range_enc;   // DFQ_DEVICE_RANGE
 };
 
 struct alignas(16) DevTask {
@@ -297,6 +298,9 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         if (task.slot >= 0) {
             mn = dec_ord(slot_min[task.slot]);
             mx = dec_ord(slot_max[task.slot]);
+        } else if (T.flags & DFQ_DEVICE_RANGE) {
+            mn = dec_ord(~T.range_enc[0]);
+            mx = dec_ord(T.range_enc[1]);
         }
         pc = make_qparams(mn, mx, T.bits, sym, T.flags, T.given_min, T.given_max);
         if (task.first && lane == 0) {
@@ -636,6 +640,9 @@ static int validate(const dfq_tensor_desc& d) {
     if (d.rows > INT32_MAX) return DFQ_ERR_UNSUPPORTED;
     const bool channel = d.mode >= DFQ_CHANNEL_ASYM;
     if (channel && (d.flags & DFQ_GIVEN_RANGE)) return DFQ_ERR_INVALID;
+    if (d.flags & DFQ_DEVICE_RANGE) {
+        if (channel || (d.flags & DFQ_GIVEN_RANGE) || !d.range_enc) return DFQ_ERR_INVALID;
+    }
     return DFQ_OK;
 }
 
@@ -659,6 +666,7 @@ static DevTensor to_dev(const dfq_tensor_desc& d) {
     t.rows = d.rows; t.row_len = d.row_len; t.khw = d.khw; t.bits = d.bits; t.mode = d.mode;
     t.flags = d.flags; t.clip_lo = d.clip_lo; t.clip_hi = d.clip_hi;
     t.given_min = d.given_min; t.given_max = d.given_max;
+    t.range_enc = (d.flags & DFQ_DEVICE_RANGE) ? d.range_enc : nullptr;
     t.inv_len = d.row_len > 0 ? 1.0f / (float)d.row_len : 0.f;
     t.code_bytes = (d.flags & DFQ_PACK_INT4) ? 0 : (d.bits <= 8 ? 1 : 2);   // 0: packed nibbles
     const int64_t n = d.rows * d.row_len;
@@ -797,7 +805,8 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
         if (total == 0) continue;
         const int plen = piece_len(d.khw, T.vec4, kChunk, packed);
         if (plen <= 0) return DFQ_ERR_UNSUPPORTED;   // khw > kChunk
-        const bool given = (d.flags & DFQ_GIVEN_RANGE) != 0;
+        // a given or device-resident range: single-pass tasks, no slot
+        const bool given = (d.flags & (DFQ_GIVEN_RANGE | DFQ_DEVICE_RANGE)) != 0;
         const int64_t blen = channel ? d.row_len : total;   // the range's extent
         // Row groups (per-channel rows of kChunk/2 .. 4 kChunk elements): R whole rows
         // split into 4 balanced pieces, one per wave of a block, the rows' ranges

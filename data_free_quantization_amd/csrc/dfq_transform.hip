@@ -299,6 +299,7 @@ struct BnFoldJob {
     float eps;
     int32_t flags;    // DFQ_BN_FOLD_ZERO_BIAS
     int64_t rows, row_len;
+    uint32_t* range_enc;
 };
 struct BnFoldChunk {
     int32_t job;
@@ -306,14 +307,107 @@ struct BnFoldChunk {
     int64_t e0, e1;   // element range of the job's weight
 };
 
-__global__ void bn_fold_weight_batch_kernel(const BnFoldJob* __restrict__ jobs, const BnFoldChunk* __restrict__ chunks,
-                                            int64_t nchunks) {
+// The fold factor of row o (bn_factor), without the divide and square root for
+// an identity BatchNorm (weight 1, var + eps == 1: the factor is exactly 1).
+__device__ __forceinline__ float fold_factor(const BnFoldJob& J, int64_t o) {
+    const float go = J.g[o], ve = J.v[o] + J.eps;
+    return (go == 1.0f && ve == 1.0f) ? 1.0f : go / sqrtf(ve);
+}
+
+// w <- w * factor(row) over one chunk; w * 1 == w, so a factor of exactly 1
+// (merge_batchnorm #2, whose BN is the identity the first fold left) rewrites
+// nothing.  Row of element i: chunk-local index times 1/row_len in fp32, exact
+// after a +-1 correction (chunk-local indices stay below 2^24).
+__device__ __forceinline__ int64_t fold_row(const BnFoldJob& J, int64_t r0, int64_t base, float inv, int64_t i,
+                                            int* rem_out) {
+    const int li = (int)(i - base);
+    const int len = (int)J.row_len;
+    int q = (int)((float)li * inv);
+    int rem = li - q * len;
+    if (rem < 0) {
+        --q;
+        rem += len;
+    } else if (rem >= len) {
+        ++q;
+        rem -= len;
+    }
+    *rem_out = rem;
+    return r0 + q;
+}
+
+__device__ __forceinline__ float fold_one(const BnFoldJob& J, int64_t r0, int64_t base, float inv, int64_t i,
+                                          float w) {
+    int rem;
+    const float f = fold_factor(J, fold_row(J, r0, base, inv, i, &rem));
+    return f != 1.0f ? w * f : w;
+}
+
+__global__ void __launch_bounds__(kThreads)
+bn_fold_weight_batch_kernel(const BnFoldJob* __restrict__ jobs, const BnFoldChunk* __restrict__ chunks,
+                            int64_t nchunks) {
+    __shared__ float smn[kThreads / kWave], smx[kThreads / kWave];
     for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
         const BnFoldChunk ch = chunks[c];
         const BnFoldJob J = jobs[ch.job];
-        for (int64_t i = ch.e0 + threadIdx.x; i < ch.e1; i += blockDim.x) {
-            const int64_t o = i / J.row_len;
-            J.w[i] = J.w[i] * bn_factor(J.g[o], J.v[o], J.eps);
+        const int64_t r0 = ch.e0 / J.row_len, base = r0 * J.row_len;
+        const float inv = 1.0f / (float)J.row_len;
+        float a = INFINITY, b = -INFINITY;
+        const int64_t n = ch.e1 - ch.e0;
+        int64_t done = 0;
+        if ((reinterpret_cast<uintptr_t>(J.w + ch.e0) & 15) == 0) {   // 16-B groups
+            float4* w4 = reinterpret_cast<float4*>(J.w + ch.e0);
+            const int64_t n4 = n >> 2;
+            for (int64_t k = threadIdx.x; k < n4; k += blockDim.x) {
+                const float4 v = w4[k];
+                const int64_t i = ch.e0 + 4 * k;
+                float4 o;
+                int rem;
+                const float f = fold_factor(J, fold_row(J, r0, base, inv, i, &rem));
+                if (rem + 3 < (int)J.row_len) {   // the 4 elements share a row: one factor
+                    o.x = f != 1.0f ? v.x * f : v.x;
+                    o.y = f != 1.0f ? v.y * f : v.y;
+                    o.z = f != 1.0f ? v.z * f : v.z;
+                    o.w = f != 1.0f ? v.w * f : v.w;
+                } else {
+                    o.x = f != 1.0f ? v.x * f : v.x;
+                    o.y = fold_one(J, r0, base, inv, i + 1, v.y);
+                    o.z = fold_one(J, r0, base, inv, i + 2, v.z);
+                    o.w = fold_one(J, r0, base, inv, i + 3, v.w);
+                }
+                if (__float_as_uint(o.x) != __float_as_uint(v.x) || __float_as_uint(o.y) != __float_as_uint(v.y) ||
+                    __float_as_uint(o.z) != __float_as_uint(v.z) || __float_as_uint(o.w) != __float_as_uint(v.w))
+                    w4[k] = o;
+                a = fminf(a, fminf(fminf(o.x, o.y), fminf(o.z, o.w)));
+                b = fmaxf(b, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
+            }
+            done = 4 * n4;
+        }
+        for (int64_t k = done + threadIdx.x; k < n; k += blockDim.x) {
+            const int64_t i = ch.e0 + k;
+            const float v = J.w[i];
+            const float o = fold_one(J, r0, base, inv, i, v);
+            if (__float_as_uint(o) != __float_as_uint(v)) J.w[i] = o;
+            a = fminf(a, o);
+            b = fmaxf(b, o);
+        }
+        if (J.range_enc) {   // the folded weight's (min, max), dfq_range's encoding
+            a = wave_min(a);
+            b = wave_max(b);
+            const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
+            if (lane == 0) {
+                smn[wv] = a;
+                smx[wv] = b;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                for (int k = 1; k < kThreads / kWave; ++k) {
+                    a = fminf(a, smn[k]);
+                    b = fmaxf(b, smx[k]);
+                }
+                atomicMax(&J.range_enc[0], ~enc_ord(a));
+                atomicMax(&J.range_enc[1], enc_ord(b));
+            }
+            __syncthreads();   // smn / smx are rewritten by the next chunk
         }
     }
 }
@@ -848,19 +942,33 @@ extern "C" int dfq_act_affine(const float* x, const float* w, const float* bias,
 }
 
 // Tables of one batched fold: the jobs, and 8192-element weight chunks.
+// Elements per chunk (one block's work): 8192, or more for batches past 2^27
+// elements so the chunk table stays small (<= ~16K chunks of 24 B).
+static int64_t bn_fold_span(const dfq_bn_fold_desc* d, int32_t n) {
+    int64_t total = 0;
+    for (int32_t j = 0; j < n; ++j) total += d[j].rows * d[j].row_len;
+    return std::min<int64_t>(std::max<int64_t>(8192, ceil_div(total, (int64_t)16384 * 8192) * 8192), 1 << 20);
+}
+
 static int bn_fold_tables(const dfq_bn_fold_desc* d, int32_t n, std::vector<BnFoldJob>& jobs,
                           std::vector<BnFoldChunk>& chunks) {
+    const int64_t span = bn_fold_span(d, n);
+    {   // each weight folded once per call (sequential semantics otherwise)
+        std::vector<const float*> ws(n);
+        for (int32_t j = 0; j < n; ++j) ws[j] = d[j].w;
+        std::sort(ws.begin(), ws.end());
+        if (std::adjacent_find(ws.begin(), ws.end()) != ws.end()) return DFQ_ERR_INVALID;
+    }
     jobs.resize(n);
     for (int32_t j = 0; j < n; ++j) {
         const dfq_bn_fold_desc& x = d[j];
         if (!x.w || !x.bias || !x.bn_w || !x.bn_b || !x.bn_mean || !x.bn_var || x.rows < 0 || x.row_len < 0)
             return DFQ_ERR_INVALID;
-        for (int32_t k = 0; k < j; ++k)   // each weight folded once per call (sequential semantics otherwise)
-            if (d[k].w == x.w) return DFQ_ERR_INVALID;
+        if (x.row_len > (int64_t(1) << 22)) return DFQ_ERR_UNSUPPORTED;   // fold_one's fp32 row map
         jobs[j] = BnFoldJob{x.w, x.bias, x.bn_w, x.bn_b, x.bn_mean, x.bn_var, x.fake_w, x.fake_b, x.eps, x.flags, x.rows,
-                            x.row_len};
+                            x.row_len, x.range_enc};
         const int64_t ne = x.rows * x.row_len;
-        for (int64_t e = 0; e < ne; e += 8192) chunks.push_back(BnFoldChunk{j, 0, e, std::min<int64_t>(e + 8192, ne)});
+        for (int64_t e = 0; e < ne; e += span) chunks.push_back(BnFoldChunk{j, 0, e, std::min<int64_t>(e + span, ne)});
     }
     return DFQ_OK;
 }
@@ -870,10 +978,10 @@ static int64_t round256(int64_t b) { return ceil_div(b, (int64_t)256) * 256; }
 extern "C" int64_t dfq_bn_fold_ws_bytes(const dfq_bn_fold_desc* d, int32_t n) {
     if (n < 0 || (n > 0 && !d)) return -1;
     int64_t nchunks = 0;
-    for (int32_t j = 0; j < n; ++j) {
+    for (int32_t j = 0; j < n; ++j)
         if (d[j].rows < 0 || d[j].row_len < 0) return -1;
-        nchunks += ceil_div(d[j].rows * d[j].row_len, (int64_t)8192);
-    }
+    const int64_t span = bn_fold_span(d, n);
+    for (int32_t j = 0; j < n; ++j) nchunks += ceil_div(d[j].rows * d[j].row_len, span);
     return round256((int64_t)sizeof(BnFoldJob) * n) + round256((int64_t)sizeof(BnFoldChunk) * nchunks);
 }
 
@@ -902,6 +1010,17 @@ extern "C" int dfq_bn_fold_batch(const dfq_bn_fold_desc* d, int32_t n, void* ws,
     if (!chunks.empty()) std::memcpy(blob.data() + jb, chunks.data(), sizeof(BnFoldChunk) * chunks.size());
     hipError_t e = own ? hipMemcpyAsync(base, blob.data(), need, hipMemcpyHostToDevice, s)
                        : stage_h2d(base, blob.data(), need, s);
+    // zero the range outputs: one memset per run of adjacent 2-word records
+    std::vector<uint32_t*> rp;
+    for (int32_t j = 0; j < n; ++j)
+        if (d[j].range_enc) rp.push_back(d[j].range_enc);
+    std::sort(rp.begin(), rp.end());
+    for (size_t k = 0; k < rp.size() && e == hipSuccess;) {
+        size_t m = k + 1;
+        while (m < rp.size() && rp[m] == rp[m - 1] + 2) ++m;
+        e = hipMemsetAsync(rp[k], 0, sizeof(uint32_t) * 2 * (m - k), s);
+        k = m;
+    }
     if (e == hipSuccess && !chunks.empty()) {
         hipLaunchKernelGGL(bn_fold_weight_batch_kernel, dim3((int)std::min<size_t>(chunks.size(), 4096)),
                            dim3(kThreads), 0, s, dj, dc, (int64_t)chunks.size());

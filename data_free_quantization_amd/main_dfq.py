@@ -188,11 +188,13 @@ def main(argv=None):
     state = {} if (args.bc_mode == "fused" or args.export) else None
     if args.quantize:
         set_layer_bits(graph, args.bits_weight, args.bits_activation, args.bits_bias, targ_layer)
-        model = merge_batchnorm(model, graph, bottoms, targ_layer)
+        sharded = args.world_size > 1
+        fold_ranges = {} if (args.granularity == "tensor" and not sharded) else None
+        model = merge_batchnorm(model, graph, bottoms, targ_layer, ranges=fold_ranges)
         fused_clip = [-15, 15] if (args.clip_weight and args.bc_mode == "fused") else None
         graph = quantize_targ_layer(graph, args.bits_weight, args.bits_bias, targ_layer,
                                     granularity=args.granularity, symmetric=args.symmetric, clip=fused_clip,
-                                    state=state, shard=args.world_size > 1)
+                                    state=state, shard=sharded, weight_ranges=fold_ranges)
         set_quant_minmax(graph, bottoms)   # main_dfq.py:217
     if args.clip_weight and not (args.quantize and args.bc_mode == "fused"):
         clip_weight(graph, range_clip=[-15, 15], targ_type=targ_layer)

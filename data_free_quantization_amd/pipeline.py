@@ -60,10 +60,12 @@ def run_dfq(model: nn.Module, graph, bottoms, targ, *, relu: bool = True, equali
     state = {} if (correction and bc_mode == "fused") else None
     if quantize:
         set_layer_bits(graph, bits_weight, bits_activation, bits_bias, targ)
-        stage("bn2", merge_batchnorm, model, graph, bottoms, targ)
+        # the second fold hands the folded weights' ranges to the quantize sweep
+        fold_ranges = {} if granularity == "tensor" else None
+        stage("bn2", merge_batchnorm, model, graph, bottoms, targ, ranges=fold_ranges)
         fused_clip = tuple(clip_range) if (clip and bc_mode == "fused") else None
         stage("quant", quantize_targ_layer, graph, bits_weight, bits_bias, targ, granularity=granularity,
-              symmetric=symmetric, clip=fused_clip, state=state)
+              symmetric=symmetric, clip=fused_clip, state=state, weight_ranges=fold_ranges)
     if clip and not (quantize and bc_mode == "fused"):
         stage("clip", clip_weight, graph, range_clip=list(clip_range), targ_type=targ)
     if correction:

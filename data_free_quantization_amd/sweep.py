@@ -31,6 +31,9 @@ class SweepItem:
     clip: Optional[Sequence[float]] = None
     rows: Optional[int] = None
     pack_int4: bool = False                  # codes as packed nibbles (bits <= 4; n/2 bytes)
+    # per-tensor modes: the (min, max) already on the device in dfq_range's encoding
+    # (2 int32 words, e.g. merge_batchnorm(ranges=...)'s by-product): one HBM pass
+    range_enc: Optional[torch.Tensor] = None
 
     def mode(self) -> int:
         if self.per_channel:
@@ -90,6 +93,12 @@ class SweepPlan:
             d.bits = it.bits
             d.mode = it.mode()
             d.flags = (_lib.DFQ_CLIP if it.clip is not None else 0) | (_lib.DFQ_PACK_INT4 if it.pack_int4 else 0)
+            if it.range_enc is not None and not it.per_channel:
+                r = it.range_enc
+                if not (r.is_cuda and r.dtype == torch.int32 and r.numel() >= 2 and r.is_contiguous()):
+                    raise TypeError("range_enc: 2 contiguous int32 words on the GPU")
+                d.flags |= _lib.DFQ_DEVICE_RANGE
+                d.range_enc = it.range_enc.data_ptr()
             if it.clip is not None:
                 d.clip_lo, d.clip_hi = float(it.clip[0]), float(it.clip[1])
         self._plan = C.c_void_p()

@@ -31,11 +31,16 @@ _CONV_TYPES = (nn.Conv2d, QConv2d, QuantConv2d, QuantNConv2d)
 _LINEAR_TYPES = (nn.Linear, QLinear, QuantLinear, QuantNLinear)
 
 
-def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d]):
+def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d], *, ranges: Optional[Dict] = None):
     """Fold each BatchNorm2d into the target layer feeding it, keep |gamma| and beta
     as ``fake_weight``/``fake_bias`` buffers, and turn the BN into an identity
     (utils/layer_transform.py:240-285).  Every fold of the model runs in one
-    ``dfq_bn_fold_batch`` call (two launches)."""
+    ``dfq_bn_fold_batch`` call (two launches).
+
+    ``ranges`` (extension): a dict that receives {layer: 2 int32 device words},
+    each folded weight's (min, max) as a by-product of the fold's read, for
+    ``quantize_targ_layer(weight_ranges=...)`` right after (main_dfq.py:211-214:
+    the second fold, whose factors are exactly 1, then only reads the weights)."""
     pairs = []
     for layer_idx in graph:
         if bottoms[layer_idx] is None:
@@ -52,9 +57,9 @@ def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d]):
     # batch call per fold then, in graph order
     if len({id(layer.weight) for _, layer in pairs}) < len(pairs):
         for pair in pairs:
-            _fold_batch([pair])
+            _fold_batch([pair], ranges)
     else:
-        _fold_batch(pairs)
+        _fold_batch(pairs, ranges)
     return model
 
 
@@ -69,11 +74,11 @@ def _carve(total_sizes, fill_zero, device):
 # dfq_bn_fold_desc as a numpy record (same layout as _lib.BnFoldDesc): the table
 # of a model's folds is filled column-wise instead of field by field
 _BN_DESC = np.dtype([("ptr", "<u8", (8,)), ("eps", "<f4"), ("flags", "<i4"), ("rows", "<i8"),
-                     ("row_len", "<i8")])
+                     ("row_len", "<i8"), ("range_enc", "<u8")])
 assert _BN_DESC.itemsize == C.sizeof(_lib.BnFoldDesc)
 
 
-def _fold_batch(pairs):
+def _fold_batch(pairs, ranges=None):
     with torch.no_grad():
         dev = pairs[0][1].weight.device
         for bn, layer in pairs:
@@ -98,6 +103,11 @@ def _fold_batch(pairs):
                        bn.running_mean.data_ptr(), bn.running_var.data_ptr(), fw.data_ptr(), fb.data_ptr())
         tab["eps"] = [float(bn.eps) for bn, _ in pairs]
         tab["flags"] = [_lib.DFQ_BN_FOLD_ZERO_BIAS if id(layer) in fresh else 0 for _, layer in pairs]
+        if ranges is not None:   # 8 bytes per fold, in one allocation (zeroed by the call)
+            rbuf = torch.empty(2 * n, dtype=torch.int32, device=dev)
+            tab["range_enc"] = rbuf.data_ptr() + 8 * np.arange(n, dtype=np.uint64)
+            for j, (_, layer) in enumerate(pairs):
+                ranges[layer] = rbuf[2 * j:2 * j + 2]
         tab["rows"] = [layer.weight.size(0) for _, layer in pairs]
         tab["row_len"] = [layer.weight.numel() // layer.weight.size(0) for _, layer in pairs]
         descs = tab.ctypes.data_as(C.POINTER(_lib.BnFoldDesc))
@@ -137,7 +147,7 @@ def _identity_forward(bn):
 
 def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, granularity="tensor",
                         symmetric=False, clip=None, state: Optional[Dict] = None, shard: bool = False,
-                        group=None):
+                        group=None, weight_ranges: Optional[Dict] = None):
     """Fake-quantize every target layer's weight (and bias when bits_bias < 32) in
     place, all layers in one grouped launch.
 
@@ -146,6 +156,11 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
     ``symmetric=True``, ``clip=(lo, hi)`` fused (the clip_weight clamp), and
     ``state`` -- a dict filled with per-layer codes/scale/zero and the BC error
     sums E[o,i] of this quantization.
+
+    ``weight_ranges`` (per-tensor modes): {layer: device range} from
+    ``merge_batchnorm(ranges=...)`` run just before, with no write to the weights in
+    between (main_dfq's order): those weights are quantized in one HBM pass
+    (DFQ_DEVICE_RANGE) instead of a reduce pass and a quantize pass.
 
     ``shard=True`` with torch.distributed initialised (main_dfq --world_size N,
     every rank holding the model): each rank sweeps its LPT share of the tensors
@@ -174,7 +189,8 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
         npar = rows
         khw = khw_of(w)
         it = SweepItem(src=w, dst=w, bits=bit_weight, per_channel=per_channel, symmetric=symmetric, clip=clip,
-                       khw=khw, rows=rows)
+                       khw=khw, rows=rows,
+                       range_enc=weight_ranges.get(layer) if (weight_ranges and not per_channel) else None)
         items.append(it)
         keys.append(layer_idx)
         if layer.bias is not None and bits_bias < 32:

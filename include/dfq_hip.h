@@ -65,6 +65,12 @@ int dfq_preload(void);
                                   above half a task (1024 elements by default) with rows > 1 is
                                   DFQ_ERR_UNSUPPORTED (two rows' tasks would share a byte) */
 
+#define DFQ_DEVICE_RANGE  0x10 /* TENSOR modes: the range is read on the device, when the sweep runs,
+                                  from range_enc = {~enc(min), enc(max)} (dfq_range's encoding, or
+                                  the by-product of dfq_bn_fold_batch): one HBM pass, no reduce
+                                  launch.  Arithmetic as for the data range (the values are the
+                                  tensor's fp32 min and max).  Not with DFQ_GIVEN_RANGE */
+
 /* One fp32 tensor viewed as [rows, row_len], row_len = I*KH*KW (KCRS) or I (Linear).
  * Outputs are written only where the pointer is non-NULL:
  *   dst    fp32 dequantized values (may alias src: in-place, like weight.data.copy_)
@@ -87,11 +93,12 @@ typedef struct dfq_tensor_desc {
     int32_t      khw;       /* spatial size for esum (1 for Linear / 1x1) */
     int32_t      bits;      /* 2..16 */
     int32_t      mode;      /* DFQ_TENSOR_ASYM ... DFQ_CHANNEL_SYM */
-    int32_t      flags;     /* DFQ_CLIP | DFQ_GIVEN_RANGE | DFQ_SCALE_F32 | DFQ_PACK_INT4 */
+    int32_t      flags;     /* DFQ_CLIP | DFQ_GIVEN_RANGE | DFQ_SCALE_F32 | DFQ_PACK_INT4 | DFQ_DEVICE_RANGE */
     float        clip_lo;
     float        clip_hi;
     double       given_min;
     double       given_max;
+    const uint32_t* range_enc; /* DFQ_DEVICE_RANGE: 2 device words, else NULL */
 } dfq_tensor_desc;
 
 /* ---- library ------------------------------------------------------------ */
@@ -180,12 +187,18 @@ typedef struct dfq_bn_fold_desc {
                          * (the zeros the reference gives a bias-less layer) */
     int64_t rows;
     int64_t row_len;
+    uint32_t* range_enc; /* may be NULL: 2 device words receiving the folded weight's (min, max) in
+                          * dfq_range's encoding (zeroed by the call), for a later sweep with
+                          * DFQ_DEVICE_RANGE.  Rows whose factor is exactly 1 (merge_batchnorm #2)
+                          * are read, not rewritten (w * 1 == w) */
 } dfq_bn_fold_desc;
 /* Device workspace bytes for dfq_bn_fold_batch's job tables (-1: bad arguments). */
 int64_t dfq_bn_fold_ws_bytes(const dfq_bn_fold_desc* descs, int32_t n);
 /* ws: >= dfq_bn_fold_ws_bytes bytes, 256-B aligned, stream-ordered with `stream`
  * (e.g. the framework's caching allocator), or NULL: private tables (a
- * hipMalloc / hipFree per call).  Blocking: the stream is synchronized. */
+ * hipMalloc / hipFree per call).  With ws the call is stream-ordered (tables go
+ * up through the library's pinned staging ring; no host wait); with NULL it
+ * synchronizes the stream before freeing its private tables. */
 int dfq_bn_fold_batch(const dfq_bn_fold_desc* descs, int32_t n, void* ws, int64_t ws_bytes, void* stream);
 
 /* ---- weight clipping (clip_weight.py:18-29): w = min(max(w, lo), hi), in place */

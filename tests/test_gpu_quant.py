@@ -293,6 +293,66 @@ def test_many_models_per_tensor():
     plan.destroy()
 
 
+@pytest.mark.parametrize("source", ["dfq_range", "bn_fold"])
+def test_device_range_single_pass(source):
+    """DFQ_DEVICE_RANGE: per-tensor sweeps taking their (min, max) from device words
+    -- written by dfq_range, or by the second BN fold (identity BN, factor exactly
+    1: weights read, not rewritten) -- are ONE launch and bit-exact with the
+    oracle's two-pass result (MobileNetV2 ×4, asym and sym, clip + E)."""
+    import ctypes as C
+    import torch.nn as nn
+    from data_free_quantization_amd import _lib, zoo
+    from data_free_quantization_amd.sweep import allocate, SweepPlan, khw_of
+    from data_free_quantization_amd.utils.layer_transform import _fold_batch
+    m = zoo.build("mobilenetv2", seed=11)
+    layers = [l.weight.detach() for l in zoo.target_layers(m)]
+    L = _lib.load()
+    for sym in (False, True):
+        mode = O.TENSOR_SYM if sym else O.TENSOR_ASYM
+        ref = [O.quantize(w.numpy(), 8, mode, rows=1, khw=khw_of(w), flags=1, clip=(-0.3, 0.3), want_esum=True)
+               for w in layers]
+        items, keep = [], []
+        for c in range(4):
+            ws = [w.to(DEV).clone().contiguous() for w in layers]
+            if source == "dfq_range":
+                rng = []
+                for w in ws:
+                    r = torch.empty(2, dtype=torch.int32, device=DEV)
+                    _lib.check(L.dfq_range(w.data_ptr(), w.numel(), r.data_ptr(), _lib.stream_of(w)), "dfq_range")
+                    rng.append(r)
+            else:   # merge_batchnorm #2: identity BatchNorms after the first fold
+                pairs = []
+                for w in ws:
+                    conv = nn.Conv2d(1, w.shape[0], 1).to(DEV)
+                    conv.weight = nn.Parameter(w, requires_grad=False)
+                    bn = nn.BatchNorm2d(w.shape[0]).to(DEV)   # weight 1, bias 0, mean 0, var 1
+                    bn.eps = 0
+                    pairs.append((bn, conv))
+                    keep.append((bn, conv))
+                before = [w.clone() for w in ws]
+                ranges = {}
+                _fold_batch(pairs, ranges)
+                torch.cuda.synchronize()
+                assert all(torch.equal(a, b) for a, b in zip(before, ws))   # factor 1: weights untouched
+                rng = [ranges[conv] for _, conv in pairs]
+            for w, r in zip(ws, rng):
+                it = allocate(w, bits=8, per_channel=False, symmetric=sym, khw=khw_of(w), want_esum=True,
+                              clip=(-0.3, 0.3))
+                it.range_enc = r
+                items.append(it)
+        plan = SweepPlan(items)
+        assert plan.stats["launches"] == 1 and plan.stats["n_tasks_reduce"] == 0
+        plan.execute()
+        torch.cuda.synchronize()
+        for i, it in enumerate(items):
+            o = ref[i % len(layers)]
+            assert np.array_equal(it.dst.cpu().numpy(), o["dq"])
+            assert np.array_equal(it.codes.cpu().numpy(), o["codes"])
+            assert np.array_equal(it.esum.cpu().numpy(), o["esum"])
+            assert np.array_equal(it.scale.cpu().numpy(), o["scale"])
+        plan.destroy()
+
+
 def _chunk_cases():
     from tests.helpers import chunk_cases
     return chunk_cases()
