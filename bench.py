@@ -57,7 +57,7 @@ def parse():
     p.add_argument("--no-pipeline", action="store_true", help="skip the one-off full-DFQ pipeline timing")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the other BASELINE configs (ResNet-50, DeepLab, INT4, per-tensor; sharded single model)")
-    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r01.json"))
+    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r02.json"))
     return p.parse_args()
 
 
