@@ -234,6 +234,20 @@ def single_model_latency(dev, stream, reps=200):
         out[model] = {"us": round(ms * 1e3, 2), "algo_GBs": round(plan.stats["algo_bytes"] / ms / 1e6, 1),
                       "launches": plan.stats["launches"]}
         plan.destroy()
+    # BASELINE.md's GPU target rows as defined there (per-channel W8 + codes + clip;
+    # E only where the row says "+ BC"), time at 60 % of 8 TB/s
+    rows = []
+    for name, model, es, target_us in (("MobileNetV2 per-channel W8", "mobilenetv2", False, 6.5),
+                                       ("ResNet-50 per-channel W8 + BC", "resnet50", True, 47.8),
+                                       ("DeepLab per-channel W8", "deeplab", False, 10.8)):
+        items, _, _, _ = build_batch(model, dev, copies=1, seed=5, esum=es)
+        plan = SweepPlan(items)
+        ms = time_plan(plan, stream, dev, reps, 20)
+        rows.append({"row": name, "us": round(ms * 1e3, 2), "target_us": target_us,
+                     "algo_MB": round(plan.stats["algo_bytes"] / 1e6, 1),
+                     "algo_GBs": round(plan.stats["algo_bytes"] / ms / 1e6, 1)})
+        plan.destroy()
+    out["baseline_md_rows"] = rows
     return out
 
 
@@ -443,6 +457,20 @@ def pipeline_timing(dev, model="mobilenetv2"):
     return out
 
 
+def pipeline_cold(model="mobilenetv2"):
+    """The first run of the stage order in a FRESH process (child process,
+    scripts/cold_pipeline.py: dfq_preload as main_dfq does, then a cold and a warm
+    run), ms per stage; None if the child fails."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, str(ROOT / "scripts" / "cold_pipeline.py"), model, "--preload"],
+                           capture_output=True, text=True, timeout=300)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        return json.loads(line)
+    except Exception:
+        return None
+
+
 def same_mix_probe(n, dev, stream, reps=10):
     """Achievable-ceiling probes with the sweep's 1x1-layer traffic mix (read 4 B,
     write 4 + 1 + 4 B per element) and no arithmetic: a grid-stride VGPR stream,
@@ -565,6 +593,8 @@ def main():
         single = None if args.no_secondary else single_model_latency(dev, stream)
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
         pipe = None if args.no_pipeline else {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")}
+        if pipe is not None:
+            pipe["cold_process_mobilenetv2"] = pipeline_cold("mobilenetv2")
         res = {
             "metric": METRIC,
             "value": round(value, 2),
