@@ -10,6 +10,7 @@ import ctypes as C
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -70,37 +71,42 @@ def allocate(src: torch.Tensor, bits=8, per_channel=True, symmetric=True, khw=1,
         khw=khw, clip=clip, rows=rows)
 
 
+_DESC = np.dtype([("src", "<u8"), ("dst", "<u8"), ("codes", "<u8"), ("scale", "<u8"), ("zero", "<u8"),
+                  ("esum", "<u8"), ("rows", "<i8"), ("row_len", "<i8"), ("khw", "<i4"), ("bits", "<i4"),
+                  ("mode", "<i4"), ("flags", "<i4"), ("clip_lo", "<f4"), ("clip_hi", "<f4"),
+                  ("given_min", "<f8"), ("given_max", "<f8"), ("range_enc", "<u8")])
+assert _DESC.itemsize == C.sizeof(_lib.TensorDesc)
+assert all(_DESC.fields[f][1] == getattr(_lib.TensorDesc, f).offset for f, _ in _lib.TensorDesc._fields_)
+
+
 class SweepPlan:
     def __init__(self, items: List[SweepItem]):
         self.items = list(items)
         L = _lib.load()
-        descs = (_lib.TensorDesc * max(len(self.items), 1))()
-        for i, it in enumerate(self.items):
+        rows_ = []
+        for it in self.items:
             _lib.require_device(it.src, it.dst, it.scale, it.zero, it.esum)
             if it.codes is not None and not it.codes.is_cuda:
                 raise RuntimeError("codes must live on the GPU")
             rows = it.rows if it.rows is not None else (it.src.shape[0] if (it.per_channel and it.src.dim()) else 1)
-            d = descs[i]
-            d.src = it.src.data_ptr()
-            d.dst = it.dst.data_ptr() if it.dst is not None else None
-            d.codes = it.codes.data_ptr() if it.codes is not None else None
-            d.scale = it.scale.data_ptr() if it.scale is not None else None
-            d.zero = it.zero.data_ptr() if it.zero is not None else None
-            d.esum = it.esum.data_ptr() if it.esum is not None else None
-            d.rows = rows
-            d.row_len = it.src.numel() // rows if rows else 0
-            d.khw = it.khw
-            d.bits = it.bits
-            d.mode = it.mode()
-            d.flags = (_lib.DFQ_CLIP if it.clip is not None else 0) | (_lib.DFQ_PACK_INT4 if it.pack_int4 else 0)
+            flags = (_lib.DFQ_CLIP if it.clip is not None else 0) | (_lib.DFQ_PACK_INT4 if it.pack_int4 else 0)
+            rng = 0
             if it.range_enc is not None and not it.per_channel:
                 r = it.range_enc
                 if not (r.is_cuda and r.dtype == torch.int32 and r.numel() >= 2 and r.is_contiguous()):
                     raise TypeError("range_enc: 2 contiguous int32 words on the GPU")
-                d.flags |= _lib.DFQ_DEVICE_RANGE
-                d.range_enc = it.range_enc.data_ptr()
-            if it.clip is not None:
-                d.clip_lo, d.clip_hi = float(it.clip[0]), float(it.clip[1])
+                flags |= _lib.DFQ_DEVICE_RANGE
+                rng = r.data_ptr()
+            clo, chi = (float(it.clip[0]), float(it.clip[1])) if it.clip is not None else (0.0, 0.0)
+            ptr = lambda t: t.data_ptr() if t is not None else 0   # noqa: E731
+            rows_.append((it.src.data_ptr(), ptr(it.dst), ptr(it.codes), ptr(it.scale), ptr(it.zero), ptr(it.esum),
+                          rows, it.src.numel() // rows if rows else 0, it.khw, it.bits, it.mode(), flags, clo, chi,
+                          0.0, 0.0, rng))
+        # the descriptor table as a numpy record array (layout of _lib.TensorDesc),
+        # filled row-wise from plain tuples instead of ctypes field by field
+        tab = np.array(rows_ if rows_ else [(0,) * 6 + (0, 0, 1, 8, 0, 0, 0.0, 0.0, 0.0, 0.0, 0)], dtype=_DESC)
+        self._tab = tab
+        descs = tab.ctypes.data_as(C.POINTER(_lib.TensorDesc))
         self._plan = C.c_void_p()
         self._device = self.items[0].src.device if self.items else None
         self._ws = None

@@ -87,7 +87,11 @@ def _fold_batch(pairs, ranges=None):
         # bias as 0 (DFQ_BN_FOLD_ZERO_BIAS) and writes every element of it
         need_bias = [layer for _, layer in pairs if layer.bias is None]
         for layer, z in zip(need_bias, _carve([l.weight.size(0) for l in need_bias], False, dev)):
-            layer.bias = nn.Parameter(z, requires_grad=False)
+            p = nn.Parameter(z, requires_grad=False)
+            if "bias" in layer._parameters:   # registered as None: what Module.__setattr__ would do
+                layer._parameters["bias"] = p
+            else:
+                layer.bias = p
         fresh = {id(layer) for layer in need_bias}
         nc = [bn.weight.numel() for bn, _ in pairs]
         fakes = _carve(nc * 2, False, dev)
@@ -119,7 +123,7 @@ def _fold_batch(pairs, ranges=None):
         rc = L.dfq_bn_fold_batch(descs, n, ws.data_ptr(), ws.numel(), _lib.stream_of(pairs[0][1].weight))
         _lib.check(rc, "dfq_bn_fold_batch")
         for bn, _ in pairs:
-            bn.eps = 0
+            bn.__dict__["eps"] = 0   # plain attributes: what Module.__setattr__ ends in
             _identity_forward(bn)
 
 
@@ -142,7 +146,7 @@ def _folded_bn_forward(self, input):
 
 def _identity_forward(bn):
     if "forward" not in bn.__dict__:   # one instance attribute (no per-BN hook objects)
-        bn.forward = types.MethodType(_folded_bn_forward, bn)
+        bn.__dict__["forward"] = types.MethodType(_folded_bn_forward, bn)
 
 
 def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, granularity="tensor",
@@ -204,18 +208,17 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
         dev = wl[0].src.device
         cdt = (torch.int8 if symmetric else torch.uint8) if bit_weight <= 8 else torch.int16
         up = lambda k: -(-k // 16) * 16   # noqa: E731  -- 16-element aligned pieces (vector paths)
-        codes = torch.empty(sum(up(it.src.numel()) for it in wl), dtype=cdt, device=dev)
-        f32 = torch.empty(sum(2 * up(it.rows) + up(it.src.numel() // it.khw) for it in wl), dtype=torch.float32,
-                          device=dev)
-        co = fo = 0
+        csz, fsz = [], []
         for it in wl:
             n, r, ne = it.src.numel(), it.rows, it.src.numel() // it.khw
-            it.codes = codes[co:co + n].view(it.src.shape)
-            it.scale = f32[fo:fo + r]
-            it.zero = f32[fo + up(r):fo + up(r) + r]
-            it.esum = f32[fo + 2 * up(r):fo + 2 * up(r) + ne]
-            co += up(n)
-            fo += 2 * up(r) + up(ne)
+            csz += [n, up(n) - n]
+            fsz += [r, up(r) - r, r, up(r) - r, ne, up(ne) - ne]
+        codes = torch.empty(sum(csz), dtype=cdt, device=dev)
+        f32 = torch.empty(sum(fsz), dtype=torch.float32, device=dev)
+        cv, fv = torch.split(codes, csz), torch.split(f32, fsz)   # every view in one call each
+        for k, it in enumerate(wl):
+            it.codes = cv[2 * k].view(it.src.shape)
+            it.scale, it.zero, it.esum = fv[6 * k], fv[6 * k + 2], fv[6 * k + 4]
     plan = SweepPlan(items)
     plan.execute()
     plan.destroy()   # stream-ordered: the task tables return to torch's allocator
