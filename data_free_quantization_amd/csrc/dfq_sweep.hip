@@ -70,7 +70,10 @@ constexpr int kNumVariants = 14;
 // DevTask.nrows <= kGroupTag: a row-group piece of R = kGroupTag - nrows + 1 rows
 constexpr int kGroupTag = -64;
 constexpr int kGroupMaxRows = 16;
-constexpr int kDefaultVariant = 6;   // = 5 with 87 instead of 105 VGPRs (profiles/r01/ab_*_v568.json)
+#ifndef DFQ_DEFAULT_VARIANT   // compile-time override for side-by-side A/B builds (scripts/ab_variant_libs.py)
+#define DFQ_DEFAULT_VARIANT 6
+#endif
+constexpr int kDefaultVariant = DFQ_DEFAULT_VARIANT;   // 6 = 5 with 87 instead of 105 VGPRs (profiles/r01/ab_*_v568.json)
 
 struct alignas(16) DevTensor {
     const float* src;
