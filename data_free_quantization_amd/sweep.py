@@ -18,7 +18,9 @@ from . import _lib
 
 @dataclass
 class SweepItem:
-    """One fp32 tensor viewed as [rows, row_len] and what to write for it."""
+    """One fp32 tensor viewed as [rows, row_len] and what to write for it.  The
+    outputs (codes, scale, zero, esum) may also be raw device addresses (int) into
+    memory the caller keeps alive until the plan has run."""
     src: torch.Tensor
     bits: int = 8
     per_channel: bool = True
@@ -85,8 +87,8 @@ class SweepPlan:
         L = _lib.load()
         rows_ = []
         for it in self.items:
-            _lib.require_device(it.src, it.dst, it.scale, it.zero, it.esum)
-            if it.codes is not None and not it.codes.is_cuda:
+            _lib.require_device(it.src, it.dst, *(t for t in (it.scale, it.zero, it.esum) if not isinstance(t, int)))
+            if it.codes is not None and not isinstance(it.codes, int) and not it.codes.is_cuda:
                 raise RuntimeError("codes must live on the GPU")
             rows = it.rows if it.rows is not None else (it.src.shape[0] if (it.per_channel and it.src.dim()) else 1)
             flags = (_lib.DFQ_CLIP if it.clip is not None else 0) | (_lib.DFQ_PACK_INT4 if it.pack_int4 else 0)
@@ -98,7 +100,7 @@ class SweepPlan:
                 flags |= _lib.DFQ_DEVICE_RANGE
                 rng = r.data_ptr()
             clo, chi = (float(it.clip[0]), float(it.clip[1])) if it.clip is not None else (0.0, 0.0)
-            ptr = lambda t: t.data_ptr() if t is not None else 0   # noqa: E731
+            ptr = lambda t: t if isinstance(t, int) else (t.data_ptr() if t is not None else 0)   # noqa: E731
             rows_.append((it.src.data_ptr(), ptr(it.dst), ptr(it.codes), ptr(it.scale), ptr(it.zero), ptr(it.esum),
                           rows, it.src.numel() // rows if rows else 0, it.khw, it.bits, it.mode(), flags, clo, chi,
                           0.0, 0.0, rng))

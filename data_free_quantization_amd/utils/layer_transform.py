@@ -13,6 +13,7 @@ Graph/bottoms follow SURVEY.md 8b.  Target tensors must be on a ROCm device.
 from __future__ import annotations
 
 import ctypes as C
+from collections.abc import Mapping
 import types
 from typing import Dict, Optional
 
@@ -203,30 +204,68 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
             keys.append(None)
     if not items:
         return graph
-    if state is not None:   # codes / scale / zero / E of every layer: views of two allocations
+    if state is not None:   # codes / scale / zero / E of every layer in two allocations
         wl = [it for it, k in zip(items, keys) if k is not None]
         dev = wl[0].src.device
         cdt = (torch.int8 if symmetric else torch.uint8) if bit_weight <= 8 else torch.int16
         up = lambda k: -(-k // 16) * 16   # noqa: E731  -- 16-element aligned pieces (vector paths)
-        csz, fsz = [], []
+        spans, co, fo = [], 0, 0
         for it in wl:
             n, r, ne = it.src.numel(), it.rows, it.src.numel() // it.khw
-            csz += [n, up(n) - n]
-            fsz += [r, up(r) - r, r, up(r) - r, ne, up(ne) - ne]
-        codes = torch.empty(sum(csz), dtype=cdt, device=dev)
-        f32 = torch.empty(sum(fsz), dtype=torch.float32, device=dev)
-        cv, fv = torch.split(codes, csz), torch.split(f32, fsz)   # every view in one call each
-        for k, it in enumerate(wl):
-            it.codes = cv[2 * k].view(it.src.shape)
-            it.scale, it.zero, it.esum = fv[6 * k], fv[6 * k + 2], fv[6 * k + 4]
+            spans.append((co, fo, n, r, ne))
+            co += up(n)
+            fo += 2 * up(r) + up(ne)
+        codes = torch.empty(max(co, 1), dtype=cdt, device=dev)
+        f32 = torch.empty(max(fo, 1), dtype=torch.float32, device=dev)
+        cb, fb, cs = codes.data_ptr(), f32.data_ptr(), codes.element_size()
+        for it, (c0, f0, n, r, ne) in zip(wl, spans):   # raw addresses: no per-layer views here
+            it.codes = cb + cs * c0
+            it.scale, it.zero, it.esum = fb + 4 * f0, fb + 4 * (f0 + up(r)), fb + 4 * (f0 + 2 * up(r))
     plan = SweepPlan(items)
     plan.execute()
     plan.destroy()   # stream-ordered: the task tables return to torch's allocator
     if state is not None:
-        for k, it in zip(keys, items):
-            if k is not None:
-                state[k] = dict(codes=it.codes, scale=it.scale, zero=it.zero, esum=it.esum, khw=it.khw)
+        wk = [k for k in keys if k is not None]
+        for k, it, sp in zip(wk, wl, spans):
+            state[k] = _StateEntry(codes, f32, sp, tuple(it.src.shape), it.khw, up)
     return graph
+
+
+class _StateEntry(Mapping):
+    """quantize_targ_layer's per-layer outputs {codes, scale, zero, esum, khw}:
+    views of the two shared allocations, made on first access."""
+
+    __slots__ = ("_codes", "_f32", "_span", "_shape", "_khw", "_up", "_views")
+
+    def __init__(self, codes, f32, span, shape, khw, up):
+        self._codes, self._f32, self._span, self._shape, self._khw, self._up = codes, f32, span, shape, khw, up
+        self._views = {}
+
+    def __getitem__(self, key):
+        v = self._views.get(key)
+        if v is not None:
+            return v
+        c0, f0, n, r, ne = self._span
+        if key == "codes":
+            v = self._codes[c0:c0 + n].view(self._shape)
+        elif key == "scale":
+            v = self._f32[f0:f0 + r]
+        elif key == "zero":
+            v = self._f32[f0 + self._up(r):f0 + self._up(r) + r]
+        elif key == "esum":
+            v = self._f32[f0 + 2 * self._up(r):f0 + 2 * self._up(r) + ne]
+        elif key == "khw":
+            return self._khw
+        else:
+            raise KeyError(key)
+        self._views[key] = v
+        return v
+
+    def __iter__(self):
+        return iter(("codes", "scale", "zero", "esum", "khw"))
+
+    def __len__(self):
+        return 5
 
 
 def _quantize_targ_layer_sharded(graph, bit_weight, bits_bias, targ_type, *, granularity, symmetric, clip, state,
