@@ -14,6 +14,7 @@ The arithmetic is HIP:
 from __future__ import annotations
 
 import ctypes as C
+from collections.abc import Mapping
 import logging
 
 import numpy as np
@@ -152,20 +153,42 @@ def _error_sums(weight, bits, signed, precomputed=None):
     return r.esum.view(o, i2), o, i2
 
 
+class _Snapshot(Mapping):
+    """{name: clone} whose values are views of ONE buffer, made on first access
+    (the walk itself never reads them)."""
+
+    def __init__(self, flat, spans):
+        self._flat, self._spans, self._views = flat, spans, {}
+
+    def __getitem__(self, name):
+        v = self._views.get(name)
+        if v is None:
+            off, shape, n = self._spans[name]
+            v = self._views[name] = self._flat[off:off + n].view(shape)
+        return v
+
+    def __iter__(self):
+        return iter(self._spans)
+
+    def __len__(self):
+        return len(self._spans)
+
+
 def _snapshot(chain, tensors):
-    """{name: t.clone()} as views of ONE buffer, filled by COPY ops recorded in the
-    chain (bias_correction.py:196,255 clone each bias), so the copies run in walk
+    """{name: t.clone()} (bias_correction.py:196,255 clone each bias) in one
+    buffer, filled by COPY ops recorded in the chain, so the copies run in walk
     order with the rest of the chain's work."""
     if not tensors:
         return {}
     vals = list(tensors.values())
     flat = torch.empty(sum(t.numel() for t in vals), dtype=torch.float32, device=vals[0].device)
-    out, off = {}, 0
+    spans, off = {}, 0
     for name, t in tensors.items():
+        n = t.numel()
         chain.copy(t, flat, off)
-        out[name] = flat[off:off + t.numel()].view(t.shape)
-        off += t.numel()
-    return out
+        spans[name] = (off, t.shape, n)
+        off += n
+    return _Snapshot(flat, spans)
 
 
 _BC_OP = np.dtype([("kind", "<i4"), ("flag", "<i4"), ("a", "<u8"), ("b", "<u8"), ("out", "<u8"), ("out2", "<u8"),
@@ -286,7 +309,9 @@ def _record_apply(chain, layer, E, o, i2, connect_type, expect, f):
 
 def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.BatchNorm2d, signed=False, *,
                     error_sums=None):
-    """Returns (bias_before_correction, bias_after_correction) keyed "layer_<idx>".
+    """Returns (bias_before_correction, bias_after_correction) keyed "layer_<idx>"
+    (read-only mappings whose tensors are views made on first access; the
+    reference returns dicts of clones).
 
     ``error_sums`` (extension, ``--bc_mode fused``): {graph key: E} from the fused
     quantize sweep, used instead of re-quantizing the (already quantized) weight."""
