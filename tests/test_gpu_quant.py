@@ -599,3 +599,37 @@ def test_row_groups_equal_default_tasks(pack, monkeypatch):
     for a, b in zip(outs[0][1], outs[1][1]):
         for f in ("dst", "codes", "scale", "zero", "esum"):
             assert torch.equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_device_range_argument_errors():
+    """DFQ_DEVICE_RANGE is a per-tensor flag with a range pointer: per-channel
+    modes, a missing pointer, or DFQ_GIVEN_RANGE together with it are rejected
+    before anything is enqueued (include/dfq_hip.h)."""
+    import ctypes as C
+    from data_free_quantization_amd import _lib
+    from data_free_quantization_amd.sweep import _DESC
+    L = _lib.load()
+    w = torch.randn(8, 16, device=DEV)
+    r = torch.zeros(2, dtype=torch.int32, device=DEV)
+
+    def rc(mode, flags, rng):
+        tab = np.zeros(1, dtype=_DESC)
+        tab[0]["src"] = tab[0]["dst"] = w.data_ptr()
+        tab[0]["rows"], tab[0]["row_len"], tab[0]["khw"], tab[0]["bits"] = 8 if mode >= 2 else 1, \
+            128 if mode < 2 else 16, 1, 8
+        tab[0]["mode"], tab[0]["flags"], tab[0]["range_enc"] = mode, flags, rng
+        return int(L.dfq_sweep_plan_ws_bytes(tab.ctypes.data_as(C.POINTER(_lib.TensorDesc)), 1))
+
+    assert rc(_lib.DFQ_TENSOR_ASYM, _lib.DFQ_DEVICE_RANGE, r.data_ptr()) > 0
+    assert rc(_lib.DFQ_CHANNEL_ASYM, _lib.DFQ_DEVICE_RANGE, r.data_ptr()) < 0
+    assert rc(_lib.DFQ_TENSOR_ASYM, _lib.DFQ_DEVICE_RANGE, 0) < 0
+    assert rc(_lib.DFQ_TENSOR_SYM, _lib.DFQ_DEVICE_RANGE | _lib.DFQ_GIVEN_RANGE, r.data_ptr()) < 0
+
+
+def test_preload_is_idempotent():
+    """dfq_preload (code objects + the CLE stream on the current device) can run
+    any number of times."""
+    from data_free_quantization_amd import _lib
+    L = _lib.load()
+    assert L.dfq_preload() == 0 and L.dfq_preload() == 0
+    _lib.preload()
