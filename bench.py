@@ -10,7 +10,7 @@ shapes, already resident in HBM).  The list defeats the 256 MB Infinity Cache
 At N GPUs the SAME layer list is LPT-sharded over the ranks (strong scaling,
 data_free_quantization_amd/distributed.py): rank 0 holds every weight and
 scatters each rank its slab once before timing; a step is every rank sweeping
-its share with outputs left sharded.  Also reported (``sharded_modes``): the
+its share (per-tensor copies, as at N = 1) with outputs left sharded.  Also reported (``sharded_modes``): the
 step with a gather of every output slab to rank 0, rank 0 -> ranks scatter +
 sweep + gather (rank 0 holds everything, end to end), the in-place all-gather,
 and the replicated form (every rank sweeps the whole list; weak scaling).
@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--no-pipeline", action="store_true", help="skip the one-off full-DFQ pipeline timing")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the other BASELINE configs (ResNet-50, DeepLab, INT4, per-tensor; sharded single model)")
+    p.add_argument("--layout", default="tensor", choices=["tensor", "arena"],
+                   help="N=1 tensor placement: one allocation per tensor, or the sharded path's per-field arenas")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r02.json"))
     return p.parse_args()
 
@@ -521,7 +523,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     std_of = lambda shp: (2.0 / (shp[2] * shp[3] * shp[0])) ** 0.5 if len(shp) == 4 else 0.01   # noqa: E731
     sw = plan = None
-    if world > 1:
+    if world > 1 or args.layout == "arena":
         import torch.distributed as dist
         # rank 0 holds the whole layer list and scatters each rank its slab (untimed)
         sw = D.ShardedSweep(specs, replicate=True, device=dev)
@@ -532,16 +534,21 @@ def main():
         sw.scatter()
         st = sw.plan_stats
         run = lambda: sw.run(stream)   # noqa: E731
-    else:
-        # one rank: no exchange, so no slabs -- every tensor is its own allocation, in
-        # the order eager code makes them (input, then its outputs).  One arena per
-        # field measured bimodal from box to box (1.08 or 1.31-1.37 ms per step,
-        # profiles/r02/ab_arena.md), per-tensor allocations 1.09-1.14.
+    if args.layout == "tensor":
+        # The timed sweep runs on one allocation per tensor, in the order eager code
+        # makes them (input, then its outputs).  At N > 1 each rank copies its
+        # scattered share out of the slab arena; the arenas stay for the collective
+        # forms (sharded_modes).  The sweep over per-field arenas is placement-bound:
+        # 1.08 or 1.31-1.37 ms per step from box to box, and 1.36 against 1.11 for
+        # per-tensor allocations on one box in five interleaved process pairs
+        # (profiles/r02/ab_layout.jsonl, ab_arena.md).
         from data_free_quantization_amd.sweep import SweepPlan, allocate
         gen = torch.Generator(device=dev).manual_seed(1234)
         items = []
-        for s in specs:
-            w = torch.empty(s.shape, device=dev).normal_(0.0, std_of(s.shape), generator=gen)
+        for i in (sw.mine if sw is not None else range(len(specs))):
+            s = specs[i]
+            w = sw.weight(i).clone() if sw is not None else \
+                torch.empty(s.shape, device=dev).normal_(0.0, std_of(s.shape), generator=gen)
             items.append(allocate(w, bits=s.bits, per_channel=s.per_channel, symmetric=s.symmetric, khw=s.khw,
                                   want_esum=s.want_esum, clip=s.clip, pack_int4=s.pack_int4))
         plan = SweepPlan(items)
@@ -620,8 +627,9 @@ def main():
                 "layers_per_copy": len(shapes),
                 "weights_per_copy": per_copy,
                 "parallelism": (f"{world} ranks, one process per GPU: the layer list LPT-sharded over the ranks "
-                                "(rank 0 scatters the input slabs before timing), outputs left sharded "
-                                "(no collective in the timed step); gathered forms in sharded_modes")
+                                "(rank 0 scatters the input slabs before timing; each rank sweeps per-tensor "
+                                "copies of its share), outputs left sharded (no collective in the timed step); "
+                                "gathered forms over the slab arenas in sharded_modes")
                 if world > 1 else "1 rank: the whole layer list on one GPU (per-tensor allocations, no exchange)",
             },
             "roofline": {
