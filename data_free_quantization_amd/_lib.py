@@ -221,9 +221,12 @@ def check(rc: int, what: str, shape_error=RuntimeError):
     raise DFQLibraryError(msg)
 
 
+_F32 = torch.float32
+
+
 def require_device(*tensors: Optional[torch.Tensor]):
     for t in tensors:
-        if t is None:
+        if t is None or (t.is_cuda and t.dtype is _F32 and t.is_contiguous()):
             continue
         if not t.is_cuda:
             raise RuntimeError(
@@ -231,8 +234,7 @@ def require_device(*tensors: Optional[torch.Tensor]):
                 f"got a tensor on {t.device} (move the model with .cuda() first)")
         if t.dtype != torch.float32:
             raise TypeError(f"expected float32 tensors, got {t.dtype}")
-        if not t.is_contiguous():
-            raise ValueError("expected contiguous tensors")
+        raise ValueError("expected contiguous tensors")
 
 
 def ptr(t: Optional[torch.Tensor]):

@@ -181,6 +181,7 @@ def _snapshot(chain, tensors):
     if not tensors:
         return {}
     vals = list(tensors.values())
+    _lib.require_device(*vals)
     flat = torch.empty(sum(t.numel() for t in vals), dtype=torch.float32, device=vals[0].device)
     spans, off = {}, 0
     for name, t in tensors.items():
@@ -240,9 +241,7 @@ class _BcChain:
         self.keep.append(fake_b)
         self.ops.append((_lib.DFQ_BC_OP_PROPAGATE, _lib.REF_THREADS, vec, None, (fake_b, 0), None, numel, 0, f))
 
-    def copy(self, src, dst, off):
-        _lib.require_device(src, dst)
-        assert src.dtype == torch.float32 and src.is_contiguous()
+    def copy(self, src, dst, off):   # src / dst validated by the caller (_snapshot)
         self.keep += [src, dst]
         self.ops.append((_lib.DFQ_BC_OP_COPY, 0, (src, 0), None, (dst, off), None, src.numel(), 0, 0))
 

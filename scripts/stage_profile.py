@@ -41,5 +41,5 @@ for rep in range(3):
         pipeline.run_dfq(m, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel",
                          symmetric=True, bc_mode="fused")
 s = io.StringIO()
-pstats.Stats(pr, stream=s).sort_stats("cumtime").print_stats(30)
+pstats.Stats(pr, stream=s).sort_stats(sys.argv[2] if len(sys.argv) > 2 else "cumtime").print_stats(30)
 print(s.getvalue())
