@@ -354,7 +354,29 @@ bn_fold_weight_batch_kernel(const BnFoldJob* __restrict__ jobs, const BnFoldChun
         float a = INFINITY, b = -INFINITY;
         const int64_t n = ch.e1 - ch.e0;
         int64_t done = 0;
-        if ((reinterpret_cast<uintptr_t>(J.w + ch.e0) & 15) == 0) {   // 16-B groups
+        // every row of the chunk with a factor of exactly 1 (merge_batchnorm #2): a
+        // read-only stream for the range, 4 x 16 B in flight per thread
+        int ident = 1;
+        for (int64_t r = r0 + threadIdx.x; r <= (ch.e1 - 1) / J.row_len; r += blockDim.x)
+            ident &= fold_factor(J, r) == 1.0f;
+        ident = __syncthreads_and(ident);
+        if (ident && (reinterpret_cast<uintptr_t>(J.w + ch.e0) & 15) == 0) {
+            const float4* w4 = reinterpret_cast<const float4*>(J.w + ch.e0);
+            const int64_t n4 = n >> 2;
+            for (int64_t k = threadIdx.x; k < n4; k += 4 * (int64_t)blockDim.x) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k + u * (int64_t)blockDim.x < n4) v[u] = w4[k + u * blockDim.x];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k + u * (int64_t)blockDim.x < n4) {
+                        a = fminf(a, fminf(fminf(v[u].x, v[u].y), fminf(v[u].z, v[u].w)));
+                        b = fmaxf(b, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
+                    }
+            }
+            done = 4 * n4;
+        } else if ((reinterpret_cast<uintptr_t>(J.w + ch.e0) & 15) == 0) {   // 16-B groups
             float4* w4 = reinterpret_cast<float4*>(J.w + ch.e0);
             const int64_t n4 = n >> 2;
             for (int64_t k = threadIdx.x; k < n4; k += blockDim.x) {
