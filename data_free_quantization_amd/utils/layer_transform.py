@@ -428,9 +428,56 @@ _EPS = 1e-6
 CASE_D = []
 
 
+class _MinMaxBatch:
+    """set_quant_minmax's (min, max) readbacks in one D2H copy.  The walk's control
+    flow never depends on the values, so it runs twice: ``record`` enqueues every
+    statistic kernel and writes each (min, max) into its own slot of one device
+    buffer (the walk sees placeholders and its range writes are discarded); one
+    copy brings all slots back; ``replay`` runs the walk again on the host only,
+    handing out the values in call order."""
+
+    def __init__(self, cap, device):
+        self.device = device
+        self.bufs = [torch.empty(2 * cap, dtype=torch.float32, device=device)]
+        self.cap, self.n, self.vals, self.replay = cap, 0, None, False
+
+    def minmax(self, a, w, n_sigma, w_is_var):
+        k = self.n
+        self.n += 1
+        if self.replay:
+            return self.vals[2 * k], self.vals[2 * k + 1]
+        b, j = divmod(k, self.cap)
+        if b == len(self.bufs):
+            self.bufs.append(torch.empty(2 * self.cap, dtype=torch.float32, device=self.device))
+        _lib.require_device(a, w)
+        rc = _lib.load().dfq_act_minmax(_lib.ptr(a), _lib.ptr(w), a.numel(), int(w_is_var), _EPS, float(n_sigma),
+                                        self.bufs[b].data_ptr() + 8 * j, _lib.stream_of(a))
+        _lib.check(rc, "dfq_act_minmax")
+        return 0.0, 0.0
+
+    def fetch(self):
+        vals = []
+        for b in self.bufs:
+            vals += b.tolist()
+        self.vals, self.n, self.replay = vals, 0, True
+
+
+_MM: Optional[_MinMaxBatch] = None
+
+
+class _NoWrites:
+    def fill(self, buf, value):
+        pass
+
+    def flush(self):
+        pass
+
+
 def _moments(weight, bias, kind, sqrt_w=False, into=None):
     """(mean, var) of one BN branch: kind 0 (no activation), 1 (ReLU), 2 (ReLU6);
     ``into``: (mean, var) accumulated in place (mean += m; var += v)."""
+    if _MM is not None and _MM.replay:   # host-only pass: the statistics already ran
+        return into if into is not None else (None, None)
     _lib.require_device(weight, bias)
     n = bias.numel()
     if into is None:
@@ -448,6 +495,8 @@ def _moments(weight, bias, kind, sqrt_w=False, into=None):
 
 def _moments_inplace(mean, var, kind):
     """mean, var <- calculate_mean(_6)(sqrt(var + eps), mean), calculate_var(_6)(...)."""
+    if _MM is not None and _MM.replay:
+        return
     rc = _lib.load().dfq_act_moments(_lib.ptr(var), _lib.ptr(mean), mean.numel(), kind, 1, _EPS, 0,
                                      _lib.ptr(mean), _lib.ptr(var), _lib.stream_of(mean))
     _lib.check(rc, "dfq_act_moments")
@@ -455,6 +504,8 @@ def _moments_inplace(mean, var, kind):
 
 def _minmax(a, w, n_sigma, w_is_var=False):
     """(float(min(a - N*w)), float(max(a + N*w))), w := sqrt(w + eps) if w_is_var."""
+    if _MM is not None:
+        return _MM.minmax(a, w, n_sigma, w_is_var)
     _lib.require_device(a, w)
     out = torch.empty(2, dtype=torch.float32, device=a.device)
     rc = _lib.load().dfq_act_minmax(_lib.ptr(a), _lib.ptr(w), a.numel(), int(w_is_var), _EPS, float(n_sigma),
@@ -475,6 +526,9 @@ def _get_max_value(bias, weight, n):
 def _through_layer(vec, layer_type, layer):
     """Case (d.): a statistic vector pushed through a conv (weight summed over
     KH*KW, groups) or linear layer with its bias (utils/layer_transform.py:470-479)."""
+    if _MM is not None and _MM.replay:
+        layer.bias.detach()   # AttributeError on a bias-less layer, as in the recording pass
+        return None
     w = layer.weight.detach().data
     b = layer.bias.detach().data   # AttributeError on a bias-less layer, as the reference
     o, i2 = w.shape[0], w.shape[1]
@@ -527,7 +581,29 @@ def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchN
     BN in between (case d.)."""
     if verbose:
         print("SET QUANT MIN MAX")
-    CASE_D.clear()
+    global _MM
+    batch = (_moments is _MOMENTS_DEV and _moments_inplace is _MOMENTS_INPLACE_DEV and _minmax is _MINMAX_DEV
+             and _through_layer is _THROUGH_DEV and _MM is None)
+    dev = next((m.fake_bias.device for m in graph.values() if isinstance(m, bn_type) and
+                getattr(m, "fake_bias", None) is not None and m.fake_bias.is_cuda), None)
+    if not batch or dev is None:   # injected statistics (oracle-backed tests) or nothing on the GPU
+        CASE_D.clear()
+        _set_quant_minmax_walk(graph, bottoms, is_detection, bn_type, N, _RangeWrites())
+        return
+    _MM = _MinMaxBatch(4 * len(graph) + 16, dev)
+    try:
+        CASE_D.clear()
+        _set_quant_minmax_walk(graph, bottoms, is_detection, bn_type, N, _NoWrites())   # record
+        _MM.fetch()
+        CASE_D.clear()
+        _set_quant_minmax_walk(graph, bottoms, is_detection, bn_type, N, _RangeWrites())   # replay
+    finally:
+        _MM = None
+
+
+def _set_quant_minmax_walk(graph, bottoms, is_detection, bn_type, N, writes):
+    """The walk of set_quant_minmax (utils/layer_transform.py:356-618); ``writes``
+    receives the running_min / running_max fills."""
 
     def get_quant_module(layer, key):
         if type(layer) == str:
@@ -542,7 +618,6 @@ def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchN
         return 1 if use_relu == "relu" else 2 if use_relu == "relu6" else 0
 
     bn_module, relu_attached = {}, {}
-    writes = _RangeWrites()
     try:
         for idx_layer in graph:
             bot = bottoms[idx_layer]
@@ -597,8 +672,8 @@ def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchN
                         layer_cur, bid = node_cur
                         depth = len(bid)
                         tmp_list.pop(0)
-                        bias = layer_cur.fake_bias.detach().clone()
-                        weight = layer_cur.fake_weight.detach().clone()
+                        bias = layer_cur.fake_bias.detach()   # read only: no clone needed
+                        weight = layer_cur.fake_weight.detach()
                         mean = var = None
                         value_min = value_max = None
                         if "add" in connect_type:
@@ -616,8 +691,8 @@ def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchN
                             else:
                                 for idx in range(idx_bound):
                                     node_tmp, use_relu_tmp, connect_type = tmp_list[idx]
-                                    bias = node_tmp[0].fake_bias.detach().clone()
-                                    weight = node_tmp[0].fake_weight.detach().clone()
+                                    bias = node_tmp[0].fake_bias.detach()
+                                    weight = node_tmp[0].fake_weight.detach()
                                     if "add" in connect_type:
                                         _moments(weight, bias, kind_of(use_relu_tmp), into=(mean, var))
                                         if "relu6" in connect_type:
@@ -668,6 +743,8 @@ def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchN
     finally:
         writes.flush()
 
+
+_MOMENTS_DEV, _MOMENTS_INPLACE_DEV, _MINMAX_DEV, _THROUGH_DEV = _moments, _moments_inplace, _minmax, _through_layer
 
 _RAW_OPS = {}
 _IN_QUANT = False   # re-entrancy guard: ops inside a quantizer are never intercepted
