@@ -593,10 +593,20 @@ def set_quant_minmax(graph, bottoms, is_detection=False, bn_type=torch.nn.BatchN
     _MM = _MinMaxBatch(4 * len(graph) + 16, dev)
     try:
         CASE_D.clear()
-        _set_quant_minmax_walk(graph, bottoms, is_detection, bn_type, N, _NoWrites())   # record
+        err = None
+        try:
+            _set_quant_minmax_walk(graph, bottoms, is_detection, bn_type, N, _NoWrites())   # record
+        except Exception as e:   # the reference's own errors: replay up to them, then raise
+            err = e
         _MM.fetch()
         CASE_D.clear()
-        _set_quant_minmax_walk(graph, bottoms, is_detection, bn_type, N, _RangeWrites())   # replay
+        try:   # replay: the fills made before an error take effect, as in the reference
+            _set_quant_minmax_walk(graph, bottoms, is_detection, bn_type, N, _RangeWrites())
+        except Exception:
+            if err is None:
+                raise
+        if err is not None:
+            raise err
     finally:
         _MM = None
 
