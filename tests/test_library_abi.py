@@ -99,3 +99,49 @@ def test_missing_library_fails_loudly(tmp_path):
     from data_free_quantization_amd import _lib
     with pytest.raises(_lib.DFQLibraryError, match="no CPU fallback"):
         _lib.load(tmp_path / "libdfq_hip.so")
+
+
+def _header_constants():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    consts = {k: int(v, 0) for k, v in re.findall(r"#define (DFQ_[A-Z0-9_]+)\s+(-?(?:0x[0-9a-fA-F]+|\d+))", text)}
+    for body in re.findall(r"enum\s*\{([^}]*)\}", text):
+        for k, v in re.findall(r"(DFQ_[A-Z0-9_]+)\s*=\s*(-?(?:0x[0-9a-fA-F]+|\d+))", body):
+            consts[k] = int(v, 0)
+    return consts
+
+
+def test_python_constants_match_header():
+    """Every DFQ_* constant the Python layer defines has the header's value."""
+    from data_free_quantization_amd import _lib
+    consts = _header_constants()
+    mine = {k: getattr(_lib, k) for k in dir(_lib) if k.startswith("DFQ_") and isinstance(getattr(_lib, k), int)}
+    assert len(mine) >= 15
+    for k, v in mine.items():
+        assert k in consts, k
+        assert consts[k] == v, (k, consts[k], v)
+
+
+def _struct_fields(name):
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    body = re.search(r"typedef struct " + name + r"\s*\{(.*?)\}\s*" + name + ";", text, flags=re.S).group(1)
+    return re.findall(r"([A-Za-z_][A-Za-z0-9_]*)\s*;", body)
+
+
+@pytest.mark.parametrize("cname,pyname", [("dfq_tensor_desc", "TensorDesc"), ("dfq_bn_fold_desc", "BnFoldDesc"),
+                                          ("dfq_bc_op", "BcOp")])
+def test_ctypes_structs_follow_header_field_order(cname, pyname):
+    """The ctypes mirrors (and the numpy record tables built on them) list the
+    header's fields in the header's order."""
+    from data_free_quantization_amd import _lib
+    want = _struct_fields(cname)
+    got = [f for f, _ in getattr(_lib, pyname)._fields_]
+    assert got == want, (got, want)
+
+
+def test_numpy_tables_match_ctypes_layouts():
+    from data_free_quantization_amd import _lib
+    from data_free_quantization_amd.sweep import _DESC
+    from data_free_quantization_amd.utils.layer_transform import _BN_DESC
+    from data_free_quantization_amd.bias_correction import _BC_OP
+    for dt, st in ((_DESC, _lib.TensorDesc), (_BN_DESC, _lib.BnFoldDesc), (_BC_OP, _lib.BcOp)):
+        assert dt.itemsize == ctypes.sizeof(st)
