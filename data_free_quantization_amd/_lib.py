@@ -27,7 +27,7 @@ EXPORTS = [
     "dfq_quantize_ws_bytes", "dfq_quantize_tensor", "dfq_chunk_range", "dfq_range", "dfq_fake_quant_given",
     "dfq_sweep_plan_create", "dfq_sweep_plan_ws_bytes", "dfq_sweep_plan_create_ws", "dfq_sweep_plan_execute",
     "dfq_sweep_plan_stats", "dfq_sweep_plan_destroy",
-    "dfq_bn_fold", "dfq_bn_fold_ws_bytes", "dfq_bn_fold_batch", "dfq_clamp",
+    "dfq_bn_fold", "dfq_bn_fold_ws_bytes", "dfq_bn_fold_batch", "dfq_clamp", "dfq_clamp_batch",
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
     "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
@@ -133,6 +133,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_sweep_plan_destroy": ([P], C.c_int),
         "dfq_bn_fold": ([P, P, P, P, P, P, P, P, F32, I64, I64, P], C.c_int),
         "dfq_clamp": ([P, I64, F32, F32, P], C.c_int),
+        "dfq_clamp_batch": ([C.POINTER(P), C.POINTER(I64), I32, F32, F32, P], C.c_int),
         "dfq_bn_fold_ws_bytes": ([C.POINTER(BnFoldDesc), I32], C.c_int64),
         "dfq_bn_fold_batch": ([C.POINTER(BnFoldDesc), I32, P, I64, P], C.c_int),
         "dfq_cle_ws_bytes": ([I64], SZ),

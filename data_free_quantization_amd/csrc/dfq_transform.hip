@@ -600,6 +600,54 @@ extern "C" int dfq_clamp(float* w, int64_t n, float lo, float hi, void* stream) 
     return DFQ_OK;
 }
 
+// Up to kClampBatch weights per launch, the batch in the kernel arguments
+// (blockIdx.y picks the tensor; each is 16-B aligned, float4 body + scalar tail).
+constexpr int kClampBatch = 64;
+struct ClampBatch {
+    float* w[kClampBatch];
+    int64_t n[kClampBatch];
+};
+
+__global__ void __launch_bounds__(kThreads) clamp_batch_kernel(ClampBatch b, float lo, float hi) {
+    float* __restrict__ w = b.w[blockIdx.y];
+    const int64_t n = b.n[blockIdx.y];
+    const int64_t n4 = n >> 2;
+    float4* w4 = reinterpret_cast<float4*>(w);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        float4 v = w4[i];
+        v.x = fminf(fmaxf(v.x, lo), hi);
+        v.y = fminf(fmaxf(v.y, lo), hi);
+        v.z = fminf(fmaxf(v.z, lo), hi);
+        v.w = fminf(fmaxf(v.w, lo), hi);
+        w4[i] = v;
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        w[i] = fminf(fmaxf(w[i], lo), hi);
+}
+
+extern "C" int dfq_clamp_batch(float* const* w, const int64_t* n, int32_t count, float lo, float hi, void* stream) {
+    if (count < 0 || (count > 0 && (!w || !n))) return DFQ_ERR_INVALID;
+    for (int32_t k = 0; k < count; ++k)
+        if (!w[k] || n[k] < 0 || reinterpret_cast<uintptr_t>(w[k]) % 16) return DFQ_ERR_INVALID;
+    for (int32_t k0 = 0; k0 < count; k0 += kClampBatch) {
+        ClampBatch b{};
+        int cnt = 0;
+        int64_t most = 0;
+        for (int32_t k = k0; k < std::min(count, k0 + kClampBatch); ++k) {
+            if (n[k] == 0) continue;
+            b.w[cnt] = w[k];
+            b.n[cnt] = n[k];
+            most = std::max(most, n[k]);
+            ++cnt;
+        }
+        if (cnt == 0) continue;
+        hipLaunchKernelGGL(clamp_batch_kernel, dim3(blocks_for(most, 16), cnt), dim3(kThreads), 0,
+                           static_cast<hipStream_t>(stream), b, lo, hi);
+        DFQ_LAUNCH_CHECK();
+    }
+    return DFQ_OK;
+}
+
 extern "C" int dfq_bias_absorb(const float* w2, float* b1, float* b2, float* bn_w, float* bn_b, int64_t c1,
                                int64_t o2, int64_t i2, int64_t khw2, float n_sigma, void* stream) {
     if (!w2 || !b1 || !b2 || !bn_w || !bn_b || c1 <= 0 || o2 <= 0 || i2 <= 0 || khw2 <= 0) return DFQ_ERR_INVALID;

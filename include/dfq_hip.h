@@ -203,6 +203,9 @@ int dfq_bn_fold_batch(const dfq_bn_fold_desc* descs, int32_t n, void* ws, int64_
 
 /* ---- weight clipping (clip_weight.py:18-29): w = min(max(w, lo), hi), in place */
 int dfq_clamp(float* w, int64_t n, float lo, float hi, void* stream);
+/* clip_weight over every target layer: `count` weights (16-B aligned, w[k] of
+ * n[k] floats), up to 64 per launch. */
+int dfq_clamp_batch(float* const* w, const int64_t* n, int32_t count, float lo, float hi, void* stream);
 
 /* ---- cross-layer equalization (Cross_layer_equal.py) -------------------- */
 /* Workspace bytes for one relation with c1 = W1.shape[0] channels. */
