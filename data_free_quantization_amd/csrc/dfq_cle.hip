@@ -2006,7 +2006,15 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
 // One CLE iteration's launches (steps, metric, stop rule) on stream s.
 static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
     // grid caps: 2,048 / 4,096 blocks (caps of 128-1,024 measured 4-150 % slower on MobileNetV2)
-    constexpr int64_t kStepGrid = 2048, kTileGrid = 4096;
+    // step / tile grid caps (A/B: DFQ_CLE_STEP_GRID / DFQ_CLE_TILE_GRID, diagnostics library)
+    static const int64_t kStepGrid = [] {
+        const char* e = ab_env("DFQ_CLE_STEP_GRID");
+        return e && *e ? std::max<int64_t>(1, atoll(e)) : int64_t(2048);
+    }();
+    static const int64_t kTileGrid = [] {
+        const char* e = ab_env("DFQ_CLE_TILE_GRID");
+        return e && *e ? std::max<int64_t>(1, atoll(e)) : int64_t(4096);
+    }();
     // fused schedule: this iteration's ranges were taken at the end of the previous
     // one (or by plan_run before the first); the next iteration's ride with the tiles
     for (int32_t k = 0; k < p->steps; ++k) {
