@@ -465,9 +465,11 @@ _FUZZ_SEEDS = [int(v) for v in __import__("os").environ.get("DFQ_FUZZ_SEEDS", "1
 def test_random_mixed_plans_vs_oracle(seed):
     """Fuzz: one plan of 40 random tensors -- rows 1..300, odd and even row lengths,
     KH*KW in {1, 4, 9, 25, 49}, all four modes, 2..16 bits, clip, given per-tensor
-    ranges (Python doubles and fp32 bounds), E sums, packed nibbles, unaligned
+    ranges (Python doubles and fp32 bounds), device-resident ranges
+    (DFQ_DEVICE_RANGE, fp64 or fp32 scale), E sums, packed nibbles, unaligned
     views -- every output bit-exact with the oracle."""
     from data_free_quantization_amd import _lib
+    import ctypes as C
     from data_free_quantization_amd.sweep import SweepItem, SweepPlan, code_dtype
     rng = np.random.default_rng(seed)
     items, refs = [], []
@@ -490,6 +492,9 @@ def test_random_mixed_plans_vs_oracle(seed):
         if mode < 2 and rng.random() < 0.3:
             flags |= O.F_GIVEN | (O.F_F32 if rng.random() < 0.5 else 0)
             given = (float(x.min()) * 0.8, float(x.max()) * 0.9)
+        dev_range = mode < 2 and not (flags & O.F_GIVEN) and rng.random() < 0.4   # DFQ_DEVICE_RANGE
+        if dev_range and rng.random() < 0.5:
+            flags |= O.F_F32
         esum = rng.random() < 0.5
         pack = bits <= 4 and rng.random() < 0.5 and not (mode >= 2 and row_len % 2 and 2 * row_len > 2048 and rows > 1)
         npar = rows if mode >= 2 else 1
@@ -500,13 +505,14 @@ def test_random_mixed_plans_vs_oracle(seed):
                        esum=torch.empty(rows * row_len // khw, device=DEV) if esum else None, khw=khw, clip=clip,
                        rows=rows if mode >= 2 else 1, pack_int4=pack)
         items.append(it)
-        refs.append((x, mode, bits, khw, flags, clip, given, esum, pack))
+        refs.append((x, mode, bits, khw, flags, clip, given, esum, pack, dev_range))
     plan = SweepPlan(items)
     # given ranges go through the descriptor (SweepItem has no field for them)
     L = _lib.load()
     descs = (_lib.TensorDesc * len(items))()
+    ranges = []
     for i, (it, r) in enumerate(zip(items, refs)):
-        x, mode, bits, khw, flags, clip, given, esum, pack = r
+        x, mode, bits, khw, flags, clip, given, esum, pack, dev_range = r
         d = descs[i]
         d.src, d.dst = it.src.data_ptr(), it.dst.data_ptr()
         d.codes, d.scale, d.zero = it.codes.data_ptr(), it.scale.data_ptr(), it.zero.data_ptr()
@@ -518,13 +524,19 @@ def test_random_mixed_plans_vs_oracle(seed):
         if clip is not None:
             d.clip_lo, d.clip_hi = clip
         d.given_min, d.given_max = given
+        if dev_range:   # the tensor's range left on the device by dfq_range
+            rb = torch.empty(2, dtype=torch.int32, device=DEV)
+            _lib.check(L.dfq_range(it.src.data_ptr(), it.src.numel(), rb.data_ptr(),
+                                   C.c_void_p(torch.cuda.current_stream().cuda_stream)), "dfq_range")
+            ranges.append(rb)
+            d.flags |= _lib.DFQ_DEVICE_RANGE
+            d.range_enc = rb.data_ptr()
     plan.destroy()
-    import ctypes as C
     p = C.c_void_p()
     _lib.check(L.dfq_sweep_plan_create(descs, len(items), C.byref(p)), "create")
     _lib.check(L.dfq_sweep_plan_execute(p, C.c_void_p(torch.cuda.current_stream().cuda_stream)), "execute")
     torch.cuda.synchronize()
-    for it, (x, mode, bits, khw, flags, clip, given, esum, pack) in zip(items, refs):
+    for it, (x, mode, bits, khw, flags, clip, given, esum, pack, _dr) in zip(items, refs):
         o = O.quantize(x, bits, mode, rows=x.shape[0] if mode >= 2 else 1, khw=khw, flags=flags,
                        clip=clip or (0.0, 0.0), given=given, want_esum=esum)
         tag = (x.shape, mode, bits, khw, flags, pack)
