@@ -430,11 +430,21 @@ def set_layer_bits(graph, bits_weight=8, bits_activation=8, bits_bias=16, targ_t
     8-bit."""
     print("Setting num_bits for targ layers...")
     assert targ_type is not None, "targ_type cannot be None"
+    # the new observers' running_min / running_max: views of ONE device buffer of
+    # zeros per device (one H2D copy instead of two per layer)
+    need = [graph[idx] for idx in graph if type(graph[idx]) in targ_type and hasattr(graph[idx], "quant")]
+    by_dev = {}
+    for m in need:
+        by_dev.setdefault(next(m.parameters()).device, []).append(m)
+    for dev, mods in by_dev.items():
+        zeros = torch.zeros(2 * len(mods)).to(dev)
+        for k, m in enumerate(mods):
+            q = QuantMeasure(bits_activation)
+            q._buffers["running_min"] = zeros[2 * k:2 * k + 1]
+            q._buffers["running_max"] = zeros[2 * k + 1:2 * k + 2]
+            m.quant = q
     for idx in graph:
         if type(graph[idx]) in targ_type:
-            if hasattr(graph[idx], "quant"):
-                dev = next(graph[idx].parameters()).device
-                graph[idx].quant = QuantMeasure(bits_activation).to(dev)
             if hasattr(graph[idx], "num_bits"):
                 graph[idx].num_bits = bits_weight
             if hasattr(graph[idx], "num_bits_bias"):
