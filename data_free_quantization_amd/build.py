@@ -29,6 +29,9 @@ FLAGS = [
     "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+    # only the C ABI is exported, and each library binds to its own internals
+    # (libdfq_hip.so and libdfq_diag.so loaded together must not interpose)
+    "-fvisibility=hidden", "-fvisibility-inlines-hidden",
 ]
 
 
@@ -62,7 +65,7 @@ def _build_one(out: Path, sources, defines, force: bool, verbose: bool) -> Path:
         subprocess.run(cmd, check=True)
         objs.append(str(obj))
     tmp = out.with_suffix(".so.tmp")
-    cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *objs]
+    cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-Wl,-Bsymbolic", "-o", str(tmp), *objs]
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
     for o in objs:

@@ -16,6 +16,10 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* The library is built with hidden visibility: only these entry points are
+ * exported (two builds in one process -- the product and the diagnostics
+ * library -- then never bind to each other's internals). */
+#pragma GCC visibility push(default)
 
 /* ---- measurement --------------------------------------------------------
  * Same-mix streaming probe (no arithmetic): y = x, codes = bits of x, esum = x,
@@ -39,6 +43,7 @@ int dfq_probe_lds(const float* x, float* y, void* codes, float* esum, int64_t n,
  * device memory (zeroed on the stream). */
 int dfq_probe_grid_barrier(int32_t nbar, int32_t blocks_per_cu, int32_t mode, void* ws, void* stream);
 
+#pragma GCC visibility pop
 #ifdef __cplusplus
 }
 #endif

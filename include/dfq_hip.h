@@ -25,6 +25,10 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* The library is built with hidden visibility: only these entry points are
+ * exported (two builds in one process -- the product and the diagnostics
+ * library -- then never bind to each other's internals). */
+#pragma GCC visibility push(default)
 
 #define DFQ_ABI_VERSION 1
 
@@ -354,6 +358,7 @@ int dfq_act_minmax(const float* a, const float* w, int64_t n, int32_t w_is_var, 
 int dfq_act_affine(const float* x, const float* w, const float* bias, int64_t o, int64_t i2, int64_t khw,
                    int64_t groups, float* out, void* stream);
 
+#pragma GCC visibility pop
 #ifdef __cplusplus
 }
 #endif
