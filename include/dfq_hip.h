@@ -115,8 +115,10 @@ const char* dfq_last_hip_error(void);
  *      utils/quantize.py:16-89) ------------------------------------------- */
 /* Workspace bytes dfq_quantize_tensor needs for this descriptor (0 is possible). */
 int dfq_quantize_ws_bytes(const dfq_tensor_desc* desc, size_t* bytes);
-/* Blocking (returns after the stream drains: the reference quantize() is
- * synchronous too).  ws: device memory of >= dfq_quantize_ws_bytes bytes. */
+/* Asynchronous on `stream` (the task table goes up through the library's pinned
+ * staging ring; no host wait).  ws: device memory of >= dfq_quantize_ws_bytes
+ * bytes that stays allocated until the stream reaches the kernel (a
+ * stream-ordered allocator does that). */
 int dfq_quantize_tensor(const dfq_tensor_desc* desc, void* ws, size_t ws_bytes, void* stream);
 /* quantize()'s data range when min/max are None and num_chunks splits the batch
  * (utils/quantize.py:26-37): x viewed as [rows = B // num_chunks, row_len];
@@ -153,12 +155,14 @@ typedef struct dfq_sweep_stats {
     int32_t variant;          /* kernel variant (env DFQ_SWEEP_VARIANT at create) */
     int32_t reserved;
 } dfq_sweep_stats;
-/* Blocking (uploads the descriptor/task tables once).  descs is copied. */
+/* Uploads the descriptor/task tables once into a private allocation (a blocking
+ * copy).  descs is copied. */
 int dfq_sweep_plan_create(const dfq_tensor_desc* descs, int32_t n, dfq_sweep_plan** plan);
 /* The same with the tables in a caller workspace of >= dfq_sweep_plan_ws_bytes
  * bytes (256-B aligned, stream-ordered with `stream`, alive while the plan runs;
  * e.g. the framework's caching allocator): no hipMalloc / hipFree, and destroy
- * needs no device sync.  The upload is on `stream`, which is synchronized. */
+ * needs no device sync.  The upload is stream-ordered on `stream` (pinned
+ * staging ring, no host wait). */
 int64_t dfq_sweep_plan_ws_bytes(const dfq_tensor_desc* descs, int32_t n);
 int dfq_sweep_plan_create_ws(const dfq_tensor_desc* descs, int32_t n, void* ws, int64_t ws_bytes, void* stream,
                              dfq_sweep_plan** plan);
