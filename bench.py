@@ -59,6 +59,9 @@ def parse():
                    help="skip the other BASELINE configs (ResNet-50, DeepLab, INT4, per-tensor; sharded single model)")
     p.add_argument("--layout", default="tensor", choices=["tensor", "arena"],
                    help="N=1 tensor placement: one allocation per tensor, or the sharded path's per-field arenas")
+    p.add_argument("--no-parity", action="store_true",
+                   help="skip the parity checks of the timed outputs (vs the C oracle) and of the MobileNetV2 "
+                        "pipeline (vs the reference fixture)")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r02.json"))
     return p.parse_args()
 
@@ -427,6 +430,37 @@ def cpu_baseline(args, shapes, seconds):
             "oracle_c_1thread_GBs": gbs(t_c)}
 
 
+def parity_of_timed(items, layers_per_copy, dev):
+    """Checker leg (test infrastructure, like cpu_baseline): the timed plan's
+    outputs on the first, middle and last weight set of this rank's list vs the C
+    oracle (oracle/dfq_oracle.c) run on the same input tensors -- dq, codes, scale,
+    zero and the bias-correction sums E, element by element (tests/parity.py)."""
+    from tests.parity import sweep_mismatches
+    torch.cuda.synchronize(dev)
+    copies = len(items) // layers_per_copy
+    sets = sorted({0, copies // 2, copies - 1}) if copies else []
+    sample = [it for c in sets for it in items[c * layers_per_copy:(c + 1) * layers_per_copy]]
+    t0 = time.perf_counter()
+    out = sweep_mismatches(sample)
+    out["weight_sets"] = sets
+    out["seconds"] = round(time.perf_counter() - t0, 2)
+    return out
+
+
+def pipeline_parity(dev):
+    """The whole main_dfq stage order on MobileNetV2 (reference-mode bias
+    correction, per-tensor INT8, the fixture's configuration) vs the reference's
+    own run: mismatch counts per stage (tests/parity.py, tests/golden)."""
+    import contextlib
+    import io
+    import logging
+    from tests.parity import pipeline_mismatches
+    logging.getLogger("data_free_quantization_amd.bias_correction").setLevel(logging.ERROR)
+    with contextlib.redirect_stdout(io.StringIO()):
+        out = pipeline_mismatches("mobilenetv2", 8, dev)
+    return out
+
+
 def pipeline_timing(dev, model="mobilenetv2"):
     """One-off: the full main_dfq stage order on one model (per-channel sym INT8,
     fused BC) on the GPU; milliseconds per stage of the fastest of three warm runs
@@ -577,6 +611,17 @@ def main():
     value = weight_bytes / t_step / 1e9
     launch_ms = dev_ms / args.steps          # device time of one execute() (st["launches"] kernels)
     achieved = st["algo_bytes"] / (launch_ms / 1e3) / 1e9
+    # parity of what was just timed: the first, middle and last weight set of this
+    # rank's share vs the C oracle on the same input tensors (every field)
+    timed_parity = None
+    if plan is not None and not args.no_parity:
+        timed_parity = parity_of_timed(plan.items, len(shapes), dev)
+        if world > 1:   # every rank checked its own share: the job's total
+            tot = torch.tensor([timed_parity["mismatches"], timed_parity["tensors"]], dtype=torch.int64,
+                               device=dev)
+            dist.all_reduce(tot)
+            timed_parity["all_ranks"] = {"mismatches": int(tot[0]), "tensors": int(tot[1])}
+            timed_parity["mismatches"] = int(tot[0])
     modes = sharded_modes(sw, dev, stream) if world > 1 else None
     for obj in (sw, plan):
         if obj is not None:
@@ -599,6 +644,11 @@ def main():
             second.append(fold_quant_pair(dev, stream))
         single = None if args.no_secondary else single_model_latency(dev, stream)
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
+        parity = None
+        if not args.no_parity:
+            parity = {"timed_sweep": timed_parity, "pipeline_mobilenetv2": pipeline_parity(dev)}
+            parity["mismatches"] = parity["pipeline_mobilenetv2"]["mismatches"] + \
+                (timed_parity["mismatches"] if timed_parity else 0)
         pipe = None if args.no_pipeline else {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")}
         if pipe is not None:
             pipe["cold_process_mobilenetv2"] = pipeline_cold("mobilenetv2")
@@ -653,6 +703,7 @@ def main():
                                        "5.2-6.5 TB/s, the sweep 5.9-6.3); a VGPR grid-stride stream of the "
                                        f"same mix: {probe_stream} GB/s",
             },
+            "parity": parity,
             "sharded_modes": modes,
             "cpu_baseline": cpu,
             "secondary_configs": second,

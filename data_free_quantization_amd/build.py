@@ -9,6 +9,7 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -21,6 +22,8 @@ SOURCES = ["dfq_lib.hip", "dfq_sweep.hip", "dfq_transform.hip", "dfq_cle.hip"]
 # switches) plus the probes (include/dfq_diag.h).  Never loaded by the product path.
 DIAG_LIB = PKG / "libdfq_diag.so"
 DIAG_SOURCES = SOURCES + ["dfq_probe.hip"]
+# linker version script: the dynamic symbol table holds dfq_* and nothing else
+EXPORTS = CSRC / "exports.map"
 ARCH = os.environ.get("DFQ_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: no FMA contraction (bit parity with torch CPU eager ops).
@@ -51,21 +54,26 @@ def _stale(out: Path, deps) -> bool:
 
 def _build_one(out: Path, sources, defines, force: bool, verbose: bool) -> Path:
     deps = [CSRC / s for s in sources] + [CSRC / "dfq_common.h", ROOT / "include" / "dfq_hip.h",
-                                          ROOT / "include" / "dfq_diag.h", Path(__file__)]
+                                          ROOT / "include" / "dfq_diag.h", EXPORTS, Path(__file__)]
     if not force and not _stale(out, deps):
         return out
-    objs = []
     tag = out.stem
+    objs, cmds = [], []
     for s in sources:
         obj = CSRC / f"{Path(s).stem}.{tag}.o"
-        cmd = [hipcc(), *FLAGS, *defines, "-I", str(ROOT / "include"), "-I", str(CSRC), "-c", str(CSRC / s),
-               "-o", str(obj)]
-        if verbose:
-            print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        cmds.append([hipcc(), *FLAGS, *defines, "-I", str(ROOT / "include"), "-I", str(CSRC), "-c", str(CSRC / s),
+                     "-o", str(obj)])
         objs.append(str(obj))
+    if verbose:
+        for cmd in cmds:
+            print(" ".join(cmd), file=sys.stderr)
+    # translation units compile in parallel (one hipcc each)
+    with ThreadPoolExecutor(max_workers=min(len(cmds), max(1, (os.cpu_count() or 1) // 2), 8)) as ex:
+        for f in [ex.submit(subprocess.run, cmd, check=True) for cmd in cmds]:
+            f.result()
     tmp = out.with_suffix(".so.tmp")
-    cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-Wl,-Bsymbolic", "-o", str(tmp), *objs]
+    cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-Wl,-Bsymbolic", f"-Wl,--version-script={EXPORTS}",
+           "-o", str(tmp), *objs]
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
     for o in objs:

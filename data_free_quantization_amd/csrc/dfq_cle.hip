@@ -1331,8 +1331,11 @@ __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32
 // chunk, and the block that finishes the last chunk runs the stop rule -- two
 // launches fewer per iteration.  Hand-offs between blocks go through
 // agent-coherent stores / loads and monotone arrival counters (cnt: one per
-// chunk, then one for the chunks; zeroed by plan_run, iteration i's target is
-// (i + 1) x members), so no L2 write-back is needed inside the launch.
+// chunk, then one for the launch; zeroed by plan_run, iteration i's target is
+// (i + 1) x members), each arrival an agent-scope release and each winner's
+// read an acquire.  The launch counter's members are the chunks with tiles AND
+// the range blocks, so the stop rule (which advances st->iters, whose parity the
+// range blocks write under) runs only after every block has read it.
 struct CleFin {
     uint32_t* cnt;
     float* part;
@@ -1350,21 +1353,48 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
                           uint32_t* __restrict__ rng, int64_t M, CleFin F, CleState* __restrict__ st) {
     __shared__ float lds[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
     __shared__ int flag;
+    // st->iters and st->done are read here, before this block's arrival below, and
+    // written only by the stop rule, which runs after EVERY block of the launch
+    // (tile-chunk winners and range blocks alike) has arrived: a range block that
+    // is dispatched late still sees this iteration's parity.
     if (st->done) return;
     const uint32_t round = (uint32_t)st->iters + 1u;
+    const int64_t nrb = (int64_t)gridDim.x - ntb;
+    // Arrival on counter c (agent-scope release: this block's coherent stores are
+    // visible before the count is); returns whether this block arrived last.
+    auto arrive = [&](uint32_t* c, uint32_t members) -> bool {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t a = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            flag = a == round * members - 1u;
+            if (flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the winner sees every arrival's stores
+        }
+        __syncthreads();
+        return flag != 0;
+    };
+    // The last arrival of the launch: tiny chunks' sums, then the per-layer means,
+    // the history and the stop rule.
+    auto finish = [&]() {
+        if (threadIdx.x == 0)
+            for (int64_t k = 0; k < F.nchunks; ++k) {
+                const CleChunk c2 = chunks[k];
+                if (c2.len < 8) st_coh(F.part + (int64_t)c2.layer * F.S + c2.t, 0.f + cle_tiny_chunk_sum(layers, c2));
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
+        cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
+                                   stage_part ? lds + 2048 : nullptr);
+    };
+    const uint32_t fin_members = (uint32_t)(F.nbig + nrb);
     if ((int64_t)blockIdx.x >= ntb) {
-        cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + 1) & 1, blockIdx.x - ntb, gridDim.x - ntb, lds);
+        cle_range_body(rels, tasks, t0, t1, rng, M, (round & 1u), blockIdx.x - ntb, nrb, lds);
+        if (arrive(F.cnt + F.nchunks, fin_members)) finish();
         return;
     }
     auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this unit's coherent stores are done
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t a = __hip_atomic_fetch_add(F.cnt + un.chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            flag = a == round * (uint32_t)(nb1 + 1) - 1u;
-        }
-        __syncthreads();
-        if (!flag) return;   // not the chunk's last tile
+        if (!arrive(F.cnt + un.chunk, (uint32_t)(nb1 + 1))) return;   // not the chunk's last tile
         {
             // the chunk's level-1 sums and tail words in one parallel pass of coherent
             // loads into LDS (free again: the unit is done), then one wave sums them
@@ -1384,30 +1414,21 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
                 if (threadIdx.x == 0) st_coh(F.part + (int64_t)ch.layer * F.S + ch.t, 0.f + fa);
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t a = __hip_atomic_fetch_add(F.cnt + F.nchunks, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-            flag = a == round * (uint32_t)F.nbig - 1u;
-        }
-        __syncthreads();
-        if (!flag) return;   // not the last chunk
-        if (threadIdx.x == 0)
-            for (int64_t k = 0; k < F.nchunks; ++k) {
-                const CleChunk c2 = chunks[k];
-                if (c2.len < 8) st_coh(F.part + (int64_t)c2.layer * F.S + c2.t, 0.f + cle_tiny_chunk_sum(layers, c2));
-            }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
-        cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
-                                   stage_part ? lds + 2048 : nullptr);
+        if (arrive(F.cnt + F.nchunks, fin_members)) finish();   // the launch's last arrival
     };
     cle_tiles_body(layers, chunks, b1off, units, nunits, b1buf, tailbuf, blockIdx.x, ntb, lds,
                    lds + kCleTile + kCleTailWords, hook);
 }
 
+// Grid-barrier words of the persistent loop (layout below); the plan's tables
+// reserve them in every build.
+constexpr int kCleMaxXcd = 16;
+constexpr int kCleRegBar = 64 + 32 * 3 * kCleMaxXcd;   // the registration barrier's two words
+constexpr int kCleBarWords = kCleRegBar + 64;
+
+// The persistent loop is a diagnostics-library A/B (measured slower, see
+// cle_persist_grid): the product build does not compile it.
+#ifdef DFQ_DIAGNOSTICS
 // ---------------------------------------------------------------------------
 // Persistent loop (fused schedule): ONE cooperative launch runs up to `batch`
 // whole iterations -- every chain step's rescale, the metric tiles with the next
@@ -1492,9 +1513,6 @@ __device__ __forceinline__ bool cle_grid_sync(uint32_t* bar, uint32_t nblk, CleS
 // generation, [64 + 32 x] XCD x arrivals, [64 + 32 (16 + x)] XCD x generation,
 // [64 + 32 (32 + x)] XCD x block count (registration), [kCleRegBar] the
 // registration barrier.
-constexpr int kCleMaxXcd = 16;
-constexpr int kCleRegBar = 64 + 32 * 3 * kCleMaxXcd;   // the registration barrier's two words
-constexpr int kCleBarWords = kCleRegBar + 64;
 
 struct CleXcdSync {
     uint32_t* bar;
@@ -1610,7 +1628,6 @@ __global__ void __launch_bounds__(kThreads) cle_persist_kernel(ClePersist P) {
     }
 }
 
-#ifdef DFQ_DIAGNOSTICS
 // Diagnostics: the persistent loop's grid barrier alone (nbar barriers, no work).
 // mode 0: the two-level XCD barrier; 1: the flat barrier (every block releases).
 __global__ void __launch_bounds__(kThreads) cle_barrier_probe_kernel(uint32_t* bar, CleState* st, int32_t nbar,
@@ -1810,7 +1827,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     std::vector<int32_t> w1_src(n_rel, -1);
     bool fused = true;
     {
-        const char* fe = getenv("DFQ_CLE_FUSED");
+        const char* fe = ab_env("DFQ_CLE_FUSED");   // diagnostics A/B: per-step range launches
         if (fe && fe[0] == '0') fused = false;
         std::vector<std::vector<int32_t>> chain_of(n_rel);
         for (int32_t r = 0; r < n_rel; ++r) chain_of[find(r)].push_back(r);
@@ -2082,6 +2099,10 @@ constexpr int32_t kClePersistBatch = 256;   // persistent loop: iterations per c
 // per SIMD), so it is a diagnostics-library A/B only: DFQ_CLE_PERSIST_BPC=<blocks
 // per CU> turns it on there; the product library never takes it.
 static int32_t cle_persist_grid(dfq_cle_plan* p) {
+#ifndef DFQ_DIAGNOSTICS
+    (void)p;
+    return 0;
+#else
     if (p->persist_grid >= 0) return p->persist_grid;
     p->persist_grid = 0;
     int bpc = 0;
@@ -2096,6 +2117,7 @@ static int32_t cle_persist_grid(dfq_cle_plan* p) {
         return 0;
     p->persist_grid = cus * std::min(bpc, occ);
     return p->persist_grid;
+#endif
 }
 
 extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count, int32_t max_iters,
@@ -2160,6 +2182,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
                            p->d_state, 0);
         DFQ_LAUNCH_CHECK();
     }
+#ifdef DFQ_DIAGNOSTICS
     // Persistent loop (fused schedule): one cooperative launch per kClePersistBatch
     // iterations, the stop rule read back once per launch.
     if (!init.done && cle_persist_grid(p) > 0) {
@@ -2198,6 +2221,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
             DFQ_HIP_CHECK(hipMemcpy(diffs, p->d_hist, sizeof(double) * init.iters, hipMemcpyDeviceToHost));
         return DFQ_OK;
     }
+#endif
     // kCleBatch iterations as one HIP graph (kernels of finished runs return at
     // once: the stop rule lives in d_state); DFQ_CLE_GRAPH=0: eager launches.
     const char* ge = ab_env("DFQ_CLE_GRAPH");

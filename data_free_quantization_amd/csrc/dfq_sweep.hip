@@ -705,10 +705,10 @@ static bool group_rows_enabled() {
     return e && e[0] == '1';
 }
 
-// DFQ_SWEEP_BLOCKROW=0: long rows through the reduce launch instead (a supported
-// alternative schedule, parity-tested against the default).
+// DFQ_SWEEP_BLOCKROW=0 (diagnostics library): long rows through the reduce launch
+// instead (an alternative schedule, parity-tested against the default).
 static bool blockrow_enabled() {
-    const char* e = getenv("DFQ_SWEEP_BLOCKROW");
+    const char* e = ab_env("DFQ_SWEEP_BLOCKROW");
     return !(e && e[0] == '0');
 }
 

@@ -292,6 +292,16 @@ class ShardedSweep:
             self._plan = self._gpu_plan()
         if self._plan is not None:
             self._plan.execute(stream)
+            self._run_stream = stream
+
+    def _await_run(self):
+        """Collectives are ordered against the current stream only: make it wait for
+        a sweep that run() enqueued on another stream before sending its outputs."""
+        s = getattr(self, "_run_stream", None)
+        if s is not None and self.device.type == "cuda":
+            cur = torch.cuda.current_stream(self.device)
+            if s != cur:
+                cur.wait_stream(s)
 
     @property
     def plan_stats(self) -> Optional[Dict]:
@@ -358,6 +368,7 @@ class ShardedSweep:
         path is exercised."""
         if not dist.is_initialized():
             return
+        self._await_run()
         L = self.layout
         if to == "all":
             if not self.replicate:

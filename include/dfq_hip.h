@@ -178,8 +178,9 @@ int dfq_bn_fold(float* w, float* bias, float* bn_w, float* bn_b, float* bn_mean,
                 float* fake_w, float* fake_b, float eps, int64_t rows, int64_t row_len,
                 void* stream);
 
-/* All BN folds of a model in two launches (blocking): one descriptor per
- * (BN, producer layer) pair, each weight at most once per call; eps per BN. */
+/* All BN folds of a model in two launches: one descriptor per (BN, producer
+ * layer) pair, each weight at most once per call; eps per BN.  Stream-ordered
+ * with a workspace, blocking without one (see ws below). */
 enum { DFQ_BN_FOLD_ZERO_BIAS = 1 };
 typedef struct dfq_bn_fold_desc {
     float* w;

@@ -114,8 +114,9 @@ def test_device_cle_matches_oracle(signed, eps, smm, thr, count, monkeypatch):
     # fused schedule: 2 rescale steps + ONE launch of metric tiles with the next
     # iteration's ranges, the chunk combine and the stop rule folded in; else
     # 2 x (range + rescale) + that launch
-    expect = 3 if os.environ.get("DFQ_CLE_FUSED", "1") != "0" else 5
-    if os.environ.get("DFQ_LIB") == "diag" and os.environ.get("DFQ_CLE_UNFUSED_FIN"):
+    diag = os.environ.get("DFQ_LIB") == "diag"   # the A/B switches exist in the diagnostics library only
+    expect = 3 if not (diag and os.environ.get("DFQ_CLE_FUSED") == "0") else 5
+    if diag and os.environ.get("DFQ_CLE_UNFUSED_FIN"):
         expect += 2   # A/B: the chunk combine and the stop rule as launches of their own
     assert cle.LAST_RUN["launches_per_iteration"] == expect
     assert cle.LAST_RUN["diffs"] == diffs

@@ -1,0 +1,67 @@
+"""Deterministic checks around the round-2 one-off world-2 export mismatch (DESIGN.md
+section 6).  The failing run computed the single-process side inside the pytest
+process after tests that had loaded libdfq_diag.so, and the default CLE path
+then had a real race: in cle_loop_tiles_fin_kernel the range blocks read the
+iteration parity from st->iters when they started, while the stop rule of the
+same launch advanced it.  Fixed by counting the range blocks into
+the launch's final hand-off; these tests pin the fix.
+
+* the whole MobileNetV2 / DeepLab stage order, several times in one process after
+  the diagnostics library has been loaded, equals the reference fixture;
+* the fused tiles+stop-rule launch with a range grid far above residency (every
+  range task its own block, diagnostics DFQ_CLE_STEP_GRID) equals the fixture and
+  the unfused path (stop rule as a launch of its own), in a fresh process.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tests.parity import pipeline_mismatches
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("name", ["mobilenetv2", "deeplab"])
+def test_pipeline_repeats_after_diag_library_loaded(name):
+    from data_free_quantization_amd import _lib
+    _lib.load_diag()          # loaded beside the product library, as the A/B tests leave it
+    assert _lib.load() is not _lib.load_diag()
+    for rep in range(3):
+        r = pipeline_mismatches(name, 8)
+        assert r["mismatches"] == 0, (rep, r)
+
+
+_SCRIPT = r"""
+import json, os, sys
+sys.path.insert(0, os.environ["DFQ_ROOT"])
+from tests.parity import pipeline_mismatches
+from data_free_quantization_amd import Cross_layer_equal as cle
+out = []
+for fin in ("fused", "unfused", "fused"):
+    if fin == "unfused":
+        os.environ["DFQ_CLE_UNFUSED_FIN"] = "1"
+    else:
+        os.environ.pop("DFQ_CLE_UNFUSED_FIN", None)
+    for name in ("mobilenetv2", "resnet50"):
+        r = pipeline_mismatches(name, 8)
+        out.append({"fin": fin, "model": name, "mismatches": r["mismatches"],
+                    "launches": cle.LAST_RUN.get("launches_per_iteration"), "iters": r["cle_iterations"]})
+print("RESULT " + json.dumps(out))
+"""
+
+
+def test_cle_fused_fin_with_oversized_range_grid():
+    env = dict(os.environ, DFQ_ROOT=ROOT, DFQ_LIB="diag", DFQ_CLE_STEP_GRID="1000000", DFQ_CLE_MODE="device",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, "-c", _SCRIPT], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1][7:])
+    assert all(x["mismatches"] == 0 for x in res), res
+    fused = [x["launches"] for x in res if x["fin"] == "fused"]
+    unfused = [x["launches"] for x in res if x["fin"] == "unfused"]
+    assert min(unfused) > max(fused)   # the A/B really switched paths

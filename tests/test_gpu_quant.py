@@ -256,6 +256,8 @@ def test_large_ranges_vs_oracle(monkeypatch):
             assert np.array_equal(it.codes.cpu().numpy().view(o["codes"].dtype), o["codes"]), (x.shape, mode)
             assert np.array_equal(it.scale.cpu().numpy(), o["scale"]), (x.shape, mode)
             assert np.array_equal(it.esum.cpu().numpy(), o["esum"]), (x.shape, mode)
+    from data_free_quantization_amd import _lib
+    monkeypatch.setattr(_lib, "_LIB", _lib.load_diag())   # the switch is a diagnostics-library A/B
     monkeypatch.setenv("DFQ_SWEEP_BLOCKROW", "0")
     plan2, items2 = run()
     for a, b in zip(items, items2):

@@ -66,6 +66,31 @@ def test_product_library_carries_no_diagnostics():
     assert LIB.stat().st_size < DIAG_LIB.stat().st_size
 
 
+def _dynsyms(path, *flags):
+    out = subprocess.run(["nm", "-D", *flags, str(path)], capture_output=True, text=True, check=True).stdout
+    return [ln.split()[-1] for ln in out.splitlines() if ln.strip()]
+
+
+@pytest.mark.parametrize("path", [LIB, DIAG_LIB], ids=["product", "diagnostics"])
+def test_only_the_c_abi_is_exported(path):
+    """csrc/exports.map: the dynamic symbol table of each library holds its dfq_*
+    entry points and nothing else (no kernel stub handles, templates or inline
+    helpers that a second library loaded in the process could interpose)."""
+    if not path.exists():
+        pytest.skip("libraries not built (run __graft_entry__.build())")
+    defined = _dynsyms(path, "--defined-only")
+    assert defined and all(n.startswith("dfq_") for n in defined), [n for n in defined if not n.startswith("dfq_")]
+
+
+def test_product_library_reads_no_environment():
+    """The A/B switches (DFQ_SWEEP_*, DFQ_CLE_*) are read by libdfq_diag.so only:
+    the product library does not even import getenv."""
+    if not LIB.exists() or not DIAG_LIB.exists():
+        pytest.skip("libraries not built (run __graft_entry__.build())")
+    assert not any(n.split("@")[0] in ("getenv", "secure_getenv") for n in _dynsyms(LIB, "--undefined-only"))
+    assert any(n.split("@")[0] == "getenv" for n in _dynsyms(DIAG_LIB, "--undefined-only"))
+
+
 def test_version_and_errors(lib):
     from data_free_quantization_amd import _lib
     L = _lib.load()
