@@ -20,9 +20,12 @@ this module restates those steps on PIL + numpy:
 * ``Evaluator`` / ``forward_all``: confusion matrix over the 21 classes
   (label 255 ignored), pixel accuracy and mean IoU.
 
-Parity unpinned: torchvision and the reference's dataset code are absent, so
-these are restatements of their published behaviour, checked in
-tests/test_evaluate.py on hand-computed cases.
+Parity: the segmentation transform (FixScaleCrop, Normalize, ToTensor) is pinned
+bit-exact to the reference's own custom_transforms.py (importable in the dev
+container; fixtures tests/golden/seg_transforms.npz).  The classification path
+stays "parity unpinned": torchvision (its Resize / CenterCrop / Normalize and
+ImageFolder) is not installed here, so those are restatements of its published
+behaviour, checked in tests/test_evaluate.py on hand-computed cases.
 """
 from __future__ import annotations
 
@@ -128,9 +131,7 @@ class VOCSegmentation(torch.utils.data.Dataset):
         Image = _pil()
         img = Image.open(self.images[i]).convert("RGB")
         mask = Image.open(self.labels[i])
-        img, mask = fix_scale_crop(img, mask, self.crop_size)
-        return {"image": _normalize(np.asarray(img, dtype=np.uint8)),
-                "label": torch.from_numpy(np.array(mask, dtype=np.int64))}
+        return seg_transform(img, mask, self.crop_size)
 
 
 def fix_scale_crop(img, mask, crop: int):
@@ -150,6 +151,29 @@ def fix_scale_crop(img, mask, crop: int):
     return img.crop(box), mask.crop(box)
 
 
+def seg_normalize(img) -> np.ndarray:
+    """The segmentation code's Normalize (custom_transforms.py:17-27) in its own
+    numpy arithmetic: float32 image / 255 (fp32), then -= mean and /= std with the
+    tuples as float64 arrays (computed in fp64, stored back to fp32) -- not
+    torchvision's fp32 Normalize of the classification path."""
+    x = np.array(img).astype(np.float32)
+    x /= 255.0
+    x -= MEAN
+    x /= STD
+    return x
+
+
+def seg_transform(img, mask, crop: int):
+    """The VOC validation transform (pascal.py:108-112): FixScaleCrop, Normalize,
+    ToTensor.  Returns {"image": CHW float32, "label": HW float32} as the
+    reference's ToTensor does (custom_transforms.py:33-46).  Pinned bit-exact to
+    the reference (tests/golden/seg_transforms.npz)."""
+    img, mask = fix_scale_crop(img, mask, crop)
+    x = seg_normalize(img).transpose((2, 0, 1))
+    m = np.array(mask).astype(np.float32)
+    return {"image": torch.from_numpy(np.ascontiguousarray(x)).float(), "label": torch.from_numpy(m).float()}
+
+
 class Evaluator:
     """Confusion-matrix segmentation metrics (labels outside [0, n) are ignored)."""
 
@@ -159,7 +183,7 @@ class Evaluator:
 
     def add_batch(self, gt: np.ndarray, pred: np.ndarray):
         gt, pred = np.asarray(gt).ravel(), np.asarray(pred).ravel()
-        keep = (gt >= 0) & (gt < self.num_class)
+        keep = (gt >= 0) & (gt < self.num_class)   # float labels (the reference's ToTensor) too
         idx = self.num_class * gt[keep].astype(np.int64) + pred[keep].astype(np.int64)
         self.confusion += np.bincount(idx, minlength=self.num_class ** 2).reshape(self.num_class, self.num_class)
 
@@ -209,4 +233,5 @@ def inference_seg(model, base_dir: str, device="cuda:0", batch_size: int = 32, w
 
 
 __all__: Sequence[str] = ["ImageFolder", "VOCSegmentation", "Evaluator", "cls_transform", "fix_scale_crop",
+                          "seg_normalize", "seg_transform",
                           "forward_all", "inference_cls", "inference_seg"]

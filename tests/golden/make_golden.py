@@ -694,6 +694,37 @@ def state_dict_keys():
     print("state_dict keys:", {k: len(v) for k, v in res.items()})
 
 
+def seg_transforms():
+    """The reference's segmentation validation transform (dataset_utils/segmentation/
+    pascal.py:108-112: FixScaleCrop -> Normalize -> ToTensor, custom_transforms.py)
+    on seeded PIL images and masks of landscape, portrait, square and
+    non-integer-scale shapes: inputs and outputs of every case, for
+    tests/test_evaluate.py (data_free_quantization_amd.evaluate)."""
+    from PIL import Image
+    from dataset_utils.segmentation import custom_transforms as tr
+    rng = np.random.default_rng(2024)
+    cases = [((53, 37), 32), ((37, 53), 32), ((40, 40), 32), ((97, 61), 45), ((61, 97), 45), ((33, 100), 31),
+             ((64, 48), 64), ((29, 30), 45)]   # (w, h), crop; the last two upscale
+    out, meta = {}, []
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    comp = [tr.FixScaleCrop(crop_size=0), tr.Normalize(mean=mean, std=std), tr.ToTensor()]
+    for i, ((w, h), crop) in enumerate(cases):
+        img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        mask = rng.integers(0, 21, (h, w), dtype=np.uint8)
+        mask[rng.random((h, w)) < 0.05] = 255
+        comp[0].crop_size = crop
+        sample = {"image": Image.fromarray(img), "label": Image.fromarray(mask)}
+        for t in comp:
+            sample = t(sample)
+        out[f"img{i}"], out[f"mask{i}"] = img, mask
+        out[f"out_img{i}"] = sample["image"].numpy()
+        out[f"out_label{i}"] = sample["label"].numpy()
+        meta.append({"w": w, "h": h, "crop": crop})
+    out["meta"] = np.array(json.dumps({"cases": meta, "mean": mean, "std": std}))
+    np.savez_compressed(HERE / "seg_transforms.npz", **out)
+    print("seg_transforms:", len(cases), "cases")
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["quant", "transform", "mobilenetv2", "resnet50", "deeplab"]
     if any(w.startswith("mklgap_") for w in which):
@@ -723,5 +754,7 @@ if __name__ == "__main__":
             forward_logits(m)
     if "keys" in which:
         state_dict_keys()
+    if "seg" in which:
+        seg_transforms()
     if "literal" in which:
         print("literal bias_correction is a no-op:", literal_bc())

@@ -3,6 +3,8 @@ main_dfq.py:66-113's inference_all.  CPU only: synthetic ImageFolder / VOC trees
 written with PIL, hand-computed expectations.  (torchvision and the reference's
 dataset code are absent, so the transforms are checked against their published
 arithmetic, not against those libraries: parity unpinned.)"""
+from pathlib import Path
+
 import numpy as np
 import pytest
 import torch
@@ -109,3 +111,22 @@ def test_inference_seg_end_to_end(tmp_path):
 
     miou = E.inference_seg(_Seg(), str(base), device="cpu", batch_size=2, workers=0, crop_size=64)
     assert miou > 0.9
+
+
+def test_seg_transform_matches_reference_fixture():
+    """FixScaleCrop -> Normalize -> ToTensor (the reference's VOC validation
+    transform, dataset_utils/segmentation/pascal.py:108-112) on seeded images and
+    masks: image and label tensors bit-exact with the reference's own output
+    (tests/golden/seg_transforms.npz, make_golden.py seg)."""
+    import json
+    from PIL import Image
+    from data_free_quantization_amd.evaluate import seg_transform
+    z = np.load(Path(__file__).resolve().parent / "golden" / "seg_transforms.npz", allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    assert len(meta["cases"]) >= 6
+    for i, c in enumerate(meta["cases"]):
+        out = seg_transform(Image.fromarray(z[f"img{i}"]), Image.fromarray(z[f"mask{i}"]), c["crop"])
+        img, lab = out["image"].numpy(), out["label"].numpy()
+        assert img.dtype == np.float32 and img.shape == (3, c["crop"], c["crop"]), (i, c)
+        assert np.array_equal(img.view(np.uint32), z[f"out_img{i}"].view(np.uint32)), (i, c)
+        assert np.array_equal(lab, z[f"out_label{i}"]) and lab.dtype == z[f"out_label{i}"].dtype, (i, c)
