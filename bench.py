@@ -424,10 +424,74 @@ def cpu_baseline(args, shapes, seconds):
                       f"clamp + BC error sums) on {threads} intra-op threads (this process's host-CPU share: "
                       f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, os.cpu_count()={os.cpu_count()}, "
                       f"affinity {affinity})",
+            "threads_note": (f"cores = torch's intra-op threads = OMP_NUM_THREADS ({os.environ.get('OMP_NUM_THREADS')}), "
+                             f"the CPU share the GPU box gives this process; os.cpu_count() ({os.cpu_count()}) counts "
+                             "the whole host, and that many threads on this share would oversubscribe it.  The "
+                             "per-channel port equals its 1-thread rate because the reference's per-row quantize() "
+                             "calls (one Python call per output channel, tiny rows) bound it, not arithmetic; the "
+                             "per-tensor mode below shows the thread scaling"),
             "value_1thread": gbs(t_port1),
             "per_tensor_GBs": gbs(t_tensor), "per_tensor_1thread_GBs": gbs(t_tensor1),
             "per_tensor_sample": "quantize_targ_layer's arithmetic (one range per tensor), best of 5",
             "oracle_c_1thread_GBs": gbs(t_c)}
+
+
+def cpu_baseline_transforms(dev, seconds):
+    """The reference's CLE loop and bias-correction error reduction as torch CPU
+    ops (oracle/torch_port.py: Cross_layer_equal.py:11-116, bias_correction.py:
+    111-144,231), on MobileNetV2 after the first BN fold (seed 0, the pipeline
+    fixture's model), with this process's host threads.  CLE: whole iterations
+    until ~``seconds`` are spent (the reference's per-channel Python loop makes
+    one iteration take seconds), each iteration's diff checked against the
+    reference's own (tests/golden/pipeline_mobilenetv2.npz); the full loop is
+    that per-iteration time x the reference's iteration count.  BC: best of 3
+    passes of _quantize_error + spatial sum over every target weight."""
+    import numpy as np
+    import torch.nn as nn
+    from data_free_quantization_amd import zoo
+    from data_free_quantization_amd.utils.layer_transform import merge_batchnorm
+    from data_free_quantization_amd.utils.relation import create_relation
+    from data_free_quantization_amd.utils.tracer import build_graph
+    from oracle import torch_port as TP
+    from tests.helpers import pipeline
+    targ = (nn.Conv2d, nn.Linear)
+    m = zoo.build("mobilenetv2", seed=0, relu=True).to(dev)
+    g = build_graph(m, "positional")
+    G, B = g.getGraph(), g.getBottoms()
+    merge_batchnorm(m, G, B, targ)
+    rels = create_relation(G, B, targ)
+    tk = [k for k in G if type(G[k]) in targ]
+    weights = {k: G[k].weight.detach().cpu().clone() for k in tk}
+    biases = {k: (G[k].bias.detach().cpu().clone() if G[k].bias is not None else None) for k in tk}
+    bn = {r.bn_idx: (G[r.bn_idx].fake_weight.detach().cpu().clone(), G[r.bn_idx].fake_bias.detach().cpu().clone())
+          for r in rels}
+    relations = [r.get_idxs() for r in rels]
+    ref_diffs = [float(x) for x in pipeline("mobilenetv2")["cle_diffs"]]
+    times, diffs = [], []
+    t_all = time.perf_counter()
+    while time.perf_counter() - t_all < seconds and len(diffs) < len(ref_diffs):
+        t0 = time.perf_counter()
+        diffs.append(TP.cle_iteration(weights, biases, bn, relations))
+        times.append(time.perf_counter() - t0)
+    per_it = float(np.median(times))
+    bc = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        for k in tk:
+            TP.quantize_error_spatial(weights[k], 8, False)
+        bc.append(time.perf_counter() - t0)
+    elems = sum(w.numel() for w in weights.values())
+    return {"threads": torch.get_num_threads(), "kind": "port",
+            "cle_s_per_iteration": round(per_it, 4), "cle_iterations_timed": len(times),
+            "cle_iterations_reference": len(ref_diffs),
+            "cle_loop_s_est": round(per_it * len(ref_diffs), 2),
+            "cle_diffs_match_reference": diffs == ref_diffs[:len(diffs)],
+            "bc_error_reduction_ms": round(min(bc) * 1e3, 3),
+            "bc_error_reduction_GBs": round(4 * elems / min(bc) / 1e9, 3),
+            "sample": f"MobileNetV2 after BN fold ({len(relations)} relations, {len(tk)} target layers, {elems} "
+                      f"weights): {len(times)} whole CLE iterations of the reference's op sequence "
+                      f"(per-channel Python loop; full loop = median iteration x {len(ref_diffs)} iterations); "
+                      f"BC: _quantize_error + spatial sum over every target weight, best of 3"}
 
 
 def parity_of_timed(items, layers_per_copy, dev):
@@ -644,6 +708,8 @@ def main():
             second.append(fold_quant_pair(dev, stream))
         single = None if args.no_secondary else single_model_latency(dev, stream)
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
+        if cpu is not None:
+            cpu["transforms"] = cpu_baseline_transforms(dev, args.cpu_seconds)
         parity = None
         if not args.no_parity:
             parity = {"timed_sweep": timed_parity, "pipeline_mobilenetv2": pipeline_parity(dev)}

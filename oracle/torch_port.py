@@ -62,3 +62,64 @@ def per_channel_sweep(w: torch.Tensor, bits=8, symmetric=True, clip=(-15.0, 15.0
 def per_tensor_sweep(w: torch.Tensor, bits=8, symmetric=False):
     """quantize_targ_layer's weight arithmetic (utils/layer_transform.py:296-299)."""
     return quantize(w, bits, float(w.min()), float(w.max()), symmetric)
+
+
+def layer_equalization(W1, W2, B1, bn_w=None, bn_b=None, s_min_max=(1e-8, 1e8), signed=False, eps=0):
+    """Cross_layer_equal.py:11-59 with the same torch CPU ops: the per-channel
+    Python loop over W2's input channels (the reference's 62-75 s on MobileNetV2)."""
+    groups = 1
+    if W1.shape[0] != W2.shape[1]:
+        groups = W1.shape[0] // W2.shape[1]
+    c_in = W1.shape[0] // groups
+    c_out = W2.shape[0] // groups
+    S = torch.zeros(W1.size(0))
+    for g in range(groups):
+        a0, a1 = g * c_in, (g + 1) * c_in
+        o0, o1 = g * c_out, (g + 1) * c_out
+        W1g, W2g = W1[a0:a1], W2[o0:o1]
+        for i in range(W2g.shape[1]):
+            if signed:
+                r1 = torch.max(torch.abs(W1g[i]))
+                r2 = torch.max(torch.abs(W2g[:, i]))
+            else:
+                r1 = torch.max(W1g[i]) - torch.min(W1g[i])
+                r2 = torch.max(W2g[:, i]) - torch.min(W2g[:, i])
+            s = (1 / (r1 + eps)) * torch.sqrt(r1 * r2 + eps)
+            s = max(s_min_max[0], min(s_min_max[1], s))
+            S[a0 + i] = s
+            W1[a0 + i].mul_(s)
+            if B1 is not None:
+                B1[a0 + i].mul_(s)
+            if bn_w is not None:
+                bn_w[a0 + i].mul_(s)
+            if bn_b is not None:
+                bn_b[a0 + i].mul_(s)
+            W2[o0:o1, i].mul_(1 / s)
+    return W1, W2, B1, S
+
+
+def cle_iteration(weights, biases, bn, relations):
+    """One pass of cross_layer_equalization's while-loop body
+    (Cross_layer_equal.py:81-115): snapshot every target weight (the deepcopy's
+    cost on the weights), equalize every relation in order, then the metric
+    np.sum([float(mean(|W - W_old|))]).  ``weights``/``biases``: name -> CPU
+    tensor (updated in place); ``bn``: name -> (fake_weight, fake_bias);
+    ``relations``: [(first, second, bn_name)].  Returns the iteration's diff."""
+    import numpy as np
+    old = {k: w.clone() for k, w in weights.items()}
+    for a, b, n in relations:
+        if biases.get(a) is None:
+            biases[a] = torch.zeros(weights[a].size(0), dtype=torch.float32)
+        fw, fb = bn[n]
+        layer_equalization(weights[a], weights[b], biases[a], fw, fb)
+    return float(np.sum([float(torch.mean(torch.abs(weights[k] - old[k]))) for k in weights]))
+
+
+def quantize_error_spatial(w: torch.Tensor, num_bits=8, signed=False) -> torch.Tensor:
+    """bias_correction.py:111-144 (_quantize_error: per-tensor quantize of a
+    clone, minus the weight) followed by the spatial sum bias correction takes of
+    it (bias_correction.py:231): E[o, i] = sum_k (Q(W) - W)[o, i, k]."""
+    p = w.detach().clone()
+    q = quantize(p, num_bits, float(p.min()), float(p.max()), signed)
+    err = q - p
+    return err.view(err.size(0), err.size(1) if err.dim() > 1 else 1, -1).sum(-1)
