@@ -1336,6 +1336,26 @@ __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32
 // read an acquire.  The launch counter's members are the chunks with tiles AND
 // the range blocks, so the stop rule (which advances st->iters, whose parity the
 // range blocks write under) runs only after every block has read it.
+// Arrival on a block-to-block hand-off counter (chunk tiles -> chunk sum -> stop
+// rule).  The words handed over (level-1 sums, chunk tails, chunk sums) are
+// written with agent-coherent stores (st_coh) and read with agent-coherent loads
+// (ld_coh), and the caller has drained its stores (s_waitcnt vmcnt(0)) first.
+//   ordered = 0 (product): the ISA's ordering -- a drained sc1 store has been
+//     performed at the agent coherence point before the counter RMW is issued,
+//     and the winner issues its sc1 loads only after its RMW has returned, so it
+//     observes every arrival's words.  No L2 write-back.
+//   ordered = 1 (diagnostics DFQ_CLE_ORDERED=1): the memory model's ordering --
+//     release on every arrival, acquire in the winner.  Each release writes the
+//     arriving block's XCD L2 back (buffer_wbl2): measured +2.7 ms (+50 %) on the
+//     MobileNetV2 loop with the round-2 schedule, same results.
+__device__ __forceinline__ bool handoff_arrive(uint32_t* c, uint32_t target, int ordered) {
+    const uint32_t a = ordered ? __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
+                               : __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = a == target;
+    if (last && ordered) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return last;
+}
+
 struct CleFin {
     uint32_t* cnt;
     float* part;
@@ -1343,6 +1363,7 @@ struct CleFin {
     double* hist;
     int64_t nchunks, nbig;   // all chunks / chunks with tiles (len >= 8)
     int32_t S, nl;
+    int32_t ordered;   // hand-off ordering (handoff_arrive)
 };
 
 __global__ void __launch_bounds__(kThreads)
@@ -1360,16 +1381,11 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
     if (st->done) return;
     const uint32_t round = (uint32_t)st->iters + 1u;
     const int64_t nrb = (int64_t)gridDim.x - ntb;
-    // Arrival on counter c (agent-scope release: this block's coherent stores are
-    // visible before the count is); returns whether this block arrived last.
+    // Arrival on counter c (handoff_arrive); returns whether this block arrived last.
     auto arrive = [&](uint32_t* c, uint32_t members) -> bool {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t a = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            flag = a == round * members - 1u;
-            if (flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the winner sees every arrival's stores
-        }
+        if (threadIdx.x == 0) flag = handoff_arrive(c, round * members - 1u, F.ordered);
         __syncthreads();
         return flag != 0;
     };
@@ -1420,6 +1436,160 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
                    lds + kCleTile + kCleTailWords, hook);
 }
 
+// ---------------------------------------------------------------------------
+// Chain-grouped iteration: ONE launch per CLE iteration.  Chains commute (no
+// tensor in common), so each chain gets its own group of blocks, sized to its
+// bytes, that runs the chain's relations in order with group-local barriers
+// (none for a one-block group), then the chain's next-iteration ranges and the
+// metric tiles of the chain's layers; the launch's last arrival runs the stop
+// rule (as cle_loop_tiles_fin_kernel).  A short chain no longer waits for the
+// longest one at every step, and an iteration is one kernel boundary instead of
+// steps + 1.
+//
+// Group barriers are monotone arrival counters (one 128-B line per group; the
+// b-th barrier of the run completes at (b + 1) x members): agent-scope release
+// before arriving, acquire after the wait.  The blocks of a group must be
+// co-resident: the plan caps the grid at the CU count (one block per CU at most,
+// whatever else shares the GPU), and a wait that exceeds ~1 s flags st->error
+// (the host reports it) instead of hanging.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kCleBarrierSpins = 1u << 20;
+
+// Wait until the counter at w reaches target (wrap-safe); ~1 s without progress
+// flags st->error and gives up (a fault cannot hang the GPU).
+__device__ __forceinline__ bool cle_spin_until(const uint32_t* w, uint32_t target, CleState* st) {
+    uint32_t spins = 0;
+    while ((int32_t)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kCleBarrierSpins) {
+            __hip_atomic_store(&st->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+    return true;
+}
+
+struct CleGroup {
+    int32_t blk0, nblk;     // blocks [blk0, blk0 + nblk)
+    int32_t nsteps;         // relations in the chain (0: a group of layers no relation touches)
+    int32_t step_off;       // index of the chain's first step bound in CleGroups::abound
+    int64_t r0, r1;         // next-iteration range tasks (fused schedule)
+    int64_t u0, u1;         // metric units of the chain's layers
+};
+
+struct CleGroups {
+    const CleGroup* groups;
+    const int32_t* group_of_blk;
+    const int64_t* abound;  // per chain: nsteps + 1 bounds into the apply task table
+    const CleTask* atasks;
+    const CleTask* rtasks;
+    uint32_t* gbar;         // [group * 32]: arrival counters
+};
+
+__device__ __forceinline__ bool cle_group_sync(uint32_t* ctr, uint32_t target, CleState* st, int* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        int good = cle_spin_until(ctr, target, st) ? 1 : 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
+        *flag = good;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+
+union CleGroupLds {
+    float tiles[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
+    CleApplyLds apply;
+};
+
+__global__ void __launch_bounds__(kThreads)
+cle_loop_group_kernel(CleGroups Gs, const CleRel* __restrict__ rels, uint32_t* __restrict__ rng, int64_t M,
+                      int is_signed, float eps, double smin, double smax, const CleLayer* __restrict__ layers,
+                      const CleChunk* __restrict__ chunks, const int64_t* __restrict__ b1off,
+                      const CleUnit* __restrict__ units, float* __restrict__ b1buf, float* __restrict__ tailbuf,
+                      CleFin F, CleState* __restrict__ st) {
+    __shared__ CleGroupLds L;
+    __shared__ int flag;
+    // read before this block's final arrival; the stop rule (which advances them)
+    // runs after every block of the launch has arrived
+    if (st->done) return;
+    const int32_t it = st->iters;
+    const uint32_t round = (uint32_t)it + 1u;
+    const int par = it & 1;
+    const CleGroup G = Gs.groups[Gs.group_of_blk[blockIdx.x]];
+    const int64_t blk = (int64_t)blockIdx.x - G.blk0, nblk = G.nblk;
+    uint32_t* ctr = Gs.gbar + 32 * (int64_t)Gs.group_of_blk[blockIdx.x];
+    // barriers per iteration: between steps, and before the post phase
+    const uint32_t per_it = (uint32_t)G.nsteps;
+    uint32_t nb = per_it * (uint32_t)it;
+    bool ok = true;
+    for (int32_t k = 0; k < G.nsteps && ok; ++k) {
+        const int64_t a0 = Gs.abound[G.step_off + k], a1 = Gs.abound[G.step_off + k + 1];
+        cle_apply_body(rels, Gs.atasks, a0, a1, rng, M, par, it == 0, is_signed, eps, smin, smax, blk, nblk, L.apply);
+        if (nblk > 1) {
+            ok = cle_group_sync(ctr, (++nb) * (uint32_t)nblk, st, &flag);
+        } else {
+            __syncthreads();
+        }
+    }
+    if (ok) {
+        // the chain's weights are final for this iteration: the next iteration's
+        // ranges (parity it + 1; its resets clear this iteration's words, no
+        // longer read) and the metric tiles of the chain's layers
+        cle_range_body(rels, Gs.rtasks, G.r0, G.r1, rng, M, par ^ 1, blk, nblk, L.tiles);
+        __syncthreads();
+    }
+    auto arrive = [&](uint32_t* c, uint32_t members) -> bool {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) flag = handoff_arrive(c, round * members - 1u, F.ordered);
+        __syncthreads();
+        return flag != 0;
+    };
+    auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1) {
+        if (!arrive(F.cnt + un.chunk, (uint32_t)(nb1 + 1))) return;   // not the chunk's last tile
+        const float* gb1 = b1buf + b1off[un.chunk];
+        const float* gtb = tailbuf + (int64_t)un.chunk * kCleTailWords;
+        const int64_t nw = 32 * nb1;
+        const bool staged = nw + kCleTailWords <= kCleTile;
+        float* lds = L.tiles;
+        if (staged) {
+            for (int64_t i = threadIdx.x; i < nw; i += kThreads) lds[i] = ld_coh(gb1 + i);
+            if (threadIdx.x < kCleTailWords) lds[nw + threadIdx.x] = ld_coh(gtb + threadIdx.x);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const float fa = staged ? cle_chunk_sum_with(ch, [&](int64_t i) { return lds[i]; },
+                                                         [&](int64_t i) { return lds[nw + i]; }, threadIdx.x)
+                                    : cle_chunk_sum(ch, gb1, gtb, threadIdx.x);
+            if (threadIdx.x == 0) st_coh(F.part + (int64_t)ch.layer * F.S + ch.t, 0.f + fa);
+        }
+        __syncthreads();   // LDS is reused by the next unit
+    };
+    if (ok)
+        cle_tiles_body(layers, chunks, b1off, units + G.u0, G.u1 - G.u0, b1buf, tailbuf, blk, nblk, L.tiles,
+                       L.tiles + kCleTile + kCleTailWords, hook);
+    // every block arrives once (after its chunk hand-offs): the last one runs the
+    // stop rule (a block that saw st->error still arrives, so nothing hangs)
+    if (arrive(F.cnt + F.nchunks, gridDim.x)) {
+        if (threadIdx.x == 0)
+            for (int64_t k = 0; k < F.nchunks; ++k) {
+                const CleChunk c2 = chunks[k];
+                if (c2.len < 8) st_coh(F.part + (int64_t)c2.layer * F.S + c2.t, 0.f + cle_tiny_chunk_sum(layers, c2));
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
+        cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(L.tiles),
+                                   stage_part ? L.tiles + 2048 : nullptr);
+        if (threadIdx.x == 0 && __hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            st->done = 1;
+    }
+}
+
 // Grid-barrier words of the persistent loop (layout below); the plan's tables
 // reserve them in every build.
 constexpr int kCleMaxXcd = 16;
@@ -1462,8 +1632,6 @@ struct ClePersist {
     float eps;
     double smin, smax;
 };
-
-constexpr uint32_t kCleBarrierSpins = 1u << 20;
 
 // Sense-reversing grid barrier: agent-scope release (this block's writes, the
 // XCD's L2 written back) before arriving, acquire after leaving.
@@ -1526,18 +1694,6 @@ __device__ __forceinline__ uint32_t xcc_id() {
     uint32_t x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
     return x & (kCleMaxXcd - 1);
-}
-
-__device__ __forceinline__ bool cle_spin_until(const uint32_t* w, uint32_t target, CleState* st) {
-    uint32_t spins = 0;
-    while ((int32_t)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > kCleBarrierSpins) {
-            __hip_atomic_store(&st->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
-        }
-    }
-    return true;
 }
 
 __device__ __forceinline__ bool cle_grid_sync_xcd(CleXcdSync& S, CleState* st) {
@@ -1694,6 +1850,15 @@ struct dfq_cle_plan {
     bool fin_fused = false;         // combine + stop rule folded into the tiles launch
     int64_t nbig = 0;               // chunks with tiles
     int32_t persist_grid = -1;      // cooperative grid of the persistent loop (0: not usable; -1: not sized)
+    // chain-grouped schedule (cle_loop_group_kernel): one launch per iteration
+    bool grouped = false;
+    int32_t ngroups = 0, group_grid = 0;
+    CleGroup* d_groups = nullptr;
+    int32_t* d_gblk = nullptr;
+    int64_t* d_gbound = nullptr;
+    CleTask* d_gat = nullptr;
+    CleTask* d_grt = nullptr;
+    uint32_t* d_gbar = nullptr;     // group barrier counters [group * 32]
 };
 
 // DFQ_CLE_TIMING: host-side phase times of create / run / destroy on stderr.
@@ -1853,30 +2018,47 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     // tasks: per-step range + rescale launches, or (fused) one range launch for
     // every relation's W2 (and untouched W1) followed by the rescale launches
     std::vector<CleTask> rt, at;
+    std::vector<CleTask>* rout = &rt;   // where the range-task builders emit
     std::vector<int64_t> rstep(1, 0), astep(1, 0);
     auto w2_range_tasks = [&](int32_t r) {
         const CleRel& c = R[r];
         if (c.i2 == 1) {
             for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
-                rt.push_back({r, kRangeW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), 0, 0});
+                rout->push_back({r, kRangeW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), 0, 0});
         } else {
             for (int64_t a = 0; a < c.o2; a += kColTileRows)
                 for (int64_t i0 = 0; i0 < c.i2; i0 += kThreads)
-                    rt.push_back({r, kRangeW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2), i0,
-                                  std::min<int64_t>(i0 + kThreads, c.i2)});
+                    rout->push_back({r, kRangeW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2), i0,
+                                     std::min<int64_t>(i0 + kThreads, c.i2)});
             for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
-                rt.push_back({r, kRangeReset, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
+                rout->push_back({r, kRangeReset, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
         }
     };
     auto w1_range_tasks = [&](int32_t r) {
         const CleRel& c = R[r];
         if (fused && w1_src[r] >= 0) {   // produced by the previous relation's rescale: reset the next parity
             for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
-                rt.push_back({r, kRangeResetW1, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
+                rout->push_back({r, kRangeResetW1, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
         } else {
             for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
-                rt.push_back({r, kRangeW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
+                rout->push_back({r, kRangeW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
         }
+    };
+    auto apply_tasks = [&](int32_t r, std::vector<CleTask>& out) {
+        const CleRel& c = R[r];
+        for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
+            out.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
+        if (c.i2 == 1) {
+            for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
+                out.push_back({r, kApplyW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), 0, 0});
+        } else {
+            for (int64_t a = 0; a < c.o2; a += kColTileRows)
+                for (int64_t i0 = 0; i0 < c.i2; i0 += kThreads)
+                    out.push_back({r, kApplyW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2), i0,
+                                   std::min<int64_t>(i0 + kThreads, c.i2)});
+        }
+        for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
+            out.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
     };
     if (fused) {
         for (int32_t r = 0; r < n_rel; ++r) {
@@ -1888,24 +2070,11 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     for (int32_t k = 0; k < steps; ++k) {
         for (int32_t r = 0; r < n_rel; ++r) {
             if (step_of[r] != k) continue;
-            const CleRel& c = R[r];
             if (!fused) {
                 w1_range_tasks(r);
                 w2_range_tasks(r);
             }
-            for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
-                at.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
-            if (c.i2 == 1) {
-                for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
-                    at.push_back({r, kApplyW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), 0, 0});
-            } else {
-                for (int64_t a = 0; a < c.o2; a += kColTileRows)
-                    for (int64_t i0 = 0; i0 < c.i2; i0 += kThreads)
-                        at.push_back({r, kApplyW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2), i0,
-                                      std::min<int64_t>(i0 + kThreads, c.i2)});
-            }
-            for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
-                at.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
+            apply_tasks(r, at);
         }
         if (!fused) rstep.push_back((int64_t)rt.size());
         astep.push_back((int64_t)at.size());
@@ -1951,6 +2120,105 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 for (int64_t g = 0; g <= nb1; ++g) units.push_back(CleUnit{ci, (int32_t)g});
         }
     }
+    // Chain-grouped schedule (cle_loop_group_kernel): one group of blocks per
+    // chain, plus one for the layers no relation touches; units reordered so each
+    // group's metric units are contiguous.
+    std::vector<CleGroup> groups;
+    std::vector<int32_t> group_of_blk;
+    std::vector<int64_t> gbound;
+    std::vector<CleTask> gat, grt;
+    bool grouped = fused && n_targets <= 128 && !units.empty() && !ab_env("DFQ_CLE_UNFUSED_FIN");
+    if (const char* ge = ab_env("DFQ_CLE_GROUPS")) grouped = grouped && ge[0] != '0';
+    if (grouped) {
+        std::vector<int32_t> chain_id(n_rel, -1), root_chain(n_rel, -1);
+        int32_t nch = 0;
+        for (int32_t r = 0; r < n_rel; ++r) {
+            const int32_t c = find(r);
+            if (root_chain[c] < 0) root_chain[c] = nch++;
+            chain_id[r] = root_chain[c];
+        }
+        std::vector<int32_t> layer_group(n_targets, nch);   // nch: no relation touches it
+        for (int32_t l = 0; l < n_targets; ++l)
+            for (int32_t r = 0; r < n_rel; ++r)
+                if (targets[l] == R[r].w1 || targets[l] == R[r].w2) layer_group[l] = chain_id[r];
+        const int32_t ngroups = nch + 1;
+        std::vector<double> work(ngroups, 0.0);
+        groups.assign(ngroups, CleGroup{});
+        for (int32_t c = 0; c < ngroups; ++c) {
+            CleGroup& g = groups[c];
+            g.step_off = (int32_t)gbound.size();
+            gbound.push_back((int64_t)gat.size());
+            g.r0 = (int64_t)grt.size();
+            for (int32_t r = 0; r < n_rel; ++r) {
+                if (chain_id[r] != c) continue;
+                apply_tasks(r, gat);
+                gbound.push_back((int64_t)gat.size());
+                g.nsteps += 1;
+                rout = &grt;
+                w1_range_tasks(r);
+                w2_range_tasks(r);
+                rout = &rt;
+                const CleRel& q = R[r];
+                work[c] += 8.0 * (double)(q.c1 * q.len1 + q.o2 * q.i2 * q.khw2) + 4.0 * (double)(q.o2 * q.i2 * q.khw2);
+            }
+            g.r1 = (int64_t)grt.size();
+        }
+        // units by group (stable: a chunk's units stay in tile order)
+        std::vector<CleUnit> sorted;
+        sorted.reserve(units.size());
+        for (int32_t c = 0; c < ngroups; ++c) {
+            groups[c].u0 = (int64_t)sorted.size();
+            for (const CleUnit& u : units)
+                if (layer_group[chunks[u.chunk].layer] == c) {
+                    sorted.push_back(u);
+                    work[c] += 12.0 * (double)std::min<int64_t>(kCleTile, chunks[u.chunk].len);
+                }
+            groups[c].u1 = (int64_t)sorted.size();
+        }
+        units.swap(sorted);
+        // blocks: at most one per CU (co-residency of every group), one at least per
+        // non-empty group, the rest in proportion to the group's bytes
+        int dev = 0, cus = 0;
+        int64_t budget = 256;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            budget = cus;
+        if (const char* e = ab_env("DFQ_CLE_GROUP_GRID")) budget = std::max<int64_t>(1, atoll(e));
+        std::vector<int64_t> nb(ngroups, 0);
+        double wsum = 0.0;
+        int64_t used = 0;
+        for (int32_t c = 0; c < ngroups; ++c)
+            if (work[c] > 0.0 || groups[c].u1 > groups[c].u0) {
+                nb[c] = 1;
+                ++used;
+                wsum += work[c];
+            }
+        if (used == 0 || used > budget) {
+            grouped = false;
+        } else {
+            const int64_t spare = budget - used;
+            std::vector<std::pair<double, int32_t>> rem;
+            int64_t given = 0;
+            for (int32_t c = 0; c < ngroups; ++c) {
+                if (!nb[c] || wsum <= 0.0) continue;
+                const double want = spare * work[c] / wsum;
+                const int64_t k = (int64_t)want;
+                nb[c] += k;
+                given += k;
+                rem.push_back({want - (double)k, c});
+            }
+            std::sort(rem.begin(), rem.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+            for (size_t i = 0; i < rem.size() && given < spare; ++i, ++given) nb[rem[i].second] += 1;
+            for (int32_t c = 0; c < ngroups; ++c) {
+                groups[c].blk0 = (int32_t)group_of_blk.size();
+                groups[c].nblk = (int32_t)nb[c];
+                for (int64_t b = 0; b < nb[c]; ++b) group_of_blk.push_back(c);
+            }
+        }
+    }
+    p->grouped = grouped;
+    p->ngroups = (int32_t)groups.size();
+    p->group_grid = (int32_t)group_of_blk.size();
     p->nunits = (int64_t)units.size();
     p->M = M;
     p->nl = n_targets;
@@ -1972,7 +2240,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_chunks = T.add<CleChunk>((int64_t)chunks.size());
     const int64_t o_units = T.add<CleUnit>((int64_t)units.size());
     const int64_t o_b1off = T.add<int64_t>((int64_t)b1off.size());
-    const int64_t host_bytes = T.total;   // the tables above are built on the host
+    const int64_t host_bytes = T.total;   // the tables above are built on the host (and the group tables)
     const int64_t o_b1 = T.add<float>(32 * nb1_total);
     const int64_t o_tail = T.add<float>(kCleTailWords * (int64_t)chunks.size());
     const int64_t o_rng = T.add<uint32_t>(4 * M);
@@ -1983,6 +2251,12 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_hist = T.add<double>(kCleHistCap);
     const int64_t o_bar = T.add<uint32_t>(kCleBarWords);
     const int64_t o_cnt = T.add<uint32_t>((int64_t)chunks.size() + 1);
+    const int64_t o_groups = T.add<CleGroup>((int64_t)groups.size());
+    const int64_t o_gblk = T.add<int32_t>((int64_t)group_of_blk.size());
+    const int64_t o_gbound = T.add<int64_t>((int64_t)gbound.size());
+    const int64_t o_gat = T.add<CleTask>((int64_t)gat.size());
+    const int64_t o_grt = T.add<CleTask>((int64_t)grt.size());
+    const int64_t o_gbar = T.add<uint32_t>(32 * (int64_t)std::max<size_t>(groups.size(), 1));
     const double tm0 = now_us();
     if ((e = hipMalloc(&p->d_tables, T.total)) != hipSuccess) return fail(e);
     const double tm1 = now_us();
@@ -1994,6 +2268,16 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     put(o_rels, R); put(o_rt, rt); put(o_at, at); put(o_layers, layers); put(o_chunks, chunks); put(o_units, units);
     put(o_b1off, b1off);
     if ((e = hipMemcpy(base, blob.data(), host_bytes, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    if (grouped) {   // the group tables sit after the device-only buffers: one more copy
+        const int64_t g0 = o_groups, g1 = o_gbar;
+        std::vector<char> gblob(g1 - g0, 0);
+        auto gput = [&](int64_t off, const auto& v) {
+            if (!v.empty()) std::memcpy(gblob.data() + (off - g0), v.data(), sizeof(v[0]) * v.size());
+        };
+        gput(o_groups, groups); gput(o_gblk, group_of_blk); gput(o_gbound, gbound); gput(o_gat, gat);
+        gput(o_grt, grt);
+        if ((e = hipMemcpy(base + g0, gblob.data(), g1 - g0, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    }
     if (cle_timing())
         fprintf(stderr, "DFQ_CLE_TIMING create: hipMalloc %lld B %.1f us, copy %lld B %.1f us\n", (long long)T.total,
                 tm1 - tm0, (long long)host_bytes, now_us() - tm1);
@@ -2013,6 +2297,12 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->d_hist = reinterpret_cast<double*>(base + o_hist);
     p->d_bar = reinterpret_cast<uint32_t*>(base + o_bar);
     p->d_cnt = reinterpret_cast<uint32_t*>(base + o_cnt);
+    p->d_groups = reinterpret_cast<CleGroup*>(base + o_groups);
+    p->d_gblk = reinterpret_cast<int32_t*>(base + o_gblk);
+    p->d_gbound = reinterpret_cast<int64_t*>(base + o_gbound);
+    p->d_gat = reinterpret_cast<CleTask*>(base + o_gat);
+    p->d_grt = reinterpret_cast<CleTask*>(base + o_grt);
+    p->d_gbar = reinterpret_cast<uint32_t*>(base + o_gbar);
     for (const auto& c : chunks) p->nbig += c.len >= 8 ? 1 : 0;
     p->fin_fused = p->nunits > 0 && p->nbig > 0 && n_targets <= 128 && !ab_env("DFQ_CLE_UNFUSED_FIN");
     p->hist_cap = kCleHistCap;
@@ -2020,8 +2310,25 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     return DFQ_OK;
 }
 
+// Hand-off ordering of the tiles / stop-rule arrivals (handoff_arrive): the
+// ISA's (0) in the product, the memory model's release/acquire (1) as a
+// diagnostics A/B (DFQ_CLE_ORDERED=1).
+static int32_t cle_ordered() {
+    const char* e = ab_env("DFQ_CLE_ORDERED");
+    return (e && e[0] == '1') ? 1 : 0;
+}
+
 // One CLE iteration's launches (steps, metric, stop rule) on stream s.
 static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
+    if (p->grouped) {   // the whole iteration in one launch
+        CleGroups Gs{p->d_groups, p->d_gblk, p->d_gbound, p->d_gat, p->d_grt, p->d_gbar};
+        CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
+        hipLaunchKernelGGL(cle_loop_group_kernel, dim3(p->group_grid), dim3(kThreads), 0, s, Gs, p->d_rels, p->d_rng,
+                           p->M, p->is_signed, p->eps, p->smin, p->smax, p->d_layers, p->d_chunks, p->d_b1off,
+                           p->d_units, p->d_b1, p->d_tail, F, p->d_state);
+        DFQ_LAUNCH_CHECK();
+        return DFQ_OK;
+    }
     // grid caps: 2,048 / 4,096 blocks (caps of 128-1,024 measured 4-150 % slower on MobileNetV2)
     // step / tile grid caps (A/B: DFQ_CLE_STEP_GRID / DFQ_CLE_TILE_GRID, diagnostics library)
     static const int64_t kStepGrid = [] {
@@ -2053,7 +2360,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
     const int64_t nr = p->fused ? p->rstep[1] - p->rstep[0] : 0;   // next iteration's range tasks
     const int64_t ntb = std::min<int64_t>(p->nunits, kTileGrid), nrb = std::min<int64_t>(nr, kStepGrid);
     if (p->fin_fused) {   // tiles (+ ranges) + chunk combine + stop rule: one launch
-        CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl};
+        CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
         hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
                            p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
                            p->d_rtasks, p->rstep[0], p->fused ? p->rstep[1] : p->rstep[0], p->d_rng, p->M, F,
@@ -2170,6 +2477,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     }
     DFQ_HIP_CHECK(hipMemsetAsync(p->d_part, 0, sizeof(float) * p->slots * std::max(p->nl, 1), s));
     DFQ_HIP_CHECK(hipMemsetAsync(p->d_cnt, 0, sizeof(uint32_t) * (p->nchunks + 1), s));
+    if (p->grouped) DFQ_HIP_CHECK(hipMemsetAsync(p->d_gbar, 0, sizeof(uint32_t) * 32 * p->ngroups, s));
     if (p->nchunks > 0) {
         hipLaunchKernelGGL(cle_loop_snap_kernel, dim3((int)std::min<int64_t>(std::max<int64_t>(p->nunits, 1), 4096)),
                            dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_units, p->nunits);
@@ -2264,6 +2572,10 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         fprintf(stderr, "DFQ_CLE_TIMING run: capture+instantiate %.1f us, loop %.1f us (%d iterations launched)\n",
                 tc1 - tc0, now_us() - tc1, launched);
     const CleState fin = *p->h_state;
+    if (fin.error) {   // a group barrier gave up (blocks not co-resident): never expected
+        set_last_hip_error(hipErrorLaunchTimeOut);
+        return DFQ_ERR_HIP;
+    }
     if (ab_env("DFQ_CLE_DEBUG")) {   // per-layer chunk sums of the last iteration run
         std::vector<float> part((size_t)p->slots * std::max(p->nl, 1));
         DFQ_HIP_CHECK(hipMemcpy(part.data(), p->d_part, sizeof(float) * part.size(), hipMemcpyDeviceToHost));
@@ -2284,7 +2596,9 @@ extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t
     if (chains) *chains = p->chains;
     if (steps) *steps = p->steps;
     if (launches) {   // per iteration: range + rescale launches, then the metric (2) and the stop rule
-        if (p->fin_fused)   // rescales (+ per-step ranges), then tiles + ranges + combine + stop rule
+        if (p->grouped)
+            *launches = 1;
+        else if (p->fin_fused)   // rescales (+ per-step ranges), then tiles + ranges + combine + stop rule
             *launches = (p->fused ? p->steps : 2 * p->steps) + 1;
         else
             *launches = (p->fused ? p->steps + ((p->nunits > 0 && p->nchunks > 0) ? 0 : 1) : 2 * p->steps) +
