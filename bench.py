@@ -29,6 +29,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 from pathlib import Path
@@ -62,7 +63,9 @@ def parse():
     p.add_argument("--no-parity", action="store_true",
                    help="skip the parity checks of the timed outputs (vs the C oracle) and of the MobileNetV2 "
                         "pipeline (vs the reference fixture)")
-    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r02.json"))
+    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r03.json"),
+                   help="the committed rocprofv3 summary of this bench command (scripts/profile.sh + "
+                        "scripts/summarize_profile.py): PMC traffic and the kernel's rocprof average")
     return p.parse_args()
 
 
@@ -485,7 +488,9 @@ def cpu_baseline_transforms(dev, seconds):
             "cle_s_per_iteration": round(per_it, 4), "cle_iterations_timed": len(times),
             "cle_iterations_reference": len(ref_diffs),
             "cle_loop_s_est": round(per_it * len(ref_diffs), 2),
-            "cle_diffs_match_reference": diffs == ref_diffs[:len(diffs)],
+            "cle_diffs_max_rel_dev_vs_reference": float(max(abs(a - b) / abs(b) for a, b in zip(diffs, ref_diffs))),
+            "cle_diffs_note": "the port runs torch.sqrt through this host's MKL path; the fixtures were made with "
+                              "MKL_CBWR=AVX2 (IEEE sqrt), so the two agree to ~1 ulp per step (DESIGN.md 3.3)",
             "bc_error_reduction_ms": round(min(bc) * 1e3, 3),
             "bc_error_reduction_GBs": round(4 * elems / min(bc) / 1e9, 3),
             "sample": f"MobileNetV2 after BN fold ({len(relations)} relations, {len(tk)} target layers, {elems} "
@@ -692,13 +697,24 @@ def main():
             obj.destroy()
     del sw, plan, run
     torch.cuda.empty_cache()
-    traffic = None
+    traffic, prof = None, None
     tj = Path(args.traffic_json)
     if tj.exists():
         try:
-            traffic = json.loads(tj.read_text()).get("hbm_bytes_per_launch")
+            tr = json.loads(tj.read_text())
+            traffic = tr.get("hbm_bytes_per_launch")
+            avg_ms = tr["rocprof_avg_ns"] / 1e6
+            prof = {"source": str(tj.relative_to(ROOT)) if tj.is_relative_to(ROOT) else str(tj),
+                    "rocprof_kernel_avg_ms": round(avg_ms, 4),
+                    "frac_at_rocprof_avg": round(tr["algo_bytes_per_launch"] / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                                                 4),
+                    "same_process_hip_event_ms": tr.get("same_process_hip_event_ms"),
+                    "note": "rocprofv3 --kernel-trace --stats of `python bench.py` (same command, committed "
+                            "build) on the lease box named in the summary; HIP-event frac above is this run's box"}
+            if tr.get("algo_bytes_per_launch") != st["algo_bytes"]:
+                prof["warning"] = "the profiled workload's algorithmic bytes differ from this run's"
         except Exception:
-            traffic = None
+            traffic, prof = None, None
     sharded = sharded_single_model(dev, stream) if world > 1 and not args.no_secondary else None
     res = None
     if rank == 0:
@@ -733,6 +749,7 @@ def main():
             "codes": f"{args.bits}-bit grid indices stored as "
                      f"{'int16' if args.bits > 8 else ('uint8' if args.asym else 'int8')}",
             "data": "synthetic random-init weights of the reference shapes (no checkpoints offline)",
+            "box": socket.gethostname(),
             "config": {
                 "workload": f"{args.model} x{copies} weight sets in one layer list: {args.granularity} "
                             f"{'asym' if args.asym else 'sym'} INT{args.bits} quantize-dequantize + codes + "
@@ -763,12 +780,16 @@ def main():
                 "grid_blocks": st["grid_blocks"],
                 "variant": st["variant"],
                 "rank": 0,
-                "same_mix_probe_GBs": probe_lds,
-                "same_mix_probe_note": "the sweep's memory pattern (LDS-DMA wave tasks, nt stores) without "
-                                       "arithmetic, measured on this box after the timed steps (box to box "
-                                       "5.2-6.5 TB/s, the sweep 5.9-6.3); a VGPR grid-stride stream of the "
-                                       f"same mix: {probe_stream} GB/s",
+                "traffic_source": ("PMC FETCH_SIZE (x2, the gfx950 correction) + WRITE_SIZE per launch from "
+                                   f"{prof['source']}: separate rocprofv3 --pmc passes over this bench command, "
+                                   "not measured in this run") if prof else None,
+                "profile": prof,
             },
+            "memory_pattern_probe": {
+                "lds_dma_GBs": probe_lds, "vgpr_stream_GBs": probe_stream,
+                "note": "the sweep's read 4 B / write 9 B per element pattern without arithmetic, on this box after "
+                        "the timed steps.  NOT a ceiling: box to box it lands 5.2-6.5 TB/s, sometimes below the "
+                        "sweep itself, so it only shows how far arithmetic and row logic cost on this box"},
             "parity": parity,
             "sharded_modes": modes,
             "cpu_baseline": cpu,

@@ -1340,10 +1340,13 @@ __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32
 // rule).  The words handed over (level-1 sums, chunk tails, chunk sums) are
 // written with agent-coherent stores (st_coh) and read with agent-coherent loads
 // (ld_coh), and the caller has drained its stores (s_waitcnt vmcnt(0)) first.
-//   ordered = 0 (product): the ISA's ordering -- a drained sc1 store has been
-//     performed at the agent coherence point before the counter RMW is issued,
-//     and the winner issues its sc1 loads only after its RMW has returned, so it
-//     observes every arrival's words.  No L2 write-back.
+//   ordered = 0 (product): the sc1 hand-off form MI355X_MICROARCH.md lists as
+//     valid (section "visibility", Valid forms, table row 1; cdna_hip_programming.md
+//     Guideline 16): every handed-off word stored sc1 and drained by every storing
+//     wave before ONE lane's agent-scope counter add (behind the workgroup
+//     barrier), the workgroup whose add came last told by the returned value, and
+//     every load of the words an sc1 load to registers issued after that add
+//     returned (the other waves after a workgroup barrier).  No L2 write-back.
 //   ordered = 1 (diagnostics DFQ_CLE_ORDERED=1): the memory model's ordering --
 //     release on every arrival, acquire in the winner.  Each release writes the
 //     arriving block's XCD L2 back (buffer_wbl2): measured +2.7 ms (+50 %) on the
@@ -1352,7 +1355,10 @@ __device__ __forceinline__ bool handoff_arrive(uint32_t* c, uint32_t target, int
     const uint32_t a = ordered ? __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
                                : __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool last = a == target;
-    if (last && ordered) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (last && ordered) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the invalidate completes before the barrier
+    }
     return last;
 }
 
@@ -1484,15 +1490,23 @@ struct CleGroups {
     const CleTask* atasks;
     const CleTask* rtasks;
     uint32_t* gbar;         // [group * 32]: arrival counters
+    int32_t sync_mode;      // cle_group_sync mode (0 in the product)
 };
 
-__device__ __forceinline__ bool cle_group_sync(uint32_t* ctr, uint32_t target, CleState* st, int* flag) {
+// mode 1 (diagnostics timing A/B only, DFQ_CLE_GSYNC_NOFENCE=1): no fences --
+// results may be stale, it prices the fences
+__device__ __forceinline__ bool cle_group_sync(uint32_t* ctr, uint32_t target, CleState* st, int* flag,
+                                               int mode = 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (mode == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int good = cle_spin_until(ctr, target, st) ? 1 : 0;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (mode == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the invalidate completes before the barrier
+        }
         if (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
         *flag = good;
     }
@@ -1530,7 +1544,7 @@ cle_loop_group_kernel(CleGroups Gs, const CleRel* __restrict__ rels, uint32_t* _
         const int64_t a0 = Gs.abound[G.step_off + k], a1 = Gs.abound[G.step_off + k + 1];
         cle_apply_body(rels, Gs.atasks, a0, a1, rng, M, par, it == 0, is_signed, eps, smin, smax, blk, nblk, L.apply);
         if (nblk > 1) {
-            ok = cle_group_sync(ctr, (++nb) * (uint32_t)nblk, st, &flag);
+            ok = cle_group_sync(ctr, (++nb) * (uint32_t)nblk, st, &flag, Gs.sync_mode);
         } else {
             __syncthreads();
         }
@@ -2216,6 +2230,12 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             }
         }
     }
+    if (grouped && cle_timing())
+        for (size_t c = 0; c < groups.size(); ++c)
+            fprintf(stderr, "DFQ_CLE_TIMING group %zu: blocks %d, steps %d, apply tasks %lld, range tasks %lld, units %lld\n",
+                    c, groups[c].nblk, groups[c].nsteps,
+                    (long long)(gbound[groups[c].step_off + groups[c].nsteps] - gbound[groups[c].step_off]),
+                    (long long)(groups[c].r1 - groups[c].r0), (long long)(groups[c].u1 - groups[c].u0));
     p->grouped = grouped;
     p->ngroups = (int32_t)groups.size();
     p->group_grid = (int32_t)group_of_blk.size();
@@ -2321,7 +2341,8 @@ static int32_t cle_ordered() {
 // One CLE iteration's launches (steps, metric, stop rule) on stream s.
 static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
     if (p->grouped) {   // the whole iteration in one launch
-        CleGroups Gs{p->d_groups, p->d_gblk, p->d_gbound, p->d_gat, p->d_grt, p->d_gbar};
+        const char* nf = ab_env("DFQ_CLE_GSYNC_NOFENCE");
+        CleGroups Gs{p->d_groups, p->d_gblk, p->d_gbound, p->d_gat, p->d_grt, p->d_gbar, (nf && nf[0] == '1') ? 1 : 0};
         CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
         hipLaunchKernelGGL(cle_loop_group_kernel, dim3(p->group_grid), dim3(kThreads), 0, s, Gs, p->d_rels, p->d_rng,
                            p->M, p->is_signed, p->eps, p->smin, p->smax, p->d_layers, p->d_chunks, p->d_b1off,

@@ -31,6 +31,14 @@ def main(tag, rnd, algo_bytes, workload):
            "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
            "algo_bytes_per_launch": algo_bytes, "rocprof_avg_ns": avg_ns,
            "algo_GBs_at_rocprof_avg": algo_bytes / avg_ns}
+    # the bench line printed by the profiled process itself: its HIP-event launch time
+    lines = [ln for ln in (src / "kt.log").read_text().splitlines() if ln.startswith("{")]
+    if lines:
+        (dst / "bench_under_rocprof.json").write_text(lines[-1] + "\n")
+        b = json.loads(lines[-1])
+        res["same_process_hip_event_ms"] = b["roofline"]["launch_ms"]
+        res["same_process_box"] = b.get("box")
+        res["rocprof_vs_hip_event"] = round(avg_ns / 1e6 / b["roofline"]["launch_ms"], 4)
     (ROOT / "profiles" / f"traffic_{rnd}.json").write_text(json.dumps(res, indent=1))
     print(json.dumps(res, indent=1))
 
