@@ -1332,10 +1332,7 @@ __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32
 // launches fewer per iteration.  Hand-offs between blocks go through
 // agent-coherent stores / loads and monotone arrival counters (cnt: one per
 // chunk, then one for the launch; zeroed by plan_run, iteration i's target is
-// (i + 1) x members), each arrival an agent-scope release and each winner's
-// read an acquire.  The launch counter's members are the chunks with tiles AND
-// the range blocks, so the stop rule (which advances st->iters, whose parity the
-// range blocks write under) runs only after every block has read it.
+// (i + 1) x members); the ordering of the hand-offs: handoff_arrive.
 // Arrival on a block-to-block hand-off counter (chunk tiles -> chunk sum -> stop
 // rule).  The words handed over (level-1 sums, chunk tails, chunk sums) are
 // written with agent-coherent stores (st_coh) and read with agent-coherent loads
@@ -1377,16 +1374,27 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
                           const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t nunits,
                           float* __restrict__ b1buf, float* __restrict__ tailbuf, int64_t ntb,
                           const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
-                          uint32_t* __restrict__ rng, int64_t M, CleFin F, CleState* __restrict__ st) {
+                          uint32_t* __restrict__ rng, int64_t M, CleFin F, CleState* __restrict__ st,
+                          int32_t par_next) {
     __shared__ float lds[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
     __shared__ int flag;
-    // st->iters and st->done are read here, before this block's arrival below, and
-    // written only by the stop rule, which runs after EVERY block of the launch
-    // (tile-chunk winners and range blocks alike) has arrived: a range block that
-    // is dispatched late still sees this iteration's parity.
+    // The stop rule (last chunk winner, this launch) advances st->iters and may set
+    // st->done while range blocks of the same launch are still being dispatched, so
+    // the range blocks take the next iteration's parity from the launch argument
+    // (iteration i of a graph batch of kCleBatch, an even count, from a batch start
+    // that is a multiple of it: parity (i + 1) & 1), never from st->iters.  A range
+    // block that starts after the stop rule said "done" skips its tasks: no later
+    // iteration reads them.  Tile blocks read st->iters before their arrival, and
+    // every tile block has arrived before the stop rule runs.
     if (st->done) return;
-    const uint32_t round = (uint32_t)st->iters + 1u;
     const int64_t nrb = (int64_t)gridDim.x - ntb;
+    if ((int64_t)blockIdx.x >= ntb) {
+        cle_range_body(rels, tasks, t0, t1, rng, M, par_next, blockIdx.x - ntb, nrb, lds);
+        return;
+    }
+    const uint32_t round = (uint32_t)st->iters + 1u;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (int32_t)(round & 1u) != par_next)   // never expected
+        __hip_atomic_store(&st->error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // Arrival on counter c (handoff_arrive); returns whether this block arrived last.
     auto arrive = [&](uint32_t* c, uint32_t members) -> bool {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1409,12 +1417,7 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
         cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
                                    stage_part ? lds + 2048 : nullptr);
     };
-    const uint32_t fin_members = (uint32_t)(F.nbig + nrb);
-    if ((int64_t)blockIdx.x >= ntb) {
-        cle_range_body(rels, tasks, t0, t1, rng, M, (round & 1u), blockIdx.x - ntb, nrb, lds);
-        if (arrive(F.cnt + F.nchunks, fin_members)) finish();
-        return;
-    }
+    const uint32_t fin_members = (uint32_t)F.nbig;
     auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1) {
         if (!arrive(F.cnt + un.chunk, (uint32_t)(nb1 + 1))) return;   // not the chunk's last tile
         {
@@ -2141,8 +2144,13 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     std::vector<int32_t> group_of_blk;
     std::vector<int64_t> gbound;
     std::vector<CleTask> gat, grt;
-    bool grouped = fused && n_targets <= 128 && !units.empty() && !ab_env("DFQ_CLE_UNFUSED_FIN");
-    if (const char* ge = ab_env("DFQ_CLE_GROUPS")) grouped = grouped && ge[0] != '0';
+    // A diagnostics A/B (DFQ_CLE_GROUPS=1): measured 2.3x SLOWER than the step
+    // launches on MobileNetV2 (15.2 vs 6.6 ms; profiles/r03/cle_grouped.md) -- one
+    // block per CU exposes the rescale tasks' dependent latencies that the step
+    // launches hide behind 8 blocks per CU, fences or not.
+    const char* ge = ab_env("DFQ_CLE_GROUPS");
+    bool grouped = ge && ge[0] == '1' && fused && n_targets <= 128 && !units.empty() &&
+                   !ab_env("DFQ_CLE_UNFUSED_FIN");
     if (grouped) {
         std::vector<int32_t> chain_id(n_rel, -1), root_chain(n_rel, -1);
         int32_t nch = 0;
@@ -2339,7 +2347,8 @@ static int32_t cle_ordered() {
 }
 
 // One CLE iteration's launches (steps, metric, stop rule) on stream s.
-static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
+// j: the iteration's position in its graph batch (its parity is j & 1).
+static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     if (p->grouped) {   // the whole iteration in one launch
         const char* nf = ab_env("DFQ_CLE_GSYNC_NOFENCE");
         CleGroups Gs{p->d_groups, p->d_gblk, p->d_gbound, p->d_gat, p->d_grt, p->d_gbar, (nf && nf[0] == '1') ? 1 : 0};
@@ -2385,7 +2394,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
         hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
                            p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
                            p->d_rtasks, p->rstep[0], p->fused ? p->rstep[1] : p->rstep[0], p->d_rng, p->M, F,
-                           p->d_state);
+                           p->d_state, (j + 1) & 1);
         DFQ_LAUNCH_CHECK();
         return DFQ_OK;
     }
@@ -2417,7 +2426,8 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s) {
     return DFQ_OK;
 }
 
-constexpr int32_t kCleBatch = 8;   // iterations enqueued between state read-backs
+constexpr int32_t kCleBatch = 8;   // iterations enqueued between state read-backs (even: see par_next)
+static_assert(kCleBatch % 2 == 0, "the tiles/range launch's parity argument assumes even batches");
 constexpr int32_t kClePersistBatch = 256;   // persistent loop: iterations per cooperative launch
 
 // The persistent loop's co-resident grid (0 = use the graph path).  Measured
@@ -2559,7 +2569,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     if (use_graph && !p->gexec && !init.done) {
         DFQ_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         int rc = DFQ_OK;
-        for (int32_t it = 0; it < kCleBatch && rc == DFQ_OK; ++it) rc = cle_enqueue_iteration(p, s);
+        for (int32_t it = 0; it < kCleBatch && rc == DFQ_OK; ++it) rc = cle_enqueue_iteration(p, s, it);
         hipGraph_t g = nullptr;
         const hipError_t ec = hipStreamEndCapture(s, &g);
         if (rc != DFQ_OK) {
@@ -2578,7 +2588,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
             DFQ_HIP_CHECK(hipGraphLaunch(p->gexec, s));
         } else {
             for (int32_t it = 0; it < kCleBatch; ++it) {
-                const int rc = cle_enqueue_iteration(p, s);
+                const int rc = cle_enqueue_iteration(p, s, it);
                 if (rc != DFQ_OK) return rc;
             }
         }

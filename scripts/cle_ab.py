@@ -22,14 +22,13 @@ os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_UNFUSED_FIN", "DFQ_CLE_GROUPS", "DFQ_CLE_GROUP_GRID", "DFQ_CLE_ORDERED", "DFQ_CLE_GSYNC_NOFENCE")
 CONFIGS = {
-    "grouped": {},
-    "grouped_ordered": {"DFQ_CLE_ORDERED": "1"},
-    "grouped_512": {"DFQ_CLE_GROUP_GRID": "512"},
-    "grouped_nofence": {"DFQ_CLE_GSYNC_NOFENCE": "1"},          # timing only: prices the barrier fences
-    "grouped_nofence_1024": {"DFQ_CLE_GSYNC_NOFENCE": "1", "DFQ_CLE_GROUP_GRID": "1024"},
-    "grouped_128": {"DFQ_CLE_GROUP_GRID": "128"},
-    "tiles_fin": {"DFQ_CLE_GROUPS": "0"},
-    "tiles_fin_ordered": {"DFQ_CLE_GROUPS": "0", "DFQ_CLE_ORDERED": "1"},
+    "tiles_fin": {},                                       # the product
+    "tiles_fin_ordered": {"DFQ_CLE_ORDERED": "1"},
+    "grouped": {"DFQ_CLE_GROUPS": "1"},
+    "grouped_ordered": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_ORDERED": "1"},
+    "grouped_512": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_GROUP_GRID": "512"},
+    "grouped_nofence": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_GSYNC_NOFENCE": "1"},   # timing only: stale results
+    "grouped_nofence_1024": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_GSYNC_NOFENCE": "1", "DFQ_CLE_GROUP_GRID": "1024"},
 }
 
 

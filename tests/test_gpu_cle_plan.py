@@ -115,13 +115,11 @@ def test_device_cle_matches_oracle(signed, eps, smm, thr, count, monkeypatch):
     # iteration's ranges, the chunk combine and the stop rule folded in; else
     # 2 x (range + rescale) + that launch
     diag = os.environ.get("DFQ_LIB") == "diag"   # the A/B switches exist in the diagnostics library only
-    if not diag or not (os.environ.get("DFQ_CLE_FUSED") == "0" or os.environ.get("DFQ_CLE_UNFUSED_FIN")
-                        or os.environ.get("DFQ_CLE_GROUPS") == "0"):
-        expect = 1   # chain-grouped: each chain's steps, ranges and tiles + the stop rule in one launch
-    else:
-        expect = 3 if os.environ.get("DFQ_CLE_FUSED") != "0" else 5
-        if os.environ.get("DFQ_CLE_UNFUSED_FIN"):
-            expect += 2   # A/B: the chunk combine and the stop rule as launches of their own
+    expect = 3 if not (diag and os.environ.get("DFQ_CLE_FUSED") == "0") else 5
+    if diag and os.environ.get("DFQ_CLE_UNFUSED_FIN"):
+        expect += 2   # A/B: the chunk combine and the stop rule as launches of their own
+    elif diag and os.environ.get("DFQ_CLE_GROUPS") == "1" and os.environ.get("DFQ_CLE_FUSED") != "0":
+        expect = 1    # A/B: chain-grouped, the whole iteration in one launch
     assert cle.LAST_RUN["launches_per_iteration"] == expect
     assert cle.LAST_RUN["diffs"] == diffs
     for k in W:
@@ -168,7 +166,7 @@ def test_device_cle_no_relations(monkeypatch):
 
 @pytest.mark.parametrize("name", ["mobilenetv2", "resnet50"])
 def test_persistent_loop_equals_graph_loop(name, monkeypatch):
-    """The graph-batched loop (the product: one chain-grouped launch per iteration) and the persistent
+    """The graph-batched multi-launch loop (the product) and the persistent
     cooperative loop (one launch, two-level grid barriers between chain steps;
     diagnostics library, DFQ_CLE_PERSIST_BPC=2 -- an A/B that measured slower)
     give the same weights, biases, scales, iteration count and diffs, bit for
