@@ -337,9 +337,36 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         return p;
     };
     auto one = [&](float xv, const QParams& p, float& qv) -> float {
-        float yv = qdq(xv, p, qv);
+        bool need;
+        float t = qdq_screen(xv, p, __builtin_amdgcn_rcpf(p.s), need);
+        if (__builtin_amdgcn_ballot_w64(need)) {   // wave-uniform, rare
+            if (need) t = qdq_exact_t(xv, p);
+        }
+        float yv = qdq_finish(t, p, qv);
         if (clip) yv = fminf(fmaxf(yv, T.clip_lo), T.clip_hi);
         return yv;
+    };
+    // four elements sharing one row's parameters: one reciprocal, one ballot
+    auto four = [&](const float4& xv, const QParams& p, float& q0, float& q1, float& q2, float& q3) -> float4 {
+        const float rs = __builtin_amdgcn_rcpf(p.s);
+        bool n0, n1, n2, n3;
+        float t0 = qdq_screen(xv.x, p, rs, n0), t1 = qdq_screen(xv.y, p, rs, n1);
+        float t2 = qdq_screen(xv.z, p, rs, n2), t3 = qdq_screen(xv.w, p, rs, n3);
+        if (__builtin_amdgcn_ballot_w64(n0 | n1 | n2 | n3)) {   // wave-uniform, rare
+            if (n0) t0 = qdq_exact_t(xv.x, p);
+            if (n1) t1 = qdq_exact_t(xv.y, p);
+            if (n2) t2 = qdq_exact_t(xv.z, p);
+            if (n3) t3 = qdq_exact_t(xv.w, p);
+        }
+        float4 y = make_float4(qdq_finish(t0, p, q0), qdq_finish(t1, p, q1), qdq_finish(t2, p, q2),
+                               qdq_finish(t3, p, q3));
+        if (clip) {
+            y.x = fminf(fmaxf(y.x, T.clip_lo), T.clip_hi);
+            y.y = fminf(fmaxf(y.y, T.clip_lo), T.clip_hi);
+            y.z = fminf(fmaxf(y.z, T.clip_lo), T.clip_hi);
+            y.w = fminf(fmaxf(y.w, T.clip_lo), T.clip_hi);
+        }
+        return y;
     };
 
     if constexpr (VEC) {
@@ -349,10 +376,8 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
             const float4 xv = reinterpret_cast<const float4*>(data)[j];
             const QParams p = params_for(4 * j);   // 4 | len, 4 | goff: one row per float4
             float q0, q1, q2, q3;
-            const float y0 = one(xv.x, p, q0);
-            const float y1 = one(xv.y, p, q1);
-            const float y2 = one(xv.z, p, q2);
-            const float y3 = one(xv.w, p, q3);
+            const float4 yq = four(xv, p, q0, q1, q2, q3);
+            const float y0 = yq.x, y1 = yq.y, y2 = yq.z, y3 = yq.w;
             if (T.dst) st<NT>(reinterpret_cast<float4*>(T.dst + base) + j, make_float4(y0, y1, y2, y3));
             if (T.codes) {
                 if (T.code_bytes == 1) {
