@@ -1893,7 +1893,8 @@ static double now_us() {
 struct CleDeviceCtx {
     std::mutex mu;
     hipStream_t st = nullptr;
-    CleState* h_state = nullptr;
+    CleState* h_state = nullptr;   // pinned: [0] the run's state, [1..2] the batch readback slots
+    hipEvent_t ev[2] = {nullptr, nullptr};
 };
 static CleDeviceCtx& cle_device_ctx(int dev) {
     static CleDeviceCtx ctx[64];
@@ -1904,7 +1905,9 @@ static CleDeviceCtx& cle_device_ctx(int dev) {
 static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
     hipError_t e = hipSuccess;
     if (!ctx.st) e = hipStreamCreateWithFlags(&ctx.st, hipStreamNonBlocking);
-    if (e == hipSuccess && !ctx.h_state) e = hipHostMalloc(&ctx.h_state, sizeof(CleState));
+    if (e == hipSuccess && !ctx.h_state) e = hipHostMalloc(&ctx.h_state, 3 * sizeof(CleState));
+    for (int i = 0; i < 2 && e == hipSuccess; ++i)
+        if (!ctx.ev[i]) e = hipEventCreateWithFlags(&ctx.ev[i], hipEventDisableTiming);
     return e;
 }
 
@@ -2582,8 +2585,14 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         DFQ_HIP_CHECK(ei);
     }
     const double tc1 = now_us();
+    // One batch in flight ahead of the stop-rule check: batch k + 1 is enqueued
+    // before the host waits for batch k's state, so the readback and the check
+    // overlap the GPU's next batch instead of idling it (round 2: ~31 us per
+    // batch boundary).  A batch enqueued after convergence runs as no-ops (every
+    // kernel returns at st->done).  Its state copy goes to the other pinned slot.
     int32_t launched = 0;
-    while (!init.done) {
+    int slot = 0;
+    auto enqueue_batch = [&](int sl) -> int {
         if (use_graph) {
             DFQ_HIP_CHECK(hipGraphLaunch(p->gexec, s));
         } else {
@@ -2593,15 +2602,29 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
             }
         }
         launched += kCleBatch;
-        DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
-        DFQ_HIP_CHECK(hipStreamSynchronize(s));
-        init = *p->h_state;
-        if (launched >= max_iters) break;
+        DFQ_HIP_CHECK(hipMemcpyAsync(ctx.h_state + 1 + sl, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
+        DFQ_HIP_CHECK(hipEventRecord(ctx.ev[sl], s));
+        return DFQ_OK;
+    };
+    if (!init.done) {
+        int rc = enqueue_batch(slot);
+        if (rc != DFQ_OK) return rc;
+        for (;;) {
+            const bool more = launched < max_iters;
+            if (more && (rc = enqueue_batch(slot ^ 1)) != DFQ_OK) return rc;
+            DFQ_HIP_CHECK(hipEventSynchronize(ctx.ev[slot]));
+            init = ctx.h_state[1 + slot];
+            if (init.done || !more) break;
+            slot ^= 1;
+        }
     }
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
     if (cle_timing())
         fprintf(stderr, "DFQ_CLE_TIMING run: capture+instantiate %.1f us, loop %.1f us (%d iterations launched)\n",
                 tc1 - tc0, now_us() - tc1, launched);
+    // the final state (a speculative batch after convergence changed nothing)
+    DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
+    DFQ_HIP_CHECK(hipStreamSynchronize(s));
     const CleState fin = *p->h_state;
     if (fin.error) {   // a group barrier gave up (blocks not co-resident): never expected
         set_last_hip_error(hipErrorLaunchTimeOut);
