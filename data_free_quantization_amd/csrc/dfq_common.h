@@ -160,7 +160,7 @@ __device__ __forceinline__ float qdq(float x, const QParams& p, float& q) {
 __device__ __forceinline__ float qdq_screen(float x, const QParams& p, float rs, bool& need) {
     const float a = (x + p.negmn) * rs;
     const float t = fminf(fmaxf(a, p.qmin - 1.0f), p.qmax + 1.0f);
-    const float d = t - floorf(t) - 0.5f;
+    const float d = __builtin_amdgcn_fractf(t) - 0.5f;   // v_fract: t - floor(t), exact for |t| < 2^24
     need = !(fabsf(d) > fabsf(t) * 0x1p-20f);
     return t;
 }
