@@ -65,8 +65,9 @@ constexpr Variant kVariants[] = {
     {1024, 64, true},     // 11: 1024-element tasks, next task's DMA in flight, NT
     {1024, 64, false},    // 12: variant 9 with the generic E sums (fewer VGPRs)
     {2048, 64, false},    // 13: variant 6 + per-task timestamps (diagnostics: dfq_debug_timeline)
+    {2048, 64, false},    // 14: variant 6 with the IEEE divide on every element (round-2 arithmetic)
 };
-constexpr int kNumVariants = 14;
+constexpr int kNumVariants = 15;
 // DevTask.nrows <= kGroupTag: a row-group piece of R = kGroupTag - nrows + 1 rows
 constexpr int kGroupTag = -64;
 constexpr int kGroupMaxRows = 16;
@@ -237,7 +238,10 @@ __device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTas
 // goff >= 0: a row-group piece whose per-row parameters are already in ls / lmn
 // (local row 0 = the row holding the piece's first element, goff = that element's
 // offset inside it).
-template <int MAXROWS, bool VEC, bool NT = false, int ESPEC = 2>
+// SCREEN: the screened reciprocal quantize (qdq_screen, the IEEE divide only near a
+// rounding boundary); false: the IEEE divide for every element (round-2 arithmetic,
+// diagnostics variant 14).  Bit-identical results.
+template <int MAXROWS, bool VEC, bool NT = false, int ESPEC = 2, bool SCREEN = true>
 __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& task, float* data, float* ls,
                                              float* lmn, const uint32_t* __restrict__ slot_min,
                                              const uint32_t* __restrict__ slot_max, int lane, float bmn = 0.f,
@@ -337,6 +341,11 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         return p;
     };
     auto one = [&](float xv, const QParams& p, float& qv) -> float {
+        if constexpr (!SCREEN) {
+            float yv = qdq(xv, p, qv);
+            if (clip) yv = fminf(fmaxf(yv, T.clip_lo), T.clip_hi);
+            return yv;
+        }
         bool need;
         float t = qdq_screen(xv, p, __builtin_amdgcn_rcpf(p.s), need);
         if (__builtin_amdgcn_ballot_w64(need)) {   // wave-uniform, rare
@@ -348,6 +357,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
     };
     // four elements sharing one row's parameters: one reciprocal, one ballot
     auto four = [&](const float4& xv, const QParams& p, float& q0, float& q1, float& q2, float& q3) -> float4 {
+        if constexpr (!SCREEN) return make_float4(one(xv.x, p, q0), one(xv.y, p, q1), one(xv.z, p, q2), one(xv.w, p, q3));
         const float rs = __builtin_amdgcn_rcpf(p.s);
         bool n0, n1, n2, n3;
         float t0 = qdq_screen(xv.x, p, rs, n0), t1 = qdq_screen(xv.y, p, rs, n1);
@@ -481,7 +491,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
 __device__ uint64_t* g_timeline = nullptr;
 __device__ int64_t g_timeline_cap = 0;
 
-template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false, int ESPEC = 2, bool TL = false>
+template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false, int ESPEC = 2, bool TL = false, bool SCREEN = true>
 __global__ void __launch_bounds__(kBlockThreads)
 sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restrict__ tasks, int64_t ntasks,
                   const uint32_t* __restrict__ slot_min, const uint32_t* __restrict__ slot_max) {
@@ -606,10 +616,10 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                 block_lds_sync();   // the slots are rewritten by the next task
             }
             if (T.vec4)
-                compute_task<MAXROWS, true, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx,
+                compute_task<MAXROWS, true, NT, ESPEC, SCREEN>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx,
                                                        goff);
             else
-                compute_task<MAXROWS, false, NT, ESPEC>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx,
+                compute_task<MAXROWS, false, NT, ESPEC, SCREEN>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx,
                                                         goff);
             if constexpr (TL) {
                 if (lane == 0 && t < g_timeline_cap) {
@@ -646,8 +656,8 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                 issue_task_load<NT>(tensors[nt.tensor], nt, wl + (cur ^ 1) * CHUNK, lane);
             }
             float* data = wl + cur * CHUNK;
-            if (T.vec4) compute_task<MAXROWS, true, NT, ESPEC>(T, task, data, ls, lmn, slot_min, slot_max, lane);
-            else compute_task<MAXROWS, false, NT, ESPEC>(T, task, data, ls, lmn, slot_min, slot_max, lane);
+            if (T.vec4) compute_task<MAXROWS, true, NT, ESPEC, SCREEN>(T, task, data, ls, lmn, slot_min, slot_max, lane);
+            else compute_task<MAXROWS, false, NT, ESPEC, SCREEN>(T, task, data, ls, lmn, slot_min, slot_max, lane);
             cur ^= 1;
         }
     }
@@ -992,6 +1002,7 @@ static MainKernel main_kernel(int variant) {
         case 11: return sweep_main_kernel<DFQ_V(11), true, 1>;
         case 12: return sweep_main_kernel<DFQ_V(12), true, 0>;
         case 13: return sweep_main_kernel<DFQ_V(13), true, 1, true>;
+        case 14: return sweep_main_kernel<DFQ_V(14), true, 1, false, false>;
         default: return sweep_main_kernel<DFQ_V(0)>;
     }
 #endif

@@ -647,3 +647,43 @@ def test_preload_is_idempotent():
     L = _lib.load()
     assert L.dfq_preload() == 0 and L.dfq_preload() == 0
     _lib.preload()
+
+
+@pytest.mark.parametrize("bits,mode", [(8, 3), (8, 2), (4, 2), (4, 3), (2, 2), (16, 3)])
+def test_screened_quantize_at_rounding_boundaries(bits, mode):
+    """The sweep's screened reciprocal quantize (csrc/dfq_common.h qdq_screen) takes
+    the IEEE divide only near a half-integer quotient.  Rows built so that most
+    elements sit ON a half-integer of their row's scale or 1-3 ulps either side
+    (ties to even, the screen's decision band), plus the clamp edges: dq, codes,
+    scale and E bit-exact with the oracle (oracle/dfq_oracle.c, the reference's
+    true division)."""
+    from data_free_quantization_amd.sweep import allocate, SweepPlan
+    rng = np.random.default_rng(bits * 10 + mode)
+    sym = mode in (1, 3)
+    qmax = (1 << (bits - 1)) - 1 if sym else (1 << bits) - 1
+    rows, cols = 96, 2 * 9 * 64
+    x = np.empty((rows, cols), np.float32)
+    for o in range(rows):
+        lo, hi = float(np.float32(-rng.uniform(0.1, 3.0))), float(np.float32(rng.uniform(0.1, 3.0)))
+        # the row's own scale and zero (what the kernel will derive from its range)
+        s = np.float32(max(max(abs(lo), abs(hi)) / qmax, 1e-8)) if sym else np.float32(max((hi - lo) / qmax, 1e-8))
+        mn = np.float32(0.0) if sym else np.float32(lo)
+        k = rng.integers(-qmax - 1 if sym else 0, qmax, cols)
+        v = ((k + 0.5) * s.astype(np.float64) + mn).astype(np.float32)
+        steps = rng.integers(-3, 4, cols).astype(np.int32)
+        v = (v.view(np.int32) + steps).view(np.float32)
+        v[0], v[1] = lo, hi   # pin the row's range
+        x[o] = np.clip(v, lo, hi)
+    t = torch.from_numpy(x.reshape(rows, 2, 9 * 64 // 9, 9)).to(DEV)   # KH*KW = 9 (3x3 error sums)
+    t = t.reshape(rows, 128, 3, 3).contiguous()
+    it = allocate(t, bits=bits, per_channel=True, symmetric=sym, khw=9, want_esum=True, clip=(-2.5, 2.5))
+    plan = SweepPlan([it])
+    plan.execute()
+    torch.cuda.synchronize()
+    xh = t.cpu().numpy()
+    o = O.quantize(xh, bits, mode, rows=rows, khw=9, flags=O.F_CLIP, clip=(-2.5, 2.5), want_esum=True)
+    assert np.array_equal(it.dst.cpu().numpy(), o["dq"])
+    assert np.array_equal(it.codes.cpu().numpy().view(o["codes"].dtype), o["codes"])
+    assert np.array_equal(it.scale.cpu().numpy(), o["scale"])
+    assert np.array_equal(it.esum.cpu().numpy(), o["esum"])
+    plan.destroy()
