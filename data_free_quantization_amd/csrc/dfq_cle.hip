@@ -133,10 +133,8 @@ struct CleScale {
 };
 
 // s = (1 / (r1 + eps)) * sqrt(r1 * r2 + eps); s = max(smin, min(smax, s))  (Python builtins)
-__device__ __forceinline__ CleScale cle_scale(const uint32_t* mins, const uint32_t* maxs, int64_t c1, int64_t c,
-                                              int is_signed, float eps, double smin, double smax) {
-    const float mn1 = dec_ord(mins[c]), mx1 = dec_ord(maxs[c]);
-    const float mn2 = dec_ord(mins[c1 + c]), mx2 = dec_ord(maxs[c1 + c]);
+__device__ __forceinline__ CleScale cle_scale_from(float mn1, float mx1, float mn2, float mx2, int is_signed, float eps,
+                                                   double smin, double smax) {
     float r1, r2;
     if (is_signed) {
         r1 = fmaxf(fabsf(mn1), fabsf(mx1));
@@ -161,6 +159,12 @@ __device__ __forceinline__ CleScale cle_scale(const uint32_t* mins, const uint32
         out.inv = (float)(1.0 / v);
     }
     return out;
+}
+
+__device__ __forceinline__ CleScale cle_scale(const uint32_t* mins, const uint32_t* maxs, int64_t c1, int64_t c,
+                                              int is_signed, float eps, double smin, double smax) {
+    return cle_scale_from(dec_ord(mins[c]), dec_ord(maxs[c]), dec_ord(mins[c1 + c]), dec_ord(maxs[c1 + c]), is_signed,
+                          eps, smin, smax);
 }
 
 __global__ void cle_apply_kernel(float* __restrict__ w1, float* __restrict__ w2, float* __restrict__ b1,
@@ -401,13 +405,15 @@ struct CleRel {
     int32_t vec2;       // W2 contiguous channel segments 16-B aligned (i2 == 1)
     int32_t fuse_next;  // >= 0: this relation's W2 is that relation's W1 -- the rescale
                         // of W2 also produces its row ranges (fused schedule)
+    int32_t dw_prev;    // >= 0: this relation's W1 is that relation's depthwise W2: its W1 row
+                        // ranges are derived (cle_rel_scale) and both run in one launch
 };
 
 // Range-launch kinds: W1 rows, W2 contiguous channels (i2 == 1), W2 row tiles
 // (i2 > 1, ordered-uint atomics), reset of the OTHER parity's W2 words.
 // Rescale-launch kinds: W1 elements, W2 elements, per-channel vectors.
 enum : int32_t { kRangeW1 = 0, kRangeW2Contig = 1, kRangeW2Tile = 2, kRangeReset = 3, kRangeResetW1 = 4 };
-enum : int32_t { kApplyW1 = 0, kApplyW2Contig = 1, kApplyW2Tile = 2, kApplyChannels = 3 };
+enum : int32_t { kApplyW1 = 0, kApplyW2Contig = 1, kApplyW2Tile = 2, kApplyChannels = 3, kApplyDwBoth = 4 };
 
 struct CleTask {
     int32_t rel;
@@ -715,6 +721,25 @@ cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
     cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + next) & 1, blockIdx.x, gridDim.x, tl);
 }
 
+// The scale of relation R for channel c (mins / maxs: the parity's range words).
+// A relation whose W1 is the depthwise W2 of relation Q (R.dw_prev) has no W1
+// range words: its W1 row c is Q's filter c after Q's rescale, fl(x * inv_Q[c]),
+// and with inv_Q > 0 that product is monotonic in x, so the row's min / max are
+// fl(min_c * inv_Q) / fl(max_c * inv_Q) -- Q's W2 range words (the filter at the
+// start of the iteration) scaled.  Every task of R can therefore compute its scale
+// in the same launch that rescales Q (kApplyDwBoth writes the filter once).
+__device__ __forceinline__ CleScale cle_rel_scale(const CleRel* __restrict__ rels, const CleRel& R,
+                                                  const uint32_t* __restrict__ mins, const uint32_t* __restrict__ maxs,
+                                                  int64_t c, int is_signed, float eps, double smin, double smax) {
+    if (R.dw_prev < 0) return cle_scale(mins + R.moff, maxs + R.moff, R.c1, c, is_signed, eps, smin, smax);
+    const CleRel& Q = rels[R.dw_prev];
+    const CleScale q = cle_scale(mins + Q.moff, maxs + Q.moff, Q.c1, c, is_signed, eps, smin, smax);
+    const float mn1 = dec_ord(mins[Q.moff + Q.c1 + c]) * q.inv;
+    const float mx1 = dec_ord(maxs[Q.moff + Q.c1 + c]) * q.inv;
+    return cle_scale_from(mn1, mx1, dec_ord(mins[R.moff + R.c1 + c]), dec_ord(maxs[R.moff + R.c1 + c]), is_signed, eps,
+                          smin, smax);
+}
+
 // LDS of one rescale task (the position-parallel and fused tiles)
 struct CleApplyLds {
     float red[2][kThreads / 64][kColTileRows];
@@ -742,12 +767,27 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
         if (tk.kind == kApplyW1) {   // W1[c, :] *= s[c], one wave per row
             for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
                 wave_scale(R.w1 + c * R.len1, R.len1, R.vec1, lane,
-                           [&] { return cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax).s; });
+                           [&] { return cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).s; });
+            }
+        } else if (tk.kind == kApplyDwBoth) {
+            // relation R's depthwise W2 filter c, which is relation tk.c0's W1 row c:
+            // *= 1/s_R[c], then *= s_next[c] (two roundings, as the reference's two
+            // in-place multiplies), written once
+            const CleRel& N = rels[tk.c0];
+            const int64_t seg = R.o2g * R.khw2;
+            for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
+                const float inv = cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).inv;
+                const float sn = cle_rel_scale(rels, N, mins, maxs, c, is_signed, eps, smin, smax).s;
+                float* p = R.w2 + c * seg;
+                for (int64_t i = lane; i < seg; i += 64) {
+                    const float y = p[i] * inv;
+                    p[i] = y * sn;
+                }
             }
         } else if (tk.kind == kApplyW2Contig) {   // W2 channel segment *= 1/s[c]
             const int64_t seg = R.o2g * R.khw2;
             for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
-                auto inv = [&] { return cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax).inv; };
+                auto inv = [&] { return cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).inv; };
                 if (R.fuse_next >= 0) {   // o2g == 1: the segment is row c of W2 = row c of the next W1
                     float vmin, vmax;
                     wave_scale_range(R.w2 + c * seg, seg, lane, vmin, vmax, inv);
@@ -771,7 +811,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             float* base = R.w2 + tk.c0 * R.khw2;
             const bool fuse = R.fuse_next >= 0;
             if (t < ncol)
-                inv_s[t] = cle_scale(mn, mx, R.c1, (tk.a / R.o2g) * R.i2 + tk.c0 + t, is_signed, eps, smin, smax).inv;
+                inv_s[t] = cle_rel_scale(rels, R, mins, maxs, (tk.a / R.o2g) * R.i2 + tk.c0 + t, is_signed, eps, smin, smax).inv;
             __syncthreads();
             for (int q = t; q < npos; q += kThreads) inv_pos[q] = inv_s[q / khw];   // 1/s per position
             __syncthreads();
@@ -826,7 +866,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                 for (int j = 0; j < kColTileRows; ++j)
                     if (act && j < nr) v[j] = R.w2[(tk.a + j) * rowlen + i];
                 const float inv =
-                    act ? cle_scale(mn, mx, R.c1, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin, smax).inv : 0.f;
+                    act ? cle_rel_scale(rels, R, mins, maxs, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin, smax).inv : 0.f;
 #pragma unroll
                 for (int j = 0; j < kColTileRows; ++j) {
                     if (j < nr) {   // uniform
@@ -851,7 +891,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                     if (act) {
                         const int64_t g = o / R.o2g;
                         if (g != g_prev) {
-                            inv = cle_scale(mn, mx, R.c1, g * R.i2 + i, is_signed, eps, smin, smax).inv;
+                            inv = cle_rel_scale(rels, R, mins, maxs, g * R.i2 + i, is_signed, eps, smin, smax).inv;
                             g_prev = g;
                         }
                         float* p = R.w2 + o * rowlen + i * R.khw2;
@@ -891,7 +931,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
 #pragma unroll
                     for (int j = 0; j < kColTileRows; ++j)
                         if (tk.a + j < tk.b) v[j] = R.w2[(tk.a + j) * rowlen + i];
-                    const float inv = cle_scale(mn, mx, R.c1, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin,
+                    const float inv = cle_rel_scale(rels, R, mins, maxs, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin,
                                                 smax).inv;
 #pragma unroll
                     for (int j = 0; j < kColTileRows; ++j)
@@ -903,7 +943,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                 for (int64_t o = tk.a; o < tk.b; ++o) {
                     const int64_t g = o / R.o2g;
                     if (g != g_prev) {
-                        inv = cle_scale(mn, mx, R.c1, g * R.i2 + i, is_signed, eps, smin, smax).inv;
+                        inv = cle_rel_scale(rels, R, mins, maxs, g * R.i2 + i, is_signed, eps, smin, smax).inv;
                         g_prev = g;
                     }
                     float* p = R.w2 + o * rowlen + i * R.khw2;
@@ -912,7 +952,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             }
         } else {
             for (int64_t c = tk.a + threadIdx.x; c < tk.b; c += kThreads) {
-                const CleScale cs = cle_scale(mn, mx, R.c1, c, is_signed, eps, smin, smax);
+                const CleScale cs = cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax);
                 if (R.b1) R.b1[c] = R.b1[c] * cs.s;
                 if (R.bnw) R.bnw[c] = R.bnw[c] * cs.s;
                 if (R.bnb) R.bnb[c] = R.bnb[c] * cs.s;
@@ -1977,6 +2017,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         c.vec1 = (d.len1 % 4 == 0 && reinterpret_cast<uintptr_t>(d.w1) % 16 == 0) ? 1 : 0;
         c.vec2 = (d.i2 == 1 && (c.o2g * d.khw2) % 4 == 0 && reinterpret_cast<uintptr_t>(d.w2) % 16 == 0) ? 1 : 0;
         c.fuse_next = -1;
+        c.dw_prev = -1;
         M += 2 * d.c1;
         R[r] = c;
     }
@@ -2035,6 +2076,33 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             for (int32_t r = 0; r < n_rel; ++r)
                 if (w1_src[r] >= 0) R[w1_src[r]].fuse_next = r;
     }
+    // Depthwise pairs (fused schedule): relation r whose W1 is the depthwise W2 of
+    // the relation q right before it in its chain runs in q's launch: its W1 row
+    // ranges are derived from q's W2 range words (cle_rel_scale), q's filter
+    // rescale and r's W1 rescale become ONE task (kApplyDwBoth), and r no longer
+    // needs W1 range words.  MobileNetV2: 5 rescale launches per iteration -> 3.
+    std::vector<int32_t> dw_next(n_rel, -1);
+    if (fused && !ab_env("DFQ_CLE_NO_DW_PAIRS")) {
+        for (int32_t r = 0; r < n_rel; ++r) {
+            const int32_t q = w1_src[r];
+            if (q < 0 || R[q].dw_prev >= 0 || dw_next[q] >= 0) continue;
+            const CleRel& cq = R[q];
+            const CleRel& cr = R[r];
+            const bool dw = cq.i2 == 1 && cq.o2g == 1 && cq.o2 == cq.c1 && cr.c1 == cq.o2 && cr.len1 == cq.khw2;
+            if (!dw) continue;
+            R[r].dw_prev = q;
+            R[q].fuse_next = -1;   // no range words to produce for r's W1
+            dw_next[q] = r;
+        }
+        // steps again: a depthwise-paired relation shares its predecessor's step
+        std::vector<int32_t> cur(n_rel, 0);
+        steps = 0;
+        for (int32_t r = 0; r < n_rel; ++r) {
+            const int32_t c = find(r);
+            step_of[r] = R[r].dw_prev >= 0 ? step_of[R[r].dw_prev] : cur[c]++;
+            steps = std::max(steps, step_of[r] + 1);
+        }
+    }
     // tasks: per-step range + rescale launches, or (fused) one range launch for
     // every relation's W2 (and untouched W1) followed by the rescale launches
     std::vector<CleTask> rt, at;
@@ -2056,6 +2124,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     };
     auto w1_range_tasks = [&](int32_t r) {
         const CleRel& c = R[r];
+        if (c.dw_prev >= 0) return;   // derived from the depthwise predecessor's W2 words
         if (fused && w1_src[r] >= 0) {   // produced by the previous relation's rescale: reset the next parity
             for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
                 rout->push_back({r, kRangeResetW1, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
@@ -2066,9 +2135,13 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     };
     auto apply_tasks = [&](int32_t r, std::vector<CleTask>& out) {
         const CleRel& c = R[r];
-        for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
-            out.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
-        if (c.i2 == 1) {
+        if (c.dw_prev < 0)   // else the predecessor's kApplyDwBoth rescales this W1
+            for (int64_t a = 0; a < c.c1; a += kCleW1RowsPerTask)
+                out.push_back({r, kApplyW1, a, std::min<int64_t>(a + kCleW1RowsPerTask, c.c1), 0, 0});
+        if (dw_next[r] >= 0) {
+            for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
+                out.push_back({r, kApplyDwBoth, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), dw_next[r], 0});
+        } else if (c.i2 == 1) {
             for (int64_t a = 0; a < c.c1; a += kCleW2ChansPerTask)
                 out.push_back({r, kApplyW2Contig, a, std::min<int64_t>(a + kCleW2ChansPerTask, c.c1), 0, 0});
         } else {
