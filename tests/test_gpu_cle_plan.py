@@ -37,7 +37,7 @@ def _conv(o, i, k, groups=1, rng=None, bias=True, dead=None):
     return m.to(DEV)
 
 
-def _graph(seed):
+def _graph(seed, dead_dw=None):
     from data_free_quantization_amd.utils.relation import Relation
     rng = np.random.default_rng(seed)
     g = OrderedDict()
@@ -51,7 +51,7 @@ def _graph(seed):
     # chain B: pointwise -> depthwise (contiguous columns) -> pointwise
     g["b1"] = _conv(40, 8, 1, rng=rng)
     g["b1bn"] = _BN(40, rng)
-    g["b2"] = _conv(40, 40, 3, groups=40, rng=rng)
+    g["b2"] = _conv(40, 40, 3, groups=40, rng=rng, dead=dead_dw)
     g["b2bn"] = _BN(40, rng, with_stats=False)
     g["b3"] = _conv(20, 40, 1, rng=rng)
     # chain C: one big layer (metric over several 32768-element chunks) -> Linear
@@ -121,6 +121,34 @@ def test_device_cle_matches_oracle(signed, eps, smm, thr, count, monkeypatch):
     elif diag and os.environ.get("DFQ_CLE_GROUPS") == "1" and os.environ.get("DFQ_CLE_FUSED") != "0":
         expect = 1    # A/B: chain-grouped, the whole iteration in one launch
     assert cle.LAST_RUN["launches_per_iteration"] == expect
+    assert cle.LAST_RUN["diffs"] == diffs
+    for k in W:
+        assert np.array_equal(g[k].weight.detach().cpu().numpy(), W[k]), k
+        if B[k] is not None:
+            assert np.array_equal(g[k].bias.detach().cpu().numpy(), B[k]), k
+    for k, (fw, fb) in BN.items():
+        if fw is not None:
+            assert np.array_equal(g[k].fake_weight.cpu().numpy(), fw), k
+            assert np.array_equal(g[k].fake_bias.cpu().numpy(), fb), k
+    for i, r in enumerate(rels):
+        assert np.array_equal(r.S.cpu().numpy(), S[i]), i
+
+
+@pytest.mark.parametrize("signed", [False, True])
+def test_device_cle_depthwise_pair_edges(signed, monkeypatch):
+    """Chain B (pointwise -> depthwise -> pointwise) runs both relations in ONE
+    launch: the second relation's W1 ranges are derived from the depthwise
+    filters' ranges scaled by the first relation's 1/s (cle_rel_scale).  Dead
+    depthwise filters (s = smin, then r1 = 0 -> s = smax for the next relation),
+    signed ranges: weights, biases, BN stats, scales and diffs bit-exact with the
+    relation-by-relation oracle replay."""
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    monkeypatch.setenv("DFQ_CLE_MODE", "device")
+    g, rels = _graph(3, dead_dw=[7, 19])
+    W, B, BN, S, diffs = _replay(g, rels, (1e-8, 1e8), 2e-7, 20, signed, 0.0)
+    cle.cross_layer_equalization(g, rels, [nn.Conv2d, nn.Linear], Treshhold=2e-7, signed=signed, Save_state=False)
+    torch.cuda.synchronize()
+    assert cle.LAST_RUN["steps"] == 2   # chain A's two relations; chain B's pair shares one step
     assert cle.LAST_RUN["diffs"] == diffs
     for k in W:
         assert np.array_equal(g[k].weight.detach().cpu().numpy(), W[k]), k
