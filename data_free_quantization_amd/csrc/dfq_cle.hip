@@ -788,6 +788,20 @@ cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
     cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + next) & 1, blockIdx.x, gridDim.x, tl);
 }
 
+// The next iteration's ranges as a launch of their own, on a graph branch that runs
+// CONCURRENTLY with the metric tiles (cle_loop_tiles_fin_kernel with no range
+// blocks): each kernel keeps its own LDS footprint (18 KB here, 35 KB for the
+// tiles), so the range blocks no longer take tile-sized LDS slots.  par: the
+// next iteration's parity from the launch argument -- the concurrent stop rule
+// advances st->iters; a block that sees st->done skips (no later iteration).
+__global__ void __launch_bounds__(kThreads)
+cle_loop_range_par_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
+                          uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int par) {
+    __shared__ float tl[2 * kThreads * kTileMaxKhw];
+    if (st->done) return;
+    cle_range_body(rels, tasks, t0, t1, rng, M, par, blockIdx.x, gridDim.x, tl);
+}
+
 // The scale of relation R for channel c (mins / maxs: the parity's range words).
 // A relation whose W1 is the depthwise W2 of relation Q (R.dw_prev) has no W1
 // range words: its W1 row c is Q's filter c after Q's rescale, fl(x * inv_Q[c]),
@@ -2015,6 +2029,8 @@ struct dfq_cle_plan {
     bool fin_fused = false;         // combine + stop rule folded into the tiles launch
     int64_t nbig = 0;               // chunks with tiles
     int32_t persist_grid = -1;      // cooperative grid of the persistent loop (0: not usable; -1: not sized)
+    bool fork = true;               // ranges on a concurrent graph branch (DFQ_CLE_NO_FORK=1: in the tiles launch)
+    int dev = 0;
     // chain-grouped schedule (cle_loop_group_kernel): one launch per iteration
     bool grouped = false;
     int32_t ngroups = 0, group_grid = 0;
@@ -2043,6 +2059,8 @@ struct CleDeviceCtx {
     hipStream_t st = nullptr;
     CleState* h_state = nullptr;   // pinned: [0] the run's state, [1..2] the batch readback slots
     hipEvent_t ev[2] = {nullptr, nullptr};
+    hipStream_t side = nullptr;                    // the range launch's graph branch
+    hipEvent_t fork[2] = {nullptr, nullptr};       // fork / join of that branch
 };
 static CleDeviceCtx& cle_device_ctx(int dev) {
     static CleDeviceCtx ctx[64];
@@ -2056,6 +2074,9 @@ static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
     if (e == hipSuccess && !ctx.h_state) e = hipHostMalloc(&ctx.h_state, 3 * sizeof(CleState));
     for (int i = 0; i < 2 && e == hipSuccess; ++i)
         if (!ctx.ev[i]) e = hipEventCreateWithFlags(&ctx.ev[i], hipEventDisableTiming);
+    if (e == hipSuccess && !ctx.side) e = hipStreamCreateWithFlags(&ctx.side, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i)
+        if (!ctx.fork[i]) e = hipEventCreateWithFlags(&ctx.fork[i], hipEventDisableTiming);
     return e;
 }
 
@@ -2430,6 +2451,8 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                     c, groups[c].nblk, groups[c].nsteps,
                     (long long)(gbound[groups[c].step_off + groups[c].nsteps] - gbound[groups[c].step_off]),
                     (long long)(groups[c].r1 - groups[c].r0), (long long)(groups[c].u1 - groups[c].u0));
+    p->fork = !ab_env("DFQ_CLE_NO_FORK");
+    (void)hipGetDevice(&p->dev);
     p->grouped = grouped;
     p->ngroups = (int32_t)groups.size();
     p->group_grid = (int32_t)group_of_blk.size();
@@ -2575,6 +2598,24 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     }
     const int64_t nr = p->fused ? p->rstep[1] - p->rstep[0] : 0;   // next iteration's range tasks
     const int64_t ntb = std::min<int64_t>(p->nunits, kTileGrid), nrb = std::min<int64_t>(nr, kStepGrid);
+    if (p->fin_fused && p->fork && nrb > 0) {
+        // tiles + chunk combine + stop rule on s; the next ranges on the side stream,
+        // concurrently (fork / join by events: captured as parallel graph branches)
+        CleDeviceCtx& ctx = cle_device_ctx(p->dev);
+        DFQ_HIP_CHECK(hipEventRecord(ctx.fork[0], s));
+        DFQ_HIP_CHECK(hipStreamWaitEvent(ctx.side, ctx.fork[0], 0));
+        hipLaunchKernelGGL(cle_loop_range_par_kernel, dim3((int)nrb), dim3(kThreads), 0, ctx.side, p->d_rels,
+                           p->d_rtasks, p->rstep[0], p->rstep[1], p->d_rng, p->M, p->d_state, (j + 1) & 1);
+        DFQ_LAUNCH_CHECK();
+        CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
+        hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)ntb), dim3(kThreads), 0, s, p->d_layers,
+                           p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
+                           p->d_rtasks, p->rstep[0], p->rstep[0], p->d_rng, p->M, F, p->d_state, (j + 1) & 1);
+        DFQ_LAUNCH_CHECK();
+        DFQ_HIP_CHECK(hipEventRecord(ctx.fork[1], ctx.side));
+        DFQ_HIP_CHECK(hipStreamWaitEvent(s, ctx.fork[1], 0));
+        return DFQ_OK;
+    }
     if (p->fin_fused) {   // tiles (+ ranges) + chunk combine + stop rule: one launch
         CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
         hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
@@ -2836,7 +2877,8 @@ extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t
         if (p->grouped)
             *launches = 1;
         else if (p->fin_fused)   // rescales (+ per-step ranges), then tiles + ranges + combine + stop rule
-            *launches = (p->fused ? p->steps : 2 * p->steps) + 1;
+            *launches = (p->fused ? p->steps : 2 * p->steps) + 1 +
+                        ((p->fused && p->fork && p->rstep[1] > p->rstep[0]) ? 1 : 0);   // + the concurrent ranges
         else
             *launches = (p->fused ? p->steps + ((p->nunits > 0 && p->nchunks > 0) ? 0 : 1) : 2 * p->steps) +
                         (p->nunits > 0 ? 1 : 0) + (p->nchunks > 0 ? 1 : 0) + 1;
