@@ -116,13 +116,16 @@ def test_device_cle_matches_oracle(signed, eps, smm, thr, count, monkeypatch):
     # 2 x (range + rescale) + that launch
     diag = os.environ.get("DFQ_LIB") == "diag"   # the A/B switches exist in the diagnostics library only
     fused = not (diag and os.environ.get("DFQ_CLE_FUSED") == "0")
-    # fused: 2 rescale steps + the tiles/stop-rule launch + the next ranges on a
-    # concurrent branch; else 2 x (range + rescale) + the tiles/stop-rule launch
-    expect = 3 if not fused else (3 if diag and os.environ.get("DFQ_CLE_NO_FORK") else 4)
-    if not fused:
-        expect = 5
+    fork = not (diag and os.environ.get("DFQ_CLE_NO_FORK"))
     if diag and os.environ.get("DFQ_CLE_UNFUSED_FIN"):
-        expect += 2   # A/B: the chunk combine and the stop rule as launches of their own
+        # A/B: the chunk combine and the stop rule as launches of their own
+        expect = 5 if fused else 7
+    elif fused:
+        # 2 rescale steps + the tiles/stop-rule launch (+ the next ranges on a
+        # concurrent graph branch)
+        expect = 4 if fork else 3
+    else:
+        expect = 5   # 2 x (range + rescale) + the tiles/stop-rule launch
     elif diag and os.environ.get("DFQ_CLE_GROUPS") == "1" and os.environ.get("DFQ_CLE_FUSED") != "0":
         expect = 1    # A/B: chain-grouped, the whole iteration in one launch
     assert cle.LAST_RUN["launches_per_iteration"] == expect
