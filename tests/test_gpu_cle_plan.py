@@ -120,14 +120,14 @@ def test_device_cle_matches_oracle(signed, eps, smm, thr, count, monkeypatch):
     if diag and os.environ.get("DFQ_CLE_UNFUSED_FIN"):
         # A/B: the chunk combine and the stop rule as launches of their own
         expect = 5 if fused else 7
+    elif fused and diag and os.environ.get("DFQ_CLE_GROUPS") == "1":
+        expect = 1    # A/B: chain-grouped, the whole iteration in one launch
     elif fused:
         # 2 rescale steps + the tiles/stop-rule launch (+ the next ranges on a
         # concurrent graph branch)
         expect = 4 if fork else 3
     else:
         expect = 5   # 2 x (range + rescale) + the tiles/stop-rule launch
-    elif diag and os.environ.get("DFQ_CLE_GROUPS") == "1" and os.environ.get("DFQ_CLE_FUSED") != "0":
-        expect = 1    # A/B: chain-grouped, the whole iteration in one launch
     assert cle.LAST_RUN["launches_per_iteration"] == expect
     assert cle.LAST_RUN["diffs"] == diffs
     for k in W:
