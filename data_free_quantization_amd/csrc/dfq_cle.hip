@@ -2029,7 +2029,7 @@ struct dfq_cle_plan {
     bool fin_fused = false;         // combine + stop rule folded into the tiles launch
     int64_t nbig = 0;               // chunks with tiles
     int32_t persist_grid = -1;      // cooperative grid of the persistent loop (0: not usable; -1: not sized)
-    bool fork = true;               // ranges on a concurrent graph branch (DFQ_CLE_NO_FORK=1: in the tiles launch)
+    bool fork = false;              // ranges on a concurrent graph branch (diagnostics DFQ_CLE_FORK=1)
     int dev = 0;
     // chain-grouped schedule (cle_loop_group_kernel): one launch per iteration
     bool grouped = false;
@@ -2451,7 +2451,10 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                     c, groups[c].nblk, groups[c].nsteps,
                     (long long)(gbound[groups[c].step_off + groups[c].nsteps] - gbound[groups[c].step_off]),
                     (long long)(groups[c].r1 - groups[c].r0), (long long)(groups[c].u1 - groups[c].u0));
-    p->fork = !ab_env("DFQ_CLE_NO_FORK");
+    // measured SLOWER (MobileNetV2 CLE 7.7 vs 4.7 ms, profiles/r03/cle_ab_l.jsonl): a
+    // parallel graph branch's fork / join costs more than the LDS slots it frees,
+    // so it is a diagnostics A/B (DFQ_CLE_FORK=1)
+    p->fork = ab_env("DFQ_CLE_FORK") != nullptr;
     (void)hipGetDevice(&p->dev);
     p->grouped = grouped;
     p->ngroups = (int32_t)groups.size();

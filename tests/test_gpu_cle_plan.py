@@ -116,7 +116,7 @@ def test_device_cle_matches_oracle(signed, eps, smm, thr, count, monkeypatch):
     # 2 x (range + rescale) + that launch
     diag = os.environ.get("DFQ_LIB") == "diag"   # the A/B switches exist in the diagnostics library only
     fused = not (diag and os.environ.get("DFQ_CLE_FUSED") == "0")
-    fork = not (diag and os.environ.get("DFQ_CLE_NO_FORK"))
+    fork = diag and bool(os.environ.get("DFQ_CLE_FORK"))
     if diag and os.environ.get("DFQ_CLE_UNFUSED_FIN"):
         # A/B: the chunk combine and the stop rule as launches of their own
         expect = 5 if fused else 7
