@@ -407,6 +407,8 @@ struct CleRel {
                         // of W2 also produces its row ranges (fused schedule)
     int32_t dw_prev;    // >= 0: this relation's W1 is that relation's depthwise W2: its W1 row
                         // ranges are derived (cle_rel_scale) and both run in one launch
+    int32_t w1_self;    // 1: its W1 rescale also writes the next iteration's W1 row ranges
+    int32_t w2_self;    // 1: its depthwise W2 rescale (kApplyDwBoth) writes the next W2 ranges
 };
 
 // Range-launch kinds: W1 rows, W2 contiguous channels (i2 == 1), W2 row tiles
@@ -569,6 +571,62 @@ __device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, boo
                 if (i + 64 * u < n) p[i + 64 * u] = v[u] * f;
         }
     }
+}
+
+// wave_scale that also returns the (min, max) of the products (every lane).
+template <class F>
+__device__ __forceinline__ void wave_scale_mm(float* __restrict__ p, int64_t n, bool vec, int lane, float& vmin,
+                                              float& vmax, F&& factor) {
+    vmin = INFINITY;
+    vmax = -INFINITY;
+    float f = 0.f;
+    bool have = false;
+    if (vec) {
+        float4* p4 = reinterpret_cast<float4*>(p);
+        const int64_t n4 = n >> 2;
+        for (int64_t i = lane; i < n4; i += 4 * 64) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n4) v[u] = p4[i + 64 * u];
+            if (!have) {
+                f = factor();
+                have = true;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n4) {
+                    v[u].x = v[u].x * f;
+                    v[u].y = v[u].y * f;
+                    v[u].z = v[u].z * f;
+                    v[u].w = v[u].w * f;
+                    p4[i + 64 * u] = v[u];
+                    vmin = fminf(vmin, fminf(fminf(v[u].x, v[u].y), fminf(v[u].z, v[u].w)));
+                    vmax = fmaxf(vmax, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
+                }
+        }
+    } else {
+        for (int64_t i = lane; i < n; i += 4 * 64) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n) v[u] = p[i + 64 * u];
+            if (!have) {
+                f = factor();
+                have = true;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i + 64 * u < n) {
+                    const float y = v[u] * f;
+                    p[i + 64 * u] = y;
+                    vmin = fminf(vmin, y);
+                    vmax = fmaxf(vmax, y);
+                }
+        }
+    }
+    vmin = wave_min(vmin);
+    vmax = wave_max(vmax);
 }
 
 // p[0..n) *= f() and the (min, max) of the products, one wave (scalar loads:
@@ -838,6 +896,8 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
     float* inv_pos = A.inv_pos;
     uint32_t* mins = rng + (int64_t)par * 2 * M;
     uint32_t* maxs = mins + M;
+    uint32_t* nmins = rng + (int64_t)(par ^ 1) * 2 * M;   // the next iteration's words (self ranges)
+    uint32_t* nmaxs = nmins + M;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     for (int64_t t = t0 + blk; t < t1; t += nblk) {
@@ -847,22 +907,46 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
         const uint32_t* mx = maxs + R.moff;
         if (tk.kind == kApplyW1 && R.len1 < 64) {   // short rows: a lane group per row
             for_short_rows(tk.a, tk.b, R.len1, [&](int64_t c, bool act, int sl, int G) {
-                if (!act || sl >= R.len1) return;   // G >= len1: one element per lane
-                float* p = R.w1 + c * R.len1 + sl;
-                const float x = *p;   // in flight while the scale's range words load
-                *p = x * cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).s;
+                float y0 = INFINITY, y1 = -INFINITY;
+                if (act && sl < R.len1) {   // G >= len1: one element per lane
+                    float* p = R.w1 + c * R.len1 + sl;
+                    const float x = *p;   // in flight while the scale's range words load
+                    const float y = x * cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).s;
+                    *p = y;
+                    y0 = y1 = y;
+                }
+                if (R.w1_self) {   // the row is final for this iteration: its next range
+                    y0 = group_min(y0, G);
+                    y1 = group_max(y1, G);
+                    if (act && sl == 0) {
+                        nmins[R.moff + c] = enc_ord(y0);
+                        nmaxs[R.moff + c] = enc_ord(y1);
+                    }
+                }
             });
         } else if (tk.kind == kApplyDwBoth && R.o2g * R.khw2 < 64) {
             const CleRel& N = rels[tk.c0];
             const int64_t seg = R.o2g * R.khw2;
             for_short_rows(tk.a, tk.b, seg, [&](int64_t c, bool act, int sl, int G) {
-                if (!act || sl >= seg) return;   // G >= seg: one element per lane
-                float* p = R.w2 + c * seg + sl;
-                const float x = *p;
-                const float inv = cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).inv;
-                const float sn = cle_rel_scale(rels, N, mins, maxs, c, is_signed, eps, smin, smax).s;
-                const float y = x * inv;
-                *p = y * sn;
+                float z0 = INFINITY, z1 = -INFINITY;
+                if (act && sl < seg) {   // G >= seg: one element per lane
+                    float* p = R.w2 + c * seg + sl;
+                    const float x = *p;
+                    const float inv = cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).inv;
+                    const float sn = cle_rel_scale(rels, N, mins, maxs, c, is_signed, eps, smin, smax).s;
+                    const float y = x * inv;
+                    const float z = y * sn;
+                    *p = z;
+                    z0 = z1 = z;
+                }
+                if (R.w2_self) {   // the filter is final for this iteration: its next range
+                    z0 = group_min(z0, G);
+                    z1 = group_max(z1, G);
+                    if (act && sl == 0) {
+                        nmins[R.moff + R.c1 + c] = enc_ord(z0);
+                        nmaxs[R.moff + R.c1 + c] = enc_ord(z1);
+                    }
+                }
             });
         } else if (tk.kind == kApplyW2Contig && R.o2g * R.khw2 < 64) {
             const int64_t seg = R.o2g * R.khw2;
@@ -888,8 +972,17 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             });
         } else if (tk.kind == kApplyW1) {   // W1[c, :] *= s[c], one wave per row
             for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
-                wave_scale(R.w1 + c * R.len1, R.len1, R.vec1, lane,
-                           [&] { return cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).s; });
+                auto sc = [&] { return cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).s; };
+                if (R.w1_self) {   // the row is final for this iteration: its next range
+                    float y0, y1;
+                    wave_scale_mm(R.w1 + c * R.len1, R.len1, R.vec1, lane, y0, y1, sc);
+                    if (lane == 0) {
+                        nmins[R.moff + c] = enc_ord(y0);
+                        nmaxs[R.moff + c] = enc_ord(y1);
+                    }
+                } else {
+                    wave_scale(R.w1 + c * R.len1, R.len1, R.vec1, lane, sc);
+                }
             }
         } else if (tk.kind == kApplyDwBoth) {
             // relation R's depthwise W2 filter c, which is relation tk.c0's W1 row c:
@@ -901,9 +994,21 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                 const float inv = cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).inv;
                 const float sn = cle_rel_scale(rels, N, mins, maxs, c, is_signed, eps, smin, smax).s;
                 float* p = R.w2 + c * seg;
+                float z0 = INFINITY, z1 = -INFINITY;
                 for (int64_t i = lane; i < seg; i += 64) {
                     const float y = p[i] * inv;
-                    p[i] = y * sn;
+                    const float z = y * sn;
+                    p[i] = z;
+                    z0 = fminf(z0, z);
+                    z1 = fmaxf(z1, z);
+                }
+                if (R.w2_self) {
+                    z0 = wave_min(z0);
+                    z1 = wave_max(z1);
+                    if (lane == 0) {
+                        nmins[R.moff + R.c1 + c] = enc_ord(z0);
+                        nmaxs[R.moff + R.c1 + c] = enc_ord(z1);
+                    }
                 }
             }
         } else if (tk.kind == kApplyW2Contig) {   // W2 channel segment *= 1/s[c]
@@ -2030,6 +2135,7 @@ struct dfq_cle_plan {
     int64_t nbig = 0;               // chunks with tiles
     int32_t persist_grid = -1;      // cooperative grid of the persistent loop (0: not usable; -1: not sized)
     bool fork = false;              // ranges on a concurrent graph branch (diagnostics DFQ_CLE_FORK=1)
+    int64_t ri0 = 0, ri1 = 0;       // fused: each iteration's range tasks (the rest come from the rescales)
     int dev = 0;
     // chain-grouped schedule (cle_loop_group_kernel): one launch per iteration
     bool grouped = false;
@@ -2147,6 +2253,8 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         c.vec2 = (d.i2 == 1 && (c.o2g * d.khw2) % 4 == 0 && reinterpret_cast<uintptr_t>(d.w2) % 16 == 0) ? 1 : 0;
         c.fuse_next = -1;
         c.dw_prev = -1;
+        c.w1_self = 0;
+        c.w2_self = 0;
         M += 2 * d.c1;
         R[r] = c;
     }
@@ -2284,12 +2392,32 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
             out.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
     };
+    int64_t ri0 = 0, ri1 = 0;
     if (fused) {
         for (int32_t r = 0; r < n_rel; ++r) {
             w1_range_tasks(r);
             w2_range_tasks(r);
         }
         rstep.push_back((int64_t)rt.size());
+        // Self ranges: a W1 that no earlier relation of its chain touches is final
+        // once its own row rescale ran, so that task writes the row's next range
+        // (no kRangeW1 task); likewise a depthwise W2 after kApplyDwBoth.  The
+        // first iteration's ranges still come from the full list [rstep0, rstep1);
+        // each iteration's tiles launch runs the rest, [ri0, ri1).
+        for (int32_t r = 0; r < n_rel; ++r) {
+            if (w1_src[r] < 0 && R[r].dw_prev < 0) R[r].w1_self = 1;
+            if (dw_next[r] >= 0) R[r].w2_self = 1;
+        }
+        if (ab_env("DFQ_CLE_NO_SELF_RANGES"))
+            for (int32_t r = 0; r < n_rel; ++r) R[r].w1_self = R[r].w2_self = 0;
+        ri0 = (int64_t)rt.size();
+        for (int64_t t = rstep[0]; t < rstep[1]; ++t) {
+            const CleTask tk = rt[t];
+            if (tk.kind == kRangeW1 && R[tk.rel].w1_self) continue;
+            if (tk.kind == kRangeW2Contig && R[tk.rel].w2_self) continue;
+            rt.push_back(tk);
+        }
+        ri1 = (int64_t)rt.size();
     }
     for (int32_t k = 0; k < steps; ++k) {
         for (int32_t r = 0; r < n_rel; ++r) {
@@ -2468,6 +2596,8 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->fused = fused;
     p->rstep = rstep;
     p->astep = astep;
+    p->ri0 = ri0;
+    p->ri1 = ri1;
     p->smin = s_min; p->smax = s_max; p->is_signed = is_signed; p->eps = eps;
     hipError_t e;
     auto fail = [&](hipError_t err) { set_last_hip_error(err); cle_plan_free(p); return DFQ_ERR_HIP; };
@@ -2599,7 +2729,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
             DFQ_LAUNCH_CHECK();
         }
     }
-    const int64_t nr = p->fused ? p->rstep[1] - p->rstep[0] : 0;   // next iteration's range tasks
+    const int64_t nr = p->fused ? p->ri1 - p->ri0 : 0;   // next iteration's range tasks
     const int64_t ntb = std::min<int64_t>(p->nunits, kTileGrid), nrb = std::min<int64_t>(nr, kStepGrid);
     if (p->fin_fused && p->fork && nrb > 0) {
         // tiles + chunk combine + stop rule on s; the next ranges on the side stream,
@@ -2608,7 +2738,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         DFQ_HIP_CHECK(hipEventRecord(ctx.fork[0], s));
         DFQ_HIP_CHECK(hipStreamWaitEvent(ctx.side, ctx.fork[0], 0));
         hipLaunchKernelGGL(cle_loop_range_par_kernel, dim3((int)nrb), dim3(kThreads), 0, ctx.side, p->d_rels,
-                           p->d_rtasks, p->rstep[0], p->rstep[1], p->d_rng, p->M, p->d_state, (j + 1) & 1);
+                           p->d_rtasks, p->ri0, p->ri1, p->d_rng, p->M, p->d_state, (j + 1) & 1);
         DFQ_LAUNCH_CHECK();
         CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
         hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)ntb), dim3(kThreads), 0, s, p->d_layers,
@@ -2623,7 +2753,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
         hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
                            p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
-                           p->d_rtasks, p->rstep[0], p->fused ? p->rstep[1] : p->rstep[0], p->d_rng, p->M, F,
+                           p->d_rtasks, p->ri0, p->fused ? p->ri1 : p->ri0, p->d_rng, p->M, F,
                            p->d_state, (j + 1) & 1);
         DFQ_LAUNCH_CHECK();
         return DFQ_OK;
@@ -2631,11 +2761,11 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     if (p->nchunks > 0 && ntb > 0 && nrb > 0) {
         hipLaunchKernelGGL(cle_loop_tiles_range_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
                            p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
-                           p->d_rtasks, p->rstep[0], p->rstep[1], p->d_rng, p->M, p->d_state);
+                           p->d_rtasks, p->ri0, p->ri1, p->d_rng, p->M, p->d_state);
         DFQ_LAUNCH_CHECK();
     } else if (nrb > 0) {
         hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)nrb), dim3(kThreads), 0, s, p->d_rels, p->d_rtasks,
-                           p->rstep[0], p->rstep[1], p->d_rng, p->M, p->d_state, 1);
+                           p->ri0, p->ri1, p->d_rng, p->M, p->d_state, 1);
         DFQ_LAUNCH_CHECK();
     }
     if (p->nchunks > 0) {
@@ -2881,7 +3011,7 @@ extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t
             *launches = 1;
         else if (p->fin_fused)   // rescales (+ per-step ranges), then tiles + ranges + combine + stop rule
             *launches = (p->fused ? p->steps : 2 * p->steps) + 1 +
-                        ((p->fused && p->fork && p->rstep[1] > p->rstep[0]) ? 1 : 0);   // + the concurrent ranges
+                        ((p->fused && p->fork && p->ri1 > p->ri0) ? 1 : 0);   // + the concurrent ranges
         else
             *launches = (p->fused ? p->steps + ((p->nunits > 0 && p->nchunks > 0) ? 0 : 1) : 2 * p->steps) +
                         (p->nunits > 0 ? 1 : 0) + (p->nchunks > 0 ? 1 : 0) + 1;
