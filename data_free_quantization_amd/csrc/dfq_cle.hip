@@ -1241,18 +1241,6 @@ __global__ void cle_loop_snap_kernel(const CleLayer* __restrict__ layers, const 
 }
 
 
-// Agent-coherent fp32 store / load (sc1: no stale copy in another XCD's L2), for
-// the few words one block hands to another inside a launch (level-1 sums, chunk
-// tails, chunk sums) without an L2 write-back.
-__device__ __forceinline__ void st_coh(float* p, float v) {
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_coh(const float* p) {
-    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT));
-}
-
 // Metric tiles taken by blocks blk, blk + nblk, ... (d: kCleTile + kCleTailWords
 // floats of LDS, b0: 512).
 struct CleNoUnitHook {

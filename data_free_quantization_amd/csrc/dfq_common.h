@@ -339,6 +339,19 @@ __device__ inline float wave_inner_sum(Get get, int64_t n, int lane) {
     return __shfl(r, 0, 64);
 }
 
+// Agent-coherent fp32 store / load (sc1: no stale copy in another XCD's L2), for
+// the words one block hands to another inside a launch (CLE: level-1 sums, chunk
+// tails, chunk sums; the BC chain: every vector a later phase reads) without an
+// L2 write-back.
+__device__ __forceinline__ void st_coh(float* p, float v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_coh(const float* p) {
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Which reduction aten_outer_col_sum uses for column c: true = the 32-column
 // multi_row_sum cascade, false = row_sum (ILP 4).
 __host__ __device__ inline bool aten_outer_col_is_cascade(int64_t R, int64_t F, int64_t c, int threads) {

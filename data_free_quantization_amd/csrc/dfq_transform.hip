@@ -5,10 +5,12 @@
 // torch CPU ops (one rounding per op; -ffp-contract=off, IEEE div/sqrt).
 #include "dfq_common.h"
 
+#include <cstdlib>
 #include <cstring>
 
 #include <algorithm>
 #include <cmath>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -126,21 +128,21 @@ __device__ __forceinline__ double ndtr_d(double a) {
     return x > 0.0 ? 1.0 - y : y;
 }
 
+__device__ __forceinline__ float bc_expect_value(float wj, float bj, int relu) {
+    if (!relu) return bj;
+    const float x = (-bj) / wj;               // -bias/weight (fp32)
+    const double xd = (double)x;
+    const float pdf = (float)(exp(-(xd * xd) / 2.0) / 2.5066282746310002);
+    const float cdf = (float)ndtr_d(xd);
+    float ex = wj * pdf + bj * (1.0f - cdf);  // torch finishes in fp32
+    if (ex < 0.0f) ex = 0.0f;                  // expect[expect < 0] = 0
+    return ex;
+}
+
 __global__ void bc_expect_kernel(const float* __restrict__ w, const float* __restrict__ b, int64_t n, int relu,
                                  int accumulate, float* __restrict__ out) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
-        const float wj = w[j], bj = b[j];
-        float ex;
-        if (relu) {
-            const float x = (-bj) / wj;               // -bias/weight (fp32)
-            const double xd = (double)x;
-            const float pdf = (float)(exp(-(xd * xd) / 2.0) / 2.5066282746310002);
-            const float cdf = (float)ndtr_d(xd);
-            ex = wj * pdf + bj * (1.0f - cdf);        // torch finishes in fp32
-            if (ex < 0.0f) ex = 0.0f;                  // expect[expect < 0] = 0
-        } else {
-            ex = bj;
-        }
+        const float ex = bc_expect_value(w[j], b[j], relu);
         out[j] = accumulate ? out[j] + ex : ex;
     }
 }
@@ -183,6 +185,180 @@ bc_propagate_kernel(const float* __restrict__ bias_vec, int64_t nrows, int64_t f
                               ? wave_cascade(get, nrows, lane, b0s, b1s, kBcScratch)
                               : wave_row_sum(get, nrows, lane, b0s, b1s, kBcScratch);
         if (lane == 0) fake_b[c] = fake_b[c] + (-sum) / (float)nrows;   // sum(-v) == -sum(v) exactly
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The bias-correction chain as ONE cooperative launch (dfq_bc_chain).  The walk
+// is a serial chain -- layer L's expectation reads the BN fake_bias that layer
+// L-1's propagate wrote -- of tiny vector ops (MobileNetV2: 173 launches of
+// 3-7 us each, 1.5 ms end to end).  Here the host cuts the op list into phases
+// with no cross-block dependency inside a phase; phases are separated by a grid
+// barrier.  Inside a phase:
+//   * every block computes each EXPECT vector into its own LDS slot (block 0
+//     also stores it), so the APPLY that reads it needs no barrier;
+//   * a PROPAGATE of the bias_vec an APPLY of the same phase produced recomputes
+//     each element as E + expect (the same single fp32 add) instead of reading
+//     what other blocks wrote;
+//   * two APPLYs of one bias give row r to the same wave (program order).
+// Everything a later phase reads is stored / loaded agent-coherent (st_coh /
+// ld_coh: the sc1 hand-off form, drained before the barrier's counter add).
+// ---------------------------------------------------------------------------
+constexpr int kBcChainThreads = 512;
+constexpr int kBcChainWaves = kBcChainThreads / 64;
+constexpr int kBcSlotFloats = 8192;        // LDS for one phase's expectation vectors
+constexpr int64_t kBcChainScratch = 1024;  // per-wave cascade scratch (b0s; b1s = /16)
+constexpr uint32_t kBcChainSpins = 1u << 21;
+
+struct BcDevOp {
+    int32_t kind, flag;
+    const float* a;
+    const float* b;
+    float* out;
+    float* out2;
+    int64_t n, i2, f, bcols;
+    int32_t lds_out;    // EXPECT: LDS slot of out
+    int32_t lds_prev;   // EXPECT accumulate: LDS slot of the running sum (-1: load out)
+    int32_t lds_b;      // APPLY: LDS slot of the expectation (-1: load b)
+    int32_t virt;       // PROPAGATE: index of the APPLY whose bias_vec it sums (-1: load a)
+    int64_t wbase;      // APPLY / PROPAGATE: global wave of row / column 0
+    uint32_t dmagic;    // APPLY: k / bcols as umulhi(k, dmagic) + k >> dshift (k < 2^31)
+    uint32_t dshift;
+};
+
+// One op of a phase, by this block.  Each handler loads its op from the table
+// itself: a by-value op struct passed down went to the stack (scratch).
+struct BcLds {
+    float* slots;
+    float* b0s;
+    float* b1s;
+    int lane;
+    int64_t nw, gw;
+    __device__ int64_t first(int64_t wbase) const { return (gw - wbase + nw) % nw; }   // wbase in [0, nw)
+};
+
+__device__ __forceinline__ void bc_op_expect(const BcDevOp* __restrict__ opp, BcLds L) {
+    const BcDevOp op = *opp;
+    const int acc = (op.flag >> 1) & 1;
+    for (int64_t j = threadIdx.x; j < op.n; j += kBcChainThreads) {
+        float v = bc_expect_value(ld_coh(op.a + j), ld_coh(op.b + j), op.flag & 1);
+        if (acc) v = (op.lds_prev >= 0 ? L.slots[op.lds_prev + j] : ld_coh(op.out + j)) + v;
+        L.slots[op.lds_out + j] = v;
+        if (blockIdx.x == 0) st_coh(op.out + j, v);
+    }
+}
+
+__device__ __forceinline__ void bc_op_apply(const BcDevOp* __restrict__ opp, BcLds L) {
+    const BcDevOp op = *opp;
+    const float* __restrict__ E = op.a;
+    const int64_t i2 = op.i2, f = op.f, bcols = op.bcols;
+    const int lane = L.lane;
+    for (int64_t r = L.first(op.wbase); r < op.n; r += L.nw) {
+        auto get = [&](int64_t j) {
+            const int64_t q = f > 1 ? j : 0;
+            return E[r * i2 + (i2 > 1 ? j : 0)] + (op.lds_b >= 0 ? L.slots[op.lds_b + q] : ld_coh(op.b + q));
+        };
+        if (op.out2)
+            for (int64_t j = lane; j < bcols; j += 64) st_coh(op.out2 + r * bcols + j, get(j));
+        const float sum = wave_inner_sum(get, bcols, lane);
+        if (lane == 0) st_coh(op.out + r, ld_coh(op.out + r) + sum / (float)bcols);
+    }
+}
+
+template <typename Get>
+__device__ __forceinline__ void bc_column(const BcDevOp& op, const BcLds& L, int64_t nrows, int64_t c, Get get) {
+    const float sum = aten_outer_col_is_cascade(nrows, op.f, c, op.flag)
+                          ? wave_cascade(get, nrows, L.lane, L.b0s, L.b1s, kBcChainScratch)
+                          : wave_row_sum(get, nrows, L.lane, L.b0s, L.b1s, kBcChainScratch);
+    if (L.lane == 0) st_coh(op.out + c, ld_coh(op.out + c) + (-sum) / (float)nrows);
+}
+
+// bias_vec[k] of the APPLY `src`, recomputed: E[row, j] + expect[j]
+__device__ __forceinline__ void bc_op_propagate_virt(const BcDevOp* __restrict__ opp, const BcDevOp* __restrict__ srcp,
+                                                  BcLds L) {
+    const BcDevOp op = *opp, src = *srcp;
+    const int64_t F = op.f, nrows = op.n / F;
+    const float* __restrict__ E = src.a;
+    const uint32_t sb = (uint32_t)src.bcols;   // numel < 2^31 on this path (host)
+    const uint32_t si2 = (uint32_t)src.i2;
+    const uint32_t emask = src.i2 > 1 ? ~0u : 0u, xmask = src.f > 1 ? ~0u : 0u;
+    const float* ex = L.slots + src.lds_b;     // forwarded only from an LDS expectation (host)
+    const uint32_t Fu = (uint32_t)F;
+    for (int64_t c = L.first(op.wbase); c < F; c += L.nw)
+        bc_column(op, L, nrows, c, [&](int64_t r) {
+            const uint32_t kk = (uint32_t)r * Fu + (uint32_t)c;
+            const uint32_t row = (uint32_t)(((uint64_t)__umulhi(kk, src.dmagic) + kk) >> src.dshift);
+            const uint32_t j = kk - row * sb;
+            return E[row * si2 + (j & emask)] + ex[j & xmask];
+        });
+}
+
+__device__ __forceinline__ void bc_op_propagate(const BcDevOp* __restrict__ opp, BcLds L) {
+    const BcDevOp op = *opp;
+    const int64_t F = op.f, nrows = op.n / F;
+    for (int64_t c = L.first(op.wbase); c < F; c += L.nw)
+        bc_column(op, L, nrows, c, [&](int64_t r) { return ld_coh(op.a + r * F + c); });
+}
+
+__device__ __forceinline__ void bc_op_copy(const BcDevOp* __restrict__ opp) {
+    const BcDevOp op = *opp;
+    for (int64_t i = (int64_t)blockIdx.x * kBcChainThreads + threadIdx.x; i < op.n;
+         i += (int64_t)gridDim.x * kBcChainThreads)
+        st_coh(op.out + i, ld_coh(op.a + i));
+}
+
+__global__ void __launch_bounds__(kBcChainThreads)
+bc_chain_kernel(const BcDevOp* __restrict__ ops, const int32_t* __restrict__ phase, int32_t nphase,
+                uint32_t* bar, int32_t* err) {
+    __shared__ float slots[kBcSlotFloats];
+    __shared__ float scratch[kBcChainWaves][kBcChainScratch + kBcChainScratch / 16];
+    __shared__ int flag;
+    BcLds L;
+    L.slots = slots;
+    L.lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    L.b0s = scratch[wv];
+    L.b1s = L.b0s + kBcChainScratch;
+    L.nw = (int64_t)gridDim.x * kBcChainWaves;
+    L.gw = (int64_t)blockIdx.x * kBcChainWaves + wv;
+    for (int32_t p = 0; p < nphase; ++p) {
+        for (int32_t k = phase[p]; k < phase[p + 1]; ++k) {
+            const int32_t kind = ops[k].kind;
+            if (kind == DFQ_BC_OP_EXPECT) {
+                bc_op_expect(ops + k, L);
+                __syncthreads();
+            } else if (kind == DFQ_BC_OP_APPLY) {
+                bc_op_apply(ops + k, L);
+            } else if (kind == DFQ_BC_OP_PROPAGATE) {
+                const int32_t virt = ops[k].virt;
+                if (virt >= 0) bc_op_propagate_virt(ops + k, ops + virt, L);
+                else bc_op_propagate(ops + k, L);
+            } else {
+                bc_op_copy(ops + k);
+            }
+        }
+        if (p + 1 == nphase) break;
+        // grid barrier: every store of this phase has completed before the one add
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t target = (uint32_t)(p + 1) * gridDim.x;
+            int good = 1;
+            uint32_t spins = 0;
+            while ((int32_t)(__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kBcChainSpins) {   // never expected (co-resident grid): report, do not hang
+                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    good = 0;
+                    break;
+                }
+            }
+            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
+            flag = good;
+        }
+        __syncthreads();
+        if (!flag) return;
     }
 }
 
@@ -912,6 +1088,282 @@ __global__ void __launch_bounds__(256) copy_batch_kernel(CopyBatch b) {
         dst[i] = src[i];
 }
 
+namespace dfq {
+namespace {
+struct BcRange {
+    uintptr_t lo = 0, hi = 0;
+};
+BcRange bc_rng(const void* p, int64_t floats) {
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+    return BcRange{lo, lo + 4 * (uintptr_t)std::max<int64_t>(floats, 0)};
+}
+bool bc_ov(const BcRange& x, const BcRange& y) { return x.lo < x.hi && y.lo < y.hi && x.lo < y.hi && y.lo < x.hi; }
+bool bc_eq(const BcRange& x, const BcRange& y) { return x.lo == y.lo && x.hi == y.hi; }
+bool bc_in(const BcRange& x, const BcRange& y) { return y.lo <= x.lo && x.hi <= y.hi; }
+
+// Phases of a validated chain for bc_chain_kernel (rules at the kernel).  false:
+// the chain does something this path does not forward (an op that aliases
+// itself, E written earlier in the chain, an expectation larger than the LDS
+// slots, 2^31+ elements): it runs as per-op launches instead.
+bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vector<BcDevOp>& dev,
+                     std::vector<int32_t>& phase) {
+    enum { kPlain, kSlot, kBias, kVec };
+    struct Wr {
+        BcRange r;
+        int kind;
+        int32_t op;   // index into dev
+    };
+    struct Slot {
+        BcRange r;
+        int32_t off;
+        bool read;   // an APPLY of this phase read it (a rewrite would change what a recompute sees)
+    };
+    std::vector<Wr> wr;
+    std::vector<BcRange> rd, ever;   // this phase's global reads; every write of the chain so far
+    std::vector<Slot> slot;
+    int32_t top = 0;
+    int64_t wcur = 0;
+    dev.clear();
+    phase.assign(1, 0);
+    auto hits_wr = [&](const BcRange& r) {
+        for (const Wr& w : wr)
+            if (bc_ov(w.r, r)) return true;
+        return false;
+    };
+    auto hits_rd = [&](const BcRange& r) {
+        for (const BcRange& x : rd)
+            if (bc_ov(x, r)) return true;
+        return false;
+    };
+    auto find_slot = [&](const BcRange& r) -> Slot* {
+        for (Slot& s : slot)
+            if (bc_in(r, s.r)) return &s;
+        return nullptr;
+    };
+    constexpr int64_t kMax = (int64_t)1 << 31;
+    for (int32_t k = 0; k < n_ops; ++k) {
+        const dfq_bc_op& op = ops[k];
+        if ((op.kind == DFQ_BC_OP_EXPECT || op.kind == DFQ_BC_OP_COPY) && op.n == 0) continue;
+        BcDevOp d{};
+        d.kind = op.kind; d.flag = op.flag; d.a = op.a; d.b = op.b; d.out = op.out; d.out2 = op.out2;
+        d.n = op.n; d.i2 = op.i2; d.f = op.f;
+        d.lds_out = d.lds_prev = d.lds_b = d.virt = -1;
+        // this op's footprint
+        std::vector<BcRange> reads, writes;
+        BcRange rmw{};
+        if (op.kind == DFQ_BC_OP_EXPECT) {
+            if (op.n > kBcSlotFloats) return false;
+            reads = {bc_rng(op.a, op.n), bc_rng(op.b, op.n)};
+            writes = {bc_rng(op.out, op.n)};
+        } else if (op.kind == DFQ_BC_OP_APPLY) {
+            d.bcols = (op.i2 == op.f || op.f == 1) ? op.i2 : op.f;
+            if (op.n * op.i2 >= kMax || op.n * d.bcols >= kMax) return false;
+            // round-up magic for k / bcols: l = ceil(log2 bcols), m = 2^32 (2^l - bcols) / bcols + 1
+            uint32_t l = 0;
+            while (((uint64_t)1 << l) < (uint64_t)d.bcols) ++l;
+            d.dshift = l;
+            d.dmagic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - (uint64_t)d.bcols)) / (uint64_t)d.bcols + 1);
+            const BcRange E = bc_rng(op.a, op.n * op.i2);
+            for (const BcRange& w : ever)
+                if (bc_ov(w, E)) return false;   // E is loaded non-coherently
+            reads = {E, bc_rng(op.b, op.f)};
+            rmw = bc_rng(op.out, op.n);
+            writes = {rmw};
+            if (op.out2) writes.push_back(bc_rng(op.out2, op.n * d.bcols));
+        } else if (op.kind == DFQ_BC_OP_PROPAGATE) {
+            if (op.n >= kMax) return false;
+            reads = {bc_rng(op.a, op.n)};
+            rmw = bc_rng(op.out, op.f);
+            writes = {rmw};
+        } else {
+            reads = {bc_rng(op.a, op.n)};
+            writes = {bc_rng(op.out, op.n)};
+        }
+        for (const BcRange& w : writes) {   // an op that aliases itself
+            for (const BcRange& r : reads)
+                if (bc_ov(w, r)) return false;
+            for (const BcRange& w2 : writes)
+                if (&w != &w2 && bc_ov(w, w2)) return false;
+        }
+        // try to join the current phase; on a conflict start a new one and retry
+        for (int attempt = 0;; ++attempt) {
+            bool ok = true;
+            std::vector<BcRange> grd;   // global (non-forwarded) reads of this op
+            int64_t wb = -1;
+            if (op.kind == DFQ_BC_OP_EXPECT) {
+                const BcRange o = writes[0];
+                Slot* s = nullptr;
+                for (Slot& x : slot)
+                    if (bc_eq(x.r, o)) s = &x;
+                if ((op.flag >> 1) & 1) {
+                    // the running sum from another phase would be read by every block while
+                    // block 0 rewrites it: not forwarded
+                    if (!s && attempt > 0) return false;
+                    if (s) d.lds_prev = s->off;
+                    else ok = false;
+                }
+                if (s && s->read) ok = false;
+                grd.push_back(reads[0]);
+                grd.push_back(reads[1]);
+                for (const BcRange& r : grd) ok = ok && !hits_wr(r);
+                // the write: the same slot again (accumulate) or a fresh one
+                for (const Wr& w : wr)
+                    if (bc_ov(w.r, o) && !(s && w.kind == kSlot && bc_eq(w.r, o))) ok = false;
+                ok = ok && !hits_rd(o);
+                if (ok) {
+                    if (s) d.lds_out = s->off;
+                    else if (top + op.n <= kBcSlotFloats) {
+                        d.lds_out = top;
+                        slot.push_back(Slot{o, top, false});
+                        top += (int32_t)((op.n + 15) / 16 * 16);
+                    } else ok = false;
+                }
+            } else if (op.kind == DFQ_BC_OP_APPLY) {
+                Slot* s = find_slot(reads[1]);
+                if (s) d.lds_b = s->off + (int32_t)((reads[1].lo - s->r.lo) / 4);
+                else grd.push_back(reads[1]);
+                grd.push_back(reads[0]);
+                for (const BcRange& r : grd) ok = ok && !hits_wr(r);
+                // bias: only an earlier APPLY of the same bias (same row owners)
+                for (const Wr& w : wr)
+                    if (bc_ov(w.r, rmw)) {
+                        if (w.kind == kBias && bc_eq(w.r, rmw)) wb = dev[w.op].wbase;
+                        else ok = false;
+                    }
+                ok = ok && !hits_rd(rmw);
+                if (writes.size() > 1) ok = ok && !hits_wr(writes[1]) && !hits_rd(writes[1]);
+                if (ok) {
+                    if (wb < 0) {
+                        wb = wcur;
+                        wcur = (wcur + op.n) % nw;
+                    }
+                    d.wbase = wb;
+                    grd.push_back(rmw);
+                    if (s) s->read = true;
+                }
+            } else if (op.kind == DFQ_BC_OP_PROPAGATE) {
+                d.virt = -1;
+                for (const Wr& w : wr)   // the recompute takes the expectation from LDS
+                    if (w.kind == kVec && bc_eq(w.r, reads[0]) && dev[w.op].lds_b >= 0) d.virt = w.op;
+                if (d.virt < 0) {
+                    grd.push_back(reads[0]);
+                    ok = ok && !hits_wr(reads[0]);
+                } else {   // the recompute reads that APPLY's E (and its LDS expectation)
+                    grd.push_back(bc_rng(dev[d.virt].a, dev[d.virt].n * dev[d.virt].i2));
+                }
+                ok = ok && !hits_wr(rmw) && !hits_rd(rmw);
+                if (ok) {
+                    d.wbase = wcur;
+                    wcur = (wcur + op.f) % nw;
+                    grd.push_back(rmw);
+                }
+            } else {
+                grd.push_back(reads[0]);
+                ok = !hits_wr(reads[0]) && !hits_wr(writes[0]) && !hits_rd(writes[0]);
+            }
+            if (ok) {
+                const int32_t me = (int32_t)dev.size();
+                for (const BcRange& r : grd) rd.push_back(r);
+                if (op.kind == DFQ_BC_OP_EXPECT) wr.push_back(Wr{writes[0], kSlot, me});
+                else if (op.kind == DFQ_BC_OP_APPLY) {
+                    wr.push_back(Wr{writes[0], kBias, me});
+                    if (writes.size() > 1) wr.push_back(Wr{writes[1], kVec, me});
+                } else wr.push_back(Wr{writes[0], kPlain, me});
+                for (const BcRange& w : writes) ever.push_back(w);
+                dev.push_back(d);
+                break;
+            }
+            if (attempt > 0 || phase.back() == (int32_t)dev.size()) return false;   // conflicts with nothing
+            phase.push_back((int32_t)dev.size());
+            wr.clear(); rd.clear(); slot.clear();
+            top = 0;
+            wcur = 0;
+            d.lds_out = d.lds_prev = d.lds_b = d.virt = -1;
+        }
+    }
+    if (phase.back() != (int32_t)dev.size()) phase.push_back((int32_t)dev.size());
+    return !dev.empty();
+}
+
+// Per-device state of the cooperative chain: the device table (op table, phase
+// offsets, barrier counter, error word) and its pinned mirror.  The call waits
+// for its launch, so one buffer per device serves every call.
+struct BcChainCtx {
+    std::mutex mu;
+    char* dbuf = nullptr;
+    char* hbuf = nullptr;
+    size_t cap = 0;
+    int grid = 0;      // default grid
+    int max_grid = 0;  // co-resident blocks (cooperative launch limit)
+};
+BcChainCtx& bc_chain_ctx(int dev) {
+    static std::mutex m;
+    static std::vector<BcChainCtx*> v;
+    std::lock_guard<std::mutex> lk(m);
+    if ((int)v.size() <= dev) v.resize(dev + 1, nullptr);
+    if (!v[dev]) v[dev] = new BcChainCtx();
+    return *v[dev];
+}
+
+constexpr int kBcNotEligible = 1;   // internal: run the per-op launches
+int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
+    const char* ev = ab_env("DFQ_BC_CHAIN");   // diagnostics A/B: "launches" = per-op launches
+    if (ev && std::strcmp(ev, "launches") == 0) return kBcNotEligible;
+    int dev = 0;
+    DFQ_HIP_CHECK(hipStreamGetDevice(s, &dev));
+    BcChainCtx& ctx = bc_chain_ctx(dev);
+    std::lock_guard<std::mutex> lock(ctx.mu);
+    if (ctx.grid == 0) {   // blocks that can be co-resident, capped: the phases are latency-bound
+        int cus = 0, per = 0;
+        DFQ_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        DFQ_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per, reinterpret_cast<const void*>(bc_chain_kernel), kBcChainThreads, 0));
+        ctx.max_grid = std::max(1, cus * per);
+        ctx.grid = std::min(ctx.max_grid, 64);
+    }
+    int grid = ctx.grid;
+    if (const char* g = ab_env("DFQ_BC_GRID")) grid = std::max(1, std::min(ctx.max_grid, atoi(g)));
+    std::vector<BcDevOp> dv;
+    std::vector<int32_t> ph;
+    if (!bc_chain_phases(ops, n_ops, (int64_t)grid * kBcChainWaves, dv, ph)) return kBcNotEligible;
+    const int32_t nphase = (int32_t)ph.size() - 1;
+    auto up256 = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t o_ph = up256(sizeof(BcDevOp) * dv.size());
+    const size_t o_bar = o_ph + up256(sizeof(int32_t) * ph.size());
+    const size_t need = o_bar + 256;
+    if (ctx.cap < need) {
+        if (ctx.dbuf) (void)hipFree(ctx.dbuf);
+        if (ctx.hbuf) (void)hipHostFree(ctx.hbuf);
+        ctx.dbuf = ctx.hbuf = nullptr;
+        ctx.cap = 0;
+        const size_t cap = std::max<size_t>(need * 2, 64 << 10);
+        DFQ_HIP_CHECK(hipMalloc(&ctx.dbuf, cap));
+        DFQ_HIP_CHECK(hipHostMalloc(&ctx.hbuf, cap, hipHostMallocDefault));
+        ctx.cap = cap;
+    }
+    std::memcpy(ctx.hbuf, dv.data(), sizeof(BcDevOp) * dv.size());
+    std::memcpy(ctx.hbuf + o_ph, ph.data(), sizeof(int32_t) * ph.size());
+    std::memset(ctx.hbuf + o_bar, 0, 256);   // barrier counter, error word
+    DFQ_HIP_CHECK(hipMemcpyAsync(ctx.dbuf, ctx.hbuf, need, hipMemcpyHostToDevice, s));
+    const BcDevOp* d_ops = reinterpret_cast<const BcDevOp*>(ctx.dbuf);
+    const int32_t* d_ph = reinterpret_cast<const int32_t*>(ctx.dbuf + o_ph);
+    uint32_t* d_bar = reinterpret_cast<uint32_t*>(ctx.dbuf + o_bar);
+    int32_t* d_err = reinterpret_cast<int32_t*>(ctx.dbuf + o_bar + 128);
+    void* args[] = {&d_ops, &d_ph, const_cast<int32_t*>(&nphase), &d_bar, &d_err};
+    DFQ_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(bc_chain_kernel), dim3(grid),
+                                             dim3(kBcChainThreads), args, 0, s));
+    int32_t* h_err = reinterpret_cast<int32_t*>(ctx.hbuf + o_bar + 128);
+    DFQ_HIP_CHECK(hipMemcpyAsync(h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    DFQ_HIP_CHECK(hipStreamSynchronize(s));
+    if (*h_err) {
+        set_last_hip_error(hipErrorLaunchTimeOut);
+        return DFQ_ERR_HIP;
+    }
+    return DFQ_OK;
+}
+}  // namespace
+}  // namespace dfq
+
 extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed_op, void* stream) {
     if (failed_op) *failed_op = -1;
     if (n_ops < 0 || (n_ops > 0 && !ops)) return DFQ_ERR_INVALID;
@@ -944,6 +1396,9 @@ extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed
                 return fail(k, DFQ_ERR_INVALID);
         }
     }
+    if (n_ops == 0) return DFQ_OK;
+    const int crc = dfq::bc_chain_coop(ops, n_ops, static_cast<hipStream_t>(stream));
+    if (crc != dfq::kBcNotEligible) return crc;
     for (int32_t k = 0; k < n_ops; ++k) {
         const dfq_bc_op& op = ops[k];
         int rc = DFQ_OK;
@@ -1156,6 +1611,7 @@ hipError_t preload_transform() {   // see dfq_preload
     hipFuncAttributes a;
     hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(bn_fold_weight_batch_kernel));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(absorb_batch_gemv_kernel));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(bc_chain_kernel));
     return e;
 }
 }  // namespace dfq
