@@ -2096,12 +2096,11 @@ struct dfq_cle_plan {
     float* d_part = nullptr;        // [layers][slots]
     int32_t slots = 8;              // torch.mean's thread buffer (the reference run's thread count)
     double* d_means = nullptr;
-    double* d_hist = nullptr;
-    int32_t hist_cap = 0;
+    double* d_hist = nullptr;       // this run's history (the tables' kCleHistCap slots, or the context's)
+    double* d_hist_tables = nullptr;
     CleState* d_state = nullptr;
     CleState* h_state = nullptr;    // pinned (the device context's, set by run)
     hipStream_t st = nullptr;       // the loop's stream (the device context's)
-    hipGraphExec_t gexec = nullptr; // kCleBatch iterations
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
     int64_t M = 0, nchunks = 0;
     int32_t nl = 0, chains = 0, steps = 0;
@@ -2114,9 +2113,9 @@ struct dfq_cle_plan {
     double smin = 1e-8, smax = 1e8;
     int32_t is_signed = 0;
     float eps = 0.f;
-    void* d_tables = nullptr;       // every device table above but d_hist: ONE allocation
+    void* d_tables = nullptr;       // every device table above: ONE allocation (unless pooled)
+    bool pooled = false;            // the tables live in the device context's pool
     void* d_snap_owned = nullptr;   // snapshots when the caller passed no workspace
-    double* d_hist_owned = nullptr; // history beyond kCleHistCap iterations
     uint32_t* d_bar = nullptr;      // persistent loop's grid barrier words
     uint32_t* d_cnt = nullptr;      // tiles_fin arrival counters [nchunks + 1]
     bool fin_fused = false;         // combine + stop rule folded into the tiles launch
@@ -2155,6 +2154,22 @@ struct CleDeviceCtx {
     hipEvent_t ev[2] = {nullptr, nullptr};
     hipStream_t side = nullptr;                    // the range launch's graph branch
     hipEvent_t fork[2] = {nullptr, nullptr};       // fork / join of that branch
+    // Table pool: one plan at a time keeps its tables here (device + pinned upload
+    // mirror), so a plan costs no hipMalloc / hipFree (hipFree waits for the whole
+    // device) and its upload is an async DMA on the loop stream.
+    char* d_pool = nullptr;
+    size_t pool_cap = 0;
+    char* h_pool = nullptr;
+    size_t hpool_cap = 0;
+    bool pool_busy = false;
+    hipEvent_t pool_ev = nullptr;                  // behind the last upload from h_pool
+    double* d_hist = nullptr;                      // histories longer than the tables' kCleHistCap
+    int64_t hist_cap = 0;
+    // The last captured batch graph and the launch arguments it was captured with:
+    // a plan whose launches are identical (same pooled tables, same counts) reuses
+    // it instead of capturing and instantiating its own (~100 us).
+    hipGraphExec_t gexec = nullptr;
+    std::vector<char> gkey;
 };
 static CleDeviceCtx& cle_device_ctx(int dev) {
     static CleDeviceCtx ctx[64];
@@ -2171,18 +2186,22 @@ static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
     if (e == hipSuccess && !ctx.side) e = hipStreamCreateWithFlags(&ctx.side, hipStreamNonBlocking);
     for (int i = 0; i < 2 && e == hipSuccess; ++i)
         if (!ctx.fork[i]) e = hipEventCreateWithFlags(&ctx.fork[i], hipEventDisableTiming);
+    if (e == hipSuccess && !ctx.pool_ev) e = hipEventCreateWithFlags(&ctx.pool_ev, hipEventDisableTiming);
     return e;
 }
 
 static void cle_plan_free(dfq_cle_plan* p) {
     const double t0 = now_us();
-    (void)hipFree(p->d_tables);
+    if (p->pooled) {   // hand the pool back (a run has synchronised its stream; an unrun
+                       // plan's upload is waited for by the next user of the pool)
+        CleDeviceCtx& ctx = cle_device_ctx(p->dev);
+        std::lock_guard<std::mutex> lock(ctx.mu);
+        ctx.pool_busy = false;
+    } else {
+        (void)hipFree(p->d_tables);
+    }
     (void)hipFree(p->d_snap_owned);
-    (void)hipFree(p->d_hist_owned);
-    const double t1 = now_us();
-    if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
-    const double t2 = now_us();
-    if (cle_timing()) fprintf(stderr, "DFQ_CLE_TIMING free: device %.1f us, graph %.1f\n", t1 - t0, t2 - t1);
+    if (cle_timing()) fprintf(stderr, "DFQ_CLE_TIMING free: %.1f us\n", now_us() - t0);
     delete p;
 }
 
@@ -2616,16 +2635,57 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_grt = T.add<CleTask>((int64_t)grt.size());
     const int64_t o_gbar = T.add<uint32_t>(32 * (int64_t)std::max<size_t>(groups.size(), 1));
     const double tm0 = now_us();
-    if ((e = hipMalloc(&p->d_tables, T.total)) != hipSuccess) return fail(e);
+    char* base = nullptr;
+    char* hblob = nullptr;
+    CleDeviceCtx& ctx = cle_device_ctx(p->dev);
+    if (!grouped) {   // the pool (the diagnostics-only grouped tables take the private path)
+        std::lock_guard<std::mutex> lock(ctx.mu);
+        if (!ctx.pool_busy && (e = cle_ctx_ready(ctx)) == hipSuccess &&
+            (e = hipEventSynchronize(ctx.pool_ev)) == hipSuccess) {
+            if (ctx.pool_cap < (size_t)T.total) {
+                (void)hipFree(ctx.d_pool);
+                ctx.d_pool = nullptr;
+                ctx.pool_cap = 0;
+                const size_t cap = (size_t)T.total + (size_t)T.total / 2;
+                if ((e = hipMalloc(&ctx.d_pool, cap)) == hipSuccess) ctx.pool_cap = cap;
+            }
+            if (e == hipSuccess && ctx.hpool_cap < (size_t)host_bytes) {
+                (void)hipHostFree(ctx.h_pool);
+                ctx.h_pool = nullptr;
+                ctx.hpool_cap = 0;
+                const size_t cap = (size_t)host_bytes + (size_t)host_bytes / 2;
+                if ((e = hipHostMalloc(&ctx.h_pool, cap, hipHostMallocDefault)) == hipSuccess) ctx.hpool_cap = cap;
+            }
+            if (e == hipSuccess) {
+                ctx.pool_busy = true;
+                p->pooled = true;
+                base = ctx.d_pool;
+                hblob = ctx.h_pool;
+            }
+        }
+        if (e != hipSuccess) return fail(e);
+    }
+    std::vector<char> blob;
+    if (!p->pooled) {
+        if ((e = hipMalloc(&p->d_tables, T.total)) != hipSuccess) return fail(e);
+        base = static_cast<char*>(p->d_tables);
+        blob.assign(host_bytes, 0);
+        hblob = blob.data();
+    } else {
+        std::memset(hblob, 0, host_bytes);
+    }
     const double tm1 = now_us();
-    char* base = static_cast<char*>(p->d_tables);
-    std::vector<char> blob(host_bytes, 0);
     auto put = [&](int64_t off, const auto& v) {
-        if (!v.empty()) std::memcpy(blob.data() + off, v.data(), sizeof(v[0]) * v.size());
+        if (!v.empty()) std::memcpy(hblob + off, v.data(), sizeof(v[0]) * v.size());
     };
     put(o_rels, R); put(o_rt, rt); put(o_at, at); put(o_layers, layers); put(o_chunks, chunks); put(o_units, units);
     put(o_b1off, b1off);
-    if ((e = hipMemcpy(base, blob.data(), host_bytes, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    if (p->pooled) {   // async on the loop stream, which every launch of the plan uses
+        if ((e = hipMemcpyAsync(base, hblob, host_bytes, hipMemcpyHostToDevice, ctx.st)) != hipSuccess) return fail(e);
+        if ((e = hipEventRecord(ctx.pool_ev, ctx.st)) != hipSuccess) return fail(e);
+    } else if ((e = hipMemcpy(base, hblob, host_bytes, hipMemcpyHostToDevice)) != hipSuccess) {
+        return fail(e);
+    }
     if (grouped) {   // the group tables sit after the device-only buffers: one more copy
         const int64_t g0 = o_groups, g1 = o_gbar;
         std::vector<char> gblob(g1 - g0, 0);
@@ -2652,7 +2712,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->d_part = reinterpret_cast<float*>(base + o_part);
     p->d_means = reinterpret_cast<double*>(base + o_means);
     p->d_state = reinterpret_cast<CleState*>(base + o_state);
-    p->d_hist = reinterpret_cast<double*>(base + o_hist);
+    p->d_hist = p->d_hist_tables = reinterpret_cast<double*>(base + o_hist);
     p->d_bar = reinterpret_cast<uint32_t*>(base + o_bar);
     p->d_cnt = reinterpret_cast<uint32_t*>(base + o_cnt);
     p->d_groups = reinterpret_cast<CleGroup*>(base + o_groups);
@@ -2663,7 +2723,6 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->d_gbar = reinterpret_cast<uint32_t*>(base + o_gbar);
     for (const auto& c : chunks) p->nbig += c.len >= 8 ? 1 : 0;
     p->fin_fused = p->nunits > 0 && p->nbig > 0 && n_targets <= 128 && !ab_env("DFQ_CLE_UNFUSED_FIN");
-    p->hist_cap = kCleHistCap;
     *out = p;
     return DFQ_OK;
 }
@@ -2674,6 +2733,30 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
 static int32_t cle_ordered() {
     const char* e = ab_env("DFQ_CLE_ORDERED");
     return (e && e[0] == '1') ? 1 : 0;
+}
+
+// Everything cle_enqueue_iteration passes to a launch (and the launch shapes): a
+// graph captured for one plan replays another exactly when these are equal.
+static std::vector<char> cle_graph_key(const dfq_cle_plan* p) {
+    std::vector<char> k;
+    auto add = [&](const auto& v) {
+        const char* c = reinterpret_cast<const char*>(&v);
+        k.insert(k.end(), c, c + sizeof(v));
+    };
+    add(p->dev); add(p->grouped); add(p->steps); add(p->fused); add(p->fin_fused); add(p->fork);
+    add(p->ri0); add(p->ri1); add(p->nunits); add(p->nchunks); add(p->nbig); add(p->M); add(p->slots); add(p->nl);
+    add(p->is_signed); add(p->eps); add(p->smin); add(p->smax); add(p->group_grid);
+    add(p->d_rels); add(p->d_rtasks); add(p->d_atasks); add(p->d_layers); add(p->d_chunks); add(p->d_rng);
+    add(p->d_part); add(p->d_means); add(p->d_hist); add(p->d_state); add(p->d_units); add(p->d_b1off); add(p->d_b1);
+    add(p->d_tail); add(p->d_cnt); add(p->d_groups); add(p->d_gblk); add(p->d_gbound); add(p->d_gat); add(p->d_grt);
+    add(p->d_gbar); add(p->st);
+    add(p->rstep.size());
+    for (int64_t x : p->rstep) add(x);
+    add(p->astep.size());
+    for (int64_t x : p->astep) add(x);
+    const char* nf = ab_env("DFQ_CLE_GSYNC_NOFENCE");
+    add(cle_ordered()); add((int)(nf && nf[0] == '1'));
+    return k;
 }
 
 // One CLE iteration's launches (steps, metric, stop rule) on stream s.
@@ -2821,23 +2904,20 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     DFQ_HIP_CHECK(cle_ctx_ready(ctx));
     if (cle_timing()) fprintf(stderr, "DFQ_CLE_TIMING run: caller sync %.1f us, context %.1f us\n", ts1 - ts0,
                               now_us() - ts1);
-    if (p->st && p->st != ctx.st && p->gexec) {   // captured on another device's stream: recapture
-        (void)hipGraphExecDestroy(p->gexec);
-        p->gexec = nullptr;
-    }
     p->st = ctx.st;
     p->h_state = ctx.h_state;
     hipStream_t s = p->st;
-    if (p->hist_cap < max_iters + 1) {
-        (void)hipFree(p->d_hist_owned);
-        p->d_hist_owned = nullptr;
-        DFQ_HIP_CHECK(hipMalloc(&p->d_hist_owned, sizeof(double) * (max_iters + 1)));
-        p->d_hist = p->d_hist_owned;
-        p->hist_cap = max_iters + 1;
-        if (p->gexec) {   // captured with the old history pointer
-            (void)hipGraphExecDestroy(p->gexec);
-            p->gexec = nullptr;
+    // the history: the tables' slots, or the context's buffer (grown once) for longer caps
+    p->d_hist = p->d_hist_tables;
+    if (max_iters + 1 > kCleHistCap) {
+        if (ctx.hist_cap < max_iters + 1) {
+            (void)hipFree(ctx.d_hist);
+            ctx.d_hist = nullptr;
+            ctx.hist_cap = 0;
+            DFQ_HIP_CHECK(hipMalloc(&ctx.d_hist, sizeof(double) * (max_iters + 1)));
+            ctx.hist_cap = max_iters + 1;
         }
+        p->d_hist = ctx.d_hist;
     }
     CleState init{};
     init.diff = 1e8;
@@ -2914,20 +2994,30 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     const char* ge = ab_env("DFQ_CLE_GRAPH");
     const bool use_graph = !(ge && ge[0] == '0');
     const double tc0 = now_us();
-    if (use_graph && !p->gexec && !init.done) {
-        DFQ_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        int rc = DFQ_OK;
-        for (int32_t it = 0; it < kCleBatch && rc == DFQ_OK; ++it) rc = cle_enqueue_iteration(p, s, it);
-        hipGraph_t g = nullptr;
-        const hipError_t ec = hipStreamEndCapture(s, &g);
-        if (rc != DFQ_OK) {
-            if (g) (void)hipGraphDestroy(g);
-            return rc;
+    bool reused = false;
+    if (use_graph && !init.done) {
+        std::vector<char> key = cle_graph_key(p);
+        reused = ctx.gexec && key == ctx.gkey;
+        if (!reused) {
+            if (ctx.gexec) (void)hipGraphExecDestroy(ctx.gexec);
+            ctx.gexec = nullptr;
+            ctx.gkey.clear();
+            DFQ_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            int rc = DFQ_OK;
+            for (int32_t it = 0; it < kCleBatch && rc == DFQ_OK; ++it) rc = cle_enqueue_iteration(p, s, it);
+            hipGraph_t g = nullptr;
+            const hipError_t ec = hipStreamEndCapture(s, &g);
+            if (rc != DFQ_OK) {
+                if (g) (void)hipGraphDestroy(g);
+                return rc;
+            }
+            DFQ_HIP_CHECK(ec);
+            const hipError_t ei = hipGraphInstantiate(&ctx.gexec, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (ei != hipSuccess) ctx.gexec = nullptr;
+            DFQ_HIP_CHECK(ei);
+            ctx.gkey = std::move(key);
         }
-        DFQ_HIP_CHECK(ec);
-        const hipError_t ei = hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        DFQ_HIP_CHECK(ei);
     }
     const double tc1 = now_us();
     // One batch in flight ahead of the stop-rule check: batch k + 1 is enqueued
@@ -2939,7 +3029,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     int slot = 0;
     auto enqueue_batch = [&](int sl) -> int {
         if (use_graph) {
-            DFQ_HIP_CHECK(hipGraphLaunch(p->gexec, s));
+            DFQ_HIP_CHECK(hipGraphLaunch(ctx.gexec, s));
         } else {
             for (int32_t it = 0; it < kCleBatch; ++it) {
                 const int rc = cle_enqueue_iteration(p, s, it);
@@ -2965,8 +3055,8 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     }
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
     if (cle_timing())
-        fprintf(stderr, "DFQ_CLE_TIMING run: capture+instantiate %.1f us, loop %.1f us (%d iterations launched)\n",
-                tc1 - tc0, now_us() - tc1, launched);
+        fprintf(stderr, "DFQ_CLE_TIMING run: capture+instantiate %.1f us%s, loop %.1f us (%d iterations launched)\n",
+                tc1 - tc0, reused ? " (graph reused)" : "", now_us() - tc1, launched);
     // the final state (a speculative batch after convergence changed nothing)
     DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
     DFQ_HIP_CHECK(hipStreamSynchronize(s));

@@ -21,12 +21,13 @@ sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_UNFUSED_FIN", "DFQ_CLE_GROUPS", "DFQ_CLE_GROUP_GRID", "DFQ_CLE_ORDERED", "DFQ_CLE_GSYNC_NOFENCE",
-            "DFQ_CLE_NO_DW_PAIRS", "DFQ_CLE_FORK", "DFQ_CLE_NO_SELF_RANGES")
+            "DFQ_CLE_NO_DW_PAIRS", "DFQ_CLE_FORK", "DFQ_CLE_NO_SELF_RANGES", "DFQ_CLE_GRAPH")
 CONFIGS = {
     "tiles_fin": {},                                       # the product
     "no_dw_pairs": {"DFQ_CLE_NO_DW_PAIRS": "1"},           # round-2 steps: one launch per relation
     "fork": {"DFQ_CLE_FORK": "1"},                         # next ranges on a concurrent graph branch
     "no_self_ranges": {"DFQ_CLE_NO_SELF_RANGES": "1"},     # every next range from a range task
+    "eager": {"DFQ_CLE_GRAPH": "0"},                       # launches enqueued one by one, no batch graph
     "tiles_fin_ordered": {"DFQ_CLE_ORDERED": "1"},
     "grouped": {"DFQ_CLE_GROUPS": "1"},
     "grouped_ordered": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_ORDERED": "1"},
@@ -59,6 +60,7 @@ def main():
         os.environ.update(CONFIGS[tag])
 
     res = {(t, m): [] for t in cfgs for m in models}
+    host = {(t, m): [] for t in cfgs for m in models}
     info = {}
     for t in cfgs:   # parity + warm-up
         use(t)
@@ -79,11 +81,14 @@ def main():
                             symmetric=True, bc_mode="fused", timings=tm)
                 torch.cuda.synchronize(dev)
                 res[(t, m)].append(tm["cle"] * 1e3)
+                host[(t, m)].append(cle.LAST_RUN.get("host_ms", {}))
     for t in cfgs:
         for m in models:
             v = res[(t, m)]
             print(json.dumps({"config": t, "model": m, "cle_ms_median": round(statistics.median(v), 3),
-                              "cle_ms_min": round(min(v), 3), **info[(t, m)]}), flush=True)
+                              "cle_ms_min": round(min(v), 3), **info[(t, m)],
+                              "host_ms_median": {k: round(statistics.median(h[k] for h in host[(t, m)]), 3)
+                                                 for k in (host[(t, m)][0] if host[(t, m)] else {})}}), flush=True)
 
 
 if __name__ == "__main__":

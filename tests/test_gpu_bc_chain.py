@@ -58,7 +58,7 @@ class Walk:
             bcols = i2 if (i2 == f or f == 1) else f
             self.vec(f"vec{l}", np.zeros(o * bcols))
             self.op(1, 0, f"E{l}", f"ex{l}", f"bias{l}", f"vec{l}", o, i2, f)
-            if g.random() < 0.3:   # a second branch of the same layer: same bias, same row owners
+            if g.random() < 0.3 and i2 > 1:   # a second branch of the same layer: same bias, same row owners
                 self.vec(f"exb{l}", np.zeros(1))
                 self.op(0, 0, f"fw{l}", f"fb{l}", f"exb{l}", None, 1)
                 self.vec(f"vecb{l}", np.zeros(o * i2))
