@@ -1661,7 +1661,7 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
     // The last arrival of the launch: tiny chunks' sums, then the per-layer means,
     // the history and the stop rule.
     auto finish = [&]() {
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0 && F.nchunks > F.nbig)   // tiny chunks exist (none in the zoo's models)
             for (int64_t k = 0; k < F.nchunks; ++k) {
                 const CleChunk c2 = chunks[k];
                 if (c2.len < 8) st_coh(F.part + (int64_t)c2.layer * F.S + c2.t, 0.f + cle_tiny_chunk_sum(layers, c2));
@@ -1847,7 +1847,7 @@ cle_loop_group_kernel(CleGroups Gs, const CleRel* __restrict__ rels, uint32_t* _
     // every block arrives once (after its chunk hand-offs): the last one runs the
     // stop rule (a block that saw st->error still arrives, so nothing hangs)
     if (arrive(F.cnt + F.nchunks, gridDim.x)) {
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0 && F.nchunks > F.nbig)   // tiny chunks exist (none in the zoo's models)
             for (int64_t k = 0; k < F.nchunks; ++k) {
                 const CleChunk c2 = chunks[k];
                 if (c2.len < 8) st_coh(F.part + (int64_t)c2.layer * F.S + c2.t, 0.f + cle_tiny_chunk_sum(layers, c2));
@@ -2859,6 +2859,13 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
 
 constexpr int32_t kCleBatch = 8;   // iterations enqueued between state read-backs (even: see par_next)
 static_assert(kCleBatch % 2 == 0, "the tiles/range launch's parity argument assumes even batches");
+// Iterations per batch: kCleBatch; the diagnostics library takes DFQ_CLE_BATCH
+// (rounded up to even) for the A/B.
+static int32_t cle_batch() {
+    const char* e = ab_env("DFQ_CLE_BATCH");
+    const int32_t b = e && *e ? std::max(2, atoi(e)) : kCleBatch;
+    return b + (b & 1);
+}
 constexpr int32_t kClePersistBatch = 256;   // persistent loop: iterations per cooperative launch
 
 // The persistent loop's co-resident grid (0 = use the graph path).  Measured
@@ -2989,14 +2996,19 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         return DFQ_OK;
     }
 #endif
-    // kCleBatch iterations as one HIP graph (kernels of finished runs return at
-    // once: the stop rule lives in d_state); DFQ_CLE_GRAPH=0: eager launches.
+    // Batches of `batch` iterations (kernels of finished runs return at once: the
+    // stop rule lives in d_state), enqueued launch by launch.  Replaying the batch
+    // as a captured HIP graph measured slower even with the capture cached (CLE
+    // on MobileNetV2 4.75 vs 4.51 ms, profiles/r03/cle_ab_p.jsonl): the graph is the
+    // diagnostics A/B DFQ_CLE_GRAPH=1.
     const char* ge = ab_env("DFQ_CLE_GRAPH");
-    const bool use_graph = !(ge && ge[0] == '0');
+    const bool use_graph = ge && ge[0] == '1';
+    const int32_t batch = cle_batch();
     const double tc0 = now_us();
     bool reused = false;
     if (use_graph && !init.done) {
         std::vector<char> key = cle_graph_key(p);
+        key.insert(key.end(), reinterpret_cast<const char*>(&batch), reinterpret_cast<const char*>(&batch + 1));
         reused = ctx.gexec && key == ctx.gkey;
         if (!reused) {
             if (ctx.gexec) (void)hipGraphExecDestroy(ctx.gexec);
@@ -3004,7 +3016,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
             ctx.gkey.clear();
             DFQ_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             int rc = DFQ_OK;
-            for (int32_t it = 0; it < kCleBatch && rc == DFQ_OK; ++it) rc = cle_enqueue_iteration(p, s, it);
+            for (int32_t it = 0; it < batch && rc == DFQ_OK; ++it) rc = cle_enqueue_iteration(p, s, it);
             hipGraph_t g = nullptr;
             const hipError_t ec = hipStreamEndCapture(s, &g);
             if (rc != DFQ_OK) {
@@ -3031,12 +3043,12 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         if (use_graph) {
             DFQ_HIP_CHECK(hipGraphLaunch(ctx.gexec, s));
         } else {
-            for (int32_t it = 0; it < kCleBatch; ++it) {
+            for (int32_t it = 0; it < batch; ++it) {
                 const int rc = cle_enqueue_iteration(p, s, it);
                 if (rc != DFQ_OK) return rc;
             }
         }
-        launched += kCleBatch;
+        launched += batch;
         DFQ_HIP_CHECK(hipMemcpyAsync(ctx.h_state + 1 + sl, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
         DFQ_HIP_CHECK(hipEventRecord(ctx.ev[sl], s));
         return DFQ_OK;

@@ -1101,12 +1101,15 @@ bool bc_ov(const BcRange& x, const BcRange& y) { return x.lo < x.hi && y.lo < y.
 bool bc_eq(const BcRange& x, const BcRange& y) { return x.lo == y.lo && x.hi == y.hi; }
 bool bc_in(const BcRange& x, const BcRange& y) { return y.lo <= x.lo && x.hi <= y.hi; }
 
-// Phases of a validated chain for bc_chain_kernel (rules at the kernel).  false:
-// the chain does something this path does not forward (an op that aliases
-// itself, E written earlier in the chain, an expectation larger than the LDS
-// slots, 2^31+ elements): it runs as per-op launches instead.
-bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vector<BcDevOp>& dev,
-                     std::vector<int32_t>& phase) {
+// Phases of a validated chain for bc_chain_kernel (rules at the kernel).
+// Returns 0, or -1: the chain does something this path does not forward (an op
+// that aliases itself, E written earlier in the chain, an expectation larger than
+// the LDS slots, 2^31+ elements) and runs as per-op launches instead; or k + 1:
+// retry with a phase break forced before op k (an accumulating expectation met a
+// conflict after its running sum's first term: that term moves to the new phase
+// with it -- 'add' branches whose second BN was just propagated into).
+int bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, const std::vector<char>& force,
+                    std::vector<BcDevOp>& dev, std::vector<int32_t>& phase) {
     enum { kPlain, kSlot, kBias, kVec };
     struct Wr {
         BcRange r;
@@ -1117,10 +1120,11 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
         BcRange r;
         int32_t off;
         bool read;   // an APPLY of this phase read it (a rewrite would change what a recompute sees)
+        int32_t src; // the op (index into ops) that started it
     };
     std::vector<Wr> wr;
     std::vector<BcRange> rd, ever;   // this phase's global reads; every write of the chain so far
-    std::vector<Slot> slot;
+    std::vector<Slot> slot, prev_slot;
     int32_t top = 0;
     int64_t wcur = 0;
     dev.clear();
@@ -1144,6 +1148,12 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
     for (int32_t k = 0; k < n_ops; ++k) {
         const dfq_bc_op& op = ops[k];
         if ((op.kind == DFQ_BC_OP_EXPECT || op.kind == DFQ_BC_OP_COPY) && op.n == 0) continue;
+        if (force[k] && phase.back() != (int32_t)dev.size()) {
+            phase.push_back((int32_t)dev.size());
+            wr.clear(); rd.clear(); slot.clear();
+            top = 0;
+            wcur = 0;
+        }
         BcDevOp d{};
         d.kind = op.kind; d.flag = op.flag; d.a = op.a; d.b = op.b; d.out = op.out; d.out2 = op.out2;
         d.n = op.n; d.i2 = op.i2; d.f = op.f;
@@ -1152,12 +1162,12 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
         std::vector<BcRange> reads, writes;
         BcRange rmw{};
         if (op.kind == DFQ_BC_OP_EXPECT) {
-            if (op.n > kBcSlotFloats) return false;
+            if (op.n > kBcSlotFloats) return -1;
             reads = {bc_rng(op.a, op.n), bc_rng(op.b, op.n)};
             writes = {bc_rng(op.out, op.n)};
         } else if (op.kind == DFQ_BC_OP_APPLY) {
             d.bcols = (op.i2 == op.f || op.f == 1) ? op.i2 : op.f;
-            if (op.n * op.i2 >= kMax || op.n * d.bcols >= kMax) return false;
+            if (op.n * op.i2 >= kMax || op.n * d.bcols >= kMax) return -1;
             // round-up magic for k / bcols: l = ceil(log2 bcols), m = 2^32 (2^l - bcols) / bcols + 1
             uint32_t l = 0;
             while (((uint64_t)1 << l) < (uint64_t)d.bcols) ++l;
@@ -1165,13 +1175,13 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
             d.dmagic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - (uint64_t)d.bcols)) / (uint64_t)d.bcols + 1);
             const BcRange E = bc_rng(op.a, op.n * op.i2);
             for (const BcRange& w : ever)
-                if (bc_ov(w, E)) return false;   // E is loaded non-coherently
+                if (bc_ov(w, E)) return -1;   // E is loaded non-coherently
             reads = {E, bc_rng(op.b, op.f)};
             rmw = bc_rng(op.out, op.n);
             writes = {rmw};
             if (op.out2) writes.push_back(bc_rng(op.out2, op.n * d.bcols));
         } else if (op.kind == DFQ_BC_OP_PROPAGATE) {
-            if (op.n >= kMax) return false;
+            if (op.n >= kMax) return -1;
             reads = {bc_rng(op.a, op.n)};
             rmw = bc_rng(op.out, op.f);
             writes = {rmw};
@@ -1181,9 +1191,9 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
         }
         for (const BcRange& w : writes) {   // an op that aliases itself
             for (const BcRange& r : reads)
-                if (bc_ov(w, r)) return false;
+                if (bc_ov(w, r)) return -1;
             for (const BcRange& w2 : writes)
-                if (&w != &w2 && bc_ov(w, w2)) return false;
+                if (&w != &w2 && bc_ov(w, w2)) return -1;
         }
         // try to join the current phase; on a conflict start a new one and retry
         for (int attempt = 0;; ++attempt) {
@@ -1198,7 +1208,11 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
                 if ((op.flag >> 1) & 1) {
                     // the running sum from another phase would be read by every block while
                     // block 0 rewrites it: not forwarded
-                    if (!s && attempt > 0) return false;
+                    if (!s && attempt > 0) {   // the first term stayed behind: move it here
+                        for (const Slot& x : prev_slot)
+                            if (bc_eq(x.r, o) && !force[x.src]) return x.src + 1;
+                        return -1;
+                    }
                     if (s) d.lds_prev = s->off;
                     else ok = false;
                 }
@@ -1214,7 +1228,7 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
                     if (s) d.lds_out = s->off;
                     else if (top + op.n <= kBcSlotFloats) {
                         d.lds_out = top;
-                        slot.push_back(Slot{o, top, false});
+                        slot.push_back(Slot{o, top, false, k});
                         top += (int32_t)((op.n + 15) / 16 * 16);
                     } else ok = false;
                 }
@@ -1237,8 +1251,7 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
                         wb = wcur;
                         wcur = (wcur + op.n) % nw;
                     }
-                    d.wbase = wb;
-                    grd.push_back(rmw);
+                    d.wbase = wb;   // (its bias read needs no entry: every writer checks the write list)
                     if (s) s->read = true;
                 }
             } else if (op.kind == DFQ_BC_OP_PROPAGATE) {
@@ -1255,7 +1268,6 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
                 if (ok) {
                     d.wbase = wcur;
                     wcur = (wcur + op.f) % nw;
-                    grd.push_back(rmw);
                 }
             } else {
                 grd.push_back(reads[0]);
@@ -1273,8 +1285,9 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
                 dev.push_back(d);
                 break;
             }
-            if (attempt > 0 || phase.back() == (int32_t)dev.size()) return false;   // conflicts with nothing
+            if (attempt > 0 || phase.back() == (int32_t)dev.size()) return -1;   // conflicts with nothing
             phase.push_back((int32_t)dev.size());
+            prev_slot.swap(slot);
             wr.clear(); rd.clear(); slot.clear();
             top = 0;
             wcur = 0;
@@ -1282,7 +1295,19 @@ bool bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vecto
         }
     }
     if (phase.back() != (int32_t)dev.size()) phase.push_back((int32_t)dev.size());
-    return !dev.empty();
+    return dev.empty() ? -1 : 0;
+}
+
+// bc_chain_phases with the breaks it asks for (each op at most once)
+bool bc_chain_plan(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vector<BcDevOp>& dev,
+                   std::vector<int32_t>& phase) {
+    std::vector<char> force(n_ops, 0);
+    for (;;) {
+        const int r = bc_chain_phases(ops, n_ops, nw, force, dev, phase);
+        if (r == 0) return true;
+        if (r < 0 || force[r - 1]) return false;
+        force[r - 1] = 1;
+    }
 }
 
 // Per-device state of the cooperative chain: the device table (op table, phase
@@ -1325,7 +1350,7 @@ int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
     if (const char* g = ab_env("DFQ_BC_GRID")) grid = std::max(1, std::min(ctx.max_grid, atoi(g)));
     std::vector<BcDevOp> dv;
     std::vector<int32_t> ph;
-    if (!bc_chain_phases(ops, n_ops, (int64_t)grid * kBcChainWaves, dv, ph)) return kBcNotEligible;
+    if (!bc_chain_plan(ops, n_ops, (int64_t)grid * kBcChainWaves, dv, ph)) return kBcNotEligible;
     const int32_t nphase = (int32_t)ph.size() - 1;
     auto up256 = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t o_ph = up256(sizeof(BcDevOp) * dv.size());
@@ -1363,6 +1388,29 @@ int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
 }
 }  // namespace
 }  // namespace dfq
+
+#ifdef DFQ_DIAGNOSTICS
+#include "dfq_diag.h"
+extern "C" int dfq_bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t waves, int32_t* n_phases,
+                                   int32_t* op_phase) {
+    if (n_ops < 0 || (n_ops > 0 && !ops) || waves < 1) return DFQ_ERR_INVALID;
+    std::vector<dfq::BcDevOp> dv;
+    std::vector<int32_t> ph;
+    if (!dfq::bc_chain_plan(ops, n_ops, waves, dv, ph)) return 1;
+    if (n_phases) *n_phases = (int32_t)ph.size() - 1;
+    if (op_phase) {   // dev ops are the non-empty ops in order
+        int32_t j = 0, p = 0;
+        for (int32_t k = 0; k < n_ops; ++k) {
+            const bool empty = (ops[k].kind == DFQ_BC_OP_EXPECT || ops[k].kind == DFQ_BC_OP_COPY) && ops[k].n == 0;
+            if (empty) { op_phase[k] = -1; continue; }
+            while (p + 1 < (int32_t)ph.size() && ph[p + 1] <= j) ++p;
+            op_phase[k] = p;
+            ++j;
+        }
+    }
+    return DFQ_OK;
+}
+#endif
 
 extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed_op, void* stream) {
     if (failed_op) *failed_op = -1;

@@ -1,0 +1,13 @@
+set -o pipefail
+export TMPDIR=/tmp
+out=gpurun_out/r03q; mkdir -p $out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_bc_chain.py tests/test_gpu_transforms.py -x -v --timeout 120 --timeout-method thread > $out/pytest_bc.log 2>&1 || { echo "pytest bc rc=$?"; tail -60 $out/pytest_bc.log; exit 1; }
+tail -2 $out/pytest_bc.log
+timeout -k 10 500 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_parity_repeat.py tests/test_gpu_cle_plan.py -x -q --timeout 280 --timeout-method thread > $out/pytest.log 2>&1 || { echo "pytest rc=$?"; tail -60 $out/pytest.log; exit 1; }
+tail -2 $out/pytest.log
+timeout -k 10 400 python -u scripts/bc_ab.py --reps 7 --configs coop,launches,grid128,grid256 > $out/bc_ab.jsonl 2>&1 || { echo "bc_ab rc=$?"; tail -30 $out/bc_ab.jsonl; exit 1; }
+grep config $out/bc_ab.jsonl
+timeout -k 10 400 python -u scripts/cle_ab.py --reps 7 --configs tiles_fin,graph,batch4,batch16 > $out/cle_ab.jsonl 2>&1 || { echo "cle_ab rc=$?"; tail -30 $out/cle_ab.jsonl; exit 1; }
+grep config $out/cle_ab.jsonl
+DFQ_CLE_TIMING=1 timeout -k 10 300 python -u scripts/cle_ab.py --reps 3 --configs tiles_fin --models mobilenetv2 > $out/cle_timing.log 2>&1 || { echo "timing rc=$?"; tail -30 $out/cle_timing.log; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d /root/repo/$out/trace -o bc -- python /root/repo/scripts/bc_ab.py --reps 2 --configs coop,launches --models mobilenetv2,resnet50 > /root/repo/$out/trace.log 2>&1 || { echo "rocprof rc=$?"; exit 1; }

@@ -42,13 +42,15 @@ sys.path.insert(0, os.environ["DFQ_ROOT"])
 from tests.parity import pipeline_mismatches
 from data_free_quantization_amd import Cross_layer_equal as cle
 SWITCHES = ("DFQ_CLE_UNFUSED_FIN", "DFQ_CLE_GROUPS", "DFQ_CLE_GROUP_GRID", "DFQ_CLE_ORDERED", "DFQ_CLE_NO_DW_PAIRS",
-            "DFQ_CLE_FORK", "DFQ_CLE_NO_SELF_RANGES")
+            "DFQ_CLE_FORK", "DFQ_CLE_NO_SELF_RANGES", "DFQ_CLE_GRAPH", "DFQ_CLE_BATCH")
 CONFIGS = {
     "tiles_fin": {},                                      # the product: steps + fused tiles / stop rule
     "tiles_fin_ordered": {"DFQ_CLE_ORDERED": "1"},        # release/acquire hand-offs
     "no_dw_pairs": {"DFQ_CLE_NO_DW_PAIRS": "1"},           # one launch per relation (round 2)
     "fork": {"DFQ_CLE_FORK": "1"},                         # next ranges on a concurrent graph branch
     "no_self_ranges": {"DFQ_CLE_NO_SELF_RANGES": "1"},     # every next range from a range task
+    "graph": {"DFQ_CLE_GRAPH": "1"},                       # batches replayed as a cached HIP graph
+    "batch4": {"DFQ_CLE_BATCH": "4"},
     "unfused": {"DFQ_CLE_UNFUSED_FIN": "1"},              # stop rule as launches of its own
     "grouped": {"DFQ_CLE_GROUPS": "1"},                   # chain-grouped A/B, one launch per iteration
     "grouped_40_blocks": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_GROUP_GRID": "40"},   # many group barriers
