@@ -2857,7 +2857,11 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     return DFQ_OK;
 }
 
-constexpr int32_t kCleBatch = 8;   // iterations enqueued between state read-backs (even: see par_next)
+// Iterations enqueued between state read-backs (even: see par_next).  4: the
+// batch after convergence (enqueued ahead of the check) runs as no-op launches,
+// and smaller batches waste fewer of them -- CLE on MobileNetV2 3.88 ms with 4,
+// 3.97 with 8 and 16 (profiles/r03/cle_ab_q.jsonl).
+constexpr int32_t kCleBatch = 4;
 static_assert(kCleBatch % 2 == 0, "the tiles/range launch's parity argument assumes even batches");
 // Iterations per batch: kCleBatch; the diagnostics library takes DFQ_CLE_BATCH
 // (rounded up to even) for the A/B.

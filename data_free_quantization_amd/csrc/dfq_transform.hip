@@ -12,6 +12,7 @@
 #include <cmath>
 #include <mutex>
 #include <new>
+#include <string>
 #include <vector>
 
 namespace dfq {
@@ -309,7 +310,7 @@ __device__ __forceinline__ void bc_op_copy(const BcDevOp* __restrict__ opp) {
 
 __global__ void __launch_bounds__(kBcChainThreads)
 bc_chain_kernel(const BcDevOp* __restrict__ ops, const int32_t* __restrict__ phase, int32_t nphase,
-                uint32_t* bar, int32_t* err) {
+                uint32_t* bar, int32_t* err, uint64_t* tl) {
     __shared__ float slots[kBcSlotFloats];
     __shared__ float scratch[kBcChainWaves][kBcChainScratch + kBcChainScratch / 16];
     __shared__ int flag;
@@ -337,6 +338,7 @@ bc_chain_kernel(const BcDevOp* __restrict__ ops, const int32_t* __restrict__ pha
                 bc_op_copy(ops + k);
             }
         }
+        if (tl && blockIdx.x == 0 && threadIdx.x == 0) tl[2 * p] = __builtin_amdgcn_s_memrealtime();
         if (p + 1 == nphase) break;
         // grid barrier: every store of this phase has completed before the one add
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -358,6 +360,7 @@ bc_chain_kernel(const BcDevOp* __restrict__ ops, const int32_t* __restrict__ pha
             flag = good;
         }
         __syncthreads();
+        if (tl && blockIdx.x == 0 && threadIdx.x == 0) tl[2 * p + 1] = __builtin_amdgcn_s_memrealtime();
         if (!flag) return;
     }
 }
@@ -1355,7 +1358,11 @@ int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
     auto up256 = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t o_ph = up256(sizeof(BcDevOp) * dv.size());
     const size_t o_bar = o_ph + up256(sizeof(int32_t) * ph.size());
-    const size_t need = o_bar + 256;
+    // diagnostics DFQ_BC_TIMELINE=1: block 0's 100 MHz clock at each phase end and
+    // barrier exit, printed per phase to stderr after the call
+    const bool timeline = ab_env("DFQ_BC_TIMELINE") != nullptr;
+    const size_t o_tl = o_bar + 256;
+    const size_t need = o_tl + (timeline ? sizeof(uint64_t) * 2 * (size_t)nphase : 0);
     if (ctx.cap < need) {
         if (ctx.dbuf) (void)hipFree(ctx.dbuf);
         if (ctx.hbuf) (void)hipHostFree(ctx.hbuf);
@@ -1374,15 +1381,43 @@ int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
     const int32_t* d_ph = reinterpret_cast<const int32_t*>(ctx.dbuf + o_ph);
     uint32_t* d_bar = reinterpret_cast<uint32_t*>(ctx.dbuf + o_bar);
     int32_t* d_err = reinterpret_cast<int32_t*>(ctx.dbuf + o_bar + 128);
-    void* args[] = {&d_ops, &d_ph, const_cast<int32_t*>(&nphase), &d_bar, &d_err};
-    DFQ_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(bc_chain_kernel), dim3(grid),
-                                             dim3(kBcChainThreads), args, 0, s));
+    uint64_t* d_tl = timeline ? reinterpret_cast<uint64_t*>(ctx.dbuf + o_tl) : nullptr;
+    // A plain launch: hipLaunchCooperativeKernel measured ~1 ms of launch overhead
+    // per call (MobileNetV2 BC stage 2.70 vs 2.13 ms with a 1.07 ms kernel,
+    // profiles/r03/bc_ab_q.jsonl).  The grid (<= 64 blocks, one per CU by its LDS
+    // and VGPRs, at most the occupancy limit) fits on the device at once, so every
+    // block becomes resident even beside other work (the spinning ones hold <= 64
+    // CUs); a barrier that still waits ~1 s reports an error instead of hanging.
+    const char* cl = ab_env("DFQ_BC_COOPLAUNCH");   // diagnostics A/B: the cooperative launch
+    if (cl && cl[0] == '1') {
+        void* args[] = {&d_ops, &d_ph, const_cast<int32_t*>(&nphase), &d_bar, &d_err, &d_tl};
+        DFQ_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(bc_chain_kernel), dim3(grid),
+                                                 dim3(kBcChainThreads), args, 0, s));
+    } else {
+        hipLaunchKernelGGL(bc_chain_kernel, dim3(grid), dim3(kBcChainThreads), 0, s, d_ops, d_ph, nphase, d_bar, d_err,
+                           d_tl);
+        DFQ_LAUNCH_CHECK();
+    }
     int32_t* h_err = reinterpret_cast<int32_t*>(ctx.hbuf + o_bar + 128);
     DFQ_HIP_CHECK(hipMemcpyAsync(h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
     if (*h_err) {
         set_last_hip_error(hipErrorLaunchTimeOut);
         return DFQ_ERR_HIP;
+    }
+    if (timeline) {
+        std::vector<uint64_t> t(2 * (size_t)nphase);
+        DFQ_HIP_CHECK(hipMemcpy(t.data(), d_tl, sizeof(uint64_t) * t.size(), hipMemcpyDeviceToHost));
+        uint64_t prev = 0;
+        for (int32_t q = 0; q < nphase; ++q) {
+            std::string kinds;
+            for (int32_t k = ph[q]; k < ph[q + 1]; ++k) kinds += "EAPC"[dv[k].kind];
+            const double work = q == 0 ? 0.0 : (double)(t[2 * q] - prev) * 0.01;
+            const double bar = q + 1 < nphase ? (double)(t[2 * q + 1] - t[2 * q]) * 0.01 : 0.0;
+            fprintf(stderr, "DFQ_BC_TIMELINE phase %d ops %s work %.2f us barrier %.2f us\n", q, kinds.c_str(), work,
+                    bar);
+            prev = t[2 * q + 1];
+        }
     }
     return DFQ_OK;
 }

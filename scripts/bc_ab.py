@@ -19,9 +19,10 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
-SWITCHES = ("DFQ_BC_CHAIN", "DFQ_BC_GRID")
+SWITCHES = ("DFQ_BC_CHAIN", "DFQ_BC_GRID", "DFQ_BC_COOPLAUNCH")
 CONFIGS = {
-    "coop": {},                                   # the product: one cooperative launch (64 blocks)
+    "coop": {},                                   # the product: one launch of 64 co-resident blocks
+    "cooplaunch": {"DFQ_BC_COOPLAUNCH": "1"},     # the same through hipLaunchCooperativeKernel
     "launches": {"DFQ_BC_CHAIN": "launches"},     # round 2: one launch per op
     "grid8": {"DFQ_BC_GRID": "8"},
     "grid16": {"DFQ_BC_GRID": "16"},

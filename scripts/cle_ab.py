@@ -24,13 +24,13 @@ SWITCHES = ("DFQ_CLE_UNFUSED_FIN", "DFQ_CLE_GROUPS", "DFQ_CLE_GROUP_GRID", "DFQ_
             "DFQ_CLE_NO_DW_PAIRS", "DFQ_CLE_FORK", "DFQ_CLE_NO_SELF_RANGES", "DFQ_CLE_GRAPH",
             "DFQ_CLE_BATCH")
 CONFIGS = {
-    "tiles_fin": {},                                       # the product (eager batches of 8)
+    "tiles_fin": {},                                       # the product (eager batches of 4)
     "no_dw_pairs": {"DFQ_CLE_NO_DW_PAIRS": "1"},           # round-2 steps: one launch per relation
     "fork": {"DFQ_CLE_FORK": "1"},                         # next ranges on a concurrent graph branch
     "no_self_ranges": {"DFQ_CLE_NO_SELF_RANGES": "1"},     # every next range from a range task
     "graph": {"DFQ_CLE_GRAPH": "1"},                       # each batch replayed as a (cached) HIP graph
-    "batch4": {"DFQ_CLE_BATCH": "4"},
-    "batch16": {"DFQ_CLE_BATCH": "16"},
+    "batch8": {"DFQ_CLE_BATCH": "8"},
+    "batch2": {"DFQ_CLE_BATCH": "2"},
     "tiles_fin_ordered": {"DFQ_CLE_ORDERED": "1"},
     "grouped": {"DFQ_CLE_GROUPS": "1"},
     "grouped_ordered": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_ORDERED": "1"},

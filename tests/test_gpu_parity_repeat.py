@@ -50,7 +50,7 @@ CONFIGS = {
     "fork": {"DFQ_CLE_FORK": "1"},                         # next ranges on a concurrent graph branch
     "no_self_ranges": {"DFQ_CLE_NO_SELF_RANGES": "1"},     # every next range from a range task
     "graph": {"DFQ_CLE_GRAPH": "1"},                       # batches replayed as a cached HIP graph
-    "batch4": {"DFQ_CLE_BATCH": "4"},
+    "batch8": {"DFQ_CLE_BATCH": "8"},
     "unfused": {"DFQ_CLE_UNFUSED_FIN": "1"},              # stop rule as launches of its own
     "grouped": {"DFQ_CLE_GROUPS": "1"},                   # chain-grouped A/B, one launch per iteration
     "grouped_40_blocks": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_GROUP_GRID": "40"},   # many group barriers
