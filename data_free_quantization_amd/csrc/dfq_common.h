@@ -192,9 +192,37 @@ __host__ __device__ inline int aten_ceil_log2(int64_t x) {
 }
 
 // multi_row_sum for one stream: sequential adds, flushed up a 4-level cascade.
+// Level step 16 (every size below 2^20): a compile-time step, so each level-0
+// block's 16 loads are issued together ahead of its 16 in-order adds (a runtime
+// step left one load in flight per add).
+template <typename Get>
+__host__ __device__ inline float aten_cascade_16(Get get, int64_t size) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int64_t i = 0;
+    while (i + 16 <= size) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = get(i + j);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a0 += v[j];
+        i += 16;
+        a1 += a0; a0 = 0.f;
+        if (i & (15 << 4)) continue;
+        a2 += a1; a1 = 0.f;
+        if (i & (15 << 8)) continue;
+        a3 += a2; a2 = 0.f;
+    }
+    for (; i < size; ++i) a0 += get(i);
+    a0 += a1;
+    a0 += a2;
+    a0 += a3;
+    return a0;
+}
+
 template <typename Get>
 __host__ __device__ inline float aten_cascade(Get get, int64_t size) {
     const int lp = aten_ceil_log2(size) / 4 > 4 ? aten_ceil_log2(size) / 4 : 4;
+    if (lp == 4) return aten_cascade_16(get, size);
     const int64_t step = (int64_t)1 << lp, mask = step - 1;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     int64_t i = 0;
