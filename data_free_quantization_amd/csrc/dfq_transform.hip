@@ -301,11 +301,11 @@ __device__ __forceinline__ void bc_op_propagate(const BcDevOp* __restrict__ opp,
         bc_column(op, L, nrows, c, [&](int64_t r) { return ld_coh(op.a + r * F + c); });
 }
 
+// member wbase of a run of copies: block wbase mod grid copies all of it
 __device__ __forceinline__ void bc_op_copy(const BcDevOp* __restrict__ opp) {
     const BcDevOp op = *opp;
-    for (int64_t i = (int64_t)blockIdx.x * kBcChainThreads + threadIdx.x; i < op.n;
-         i += (int64_t)gridDim.x * kBcChainThreads)
-        st_coh(op.out + i, ld_coh(op.a + i));
+    if (op.wbase % gridDim.x != blockIdx.x) return;
+    for (int64_t i = threadIdx.x; i < op.n; i += kBcChainThreads) st_coh(op.out + i, ld_coh(op.a + i));
 }
 
 __global__ void __launch_bounds__(kBcChainThreads)
@@ -326,8 +326,10 @@ bc_chain_kernel(const BcDevOp* __restrict__ ops, const int32_t* __restrict__ pha
         for (int32_t k = phase[p]; k < phase[p + 1]; ++k) {
             const int32_t kind = ops[k].kind;
             if (kind == DFQ_BC_OP_EXPECT) {
+                // an accumulating expectation reads only its own threads' slot words:
+                // one block barrier after the run of expectations
                 bc_op_expect(ops + k, L);
-                __syncthreads();
+                if (k + 1 == phase[p + 1] || ops[k + 1].kind != DFQ_BC_OP_EXPECT) __syncthreads();
             } else if (kind == DFQ_BC_OP_APPLY) {
                 bc_op_apply(ops + k, L);
             } else if (kind == DFQ_BC_OP_PROPAGATE) {
@@ -1126,7 +1128,7 @@ int bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, const std::
         int32_t src; // the op (index into ops) that started it
     };
     std::vector<Wr> wr;
-    std::vector<BcRange> rd, ever;   // this phase's global reads; every write of the chain so far
+    std::vector<BcRange> rd;   // this phase's global reads
     std::vector<Slot> slot, prev_slot;
     int32_t top = 0;
     int64_t wcur = 0;
@@ -1176,9 +1178,7 @@ int bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, const std::
             while (((uint64_t)1 << l) < (uint64_t)d.bcols) ++l;
             d.dshift = l;
             d.dmagic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - (uint64_t)d.bcols)) / (uint64_t)d.bcols + 1);
-            const BcRange E = bc_rng(op.a, op.n * op.i2);
-            for (const BcRange& w : ever)
-                if (bc_ov(w, E)) return -1;   // E is loaded non-coherently
+            const BcRange E = bc_rng(op.a, op.n * op.i2);   // written by no op (bc_chain_plan checks)
             reads = {E, bc_rng(op.b, op.f)};
             rmw = bc_rng(op.out, op.n);
             writes = {rmw};
@@ -1275,6 +1275,10 @@ int bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, const std::
             } else {
                 grd.push_back(reads[0]);
                 ok = !hits_wr(reads[0]) && !hits_wr(writes[0]) && !hits_rd(writes[0]);
+                // position in this phase's run of consecutive copies: run member j is
+                // block j mod grid's alone (the copies are independent)
+                if (ok) d.wbase = (!dev.empty() && phase.back() < (int32_t)dev.size() &&
+                                   dev.back().kind == DFQ_BC_OP_COPY) ? dev.back().wbase + 1 : 0;
             }
             if (ok) {
                 const int32_t me = (int32_t)dev.size();
@@ -1284,7 +1288,6 @@ int bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, const std::
                     wr.push_back(Wr{writes[0], kBias, me});
                     if (writes.size() > 1) wr.push_back(Wr{writes[1], kVec, me});
                 } else wr.push_back(Wr{writes[0], kPlain, me});
-                for (const BcRange& w : writes) ever.push_back(w);
                 dev.push_back(d);
                 break;
             }
@@ -1301,16 +1304,55 @@ int bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, const std::
     return dev.empty() ? -1 : 0;
 }
 
-// bc_chain_phases with the breaks it asks for (each op at most once)
+// The chain's phases, in one planner pass.  Before it, on the whole op list:
+//   * no APPLY's E may overlap anything an op writes (E is loaded without
+//     coherence): one sorted sweep instead of a check per pair;
+//   * the first term of every accumulated expectation ('add' branch) starts a
+//     phase, so its running sum never stays behind in an earlier phase.
+// A second pass with the one break the planner still asks for is the rare case.
 bool bc_chain_plan(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vector<BcDevOp>& dev,
                    std::vector<int32_t>& phase) {
+    std::vector<std::pair<BcRange, int>> iv;   // (range, 0 = E / 1 = written)
     std::vector<char> force(n_ops, 0);
-    for (;;) {
+    for (int32_t k = 0; k < n_ops; ++k) {
+        const dfq_bc_op& op = ops[k];
+        switch (op.kind) {
+            case DFQ_BC_OP_EXPECT:
+                iv.push_back({bc_rng(op.out, op.n), 1});
+                if ((op.flag >> 1) & 1)   // its first term: the latest plain expectation into the same slot
+                    for (int32_t j = k - 1; j >= 0; --j)
+                        if (ops[j].kind == DFQ_BC_OP_EXPECT && ops[j].out == op.out) {
+                            if (!((ops[j].flag >> 1) & 1)) {
+                                force[j] = 1;
+                                break;
+                            }
+                        }
+                break;
+            case DFQ_BC_OP_APPLY: {
+                const int64_t bcols = (op.i2 == op.f || op.f == 1) ? op.i2 : op.f;
+                iv.push_back({bc_rng(op.a, op.n * op.i2), 0});
+                iv.push_back({bc_rng(op.out, op.n), 1});
+                if (op.out2) iv.push_back({bc_rng(op.out2, op.n * bcols), 1});
+                break;
+            }
+            case DFQ_BC_OP_PROPAGATE: iv.push_back({bc_rng(op.out, op.f), 1}); break;
+            default: iv.push_back({bc_rng(op.out, op.n), 1}); break;
+        }
+    }
+    std::sort(iv.begin(), iv.end(), [](const auto& x, const auto& y) { return x.first.lo < y.first.lo; });
+    uintptr_t hi_e = 0, hi_w = 0;   // furthest end of the E / written ranges seen so far
+    for (const auto& [r, w] : iv) {
+        if (r.lo == r.hi) continue;
+        if (w ? r.lo < hi_e : r.lo < hi_w) return false;   // an E overlaps a write
+        (w ? hi_w : hi_e) = std::max(w ? hi_w : hi_e, r.hi);
+    }
+    for (int pass = 0; pass < 4; ++pass) {
         const int r = bc_chain_phases(ops, n_ops, nw, force, dev, phase);
         if (r == 0) return true;
         if (r < 0 || force[r - 1]) return false;
         force[r - 1] = 1;
     }
+    return false;
 }
 
 // Per-device state of the cooperative chain: the device table (op table, phase
