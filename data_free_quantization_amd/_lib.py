@@ -90,6 +90,7 @@ class BcOp(C.Structure):
 
 
 DFQ_BC_OP_EXPECT, DFQ_BC_OP_APPLY, DFQ_BC_OP_PROPAGATE, DFQ_BC_OP_COPY = 0, 1, 2, 3
+DFQ_BC_APPLY_VEC_SCRATCH = 1
 DFQ_BN_FOLD_ZERO_BIAS = 1
 
 _LIB: Optional[C.CDLL] = None

@@ -234,7 +234,9 @@ class _BcChain:
 
     def apply(self, E, o, i2, expect, f, bias, vec):
         self.keep += [E, bias]
-        self.ops.append((_lib.DFQ_BC_OP_APPLY, 0, (E, 0), expect, (bias, 0), vec, o, i2, f))
+        # vec is a scratch slot (None ref) read only by this chain's propagate
+        flag = _lib.DFQ_BC_APPLY_VEC_SCRATCH if vec is not None and vec[0] is None else 0
+        self.ops.append((_lib.DFQ_BC_OP_APPLY, flag, (E, 0), expect, (bias, 0), vec, o, i2, f))
 
     def propagate(self, vec, numel, fake_b, f):
         _lib.require_device(fake_b)

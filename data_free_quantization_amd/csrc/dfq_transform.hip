@@ -259,7 +259,7 @@ __device__ __forceinline__ void bc_op_apply(const BcDevOp* __restrict__ opp, BcL
             const int64_t q = f > 1 ? j : 0;
             return E[r * i2 + (i2 > 1 ? j : 0)] + (op.lds_b >= 0 ? L.slots[op.lds_b + q] : ld_coh(op.b + q));
         };
-        if (op.out2)
+        if (op.out2)   // (nullptr here: scratch every reader recomputes, bc_chain_plan)
             for (int64_t j = lane; j < bcols; j += 64) st_coh(op.out2 + r * bcols + j, get(j));
         const float sum = wave_inner_sum(get, bcols, lane);
         if (lane == 0) st_coh(op.out + r, ld_coh(op.out + r) + sum / (float)bcols);
@@ -1304,6 +1304,27 @@ int bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, const std::
     return dev.empty() ? -1 : 0;
 }
 
+// An APPLY whose bias_vec is chain scratch (DFQ_BC_APPLY_VEC_SCRATCH) and whose
+// every reader is a propagate that recomputes it (virt) writes no bias_vec.
+void bc_drop_scratch_vecs(std::vector<BcDevOp>& dev) {
+    const int32_t n = (int32_t)dev.size();
+    for (int32_t j = 0; j < n; ++j) {
+        BcDevOp& ap = dev[j];
+        if (ap.kind != DFQ_BC_OP_APPLY || !(ap.flag & DFQ_BC_APPLY_VEC_SCRATCH) || !ap.out2) continue;
+        const BcRange v = bc_rng(ap.out2, ap.n * ap.bcols);
+        bool read = false;
+        for (int32_t k = j + 1; k < n && !read; ++k) {
+            const BcDevOp& o = dev[k];
+            if (o.kind == DFQ_BC_OP_PROPAGATE && o.virt == j) continue;
+            const int64_t na = o.kind == DFQ_BC_OP_APPLY ? o.n * o.i2 : o.n;
+            const int64_t nb = o.kind == DFQ_BC_OP_APPLY ? o.f : o.n;
+            const int64_t no = o.kind == DFQ_BC_OP_PROPAGATE ? o.f : o.n;
+            read = bc_ov(v, bc_rng(o.a, na)) || (o.b && bc_ov(v, bc_rng(o.b, nb))) || bc_ov(v, bc_rng(o.out, no));
+        }
+        if (!read) ap.out2 = nullptr;
+    }
+}
+
 // The chain's phases, in one planner pass.  Before it, on the whole op list:
 //   * no APPLY's E may overlap anything an op writes (E is loaded without
 //     coherence): one sorted sweep instead of a check per pair;
@@ -1348,7 +1369,10 @@ bool bc_chain_plan(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vector<
     }
     for (int pass = 0; pass < 4; ++pass) {
         const int r = bc_chain_phases(ops, n_ops, nw, force, dev, phase);
-        if (r == 0) return true;
+        if (r == 0) {
+            bc_drop_scratch_vecs(dev);
+            return true;
+        }
         if (r < 0 || force[r - 1]) return false;
         force[r - 1] = 1;
     }

@@ -333,9 +333,14 @@ int dfq_bc_propagate(const float* bias_vec, int64_t numel, float* fake_b, int64_
  * Every op is validated before the first launch; a bad op returns its error code
  * and `*failed_op` = its index, with nothing enqueued. */
 enum { DFQ_BC_OP_EXPECT = 0, DFQ_BC_OP_APPLY = 1, DFQ_BC_OP_PROPAGATE = 2, DFQ_BC_OP_COPY = 3 };
+/* APPLY flag: out2 (bias_vec) is chain scratch -- only this chain's ops read it,
+ * and its contents after the call are unspecified, so the one-launch path may
+ * leave it unwritten where every reader recomputes it (the Python walk's vectors). */
+enum { DFQ_BC_APPLY_VEC_SCRATCH = 1 };
 typedef struct dfq_bc_op {
     int32_t      kind;      /* DFQ_BC_OP_* */
-    int32_t      flag;      /* EXPECT: relu | (accumulate << 1); PROPAGATE: ref_threads */
+    int32_t      flag;      /* EXPECT: relu | (accumulate << 1); APPLY: DFQ_BC_APPLY_VEC_SCRATCH or 0;
+                               PROPAGATE: ref_threads */
     const float* a;         /* EXPECT: fake_w  APPLY: E       PROPAGATE: bias_vec  COPY: src */
     const float* b;         /* EXPECT: fake_b  APPLY: expect */
     float*       out;       /* EXPECT: out     APPLY: bias    PROPAGATE: fake_b    COPY: dst */
