@@ -9,6 +9,7 @@
 #include <cstring>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <mutex>
 #include <new>
@@ -1400,9 +1401,15 @@ BcChainCtx& bc_chain_ctx(int dev) {
 }
 
 constexpr int kBcNotEligible = 1;   // internal: run the per-op launches
+double bc_now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
     const char* ev = ab_env("DFQ_BC_CHAIN");   // diagnostics A/B: "launches" = per-op launches
     if (ev && std::strcmp(ev, "launches") == 0) return kBcNotEligible;
+    const bool timing = ab_env("DFQ_BC_TIMING") != nullptr;   // diagnostics: host phase times on stderr
+    const double t0 = timing ? bc_now_us() : 0.0;
     int dev = 0;
     DFQ_HIP_CHECK(hipStreamGetDevice(s, &dev));
     BcChainCtx& ctx = bc_chain_ctx(dev);
@@ -1420,6 +1427,7 @@ int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
     std::vector<BcDevOp> dv;
     std::vector<int32_t> ph;
     if (!bc_chain_plan(ops, n_ops, (int64_t)grid * kBcChainWaves, dv, ph)) return kBcNotEligible;
+    const double t1 = timing ? bc_now_us() : 0.0;
     const int32_t nphase = (int32_t)ph.size() - 1;
     auto up256 = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t o_ph = up256(sizeof(BcDevOp) * dv.size());
@@ -1466,7 +1474,11 @@ int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
     }
     int32_t* h_err = reinterpret_cast<int32_t*>(ctx.hbuf + o_bar + 128);
     DFQ_HIP_CHECK(hipMemcpyAsync(h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    const double t2 = timing ? bc_now_us() : 0.0;
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
+    if (timing)
+        fprintf(stderr, "DFQ_BC_TIMING ops %d phases %d grid %d: plan %.1f us, upload+launch %.1f us, wait %.1f us\n",
+                n_ops, nphase, grid, t1 - t0, t2 - t1, bc_now_us() - t2);
     if (*h_err) {
         set_last_hip_error(hipErrorLaunchTimeOut);
         return DFQ_ERR_HIP;

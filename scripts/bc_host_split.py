@@ -1,0 +1,63 @@
+"""Where the bias-correction stage's time goes (MobileNetV2 / ResNet-50, warm,
+fused BC): the Python walk that records the chain vs the dfq_bc_chain call
+(_BcChain.flush), per configuration of the diagnostics switches in argv
+(DFQ_BC_CHAIN=launches etc. come from the environment)."""
+import contextlib
+import io
+import json
+import logging
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+os.environ.setdefault("DFQ_LIB", "diag")
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+from data_free_quantization_amd import zoo, bias_correction as BC  # noqa: E402
+from data_free_quantization_amd import pipeline  # noqa: E402
+from data_free_quantization_amd.utils.tracer import build_graph  # noqa: E402
+
+logging.getLogger("data_free_quantization_amd.bias_correction").setLevel(logging.ERROR)
+acc = {}
+orig_flush = BC._BcChain.flush
+orig_bc = pipeline.bias_correction
+
+
+def flush(self, stream):
+    t0 = time.perf_counter()
+    try:
+        return orig_flush(self, stream)
+    finally:
+        torch.cuda.synchronize()
+        acc["flush"] = acc.get("flush", 0.0) + time.perf_counter() - t0
+
+
+def bc(*a, **k):
+    t0 = time.perf_counter()
+    try:
+        return orig_bc(*a, **k)
+    finally:
+        torch.cuda.synchronize()
+        acc["stage"] = acc.get("stage", 0.0) + time.perf_counter() - t0
+
+
+BC._BcChain.flush = flush
+pipeline.bias_correction = bc
+for model in ("mobilenetv2", "resnet50"):
+    res = []
+    for rep in range(5):
+        acc.clear()
+        m = zoo.build(model, seed=0, relu=True).cuda()
+        g = build_graph(m, "positional")
+        with contextlib.redirect_stdout(io.StringIO()):
+            pipeline.run_dfq(m, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel",
+                             symmetric=True, bc_mode="fused")
+        if rep:
+            res.append((acc["stage"] * 1e3, acc["flush"] * 1e3))
+    res.sort()
+    st, fl = res[len(res) // 2]
+    print(json.dumps({"model": model, "chain": os.environ.get("DFQ_BC_CHAIN", "coop"), "stage_ms": round(st, 3),
+                      "flush_ms": round(fl, 3), "walk_ms": round(st - fl, 3)}), flush=True)
