@@ -190,6 +190,7 @@ bc_propagate_kernel(const float* __restrict__ bias_vec, int64_t nrows, int64_t f
     }
 }
 
+#ifdef DFQ_DIAGNOSTICS
 // ---------------------------------------------------------------------------
 // The bias-correction chain as ONE cooperative launch (dfq_bc_chain).  The walk
 // is a serial chain -- layer L's expectation reads the BN fake_bias that layer
@@ -367,6 +368,7 @@ bc_chain_kernel(const BcDevOp* __restrict__ ops, const int32_t* __restrict__ pha
         if (!flag) return;
     }
 }
+#endif  // DFQ_DIAGNOSTICS
 
 
 // ---------------------------------------------------------------------------
@@ -1094,6 +1096,7 @@ __global__ void __launch_bounds__(256) copy_batch_kernel(CopyBatch b) {
         dst[i] = src[i];
 }
 
+#ifdef DFQ_DIAGNOSTICS
 namespace dfq {
 namespace {
 struct BcRange {
@@ -1406,8 +1409,6 @@ double bc_now_us() {
 }
 
 int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
-    const char* ev = ab_env("DFQ_BC_CHAIN");   // diagnostics A/B: "launches" = per-op launches
-    if (ev && std::strcmp(ev, "launches") == 0) return kBcNotEligible;
     const bool timing = ab_env("DFQ_BC_TIMING") != nullptr;   // diagnostics: host phase times on stderr
     const double t0 = timing ? bc_now_us() : 0.0;
     int dev = 0;
@@ -1502,7 +1503,6 @@ int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
 }  // namespace
 }  // namespace dfq
 
-#ifdef DFQ_DIAGNOSTICS
 #include "dfq_diag.h"
 extern "C" int dfq_bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t waves, int32_t* n_phases,
                                    int32_t* op_phase) {
@@ -1558,8 +1558,14 @@ extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed
         }
     }
     if (n_ops == 0) return DFQ_OK;
-    const int crc = dfq::bc_chain_coop(ops, n_ops, static_cast<hipStream_t>(stream));
-    if (crc != dfq::kBcNotEligible) return crc;
+#ifdef DFQ_DIAGNOSTICS
+    // The one-launch chain (bc_chain_kernel): bit-identical, measured slower than
+    // these per-op launches, so a diagnostics A/B: DFQ_BC_CHAIN=coop.
+    if (const char* ev = dfq::ab_env("DFQ_BC_CHAIN"); ev && std::strcmp(ev, "coop") == 0) {
+        const int crc = dfq::bc_chain_coop(ops, n_ops, static_cast<hipStream_t>(stream));
+        if (crc != dfq::kBcNotEligible) return crc;
+    }
+#endif
     for (int32_t k = 0; k < n_ops; ++k) {
         const dfq_bc_op& op = ops[k];
         int rc = DFQ_OK;
@@ -1772,7 +1778,6 @@ hipError_t preload_transform() {   // see dfq_preload
     hipFuncAttributes a;
     hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(bn_fold_weight_batch_kernel));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(absorb_batch_gemv_kernel));
-    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(bc_chain_kernel));
     return e;
 }
 }  // namespace dfq

@@ -21,14 +21,13 @@ os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_BC_CHAIN", "DFQ_BC_GRID", "DFQ_BC_COOPLAUNCH")
 CONFIGS = {
-    "coop": {},                                   # the product: one launch of 64 co-resident blocks
-    "cooplaunch": {"DFQ_BC_COOPLAUNCH": "1"},     # the same through hipLaunchCooperativeKernel
-    "launches": {"DFQ_BC_CHAIN": "launches"},     # round 2: one launch per op
-    "grid8": {"DFQ_BC_GRID": "8"},
-    "grid16": {"DFQ_BC_GRID": "16"},
-    "grid32": {"DFQ_BC_GRID": "32"},
-    "grid128": {"DFQ_BC_GRID": "128"},
-    "grid256": {"DFQ_BC_GRID": "256"},
+    "launches": {},                                                  # the product: one launch per op
+    "coop": {"DFQ_BC_CHAIN": "coop"},                                # one launch of 64 co-resident blocks
+    "cooplaunch": {"DFQ_BC_CHAIN": "coop", "DFQ_BC_COOPLAUNCH": "1"},   # the same via hipLaunchCooperativeKernel
+    "grid16": {"DFQ_BC_CHAIN": "coop", "DFQ_BC_GRID": "16"},
+    "grid32": {"DFQ_BC_CHAIN": "coop", "DFQ_BC_GRID": "32"},
+    "grid128": {"DFQ_BC_CHAIN": "coop", "DFQ_BC_GRID": "128"},
+    "grid256": {"DFQ_BC_CHAIN": "coop", "DFQ_BC_GRID": "256"},
 }
 
 

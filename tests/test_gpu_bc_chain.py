@@ -1,6 +1,6 @@
-"""dfq_bc_chain's cooperative path (one launch, phases split by grid barriers,
-expectations forwarded through LDS, propagates recomputed from E) against the
-per-op launches (diagnostics switch DFQ_BC_CHAIN=launches), bit for bit, on
+"""dfq_bc_chain's one-launch path (diagnostics A/B DFQ_BC_CHAIN=coop: phases
+split by grid barriers, expectations forwarded through LDS, propagates
+recomputed from E) against the product's per-op launches, bit for bit, on
 synthetic walks shaped like bias_correction.py:147-258's (expect -> apply ->
 propagate into the next BN's fake_bias, 'add' branches accumulating, two
 branches of one layer, depthwise and scalar broadcasts, before / after
@@ -108,11 +108,15 @@ def _same(a, b, skip=()):
             assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
 
 
-def _per_op(walk_args, monkeypatch):
+def _coop(walk_args, monkeypatch, grid=None):
+    """The one-launch path (diagnostics library)."""
     from data_free_quantization_amd import _lib
-    monkeypatch.setenv("DFQ_BC_CHAIN", "launches")
+    monkeypatch.setenv("DFQ_BC_CHAIN", "coop")
+    if grid:
+        monkeypatch.setenv("DFQ_BC_GRID", grid)
     r = Walk(*walk_args[0], **walk_args[1]).run(_lib.load_diag())
     monkeypatch.delenv("DFQ_BC_CHAIN")
+    monkeypatch.delenv("DFQ_BC_GRID", raising=False)
     return r
 
 
@@ -121,8 +125,8 @@ def _per_op(walk_args, monkeypatch):
                                      (5, {"big_expect": True}), (6, {"alias": True})])
 def test_cooperative_chain_equals_per_op_launches(seed, kw, monkeypatch):
     from data_free_quantization_amd import _lib
-    ref = _per_op(((seed,), kw), monkeypatch)
-    got = Walk(seed, **kw).run(_lib.load())
+    ref = Walk(seed, **kw).run(_lib.load())
+    got = _coop(((seed,), kw), monkeypatch)
     _same(ref, got)
 
 
@@ -131,16 +135,15 @@ def test_cooperative_chain_grid_sizes(grid, monkeypatch):
     """Any grid gives the same bits: row / column owners move, orders do not."""
     from data_free_quantization_amd import _lib
     ref = Walk(11, layers=8).run(_lib.load())
-    monkeypatch.setenv("DFQ_BC_GRID", grid)
-    got = Walk(11, layers=8).run(_lib.load_diag())
+    got = _coop(((11,), {"layers": 8}), monkeypatch, grid)
     _same(ref, got)
 
 
-def test_cooperative_chain_repeats():
+def test_cooperative_chain_repeats(monkeypatch):
     from data_free_quantization_amd import _lib
     ref = Walk(21, layers=10).run(_lib.load())
     for _ in range(5):
-        _same(ref, Walk(21, layers=10).run(_lib.load()))
+        _same(ref, _coop(((21,), {"layers": 10}), monkeypatch))
 
 
 @pytest.mark.parametrize("seed", [31, 32])
@@ -148,6 +151,6 @@ def test_scratch_bias_vectors(seed, monkeypatch):
     """DFQ_BC_APPLY_VEC_SCRATCH: the one-launch path may leave the bias vectors
     unwritten (every reader recomputes them); everything else is bit-identical."""
     from data_free_quantization_amd import _lib
-    ref = _per_op(((seed,), {"layers": 9, "grouped": seed == 32, "scratch": True}), monkeypatch)
-    got = Walk(seed, layers=9, grouped=seed == 32, scratch=True).run(_lib.load())
+    ref = Walk(seed, layers=9, grouped=seed == 32, scratch=True).run(_lib.load())
+    got = _coop(((seed,), {"layers": 9, "grouped": seed == 32, "scratch": True}), monkeypatch)
     _same(ref, got, skip=("vec",))
