@@ -197,33 +197,60 @@ _BC_OP = np.dtype([("kind", "<i4"), ("flag", "<i4"), ("a", "<u8"), ("b", "<u8"),
 assert _BC_OP.itemsize == C.sizeof(_lib.BcOp)
 
 
+#: scratch floats per chunk of the chain's expectation / bias-vector slots
+_SCRATCH_CHUNK = 1 << 22
+#: recorded ops that trigger a flush between target layers: the device works
+#: through the walk's first layers while Python walks the rest
+_FLUSH_OPS = 32
+
+
 class _BcChain:
-    """The walk's device work recorded in graph order and enqueued by ONE
-    ``dfq_bc_chain`` call (instead of a Python call per expect / apply /
-    propagate).  Expectations and bias vectors live in one scratch buffer:
-    refs are ``(None, float offset)`` there, or ``(tensor, 0)`` for a live
-    tensor.  ``flush()`` runs what was recorded; the walk flushes before it
-    raises, so the ops before an error take effect, as in the reference."""
+    """The walk's device work recorded in graph order and enqueued by
+    ``dfq_bc_chain`` calls (instead of a Python call per expect / apply /
+    propagate).  Expectations and bias vectors live in scratch chunks allocated
+    as the walk goes, so every ref ``(tensor, float offset)`` is a device address
+    at once and the recorded ops can be flushed at any point: the walk flushes
+    every ``_FLUSH_OPS`` ops between layers (the GPU then overlaps the rest of
+    the Python walk) and before it raises, so the ops before an error take
+    effect, as in the reference."""
 
     def __init__(self, dev):
         self.dev = dev
         self.ops = []
-        self.top = 0            # scratch floats allocated
         self.keep = []          # tensors the recorded ops point into
+        self._chunk = None      # current scratch chunk
+        self._fill = 0          # floats used in it
+        self._chunks = []       # chunks the unflushed ops point into
 
     def alloc(self, n):
-        off = self.top
-        self.top += -(-n // 64) * 64   # 256-B aligned slots
-        return off
+        """A 256-B aligned scratch slot of n floats."""
+        need = -(-n // 64) * 64
+        if self._chunk is None or self._fill + need > self._chunk.numel():
+            self._chunk = torch.empty(max(need, _SCRATCH_CHUNK), dtype=torch.float32, device=self.dev)
+            self._chunks.append(self._chunk)
+            self._fill = 0
+        off = self._fill
+        self._fill += need
+        return (self._chunk, off)
 
-    def extend_last(self, off, size, n):
-        """grow the most recent slot [off, off + size) to size + n (torch.cat)"""
-        assert self.top == off + -(-size // 64) * 64, "cat target is not the last scratch slot"
-        self.top = off + -(-(size + n) // 64) * 64
-
-    def _ptr(self, ref, base):
+    def extend_last(self, ref, size, n):
+        """Grow the most recent slot ``ref`` ([size] floats) by n (torch.cat):
+        in place when its chunk has room, else into a fresh slot that a COPY op
+        fills with the size floats already written.  Returns the slot's ref."""
         t, off = ref
-        return (t.data_ptr() if t is not None else base) + 4 * off
+        assert t is self._chunk and self._fill == off + -(-size // 64) * 64, "cat target is not the last slot"
+        need = -(-(size + n) // 64) * 64
+        if off + need <= t.numel():
+            self._fill = off + need
+            return ref
+        new = self.alloc(size + n)
+        self.ops.append((_lib.DFQ_BC_OP_COPY, 0, ref, None, new, None, size, 0, 0))
+        return new
+
+    @staticmethod
+    def _ptr(ref):
+        t, off = ref
+        return t.data_ptr() + 4 * off
 
     def expect(self, bn, relu, dst, accumulate):
         w, b = bn.fake_weight, bn.fake_bias
@@ -233,10 +260,10 @@ class _BcChain:
                          b.numel(), 0, 0))
 
     def apply(self, E, o, i2, expect, f, bias, vec):
+        # vec: a scratch slot only this chain's propagate reads
         self.keep += [E, bias]
-        # vec is a scratch slot (None ref) read only by this chain's propagate
-        flag = _lib.DFQ_BC_APPLY_VEC_SCRATCH if vec is not None and vec[0] is None else 0
-        self.ops.append((_lib.DFQ_BC_OP_APPLY, flag, (E, 0), expect, (bias, 0), vec, o, i2, f))
+        self.ops.append((_lib.DFQ_BC_OP_APPLY, _lib.DFQ_BC_APPLY_VEC_SCRATCH, (E, 0), expect, (bias, 0), vec, o,
+                         i2, f))
 
     def propagate(self, vec, numel, fake_b, f):
         _lib.require_device(fake_b)
@@ -250,20 +277,21 @@ class _BcChain:
     def flush(self, stream):
         if not self.ops:
             return
-        scratch = torch.empty(max(self.top, 1), dtype=torch.float32, device=self.dev)
-        base = scratch.data_ptr()
+        ptr = lambda ref: 0 if ref is None else self._ptr(ref)   # noqa: E731
         # the op table as a numpy record array (layout of _lib.BcOp), filled row-wise
         # from plain tuples instead of ctypes field by field
-        ptr = lambda ref: 0 if ref is None else self._ptr(ref, base)   # noqa: E731
         arr = np.array([(kind, flag, ptr(a), ptr(b), ptr(out), ptr(out2), n, i2, f)
                         for (kind, flag, a, b, out, out2, n, i2, f) in self.ops], dtype=_BC_OP)
         failed = C.c_int32(-1)
         rc = _lib.load().dfq_bc_chain(arr.ctypes.data_as(C.POINTER(_lib.BcOp)), len(self.ops), C.byref(failed),
                                       stream)
         _lib.check(rc, f"dfq_bc_chain (op {failed.value})", RuntimeError)
-        # the ops run asynchronously: keep the scratch alive until they are done
-        scratch.record_stream(torch.cuda.current_stream(self.dev))
-        self.ops, self.keep, self.top = [], [], 0
+        # the ops run asynchronously: the scratch chunks stay with the current stream
+        cur = torch.cuda.current_stream(self.dev)
+        for t in self._chunks:
+            t.record_stream(cur)
+        self._chunks = [self._chunk] if self._chunk is not None else []
+        self.ops, self.keep = [], []
 
 
 def _record_branches(chain, bn_branch):
@@ -271,22 +299,22 @@ def _record_branches(chain, bn_branch):
     ops: {key: (connect_type, expect ref, numel)}."""
     res = {}
     for key, branch in bn_branch.items():
-        off, size, connect_type = None, 0, None
+        ref, size, connect_type = None, 0, None
         for layer, relu_attached, connect_type in branch:
             n = layer.fake_bias.numel()
-            if off is None:
-                off, size = chain.alloc(n), n
-                chain.expect(layer, relu_attached, (None, off), False)
+            if ref is None:
+                ref, size = chain.alloc(n), n
+                chain.expect(layer, relu_attached, ref, False)
             elif connect_type == "cat":   # torch.cat([cum, e]): e lands right after cum
-                chain.extend_last(off, size, n)
-                chain.expect(layer, relu_attached, (None, off + size), False)
+                ref = chain.extend_last(ref, size, n)
+                chain.expect(layer, relu_attached, (ref[0], ref[1] + size), False)
                 size += n
             else:                          # cum += e (in place)
                 if n != size:
                     raise RuntimeError(f"output with shape [{size}] doesn't match the broadcast shape [{n}]"
                                        if n != 1 else "a one-channel BN expectation broadcast is not supported")
-                chain.expect(layer, relu_attached, (None, off), True)
-        res[key] = (connect_type, (None, off), size)
+                chain.expect(layer, relu_attached, ref, True)
+        res[key] = (connect_type, ref, size)
     return res
 
 
@@ -303,7 +331,7 @@ def _record_apply(chain, layer, E, o, i2, connect_type, expect, f):
                      "automatically.")
         raise ValueError("Bias correction shape mismatch that cannot be handled automatically.")
     _lib.require_device(E, layer.bias.data)
-    vec = (None, chain.alloc(o * bcols))
+    vec = chain.alloc(o * bcols)
     chain.apply(E.reshape(-1), o, i2, expect, f, layer.bias.data, vec)
     return vec, o * bcols
 
@@ -382,6 +410,8 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                     bias_prev = bias
                     if getattr(layer, "bias", None) is not None:
                         after_src[layer_name] = layer.bias.data
+                    if len(chain.ops) >= _FLUSH_OPS:   # the device starts on what is recorded so far
+                        chain.flush(stream)
             after = _snapshot(chain, after_src)
         finally:   # the ops recorded before an error still take effect, as in the reference
             if chain.ops:
