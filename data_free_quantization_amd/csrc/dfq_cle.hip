@@ -887,6 +887,12 @@ struct CleApplyLds {
 };
 
 // Rescale tasks [t0, t1) of iteration parity `par`, taken by blocks blk, blk + nblk, ...
+#ifdef DFQ_DIAGNOSTICS
+// DFQ_CLE_TL (diagnostics): per rescale task of one steady-state iteration,
+// {start, end} in s_memrealtime ticks (100 MHz) and the block's XCC / CU ids.
+__device__ uint64_t* g_cle_tl = nullptr;
+#endif
+
 __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks,
                                                int64_t t0, int64_t t1, uint32_t* __restrict__ rng, int64_t M,
                                                int par, bool first_iter, int is_signed, float eps, double smin,
@@ -901,6 +907,10 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     for (int64_t t = t0 + blk; t < t1; t += nblk) {
+#ifdef DFQ_DIAGNOSTICS
+        const bool tl_on = g_cle_tl != nullptr;   // block-uniform
+        const uint64_t tl_start = tl_on ? __builtin_amdgcn_s_memrealtime() : 0;
+#endif
         const CleTask tk = tasks[t];
         const CleRel& R = rels[tk.rel];
         const uint32_t* mn = mins + R.moff;
@@ -1186,6 +1196,21 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                 if (R.sacc) R.sacc[c] = (R.sacc_init && first_iter) ? cs.s : R.sacc[c] * cs.s;
             }
         }
+#ifdef DFQ_DIAGNOSTICS
+        if (tl_on) {   // the last executed iteration's times remain
+            __syncthreads();   // the block's task is done (timing only)
+            if (threadIdx.x == 0) {
+                uint32_t hw, xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                uint64_t* r = g_cle_tl + 4 * t;
+                r[0] = tl_start;
+                r[1] = __builtin_amdgcn_s_memrealtime();
+                r[2] = ((uint64_t)xcc << 32) | hw;
+                r[3] = (uint64_t)tk.kind | ((uint64_t)tk.rel << 8) | ((uint64_t)(tk.b - tk.a) << 24);
+            }
+        }
+#endif
     }
 }
 
@@ -3008,6 +3033,16 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     const char* ge = ab_env("DFQ_CLE_GRAPH");
     const bool use_graph = ge && ge[0] == '1';
     const int32_t batch = cle_batch();
+#ifdef DFQ_DIAGNOSTICS
+    uint64_t* d_tl = nullptr;   // DFQ_CLE_TL: per rescale task timestamps (cle_apply_body)
+    const int64_t n_at = p->astep.empty() ? 0 : p->astep.back();
+    if (ab_env("DFQ_CLE_TL") && n_at > 0) {
+        DFQ_HIP_CHECK(hipMalloc(&d_tl, sizeof(uint64_t) * 4 * n_at));
+        DFQ_HIP_CHECK(hipMemsetAsync(d_tl, 0, sizeof(uint64_t) * 4 * n_at, s));
+        DFQ_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cle_tl), &d_tl, sizeof(d_tl), 0, hipMemcpyHostToDevice, s));
+        DFQ_HIP_CHECK(hipStreamSynchronize(s));
+    }
+#endif
     const double tc0 = now_us();
     bool reused = false;
     if (use_graph && !init.done) {
@@ -3073,6 +3108,48 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     if (cle_timing())
         fprintf(stderr, "DFQ_CLE_TIMING run: capture+instantiate %.1f us%s, loop %.1f us (%d iterations launched)\n",
                 tc1 - tc0, reused ? " (graph reused)" : "", now_us() - tc1, launched);
+#ifdef DFQ_DIAGNOSTICS
+    if (d_tl) {   // per step: span, task durations, the slowest tasks
+        std::vector<uint64_t> tl(4 * (size_t)n_at);
+        DFQ_HIP_CHECK(hipMemcpy(tl.data(), d_tl, sizeof(uint64_t) * tl.size(), hipMemcpyDeviceToHost));
+        uint64_t* null_tl = nullptr;
+        DFQ_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_cle_tl), &null_tl, sizeof(null_tl)));
+        (void)hipFree(d_tl);
+        for (int32_t k = 0; k < p->steps; ++k) {
+            const int64_t a0 = p->astep[k], a1 = p->astep[k + 1];
+            uint64_t t_lo = ~0ull, t_hi = 0;
+            double sum = 0;
+            std::vector<std::pair<double, int64_t>> d;
+            for (int64_t t = a0; t < a1; ++t) {
+                const uint64_t* r = &tl[4 * t];
+                if (!r[0]) continue;
+                t_lo = std::min(t_lo, r[0]);
+                t_hi = std::max(t_hi, r[1]);
+                const double us = (double)(r[1] - r[0]) * 0.01;
+                sum += us;
+                d.push_back({us, t});
+            }
+            std::sort(d.rbegin(), d.rend());
+            fprintf(stderr, "DFQ_CLE_TL step %d: %lld tasks, span %.2f us, task mean %.2f us, max %.2f us; slowest:",
+                    k, (long long)(a1 - a0), t_hi > t_lo ? (double)(t_hi - t_lo) * 0.01 : 0.0,
+                    d.empty() ? 0.0 : sum / d.size(), d.empty() ? 0.0 : d[0].first);
+            for (size_t i = 0; i < d.size() && i < 6; ++i) {
+                const uint64_t m = tl[4 * d[i].second + 3];
+                fprintf(stderr, " [%.2f us kind %d rel %d n %lld]", d[i].first, (int)(m & 255), (int)((m >> 8) & 0xffff),
+                        (long long)(m >> 24));
+            }
+            // start-time histogram: when the tasks began relative to the first
+            fprintf(stderr, "\nDFQ_CLE_TL step %d starts (us after first):", k);
+            std::vector<double> st;
+            for (int64_t t = a0; t < a1; ++t)
+                if (tl[4 * t]) st.push_back((double)(tl[4 * t] - t_lo) * 0.01);
+            std::sort(st.begin(), st.end());
+            for (double q : {0.1, 0.5, 0.9, 0.99, 1.0})
+                if (!st.empty()) fprintf(stderr, " p%.0f %.2f", q * 100, st[std::min(st.size() - 1, (size_t)(q * st.size()))]);
+            fprintf(stderr, "\n");
+        }
+    }
+#endif
     // the final state (a speculative batch after convergence changed nothing)
     DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
