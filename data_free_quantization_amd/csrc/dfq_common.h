@@ -146,29 +146,32 @@ __device__ __forceinline__ float qdq(float x, const QParams& p, float& q) {
 // The same result with the IEEE divide taken only near a rounding boundary.
 // a = (x + negmn) * rcp(s) is within 2^-22 |t| of t = fl((x + negmn) / s)
 // (v_rcp_f32: 1 ulp; the multiply: 1/2 ulp; t itself: 1/2 ulp).  The code only
-// depends on which side of a half-integer t lies, and clamping a to
-// [qmin - 1, qmax + 1] first keeps that true (beyond qmax + 1, t > qmax + 0.5
-// for every qmax < 2^16: q = qmax either way; NaN / inf go the same way as in
-// qdq).  So when c (a, clamped) is more than |c| 2^-20 (4x the error bound) away
-// from the nearest half-integer, rint(clamp(c)) == rint(clamp(t)); otherwise --
-// ties and near-ties, ~1e-5 of the elements at INT8 -- the IEEE divide decides.
-// The dequantize (q * s + mn) is unchanged.  rs = __builtin_amdgcn_rcpf(s).
+// depends on which side of a half-integer clamp(t) lies.  c = clamp(a, qmin,
+// qmax) is that value's stand-in: inside the range, when c is more than
+// |c| 2^-20 (4x the error bound) away from the nearest half-integer,
+// rint(c) == rint(clamp(t)); outside it, c is the end point (an integer, 1/2
+// from any half-integer) and t is within the error bound of a beyond it, so
+// clamp(t) rounds to the same end point; NaN / inf clamp as in qdq.  Otherwise
+// -- ties and near-ties, ~1e-5 of the elements at INT8 -- the IEEE divide
+// decides.  The dequantize (q * s + mn) is unchanged.  rs = __builtin_amdgcn_rcpf(s).
 // The caller branches on a WAVE-uniform "any lane needs it" (ballot), so the
 // divide is neither executed nor if-converted into every element's path: ~8
-// VALU fewer per element (the sweep is issue-bound at ~500 G elements/s).
-// Step 1: the screened quotient; need = the IEEE divide must decide (rare).
+// VALU fewer per element (the sweep is issue-bound at ~500 G elements/s), and the
+// one clamp serves both the test and the rounding.
+// Step 1: the screened, clamped quotient; need = the IEEE divide must decide (rare).
 __device__ __forceinline__ float qdq_screen(float x, const QParams& p, float rs, bool& need) {
     const float a = (x + p.negmn) * rs;
-    const float t = fminf(fmaxf(a, p.qmin - 1.0f), p.qmax + 1.0f);
+    const float t = fminf(fmaxf(a, p.qmin), p.qmax);
     const float d = __builtin_amdgcn_fractf(t) - 0.5f;   // v_fract: t - floor(t), exact for |t| < 2^24
     need = !(fabsf(d) > fabsf(t) * 0x1p-20f);
     return t;
 }
-// Step 2 (only where need): the reference's quotient.
-__device__ __forceinline__ float qdq_exact_t(float x, const QParams& p) { return (x + p.negmn) / p.s; }
-// Step 3: clamp, round half-even, dequantize (as qdq).
+// Step 2 (only where need): the reference's quotient, clamped.
+__device__ __forceinline__ float qdq_exact_t(float x, const QParams& p) {
+    return fminf(fmaxf((x + p.negmn) / p.s, p.qmin), p.qmax);
+}
+// Step 3: round half-even, dequantize (as qdq; t is already clamped).
 __device__ __forceinline__ float qdq_finish(float t, const QParams& p, float& q) {
-    t = fminf(fmaxf(t, p.qmin), p.qmax);
     q = rintf(t);
     const float y = q * p.s;
     return y + p.mn;
