@@ -2164,6 +2164,10 @@ struct dfq_cle_plan {
     bool fork = false;              // ranges on a concurrent graph branch (diagnostics DFQ_CLE_FORK=1)
     int64_t ri0 = 0, ri1 = 0;       // fused: each iteration's range tasks (the rest come from the rescales)
     int dev = 0;
+#ifdef DFQ_DIAGNOSTICS
+    std::vector<CleRel> h_rels;
+    std::vector<CleTask> h_atasks;
+#endif
     // chain-grouped schedule (cle_loop_group_kernel): one launch per iteration
     bool grouped = false;
     int32_t ngroups = 0, group_grid = 0;
@@ -2645,6 +2649,10 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->astep = astep;
     p->ri0 = ri0;
     p->ri1 = ri1;
+#ifdef DFQ_DIAGNOSTICS
+    p->h_rels = R;   // for the DFQ_CLE_TL report
+    p->h_atasks = at;
+#endif
     p->smin = s_min; p->smax = s_max; p->is_signed = is_signed; p->eps = eps;
     hipError_t e;
     auto fail = [&](hipError_t err) { set_last_hip_error(err); cle_plan_free(p); return DFQ_ERR_HIP; };
@@ -3150,8 +3158,12 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
                     d.empty() ? 0.0 : sum / d.size(), d.empty() ? 0.0 : d[0].first);
             for (size_t i = 0; i < d.size() && i < 6; ++i) {
                 const uint64_t m = tl[4 * d[i].second + 3];
-                fprintf(stderr, " [%.2f us kind %d rel %d n %lld]", d[i].first, (int)(m & 255), (int)((m >> 8) & 0xffff),
-                        (long long)(m >> 24));
+                const int rel = (int)((m >> 8) & 0xffff);
+                const CleRel& q = p->h_rels[rel];
+                const CleTask& tk = p->h_atasks[d[i].second];
+                fprintf(stderr, " [%.2f us kind %d rel %d n %lld c1 %lld o2 %lld i2 %lld khw2 %lld o2g %lld fuse %d cols %lld]",
+                        d[i].first, (int)(m & 255), rel, (long long)(m >> 24), (long long)q.c1, (long long)q.o2,
+                        (long long)q.i2, (long long)q.khw2, (long long)q.o2g, q.fuse_next, (long long)(tk.c1 - tk.c0));
             }
             // start-time histogram: when the tasks began relative to the first
             fprintf(stderr, "\nDFQ_CLE_TL step %d starts (us after first):", k);
