@@ -658,7 +658,6 @@ __device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t 
 // on consecutive floats, khw independent loads per row in flight -- instead of
 // one thread per column walking its khw floats serially.
 constexpr int kTileMaxKhw = 9;   // 3x3 (and 2x2); larger kernels keep the per-column walk
-constexpr int kTileRowBatch = 4; // rows whose loads a position-parallel rescale tile issues together
 
 __device__ __forceinline__ bool tile_by_position(const CleRel& R, const CleTask& tk) {
     return R.khw2 > 1 && R.khw2 <= kTileMaxKhw && (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
@@ -911,6 +910,11 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
 #ifdef DFQ_DIAGNOSTICS
         const bool tl_on = g_cle_tl != nullptr;   // block-uniform
         const uint64_t tl_start = tl_on ? __builtin_amdgcn_s_memrealtime() : 0;
+        uint64_t tl_sub = 0;   // position tiles: phase ends (10 ns ticks after start, 16 bits each)
+#define DFQ_CLE_TL_MARK(k) \
+        if (tl_on) tl_sub |= ((__builtin_amdgcn_s_memrealtime() - tl_start) & 0xffffull) << (16 * (k));
+#else
+#define DFQ_CLE_TL_MARK(k)
 #endif
         const CleTask tk = tasks[t];
         const CleRel& R = rels[tk.rel];
@@ -1051,47 +1055,36 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             if (t < ncol)
                 inv_s[t] = cle_rel_scale(rels, R, mins, maxs, (tk.a / R.o2g) * R.i2 + tk.c0 + t, is_signed, eps, smin, smax).inv;
             __syncthreads();
+            DFQ_CLE_TL_MARK(0)
             for (int q = t; q < npos; q += kThreads) inv_pos[q] = inv_s[q / khw];   // 1/s per position
             __syncthreads();
-            // kTileRowBatch rows' loads issued before any of their stores: a row's
-            // stores would otherwise hold back the next row's loads (possible
-            // aliasing), one memory round trip per row (ResNet-50's 3x3 tiles
-            // took 64 us per 16-row task, DFQ_CLE_TL)
-            float ip[kTileMaxKhw];
+            DFQ_CLE_TL_MARK(1)
+            for (int64_t o = tk.a; o < tk.b; ++o) {
+                float* rp = base + o * rowlen;
+                float v[kTileMaxKhw];
 #pragma unroll
-            for (int m = 0; m < kTileMaxKhw; ++m) ip[m] = (m < khw && t + kThreads * m < npos) ? inv_pos[t + kThreads * m] : 0.f;
-            for (int64_t o0 = tk.a; o0 < tk.b; o0 += kTileRowBatch) {
-                float v[kTileRowBatch][kTileMaxKhw];
+                for (int m = 0; m < kTileMaxKhw; ++m)
+                    if (m < khw && t + kThreads * m < npos) v[m] = rp[t + kThreads * m];
+                float lo = INFINITY, hi = -INFINITY;
 #pragma unroll
-                for (int r = 0; r < kTileRowBatch; ++r)
-#pragma unroll
-                    for (int m = 0; m < kTileMaxKhw; ++m)
-                        if (o0 + r < tk.b && m < khw && t + kThreads * m < npos)
-                            v[r][m] = base[(o0 + r) * rowlen + t + kThreads * m];
-#pragma unroll
-                for (int r = 0; r < kTileRowBatch; ++r) {
-                    if (o0 + r >= tk.b) break;   // uniform
-                    float* rp = base + (o0 + r) * rowlen;
-                    float lo = INFINITY, hi = -INFINITY;
-#pragma unroll
-                    for (int m = 0; m < kTileMaxKhw; ++m)
-                        if (m < khw && t + kThreads * m < npos) {
-                            const float y = v[r][m] * ip[m];
-                            rp[t + kThreads * m] = y;
-                            lo = fminf(lo, y);
-                            hi = fmaxf(hi, y);
-                        }
-                    if (fuse) {
-                        lo = wave_min(lo);
-                        hi = wave_max(hi);
-                        if (lane == 0) {
-                            red[0][wv][o0 + r - tk.a] = lo;
-                            red[1][wv][o0 + r - tk.a] = hi;
-                        }
+                for (int m = 0; m < kTileMaxKhw; ++m)
+                    if (m < khw && t + kThreads * m < npos) {
+                        const float y = v[m] * inv_pos[t + kThreads * m];
+                        rp[t + kThreads * m] = y;
+                        lo = fminf(lo, y);
+                        hi = fmaxf(hi, y);
+                    }
+                if (fuse) {
+                    lo = wave_min(lo);
+                    hi = wave_max(hi);
+                    if (lane == 0) {
+                        red[0][wv][o - tk.a] = lo;
+                        red[1][wv][o - tk.a] = hi;
                     }
                 }
             }
             __syncthreads();
+            DFQ_CLE_TL_MARK(2)
             if (fuse && t < tk.b - tk.a) {
                 float a = red[0][0][t], b = red[1][0][t];
                 for (int w = 1; w < kThreads / 64; ++w) {
@@ -1221,7 +1214,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                 uint64_t* r = g_cle_tl + 4 * t;
                 r[0] = tl_start;
                 r[1] = __builtin_amdgcn_s_memrealtime();
-                r[2] = ((uint64_t)xcc << 32) | hw;
+                r[2] = tl_sub ? tl_sub : (((uint64_t)xcc << 32) | hw);
                 r[3] = (uint64_t)tk.kind | ((uint64_t)tk.rel << 8) | ((uint64_t)(tk.b - tk.a) << 24);
             }
         }
@@ -1229,7 +1222,10 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
     }
 }
 
-__global__ void __launch_bounds__(kThreads)
+// 4 waves per SIMD (<= 128 VGPRs, no spill): the rescale tasks are latency-bound
+// and the whole body otherwise takes 130 VGPRs (3 waves per SIMD) for its
+// position-parallel 3x3 path.
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
                       uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
                       float eps, double smin, double smax) {
@@ -1238,6 +1234,19 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
     cle_apply_body(rels, tasks, t0, t1, rng, M, st->iters & 1, st->iters == 0, is_signed, eps, smin, smax,
                    blockIdx.x, gridDim.x, A);
 }
+
+#ifdef DFQ_DIAGNOSTICS
+// the same without the occupancy hint (A/B: DFQ_CLE_APPLY_OCC3=1)
+__global__ void __launch_bounds__(kThreads)
+cle_loop_apply_occ3_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
+                           uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
+                           float eps, double smin, double smax) {
+    __shared__ CleApplyLds A;
+    if (st->done) return;
+    cle_apply_body(rels, tasks, t0, t1, rng, M, st->iters & 1, st->iters == 0, is_signed, eps, smin, smax,
+                   blockIdx.x, gridDim.x, A);
+}
+#endif
 
 // The metric's fp32 sums (torch.mean's vectorized_inner_sum over one chunk) as a
 // fixed tree.  A chunk of len elements is 32 streams (s = 8k + l: 8 vector lanes x
@@ -2842,7 +2851,11 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
             DFQ_LAUNCH_CHECK();
         }
         if (a1 > a0) {
-            hipLaunchKernelGGL(cle_loop_apply_kernel, dim3((int)std::min<int64_t>(a1 - a0, kStepGrid)), dim3(kThreads), 0, s,
+            auto kern = cle_loop_apply_kernel;
+#ifdef DFQ_DIAGNOSTICS
+            if (ab_env("DFQ_CLE_APPLY_OCC3")) kern = cle_loop_apply_occ3_kernel;
+#endif
+            hipLaunchKernelGGL(kern, dim3((int)std::min<int64_t>(a1 - a0, kStepGrid)), dim3(kThreads), 0, s,
                                p->d_rels, p->d_atasks, a0, a1, p->d_rng, p->M, p->d_state, p->is_signed, p->eps,
                                p->smin, p->smax);
             DFQ_LAUNCH_CHECK();
@@ -3161,9 +3174,15 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
                 const int rel = (int)((m >> 8) & 0xffff);
                 const CleRel& q = p->h_rels[rel];
                 const CleTask& tk = p->h_atasks[d[i].second];
-                fprintf(stderr, " [%.2f us kind %d rel %d n %lld c1 %lld o2 %lld i2 %lld khw2 %lld o2g %lld fuse %d cols %lld]",
+                fprintf(stderr, " [%.2f us kind %d rel %d n %lld c1 %lld o2 %lld i2 %lld khw2 %lld o2g %lld fuse %d cols %lld",
                         d[i].first, (int)(m & 255), rel, (long long)(m >> 24), (long long)q.c1, (long long)q.o2,
                         (long long)q.i2, (long long)q.khw2, (long long)q.o2g, q.fuse_next, (long long)(tk.c1 - tk.c0));
+                if (q.khw2 > 1) {
+                    const uint64_t sub = tl[4 * d[i].second + 2];
+                    fprintf(stderr, " scales %.2f inv_pos %.2f rows %.2f", (double)(sub & 0xffff) * 0.01,
+                            (double)((sub >> 16) & 0xffff) * 0.01, (double)((sub >> 32) & 0xffff) * 0.01);
+                }
+                fprintf(stderr, "]");
             }
             // start-time histogram: when the tasks began relative to the first
             fprintf(stderr, "\nDFQ_CLE_TL step %d starts (us after first):", k);
