@@ -27,6 +27,37 @@
 
 namespace dfq {
 
+// Wave min / max by DPP (VALU lane permutes: quad swaps, half-row and row
+// mirrors) inside each 16-lane row, then the four rows' results by readlane:
+// the same values as the shuffle forms (min / max are exact; only the combine
+// order differs) at a fraction of their cost -- each __shfl_xor step is an LDS
+// permute round trip, and the rescale tiles reduce every row of their tile.
+__device__ __forceinline__ float dpp_f(float v, int ctrl) {
+    const int x = __float_as_int(v);
+    switch (ctrl) {   // the control must be a compile-time constant
+        case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));
+        case 0x4E: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false));
+        case 0x141: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x141, 0xF, 0xF, false));
+        default: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x140, 0xF, 0xF, false));
+    }
+}
+__device__ __forceinline__ float rl_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ void cle_wave_minmax(float& lo, float& hi) {
+    lo = fminf(lo, dpp_f(lo, 0xB1));
+    hi = fmaxf(hi, dpp_f(hi, 0xB1));
+    lo = fminf(lo, dpp_f(lo, 0x4E));
+    hi = fmaxf(hi, dpp_f(hi, 0x4E));
+    lo = fminf(lo, dpp_f(lo, 0x141));
+    hi = fmaxf(hi, dpp_f(hi, 0x141));
+    lo = fminf(lo, dpp_f(lo, 0x140));
+    hi = fmaxf(hi, dpp_f(hi, 0x140));
+    lo = fminf(fminf(rl_f(lo, 0), rl_f(lo, 16)), fminf(rl_f(lo, 32), rl_f(lo, 48)));
+    hi = fmaxf(fmaxf(rl_f(hi, 0), rl_f(hi, 16)), fmaxf(rl_f(hi, 32), rl_f(hi, 48)));
+}
+
+
 constexpr int kThreads = 256;
 
 static int blocks_for(int64_t n, int per_thread = 1) {
@@ -55,8 +86,7 @@ __global__ void cle_range_w1_kernel(const float* __restrict__ w1, CleShape sh, u
             vmin = fminf(vmin, x);
             vmax = fmaxf(vmax, x);
         }
-        vmin = wave_min(vmin);
-        vmax = wave_max(vmax);
+        cle_wave_minmax(vmin, vmax);
         if (lane == 0) {
             mins[c] = enc_ord(vmin);
             maxs[c] = enc_ord(vmax);
@@ -80,8 +110,7 @@ __global__ void cle_range_w2_contig_kernel(const float* __restrict__ w2, CleShap
             vmin = fminf(vmin, x);
             vmax = fmaxf(vmax, x);
         }
-        vmin = wave_min(vmin);
-        vmax = wave_max(vmax);
+        cle_wave_minmax(vmin, vmax);
         if (lane == 0) {
             mins[c] = enc_ord(vmin);
             maxs[c] = enc_ord(vmax);
@@ -523,8 +552,7 @@ __device__ __forceinline__ void wave_range(const float* __restrict__ p, int64_t 
                 }
         }
     }
-    vmin = wave_min(vmin);
-    vmax = wave_max(vmax);
+    cle_wave_minmax(vmin, vmax);
 }
 
 // p[0..n) *= f(), one wave; 4 loads in flight per lane before the stores.  The
@@ -625,8 +653,7 @@ __device__ __forceinline__ void wave_scale_mm(float* __restrict__ p, int64_t n, 
                 }
         }
     }
-    vmin = wave_min(vmin);
-    vmax = wave_max(vmax);
+    cle_wave_minmax(vmin, vmax);
 }
 
 // p[0..n) *= f() and the (min, max) of the products, one wave (scalar loads:
@@ -649,8 +676,7 @@ __device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t 
         vmin = fminf(vmin, y);
         vmax = fmaxf(vmax, y);
     }
-    vmin = wave_min(vmin);
-    vmax = wave_max(vmax);
+    cle_wave_minmax(vmin, vmax);
 }
 
 // W2 row tiles with KH*KW = khw in (1, kTileMaxKhw] and one group: thread t owns
@@ -1018,8 +1044,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                     z1 = fmaxf(z1, z);
                 }
                 if (R.w2_self) {
-                    z0 = wave_min(z0);
-                    z1 = wave_max(z1);
+                    cle_wave_minmax(z0, z1);
                     if (lane == 0) {
                         nmins[R.moff + R.c1 + c] = enc_ord(z0);
                         nmaxs[R.moff + R.c1 + c] = enc_ord(z1);
@@ -1075,8 +1100,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                         hi = fmaxf(hi, y);
                     }
                 if (fuse) {
-                    lo = wave_min(lo);
-                    hi = wave_max(hi);
+                    cle_wave_minmax(lo, hi);
                     if (lane == 0) {
                         red[0][wv][o - tk.a] = lo;
                         red[1][wv][o - tk.a] = hi;
@@ -1120,7 +1144,8 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                             y = v[j] * inv;
                             R.w2[(tk.a + j) * rowlen + i] = y;
                         }
-                        const float a = wave_min(act ? y : INFINITY), b = wave_max(act ? y : -INFINITY);
+                        float a = act ? y : INFINITY, b = act ? y : -INFINITY;
+                        cle_wave_minmax(a, b);
                         if (lane == 0) {
                             red[0][wv][j] = a;
                             red[1][wv][j] = b;
@@ -1147,7 +1172,8 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                             hi = fmaxf(hi, y);
                         }
                     }
-                    const float a = wave_min(lo), b = wave_max(hi);
+                    float a = lo, b = hi;
+                    cle_wave_minmax(a, b);
                     if (lane == 0) {
                         red[0][wv][j] = a;
                         red[1][wv][j] = b;
