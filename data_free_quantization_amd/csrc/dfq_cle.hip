@@ -684,6 +684,12 @@ __device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t 
 // on consecutive floats, khw independent loads per row in flight -- instead of
 // one thread per column walking its khw floats serially.
 constexpr int kTileMaxKhw = 9;   // 3x3 (and 2x2); larger kernels keep the per-column walk
+// Rows per position-parallel rescale tile (<= kColTileRows); the diagnostics
+// library takes DFQ_CLE_POS_ROWS for the A/B.
+static int64_t cle_pos_tile_rows() {
+    const char* e = ab_env("DFQ_CLE_POS_ROWS");
+    return e && *e ? std::max<int64_t>(1, std::min<int64_t>(kColTileRows, atoll(e))) : 4;
+}
 
 __device__ __forceinline__ bool tile_by_position(const CleRel& R, const CleTask& tk) {
     return R.khw2 > 1 && R.khw2 <= kTileMaxKhw && (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
@@ -2470,9 +2476,13 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             for (int64_t a = 0, k = rows_per_task(c.o2g * c.khw2); a < c.c1; a += k)
                 out.push_back({r, kApplyW2Contig, a, std::min<int64_t>(a + k, c.c1), 0, 0});
         } else {
-            for (int64_t a = 0; a < c.o2; a += kColTileRows)
+            // KH*KW > 1 tiles go position-parallel, a row at a time: fewer rows per
+            // task, more tasks in flight (ResNet-50's 3x3 W2 tiles: 16 rows took
+            // ~70 us, DFQ_CLE_TL); 1x1 tiles keep kColTileRows (loads issued together)
+            const int64_t rows = (c.khw2 > 1 && c.khw2 <= kTileMaxKhw) ? cle_pos_tile_rows() : kColTileRows;
+            for (int64_t a = 0; a < c.o2; a += rows)
                 for (int64_t i0 = 0; i0 < c.i2; i0 += kThreads)
-                    out.push_back({r, kApplyW2Tile, a, std::min<int64_t>(a + kColTileRows, c.o2), i0,
+                    out.push_back({r, kApplyW2Tile, a, std::min<int64_t>(a + rows, c.o2), i0,
                                    std::min<int64_t>(i0 + kThreads, c.i2)});
         }
         for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
