@@ -31,6 +31,7 @@ CONFIGS = {
     "no_self_ranges": {"DFQ_CLE_NO_SELF_RANGES": "1"},     # every next range from a range task
     "apply_occ3": {"DFQ_CLE_APPLY_OCC3": "1"},              # rescale kernel at 130 VGPRs (3 waves / SIMD)
     "pos_rows16": {"DFQ_CLE_POS_ROWS": "16"},               # 3x3 rescale tiles of 16 rows (round 2)
+    "pos_rows8": {"DFQ_CLE_POS_ROWS": "8"},
     "graph": {"DFQ_CLE_GRAPH": "1"},                       # each batch replayed as a (cached) HIP graph
     "batch8": {"DFQ_CLE_BATCH": "8"},
     "batch2": {"DFQ_CLE_BATCH": "2"},
