@@ -102,8 +102,10 @@ def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8
             _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps)
 
 
-def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps):
-    t0 = time.perf_counter()
+def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
+    """dfq_cle_plan_create over the relations' tensors; returns (plan, workspace,
+    device).  The workspace (W_prev snapshots, torch's caching allocator) must
+    outlive the plan."""
     targets = [graph[k].weight.data for k in graph if type(graph[k]) in Target_list]
     n = len(relations)
     descs = (_lib.CleRel * max(n, 1))()
@@ -141,31 +143,42 @@ def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count,
         raise RuntimeError("dfq_cle_plan_ws_bytes: invalid target sizes")
     ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=dev)
     plan = C.c_void_p()
-    t1 = time.perf_counter()
     _lib.check(L.dfq_cle_plan_create(descs, n, tp, tn, nt, float(s_min_max[0]), float(s_min_max[1]),
                                      int(bool(signed)), float(eps), _lib.REF_THREADS, ws.data_ptr(), ws.numel(),
                                      C.byref(plan)),
                "dfq_cle_plan_create", RuntimeError)
+    return plan, ws, dev
+
+
+def _run_plan(plan, dev, Treshhold, Count):
+    """dfq_cle_plan_run; returns (iterations, diffs, (chains, steps, launches per iteration))."""
+    L = _lib.load()
+    iters = C.c_int32(0)
+    hist = _hist_buffer()
+    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(L.dfq_cle_plan_run(plan, float(Treshhold), int(Count), MAX_ITERS, C.byref(iters), hist, stream),
+               "dfq_cle_plan_run")
+    chains, steps, launches = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+    L.dfq_cle_plan_info(plan, C.byref(chains), C.byref(steps), C.byref(launches))
+    return iters.value, [hist[i] for i in range(iters.value)], (chains.value, steps.value, launches.value)
+
+
+def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps):
+    t0 = time.perf_counter()
+    plan, ws, dev = _create_plan(graph, relations, Target_list, s_min_max, signed, eps)
     t2 = time.perf_counter()
     try:
-        iters = C.c_int32(0)
-        hist = _hist_buffer()
-        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        _lib.check(L.dfq_cle_plan_run(plan, float(Treshhold), int(Count), MAX_ITERS, C.byref(iters), hist, stream),
-                   "dfq_cle_plan_run")
-        chains, steps, launches = C.c_int32(0), C.c_int32(0), C.c_int32(0)
-        L.dfq_cle_plan_info(plan, C.byref(chains), C.byref(steps), C.byref(launches))
+        iters, diffs, (chains, steps, launches) = _run_plan(plan, dev, Treshhold, Count)
     finally:
         t3 = time.perf_counter()
-        L.dfq_cle_plan_destroy(plan)
+        _lib.load().dfq_cle_plan_destroy(plan)
     t4 = time.perf_counter()
-    if iters.value >= MAX_ITERS:
+    if iters >= MAX_ITERS:
         warnings.warn(f"cross_layer_equalization stopped at DFQ_CLE_MAX_ITERS={MAX_ITERS} iterations")
     LAST_RUN.clear()
-    LAST_RUN.update(iterations=iters.value, diffs=[hist[i] for i in range(iters.value)], chains=chains.value,
-                    steps=steps.value, launches_per_iteration=launches.value, mode="device",
-                    host_ms={"describe": (t1 - t0) * 1e3, "create": (t2 - t1) * 1e3, "run": (t3 - t2) * 1e3,
-                             "destroy": (t4 - t3) * 1e3})
+    LAST_RUN.update(iterations=iters, diffs=diffs, chains=chains, steps=steps, launches_per_iteration=launches,
+                    mode="device", host_ms={"create": (t2 - t0) * 1e3, "run": (t3 - t2) * 1e3,
+                                            "destroy": (t4 - t3) * 1e3})
 
 
 _HIST = None

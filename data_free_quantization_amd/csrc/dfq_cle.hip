@@ -686,9 +686,10 @@ __device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t 
 constexpr int kTileMaxKhw = 9;   // 3x3 (and 2x2); larger kernels keep the per-column walk
 // Rows per position-parallel rescale tile (<= kColTileRows); the diagnostics
 // library takes DFQ_CLE_POS_ROWS for the A/B.
+constexpr int kPosTileMaxRows = 4;   // a position tile's rows: their loads are in flight together
 static int64_t cle_pos_tile_rows() {
     const char* e = ab_env("DFQ_CLE_POS_ROWS");
-    return e && *e ? std::max<int64_t>(1, std::min<int64_t>(kColTileRows, atoll(e))) : 4;
+    return e && *e ? std::max<int64_t>(1, std::min<int64_t>(kColTileRows, atoll(e))) : kPosTileMaxRows;
 }
 
 __device__ __forceinline__ bool tile_by_position(const CleRel& R, const CleTask& tk) {
@@ -925,6 +926,9 @@ struct CleApplyLds {
 __device__ uint64_t* g_cle_tl = nullptr;
 #endif
 
+// POS: the step has position-parallel (KH*KW > 1) W2 tiles; without them the
+// body needs far fewer VGPRs (more waves per SIMD for the latency-bound tasks)
+template <bool POS = true>
 __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks,
                                                int64_t t0, int64_t t1, uint32_t* __restrict__ rng, int64_t M,
                                                int par, bool first_iter, int is_signed, float eps, double smin,
@@ -1073,7 +1077,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                     wave_scale(R.w2 + c * seg, seg, R.vec2, lane, inv);
                 }
             }
-        } else if (tk.kind == kApplyW2Tile && tile_by_position(R, tk)) {
+        } else if (POS && tk.kind == kApplyW2Tile && tile_by_position(R, tk) && tk.b - tk.a <= kPosTileMaxRows) {
             // position-parallel tile (KH*KW > 1): the columns' 1/s into LDS, then each
             // row's positions scaled; fused: the rows' (min, max) for the next W1
             const int t = threadIdx.x;
@@ -1090,24 +1094,25 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             for (int q = t; q < npos; q += kThreads) inv_pos[q] = inv_s[q / khw];   // 1/s per position
             __syncthreads();
             DFQ_CLE_TL_MARK(1)
-            // Software-pipelined rows: row o + 1's loads are issued before row o's
-            // stores, so waiting for them never waits for a store as well (gfx9's
-            // vmcnt counts loads and stores in order; one load round trip plus one
-            // store drain per row otherwise: ~5 us a row on ResNet-50, DFQ_CLE_TL)
-            float va[kTileMaxKhw], vb[kTileMaxKhw];
-            auto load_row = [&](float (&dst)[kTileMaxKhw], int64_t o) {
-                const float* rp = base + o * rowlen;
+            // Every row's loads in flight together, then the rows' scaled stores:
+            // one memory round trip per tile instead of one per row (~5 us a row
+            // under the step's load, ResNet-50's 3x3 tiles; DFQ_CLE_TL)
+            float v[kPosTileMaxRows][kTileMaxKhw];
+#pragma unroll
+            for (int r = 0; r < kPosTileMaxRows; ++r)
 #pragma unroll
                 for (int m = 0; m < kTileMaxKhw; ++m)
-                    if (m < khw && t + kThreads * m < npos) dst[m] = rp[t + kThreads * m];
-            };
-            auto do_row = [&](const float (&v)[kTileMaxKhw], int64_t o) {
-                float* rp = base + o * rowlen;
+                    if (tk.a + r < tk.b && m < khw && t + kThreads * m < npos)
+                        v[r][m] = base[(tk.a + r) * rowlen + t + kThreads * m];
+#pragma unroll
+            for (int r = 0; r < kPosTileMaxRows; ++r) {
+                if (tk.a + r >= tk.b) break;   // uniform
+                float* rp = base + (tk.a + r) * rowlen;
                 float lo = INFINITY, hi = -INFINITY;
 #pragma unroll
                 for (int m = 0; m < kTileMaxKhw; ++m)
                     if (m < khw && t + kThreads * m < npos) {
-                        const float y = v[m] * inv_pos[t + kThreads * m];
+                        const float y = v[r][m] * inv_pos[t + kThreads * m];
                         rp[t + kThreads * m] = y;
                         lo = fminf(lo, y);
                         hi = fmaxf(hi, y);
@@ -1115,18 +1120,10 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                 if (fuse) {
                     cle_wave_minmax(lo, hi);
                     if (lane == 0) {
-                        red[0][wv][o - tk.a] = lo;
-                        red[1][wv][o - tk.a] = hi;
+                        red[0][wv][r] = lo;
+                        red[1][wv][r] = hi;
                     }
                 }
-            };
-            load_row(va, tk.a);
-            for (int64_t o = tk.a; o < tk.b; o += 2) {   // two rows per trip: no register copies
-                if (o + 1 < tk.b) load_row(vb, o + 1);
-                do_row(va, o);
-                if (o + 1 >= tk.b) break;
-                if (o + 2 < tk.b) load_row(va, o + 2);
-                do_row(vb, o + 1);
             }
             __syncthreads();
             DFQ_CLE_TL_MARK(2)
@@ -1269,23 +1266,22 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
     }
 }
 
-// 4 waves per SIMD (<= 128 VGPRs, no spill): the rescale tasks are latency-bound
-// and the whole body otherwise takes 130 VGPRs (3 waves per SIMD) for its
-// position-parallel 3x3 path.
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+template <bool POS>
+__global__ void __launch_bounds__(kThreads)
 cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
                       uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
                       float eps, double smin, double smax) {
     __shared__ CleApplyLds A;
     if (st->done) return;
-    cle_apply_body(rels, tasks, t0, t1, rng, M, st->iters & 1, st->iters == 0, is_signed, eps, smin, smax,
-                   blockIdx.x, gridDim.x, A);
+    cle_apply_body<POS>(rels, tasks, t0, t1, rng, M, st->iters & 1, st->iters == 0, is_signed, eps, smin, smax,
+                        blockIdx.x, gridDim.x, A);
 }
 
 #ifdef DFQ_DIAGNOSTICS
-// the same without the occupancy hint (A/B: DFQ_CLE_APPLY_OCC3=1)
-__global__ void __launch_bounds__(kThreads)
-cle_loop_apply_occ3_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
+// the same capped at 128 VGPRs for 4 waves per SIMD (A/B: DFQ_CLE_APPLY_OCC4=1;
+// it spills, and measured no faster: profiles/r03/cle_ab_aa.jsonl)
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+cle_loop_apply_occ4_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
                            uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
                            float eps, double smin, double smax) {
     __shared__ CleApplyLds A;
@@ -2198,6 +2194,7 @@ struct dfq_cle_plan {
     CleState* h_state = nullptr;    // pinned (the device context's, set by run)
     hipStream_t st = nullptr;       // the loop's stream (the device context's)
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
+    std::vector<char> step_pos;          // per step: position-parallel W2 tiles (the POS rescale kernel)
     int64_t M = 0, nchunks = 0;
     int32_t nl = 0, chains = 0, steps = 0;
     bool fused = false;   // one range launch per iteration (see dfq_cle_plan_create)
@@ -2707,6 +2704,10 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->fused = fused;
     p->rstep = rstep;
     p->astep = astep;
+    p->step_pos.assign(std::max<int32_t>(steps, 1), 0);
+    for (int32_t k = 0; k < steps; ++k)
+        for (int64_t t = astep[k]; t < astep[k + 1]; ++t)
+            if (at[t].kind == kApplyW2Tile && R[at[t].rel].khw2 > 1) p->step_pos[k] = 1;
     p->ri0 = ri0;
     p->ri1 = ri1;
 #ifdef DFQ_DIAGNOSTICS
@@ -2746,6 +2747,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     char* base = nullptr;
     char* hblob = nullptr;
     CleDeviceCtx& ctx = cle_device_ctx(p->dev);
+    e = hipSuccess;   // a busy pool leaves it untouched: the private path follows
     if (!grouped) {   // the pool (the diagnostics-only grouped tables take the private path)
         std::lock_guard<std::mutex> lock(ctx.mu);
         if (!ctx.pool_busy && (e = cle_ctx_ready(ctx)) == hipSuccess &&
@@ -2902,9 +2904,9 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
             DFQ_LAUNCH_CHECK();
         }
         if (a1 > a0) {
-            auto kern = cle_loop_apply_kernel;
+            auto kern = p->step_pos[k] ? cle_loop_apply_kernel<true> : cle_loop_apply_kernel<false>;
 #ifdef DFQ_DIAGNOSTICS
-            if (ab_env("DFQ_CLE_APPLY_OCC3")) kern = cle_loop_apply_occ3_kernel;
+            if (ab_env("DFQ_CLE_APPLY_OCC4")) kern = cle_loop_apply_occ4_kernel;
 #endif
             hipLaunchKernelGGL(kern, dim3((int)std::min<int64_t>(a1 - a0, kStepGrid)), dim3(kThreads), 0, s,
                                p->d_rels, p->d_atasks, a0, a1, p->d_rng, p->M, p->d_state, p->is_signed, p->eps,
@@ -3324,7 +3326,8 @@ hipError_t preload_cle() {   // see dfq_preload
         if ((e0 = cle_ctx_ready(ctx)) != hipSuccess) return e0;
     }
     hipFuncAttributes a;
-    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_apply_kernel));
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_apply_kernel<true>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_apply_kernel<false>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_tiles_fin_kernel));
     return e;
 }

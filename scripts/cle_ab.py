@@ -22,16 +22,15 @@ os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_UNFUSED_FIN", "DFQ_CLE_GROUPS", "DFQ_CLE_GROUP_GRID", "DFQ_CLE_ORDERED", "DFQ_CLE_GSYNC_NOFENCE",
             "DFQ_CLE_NO_DW_PAIRS", "DFQ_CLE_FORK", "DFQ_CLE_NO_SELF_RANGES", "DFQ_CLE_GRAPH",
-            "DFQ_CLE_BATCH", "DFQ_CLE_APPLY_OCC3",
+            "DFQ_CLE_BATCH", "DFQ_CLE_APPLY_OCC4",
             "DFQ_CLE_POS_ROWS")
 CONFIGS = {
     "tiles_fin": {},                                       # the product (eager batches of 4)
     "no_dw_pairs": {"DFQ_CLE_NO_DW_PAIRS": "1"},           # round-2 steps: one launch per relation
     "fork": {"DFQ_CLE_FORK": "1"},                         # next ranges on a concurrent graph branch
     "no_self_ranges": {"DFQ_CLE_NO_SELF_RANGES": "1"},     # every next range from a range task
-    "apply_occ3": {"DFQ_CLE_APPLY_OCC3": "1"},              # rescale kernel at 130 VGPRs (3 waves / SIMD)
+    "apply_occ4": {"DFQ_CLE_APPLY_OCC4": "1"},              # rescale kernel capped at 128 VGPRs (4 waves / SIMD)
     "pos_rows16": {"DFQ_CLE_POS_ROWS": "16"},               # 3x3 rescale tiles of 16 rows (round 2)
-    "pos_rows8": {"DFQ_CLE_POS_ROWS": "8"},
     "graph": {"DFQ_CLE_GRAPH": "1"},                       # each batch replayed as a (cached) HIP graph
     "batch8": {"DFQ_CLE_BATCH": "8"},
     "batch2": {"DFQ_CLE_BATCH": "2"},

@@ -42,7 +42,7 @@ sys.path.insert(0, os.environ["DFQ_ROOT"])
 from tests.parity import pipeline_mismatches
 from data_free_quantization_amd import Cross_layer_equal as cle
 SWITCHES = ("DFQ_CLE_UNFUSED_FIN", "DFQ_CLE_GROUPS", "DFQ_CLE_GROUP_GRID", "DFQ_CLE_ORDERED", "DFQ_CLE_NO_DW_PAIRS",
-            "DFQ_CLE_FORK", "DFQ_CLE_NO_SELF_RANGES", "DFQ_CLE_GRAPH", "DFQ_CLE_BATCH", "DFQ_CLE_APPLY_OCC3",
+            "DFQ_CLE_FORK", "DFQ_CLE_NO_SELF_RANGES", "DFQ_CLE_GRAPH", "DFQ_CLE_BATCH", "DFQ_CLE_APPLY_OCC4",
             "DFQ_CLE_POS_ROWS")
 CONFIGS = {
     "tiles_fin": {},                                      # the product: steps + fused tiles / stop rule
@@ -50,9 +50,8 @@ CONFIGS = {
     "no_dw_pairs": {"DFQ_CLE_NO_DW_PAIRS": "1"},           # one launch per relation (round 2)
     "fork": {"DFQ_CLE_FORK": "1"},                         # next ranges on a concurrent graph branch
     "no_self_ranges": {"DFQ_CLE_NO_SELF_RANGES": "1"},     # every next range from a range task
-    "apply_occ3": {"DFQ_CLE_APPLY_OCC3": "1"},              # rescale kernel at 130 VGPRs (3 waves / SIMD)
+    "apply_occ4": {"DFQ_CLE_APPLY_OCC4": "1"},              # rescale kernel capped at 128 VGPRs (4 waves / SIMD)
     "pos_rows16": {"DFQ_CLE_POS_ROWS": "16"},               # 3x3 rescale tiles of 16 rows (round 2)
-    "pos_rows8": {"DFQ_CLE_POS_ROWS": "8"},
     "graph": {"DFQ_CLE_GRAPH": "1"},                       # batches replayed as a cached HIP graph
     "batch8": {"DFQ_CLE_BATCH": "8"},
     "unfused": {"DFQ_CLE_UNFUSED_FIN": "1"},              # stop rule as launches of its own
