@@ -2711,8 +2711,10 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->ri0 = ri0;
     p->ri1 = ri1;
 #ifdef DFQ_DIAGNOSTICS
-    p->h_rels = R;   // for the DFQ_CLE_TL report
-    p->h_atasks = at;
+    if (ab_env("DFQ_CLE_TL")) {   // for the timeline report (copies cost ~0.2 ms: only when asked)
+        p->h_rels = R;
+        p->h_atasks = at;
+    }
 #endif
     p->smin = s_min; p->smax = s_max; p->is_signed = is_signed; p->eps = eps;
     hipError_t e;
