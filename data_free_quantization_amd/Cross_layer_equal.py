@@ -102,34 +102,48 @@ def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8
             _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps)
 
 
+def _state(m, name):
+    """A module's registered buffer ``name`` without Module.__getattr__ (any other
+    object, or a plain attribute: getattr)."""
+    b = getattr(m, "_buffers", None)
+    if b is not None and name in b:
+        return b[name]
+    return getattr(m, name, None)
+
+
 def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
     """dfq_cle_plan_create over the relations' tensors; returns (plan, workspace,
     device).  The workspace (W_prev snapshots, torch's caching allocator) must
     outlive the plan."""
-    targets = [graph[k].weight.data for k in graph if type(graph[k]) in Target_list]
+    # module state straight from the parameter / buffer dicts (Module.__getattr__
+    # per access was a good part of this host time)
+    tl = tuple(Target_list)
+    targets = [v._parameters["weight"] for v in graph.values() if type(v) in tl]
     n = len(relations)
     descs = (_lib.CleRel * max(n, 1))()
     for i, rel in enumerate(relations):
         first, second, bn_idx = rel.get_idxs()
         l1, l2 = graph[first], graph[second]
-        if l1.bias is None:   # :93-94
-            l1.bias = nn.Parameter(torch.zeros(l1.weight.size(0), dtype=torch.float32, device=l1.weight.device),
+        p1 = l1._parameters
+        if p1.get("bias") is None:   # :93-94
+            l1.bias = nn.Parameter(torch.zeros(p1["weight"].size(0), dtype=torch.float32, device=p1["weight"].device),
                                    requires_grad=False)
         bn = graph[bn_idx]
-        W1, W2, B1 = l1.weight.data, l2.weight.data, l1.bias.data
-        bnw, bnb = getattr(bn, "fake_weight", None), getattr(bn, "fake_bias", None)
+        W1, W2, B1 = p1["weight"], l2._parameters["weight"], p1["bias"]
+        bnw, bnb = _state(bn, "fake_weight"), _state(bn, "fake_bias")
         _lib.require_device(W1, W2, B1, bnw, bnb)
         init = rel.S is None
         if init:
             rel.S = torch.empty(W1.size(0), dtype=torch.float32, device=W1.device)
+        s1, s2 = W1.shape, W2.shape
         d = descs[i]
         d.w1, d.w2, d.b1 = W1.data_ptr(), W2.data_ptr(), B1.data_ptr()
         d.bn_w = bnw.data_ptr() if bnw is not None else None
         d.bn_b = bnb.data_ptr() if bnb is not None else None
         d.s_acc = rel.S.data_ptr()
-        d.c1, d.len1 = W1.shape[0], W1.numel() // W1.shape[0]
-        d.o2, d.i2 = W2.shape[0], W2.shape[1]
-        d.khw2 = W2.numel() // (W2.shape[0] * W2.shape[1])
+        d.c1, d.len1 = s1[0], W1.numel() // s1[0]
+        d.o2, d.i2 = s2[0], s2[1]
+        d.khw2 = W2.numel() // (s2[0] * s2[1])
         d.s_acc_init = 1 if init else 0
     _lib.require_device(*targets)
     nt = len(targets)

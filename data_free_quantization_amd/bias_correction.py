@@ -29,6 +29,23 @@ logging.basicConfig(level=logging.INFO)
 logger = logging.getLogger(__name__)
 
 
+def _buf(m, name):
+    """A module's registered buffer without Module.__getattr__ (else getattr)."""
+    b = getattr(m, "_buffers", None)
+    if b is not None and name in b:
+        return b[name]
+    return getattr(m, name)
+
+
+def _param(m, name):
+    """A module's registered parameter (None if registered as None) without
+    Module.__getattr__ (else getattr, None if absent)."""
+    p = getattr(m, "_parameters", None)
+    if p is not None and name in p:
+        return p[name]
+    return getattr(m, name, None)
+
+
 def _bc_expect(bn_weight, bn_bias, relu, out=None):
     """calculate_mean (γφ(-β/γ) + β(1-Φ(-β/γ)), clamped at 0) when a ReLU follows the
     BN, else β; ``out`` given: accumulate into it (the 'add' branch sum)."""
@@ -253,7 +270,7 @@ class _BcChain:
         return t.data_ptr() + 4 * off
 
     def expect(self, bn, relu, dst, accumulate):
-        w, b = bn.fake_weight, bn.fake_bias
+        w, b = _buf(bn, "fake_weight"), _buf(bn, "fake_bias")
         _lib.require_device(w, b)
         self.keep += [w, b]
         self.ops.append((_lib.DFQ_BC_OP_EXPECT, int(bool(relu)) | (int(accumulate) << 1), (w, 0), (b, 0), dst, None,
@@ -301,7 +318,7 @@ def _record_branches(chain, bn_branch):
     for key, branch in bn_branch.items():
         ref, size, connect_type = None, 0, None
         for layer, relu_attached, connect_type in branch:
-            n = layer.fake_bias.numel()
+            n = _buf(layer, "fake_bias").numel()
             if ref is None:
                 ref, size = chain.alloc(n), n
                 chain.expect(layer, relu_attached, ref, False)
@@ -323,16 +340,17 @@ def _record_apply(chain, layer, E, o, i2, connect_type, expect, f):
     ref and its numel (kept for the next BN)."""
     if connect_type == "cat":
         raise RuntimeError("Tensors must have same number of dimensions: got 2 and 1")
-    if layer.bias is None:   # :89-90 references an undefined `nn`
+    bias = _param(layer, "bias")
+    if bias is None:   # :89-90 references an undefined `nn`
         raise NameError("name 'nn' is not defined")
     bcols = _broadcast_cols(i2, f)
     if o * bcols <= o:
         logger.error("Error in applying bias correction: Bias correction shape mismatch that cannot be handled "
                      "automatically.")
         raise ValueError("Bias correction shape mismatch that cannot be handled automatically.")
-    _lib.require_device(E, layer.bias.data)
+    _lib.require_device(E, bias)
     vec = chain.alloc(o * bcols)
-    chain.apply(E.reshape(-1), o, i2, expect, f, layer.bias.data, vec)
+    chain.apply(E.reshape(-1), o, i2, expect, f, bias.data, vec)
     return vec, o * bcols
 
 
@@ -358,8 +376,12 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
         # The walk only writes the bias of the layer it is on, after recording it, so
         # every "before" value is the bias at entry: one batched copy instead of a
         # clone per layer (and likewise for "after", at the end).
-        biases = {f"layer_{i}": l.bias.data for i, l in enumerate(graph.values())
-                  if i in bottoms and isinstance(l, targ_type) and getattr(l, "bias", None) is not None}
+        biases = {}
+        for i, l in enumerate(graph.values()):
+            if i in bottoms and isinstance(l, targ_type):
+                b = _param(l, "bias")
+                if b is not None:
+                    biases[f"layer_{i}"] = b.data
         chain = _BcChain(next(iter(biases.values())).device if biases else torch.device("cuda"))
         before = _snapshot(chain, biases)
         stream = None
@@ -378,13 +400,14 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                     relu_attached[idx_layer] = False
                     if bias_prev is not None:
                         vec, numel = bias_prev
-                        f = node.fake_bias.size(0)
+                        fake_b = _buf(node, "fake_bias")
+                        f = fake_b.size(0)
                         if numel == f:
                             # fake_bias.add_(bias_prev) with a 2-D bias_prev cannot broadcast in place
                             raise RuntimeError("output with shape [{}] doesn't match the broadcast shape".format(f))
                         if numel % f:
                             raise RuntimeError(f"shape '[-1, {f}]' is invalid for input of size {numel}")
-                        chain.propagate(vec, numel, node.fake_bias, f)
+                        chain.propagate(vec, numel, fake_b, f)
                         bias_prev = None
                     continue
                 if isinstance(node, torch.nn.ReLU) and bot[0] in bn_module:
@@ -392,7 +415,7 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                 if isinstance(node, targ_type):
                     bn_list, relu_list, type_list, _ = find_prev_bn(bn_module, relu_attached, graph, bottoms, bot[:])
                     pre = None if error_sums is None else error_sums.get(keys[idx_layer])
-                    E, o, i2 = _error_sums(node.weight.data, bits_weight, signed, pre)
+                    E, o, i2 = _error_sums(_param(node, "weight").data, bits_weight, signed, pre)
                     if stream is None:
                         stream = _lib.stream_of(E)
                         chain.dev = E.device
@@ -408,8 +431,9 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                     if bias is None:
                         raise UnboundLocalError("local variable 'bias' referenced before assignment")
                     bias_prev = bias
-                    if getattr(layer, "bias", None) is not None:
-                        after_src[layer_name] = layer.bias.data
+                    b = _param(layer, "bias")
+                    if b is not None:
+                        after_src[layer_name] = b.data
                     if len(chain.ops) >= _FLUSH_OPS:   # the device starts on what is recorded so far
                         chain.flush(stream)
             after = _snapshot(chain, after_src)

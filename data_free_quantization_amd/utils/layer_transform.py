@@ -81,47 +81,55 @@ assert _BN_DESC.itemsize == C.sizeof(_lib.BnFoldDesc)
 
 def _fold_batch(pairs, ranges=None):
     with torch.no_grad():
-        dev = pairs[0][1].weight.device
+        # module state straight from the parameter / buffer dicts: Module.__getattr__
+        # on every access was most of this function's host time
+        st = []
         for bn, layer in pairs:
-            _lib.require_device(layer.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var)
+            lp, bp, bb = layer._parameters, bn._parameters, bn._buffers
+            st.append((lp["weight"], lp.get("bias"), bp["weight"], bp["bias"], bb["running_mean"], bb["running_var"]))
+        _lib.require_device(*[t for row in st for t in row if t is not None])
+        dev = st[0][0].device
         # :262-263 give a bias-less layer torch.zeros; here the fold reads such a
         # bias as 0 (DFQ_BN_FOLD_ZERO_BIAS) and writes every element of it
-        need_bias = [layer for _, layer in pairs if layer.bias is None]
-        for layer, z in zip(need_bias, _carve([l.weight.size(0) for l in need_bias], False, dev)):
-            p = nn.Parameter(z, requires_grad=False)
+        need = [j for j, row in enumerate(st) if row[1] is None]
+        for j, z in zip(need, _carve([st[j][0].shape[0] for j in need], False, dev)):
+            layer = pairs[j][1]
+            b = nn.Parameter(z, requires_grad=False)
             if "bias" in layer._parameters:   # registered as None: what Module.__setattr__ would do
-                layer._parameters["bias"] = p
+                layer._parameters["bias"] = b
             else:
-                layer.bias = p
-        fresh = {id(layer) for layer in need_bias}
-        nc = [bn.weight.numel() for bn, _ in pairs]
-        fakes = _carve(nc * 2, False, dev)
+                layer.bias = b
+            st[j] = (st[j][0], b) + st[j][2:]
+        fresh = set(need)
         n = len(pairs)
+        fakes = _carve([row[2].numel() for row in st] * 2, False, dev)
         tab = np.zeros(n, dtype=_BN_DESC)
-        ptrs = tab["ptr"]
-        for j, (bn, layer) in enumerate(pairs):
-            w = layer.weight
+        rows = []
+        for j, ((bn, _), (w, b, g, beta, mean, var)) in enumerate(zip(pairs, st)):
             fw, fb = fakes[j], fakes[n + j]
             buf = bn._buffers   # register_buffer("fake_weight" / "fake_bias") without the per-call checks
             buf["fake_weight"], buf["fake_bias"] = fw, fb
-            ptrs[j] = (w.data_ptr(), layer.bias.data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(),
-                       bn.running_mean.data_ptr(), bn.running_var.data_ptr(), fw.data_ptr(), fb.data_ptr())
+            rows.append((w.data_ptr(), b.data_ptr(), g.data_ptr(), beta.data_ptr(), mean.data_ptr(), var.data_ptr(),
+                         fw.data_ptr(), fb.data_ptr()))
+        tab["ptr"] = np.array(rows, dtype=np.uint64)
         tab["eps"] = [float(bn.eps) for bn, _ in pairs]
-        tab["flags"] = [_lib.DFQ_BN_FOLD_ZERO_BIAS if id(layer) in fresh else 0 for _, layer in pairs]
+        if fresh:
+            tab["flags"][list(fresh)] = _lib.DFQ_BN_FOLD_ZERO_BIAS
         if ranges is not None:   # 8 bytes per fold, in one allocation (zeroed by the call)
             rbuf = torch.empty(2 * n, dtype=torch.int32, device=dev)
             tab["range_enc"] = rbuf.data_ptr() + 8 * np.arange(n, dtype=np.uint64)
             for j, (_, layer) in enumerate(pairs):
                 ranges[layer] = rbuf[2 * j:2 * j + 2]
-        tab["rows"] = [layer.weight.size(0) for _, layer in pairs]
-        tab["row_len"] = [layer.weight.numel() // layer.weight.size(0) for _, layer in pairs]
+        shapes = [row[0].shape for row in st]
+        tab["rows"] = [sh[0] for sh in shapes]
+        tab["row_len"] = [row[0].numel() // sh[0] for row, sh in zip(st, shapes)]
         descs = tab.ctypes.data_as(C.POINTER(_lib.BnFoldDesc))
         L = _lib.load()
         nb = int(L.dfq_bn_fold_ws_bytes(descs, n))
         if nb < 0:
             raise RuntimeError("dfq_bn_fold_ws_bytes: invalid layer shapes")
         ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=dev)   # stream-ordered (caching allocator)
-        rc = L.dfq_bn_fold_batch(descs, n, ws.data_ptr(), ws.numel(), _lib.stream_of(pairs[0][1].weight))
+        rc = L.dfq_bn_fold_batch(descs, n, ws.data_ptr(), ws.numel(), _lib.stream_of(st[0][0]))
         _lib.check(rc, "dfq_bn_fold_batch")
         for bn, _ in pairs:
             bn.__dict__["eps"] = 0   # plain attributes: what Module.__setattr__ ends in
