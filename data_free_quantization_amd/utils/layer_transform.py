@@ -193,11 +193,12 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
         raise ValueError("granularity must be 'tensor' or 'channel'")
     items = []
     keys = []
-    for layer_idx in graph:
-        layer = graph[layer_idx]
-        if type(layer) not in targ_type:
+    tt = tuple(targ_type)
+    for layer_idx, layer in graph.items():
+        if type(layer) not in tt:
             continue
-        w = layer.weight.data
+        lp = layer._parameters   # no Module.__getattr__ per access
+        w = lp["weight"].data
         rows = w.size(0) if per_channel else 1
         npar = rows
         khw = khw_of(w)
@@ -206,8 +207,8 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
                        range_enc=weight_ranges.get(layer) if (weight_ranges and not per_channel) else None)
         items.append(it)
         keys.append(layer_idx)
-        if layer.bias is not None and bits_bias < 32:
-            b = layer.bias.data
+        if lp.get("bias") is not None and bits_bias < 32:
+            b = lp["bias"].data
             items.append(SweepItem(src=b, dst=b, bits=bits_bias, per_channel=False, symmetric=False, rows=1))
             keys.append(None)
     if not items:
@@ -300,8 +301,8 @@ def _quantize_targ_layer_sharded(graph, bit_weight, bits_bias, targ_type, *, gra
                                  clip=tuple(clip) if clip is not None else None))
         srcs.append(w)
         keys.append(layer_idx)
-        if layer.bias is not None and bits_bias < 32:
-            b = layer.bias.data
+        if lp.get("bias") is not None and bits_bias < 32:
+            b = lp["bias"].data
             specs.append(D.LayerSpec(shape=tuple(b.shape), bits=bits_bias, per_channel=False, symmetric=False,
                                      want_codes=False))
             srcs.append(b)
