@@ -294,7 +294,8 @@ def _quantize_targ_layer_sharded(graph, bit_weight, bits_bias, targ_type, *, gra
         layer = graph[layer_idx]
         if type(layer) not in targ_type:
             continue
-        w = layer.weight.data
+        lp = layer._parameters
+        w = lp["weight"].data
         _lib.require_device(w)
         specs.append(D.LayerSpec(shape=tuple(w.shape), bits=bit_weight, per_channel=per_channel,
                                  symmetric=symmetric, want_codes=want, want_esum=want,
