@@ -16,6 +16,14 @@ import torch.nn as nn
 from . import _lib
 
 
+def _state(m, name):
+    """A module's registered buffer without Module.__getattr__ (else getattr)."""
+    b = getattr(m, "_buffers", None)
+    if b is not None and name in b:
+        return b[name]
+    return getattr(m, name)
+
+
 def _has_relu_between(layer_second, layer_first, graph, bottoms):
     """bias_absorption.py:10-18: any ReLU on the single-input path second -> first."""
     idx = layer_second
@@ -40,22 +48,27 @@ def bias_absorption(graph, relations, bottoms, N=3, visualize=False):
                 continue
             l1, l2, bn = graph[first], graph[second], graph[bn_idx]
             for layer in (l1, l2):
-                if layer.bias is None:
-                    layer.bias = nn.Parameter(torch.zeros(layer.weight.size(0), dtype=torch.float32,
-                                                          device=layer.weight.device), requires_grad=False)
+                lp = layer._parameters   # no Module.__getattr__ per access
+                if lp.get("bias") is None:
+                    w = lp["weight"]
+                    layer.bias = nn.Parameter(torch.zeros(w.size(0), dtype=torch.float32, device=w.device),
+                                              requires_grad=False)
             todo.append((l1, l2, bn))
         if not todo:
             print("Bias absorption done")
             return
         descs = (_lib.AbsorbDesc * len(todo))()
         for j, (l1, l2, bn) in enumerate(todo):
-            w2 = l2.weight.data
-            _lib.require_device(w2, l1.bias, l2.bias, bn.fake_weight, bn.fake_bias)
+            p1, p2 = l1._parameters, l2._parameters
+            w2, b1, b2 = p2["weight"], p1["bias"], p2["bias"]
+            fw, fb = _state(bn, "fake_weight"), _state(bn, "fake_bias")
+            _lib.require_device(w2, b1, b2, fw, fb)
+            s2 = w2.shape
             d = descs[j]
-            d.w2, d.b1, d.b2 = w2.data_ptr(), l1.bias.data.data_ptr(), l2.bias.data.data_ptr()
-            d.bn_w, d.bn_b = bn.fake_weight.data_ptr(), bn.fake_bias.data_ptr()
-            d.c1, d.o2, d.i2 = l1.weight.size(0), w2.shape[0], w2.shape[1]
-            d.khw2 = w2.numel() // (w2.shape[0] * w2.shape[1])
+            d.w2, d.b1, d.b2 = w2.data_ptr(), b1.data_ptr(), b2.data_ptr()
+            d.bn_w, d.bn_b = fw.data_ptr(), fb.data_ptr()
+            d.c1, d.o2, d.i2 = p1["weight"].size(0), s2[0], s2[1]
+            d.khw2 = w2.numel() // (s2[0] * s2[1])
         L = _lib.load()
         stream = _lib.stream_of(todo[0][1].weight)
         nb = int(L.dfq_bias_absorb_ws_bytes(descs, len(todo)))
