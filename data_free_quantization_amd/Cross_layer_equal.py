@@ -102,6 +102,12 @@ def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8
             _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps)
 
 
+_CLE_REL = np.dtype([("w1", "<u8"), ("w2", "<u8"), ("b1", "<u8"), ("bn_w", "<u8"), ("bn_b", "<u8"), ("s_acc", "<u8"),
+                     ("c1", "<i8"), ("len1", "<i8"), ("o2", "<i8"), ("i2", "<i8"), ("khw2", "<i8"),
+                     ("s_acc_init", "<i4"), ("reserved", "<i4")])
+assert _CLE_REL.itemsize == C.sizeof(_lib.CleRel)
+
+
 def _state(m, name):
     """A module's registered buffer ``name`` without Module.__getattr__ (any other
     object, or a plain attribute: getattr)."""
@@ -120,8 +126,8 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
     tl = tuple(Target_list)
     targets = [v._parameters["weight"] for v in graph.values() if type(v) in tl]
     n = len(relations)
-    descs = (_lib.CleRel * max(n, 1))()
-    for i, rel in enumerate(relations):
+    rows = []
+    for rel in relations:
         first, second, bn_idx = rel.get_idxs()
         l1, l2 = graph[first], graph[second]
         p1 = l1._parameters
@@ -136,15 +142,13 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
         if init:
             rel.S = torch.empty(W1.size(0), dtype=torch.float32, device=W1.device)
         s1, s2 = W1.shape, W2.shape
-        d = descs[i]
-        d.w1, d.w2, d.b1 = W1.data_ptr(), W2.data_ptr(), B1.data_ptr()
-        d.bn_w = bnw.data_ptr() if bnw is not None else None
-        d.bn_b = bnb.data_ptr() if bnb is not None else None
-        d.s_acc = rel.S.data_ptr()
-        d.c1, d.len1 = s1[0], W1.numel() // s1[0]
-        d.o2, d.i2 = s2[0], s2[1]
-        d.khw2 = W2.numel() // (s2[0] * s2[1])
-        d.s_acc_init = 1 if init else 0
+        rows.append((W1.data_ptr(), W2.data_ptr(), B1.data_ptr(), 0 if bnw is None else bnw.data_ptr(),
+                     0 if bnb is None else bnb.data_ptr(), rel.S.data_ptr(), s1[0], W1.numel() // s1[0], s2[0], s2[1],
+                     W2.numel() // (s2[0] * s2[1]), 1 if init else 0, 0))
+    # the descriptor table as a numpy record array (layout of _lib.CleRel), one row per
+    # relation from plain tuples instead of ctypes field by field
+    tab = np.array(rows if rows else [(0,) * 13], dtype=_CLE_REL)
+    descs = tab.ctypes.data_as(C.POINTER(_lib.CleRel))
     _lib.require_device(*targets)
     nt = len(targets)
     tp = (C.c_void_p * max(nt, 1))(*[t.data_ptr() for t in targets])
