@@ -7,6 +7,7 @@ stream and replays with no host work beyond one C call.
 from __future__ import annotations
 
 import ctypes as C
+import math
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -158,4 +159,5 @@ class SweepPlan:
 
 def khw_of(weight: torch.Tensor) -> int:
     """Spatial size KH*KW of a KCRS conv weight (1 for Linear)."""
-    return int(weight[0, 0].numel()) if weight.dim() >= 3 else 1
+    s = weight.shape   # from the shape: no view per call
+    return math.prod(s[2:]) if len(s) >= 3 else 1

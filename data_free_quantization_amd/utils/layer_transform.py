@@ -198,7 +198,7 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
         if type(layer) not in tt:
             continue
         lp = layer._parameters   # no Module.__getattr__ per access
-        w = lp["weight"].data
+        w = lp["weight"]   # written in place by the kernel: no .data view needed
         rows = w.size(0) if per_channel else 1
         npar = rows
         khw = khw_of(w)
@@ -208,7 +208,7 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
         items.append(it)
         keys.append(layer_idx)
         if lp.get("bias") is not None and bits_bias < 32:
-            b = lp["bias"].data
+            b = lp["bias"]
             items.append(SweepItem(src=b, dst=b, bits=bits_bias, per_channel=False, symmetric=False, rows=1))
             keys.append(None)
     if not items:

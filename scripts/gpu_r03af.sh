@@ -10,3 +10,5 @@ l=[x for x in open('gpurun_out/r03af/bench.log') if x.startswith('{')][-1]
 d=json.loads(l)
 print(json.dumps(d['pipeline_ms']))
 PY
+timeout -k 10 300 python -u scripts/pipeline_cprofile.py mobilenetv2 > $out/cprofile.log 2>&1 || { echo "cprofile rc=$?"; tail -20 $out/cprofile.log; exit 1; }
+head -3 $out/cprofile.log

@@ -16,6 +16,24 @@ from data_free_quantization_amd.pipeline import run_dfq  # noqa: E402
 from data_free_quantization_amd.utils.tracer import build_graph  # noqa: E402
 
 logging.getLogger("data_free_quantization_amd.bias_correction").setLevel(logging.ERROR)
+
+# cProfile does not see calls into ctypes functions (their time lands in the
+# caller's tottime): wrap every dfq_* entry point in a Python function of its own
+# name so the C side (planners, uploads, launches) shows up per entry point.
+from data_free_quantization_amd import _lib  # noqa: E402
+
+_L = _lib.load()
+for _name in [n for n in dir(_L) if n.startswith("dfq_")] + [
+        n for n in ("dfq_bn_fold_batch", "dfq_bn_fold_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run",
+                    "dfq_cle_plan_destroy", "dfq_sweep_plan_create_ws", "dfq_sweep_plan_ws_bytes",
+                    "dfq_sweep_plan_execute", "dfq_sweep_plan_destroy", "dfq_sweep_plan_stats", "dfq_bc_chain",
+                    "dfq_bias_absorb_batch", "dfq_cle_plan_ws_bytes", "dfq_cle_plan_info")]:
+    _f = getattr(_L, _name, None)
+    if _f is None or not hasattr(_f, "argtypes"):
+        continue
+    _ns = {"f": _f}
+    exec(f"def {_name}(*a):\n    return f(*a)\n", _ns)
+    setattr(_L, _name, _ns[_name])
 name = sys.argv[1] if len(sys.argv) > 1 else "mobilenetv2"
 for rep in range(2):
     m = zoo.build(name, seed=0, relu=True).cuda()
@@ -31,7 +49,11 @@ for rep in range(2):
         pr.disable()
     print(rep, {k: round(v * 1e3, 3) for k, v in t.items()})
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(30)
-print("---- callees of _fold_batch / merge_batchnorm")
-st.sort_stats("cumulative").print_callees("_fold_batch")
-st.print_callees("merge_batchnorm")
+rows = []
+for (fn, ln, name), (cc, nc, tt, ct, _) in st.stats.items():
+    rows.append((tt, ct, nc, f"{Path(fn).name}:{ln}({name})"))
+print(f"total profiled {sum(r[0] for r in rows) * 1e3:.3f} ms")
+for key, title in ((0, "tottime"), (1, "cumtime")):
+    print(f"---- top by {title} (us): tottime cumtime ncalls function")
+    for r in sorted(rows, key=lambda r: -r[key])[:45]:
+        print(f"{r[0] * 1e6:9.1f} {r[1] * 1e6:9.1f} {r[2]:6d} {r[3]}")
