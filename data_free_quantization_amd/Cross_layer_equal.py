@@ -9,6 +9,8 @@ the reference.
 """
 from __future__ import annotations
 
+import atexit
+from collections.abc import MutableMapping
 import ctypes as C
 import os
 import time
@@ -20,8 +22,50 @@ import torch.nn as nn
 
 from . import _lib
 
+class _LastRun(MutableMapping):
+    """LAST_RUN: a dict whose reads first wait for a launched (asynchronous) loop."""
+
+    def __init__(self):
+        self._d = {}
+
+    def __getitem__(self, k):
+        wait()
+        return self._d[k]
+
+    def __setitem__(self, k, v):
+        self._d[k] = v
+
+    def __delitem__(self, k):
+        del self._d[k]
+
+    def __iter__(self):
+        wait()
+        return iter(self._d)
+
+    def __len__(self):
+        wait()
+        return len(self._d)
+
+    def clear(self):
+        self._d.clear()
+
+    def update(self, *a, **k):
+        self._d.update(*a, **k)
+
+    def __repr__(self):
+        wait()
+        return repr(self._d)
+
+
 #: statistics of the last cross_layer_equalization call (extension, for tests/bench)
-LAST_RUN = {}
+LAST_RUN = _LastRun()
+
+#: Run the device loop asynchronously (dfq_cle_plan_launch): the call returns once
+#: the loop is under way, and whatever the caller enqueues on the current stream
+#: afterwards waits for it in the device -- the next stages' host work overlaps the
+#: loop.  ``wait()`` (or reading LAST_RUN) joins it; False: the blocking run.
+ASYNC = True
+_PENDING = None   # (plan, workspace, host times) of the launched loop
 
 
 def _layer_equalization(W1, W2, B1, Batnorm_weight=None, Batnorm_bias=None, s_min_max=(1e-8, 1e8), signed=False,
@@ -95,6 +139,7 @@ def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8
     if Save_state:
         warnings.warn("Save_state plots (ourplots.save_layer) are visualization, not part of the weight path; "
                       "skipped")
+    wait()   # a launched loop before this one (one at a time)
     with torch.no_grad():
         if os.environ.get("DFQ_CLE_MODE", "device") == "host":
             _cle_host_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps)
@@ -181,10 +226,63 @@ def _run_plan(plan, dev, Treshhold, Count):
     return iters.value, [hist[i] for i in range(iters.value)], (chains.value, steps.value, launches.value)
 
 
+def wait():
+    """Wait for the launched CLE loop, if any: fills LAST_RUN and raises the loop's
+    error (a HIP failure in the worker).  Called by every LAST_RUN read, by the
+    next cross_layer_equalization, by run_dfq / main_dfq at their end and at exit."""
+    global _PENDING
+    pend = _PENDING
+    if pend is None:
+        return
+    _PENDING = None
+    plan, ws, host = pend
+    L = _lib.load()
+    iters = C.c_int32(0)
+    hist = _hist_buffer()
+    t0 = time.perf_counter()
+    try:
+        _lib.check(L.dfq_cle_plan_join(plan, C.byref(iters), hist), "cross_layer_equalization (device loop)")
+        chains, steps, launches = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        L.dfq_cle_plan_info(plan, C.byref(chains), C.byref(steps), C.byref(launches))
+    finally:
+        L.dfq_cle_plan_destroy(plan)
+        del ws
+    n = iters.value
+    if n >= MAX_ITERS:
+        warnings.warn(f"cross_layer_equalization stopped at DFQ_CLE_MAX_ITERS={MAX_ITERS} iterations")
+    LAST_RUN.clear()
+    LAST_RUN.update(iterations=n, diffs=[hist[i] for i in range(n)], chains=chains.value, steps=steps.value,
+                    launches_per_iteration=launches.value, mode="device", launched=True,
+                    host_ms=dict(host, wait=(time.perf_counter() - t0) * 1e3))
+
+
+def _at_exit():
+    try:
+        wait()
+    except Exception as e:   # noqa: BLE001 -- report, the interpreter is going down
+        warnings.warn(f"cross_layer_equalization: {e}")
+
+
+atexit.register(_at_exit)
+
+
 def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps):
+    global _PENDING
+    wait()   # one launched loop at a time
     t0 = time.perf_counter()
     plan, ws, dev = _create_plan(graph, relations, Target_list, s_min_max, signed, eps)
     t2 = time.perf_counter()
+    if ASYNC:
+        L = _lib.load()
+        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        rc = L.dfq_cle_plan_launch(plan, float(Treshhold), int(Count), MAX_ITERS, stream)
+        if rc == _lib.DFQ_OK:
+            _PENDING = (plan, ws, {"create": (t2 - t0) * 1e3, "launch": (time.perf_counter() - t2) * 1e3})
+            LAST_RUN.clear()
+            return
+        if rc != _lib.DFQ_ERR_UNSUPPORTED:   # else: the device cannot wait on a value -- blocking run
+            L.dfq_cle_plan_destroy(plan)
+            _lib.check(rc, "dfq_cle_plan_launch")
     try:
         iters, diffs, (chains, steps, launches) = _run_plan(plan, dev, Treshhold, Count)
     finally:
@@ -195,7 +293,7 @@ def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count,
         warnings.warn(f"cross_layer_equalization stopped at DFQ_CLE_MAX_ITERS={MAX_ITERS} iterations")
     LAST_RUN.clear()
     LAST_RUN.update(iterations=iters, diffs=diffs, chains=chains, steps=steps, launches_per_iteration=launches,
-                    mode="device", host_ms={"create": (t2 - t0) * 1e3, "run": (t3 - t2) * 1e3,
+                    mode="device", launched=False, host_ms={"create": (t2 - t0) * 1e3, "run": (t3 - t2) * 1e3,
                                             "destroy": (t4 - t3) * 1e3})
 
 

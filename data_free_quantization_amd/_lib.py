@@ -30,7 +30,8 @@ EXPORTS = [
     "dfq_bn_fold", "dfq_bn_fold_ws_bytes", "dfq_bn_fold_batch", "dfq_clamp", "dfq_clamp_batch",
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
-    "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_info", "dfq_cle_plan_destroy",
+    "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_launch", "dfq_cle_plan_join",
+    "dfq_cle_plan_info", "dfq_cle_plan_destroy",
     "dfq_bias_absorb", "dfq_bias_absorb_ws_bytes", "dfq_bias_absorb_batch", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate", "dfq_bc_chain",
     "dfq_act_moments", "dfq_act_minmax", "dfq_act_affine",
 ]
@@ -149,6 +150,8 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_cle_plan_create": ([C.POINTER(CleRel), I32, C.POINTER(P), C.POINTER(I64), I32, F64, F64, I32, F32, I32,
                                  P, I64, C.POINTER(P)], C.c_int),
         "dfq_cle_plan_run": ([P, F64, I32, I32, C.POINTER(I32), C.POINTER(F64), P], C.c_int),
+        "dfq_cle_plan_launch": ([P, F64, I32, I32, P], C.c_int),
+        "dfq_cle_plan_join": ([P, C.POINTER(I32), C.POINTER(F64)], C.c_int),
         "dfq_cle_plan_info": ([P, C.POINTER(I32), C.POINTER(I32), C.POINTER(I32)], C.c_int),
         "dfq_cle_plan_destroy": ([P], C.c_int),
         "dfq_bias_absorb": ([P, P, P, P, P, I64, I64, I64, I64, F32, P], C.c_int),

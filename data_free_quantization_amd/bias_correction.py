@@ -160,14 +160,22 @@ def _quantize_error(param, num_bits=8, reduction="none", signed=False):
 
 
 def _error_sums(weight, bits, signed, precomputed=None):
-    """E [O, I] = sum over KH*KW of the per-tensor quantization error."""
-    o, i2 = weight.size(0), weight.size(1)
-    khw = weight.numel() // (o * i2)
+    """E [O, I] = sum over KH*KW of the per-tensor quantization error, as a chain
+    ref (tensor, float offset).  ``precomputed``: E as a tensor, or as a
+    (buffer, float offset, numel) ref (layer_transform.esum_source: no view)."""
+    sh = weight.shape
+    o, i2 = sh[0], sh[1]
     if precomputed is not None:
-        return precomputed.view(o, i2), o, i2
+        if isinstance(precomputed, torch.Tensor):
+            return (precomputed.view(o * i2), 0), o, i2   # the reference's .view errors on a wrong size
+        t, off, n = precomputed
+        if n != o * i2:
+            raise RuntimeError(f"shape '[{o}, {i2}]' is invalid for input of size {n}")
+        return (t, off), o, i2
+    khw = weight.numel() // (o * i2)
     r = fake_quant(weight.detach().contiguous(), bits, symmetric=signed, want_codes=False, khw=khw,
                    want_esum=True)
-    return r.esum.view(o, i2), o, i2
+    return (r.esum, 0), o, i2
 
 
 class _Snapshot(Mapping):
@@ -277,10 +285,9 @@ class _BcChain:
                          b.numel(), 0, 0))
 
     def apply(self, E, o, i2, expect, f, bias, vec):
-        # vec: a scratch slot only this chain's propagate reads
-        self.keep += [E, bias]
-        self.ops.append((_lib.DFQ_BC_OP_APPLY, _lib.DFQ_BC_APPLY_VEC_SCRATCH, (E, 0), expect, (bias, 0), vec, o,
-                         i2, f))
+        # E: a ref (tensor, float offset); vec: a scratch slot only this chain's propagate reads
+        self.keep += [E[0], bias]
+        self.ops.append((_lib.DFQ_BC_OP_APPLY, _lib.DFQ_BC_APPLY_VEC_SCRATCH, E, expect, (bias, 0), vec, o, i2, f))
 
     def propagate(self, vec, numel, fake_b, f):
         _lib.require_device(fake_b)
@@ -348,9 +355,9 @@ def _record_apply(chain, layer, E, o, i2, connect_type, expect, f):
         logger.error("Error in applying bias correction: Bias correction shape mismatch that cannot be handled "
                      "automatically.")
         raise ValueError("Bias correction shape mismatch that cannot be handled automatically.")
-    _lib.require_device(E, bias)
+    _lib.require_device(E[0], bias)
     vec = chain.alloc(o * bcols)
-    chain.apply(E.reshape(-1), o, i2, expect, f, bias.data, vec)
+    chain.apply(E, o, i2, expect, f, bias, vec)
     return vec, o * bcols
 
 
@@ -381,7 +388,7 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
             if i in bottoms and isinstance(l, targ_type):
                 b = _param(l, "bias")
                 if b is not None:
-                    biases[f"layer_{i}"] = b.data
+                    biases[f"layer_{i}"] = b   # read through data_ptr only (no .data view)
         chain = _BcChain(next(iter(biases.values())).device if biases else torch.device("cuda"))
         before = _snapshot(chain, biases)
         stream = None
@@ -415,10 +422,10 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                 if isinstance(node, targ_type):
                     bn_list, relu_list, type_list, _ = find_prev_bn(bn_module, relu_attached, graph, bottoms, bot[:])
                     pre = None if error_sums is None else error_sums.get(keys[idx_layer])
-                    E, o, i2 = _error_sums(_param(node, "weight").data, bits_weight, signed, pre)
+                    E, o, i2 = _error_sums(_param(node, "weight"), bits_weight, signed, pre)
                     if stream is None:
-                        stream = _lib.stream_of(E)
-                        chain.dev = E.device
+                        stream = _lib.stream_of(E[0])
+                        chain.dev = E[0].device
                     branches = {}
                     for j, (bn_layer, bid) in enumerate(bn_list):
                         branches.setdefault(bid[0], []).append((bn_layer, relu_list[j], type_list[j]))
@@ -433,7 +440,7 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                     bias_prev = bias
                     b = _param(layer, "bias")
                     if b is not None:
-                        after_src[layer_name] = b.data
+                        after_src[layer_name] = b
                     if len(chain.ops) >= _FLUSH_OPS:   # the device starts on what is recorded so far
                         chain.flush(stream)
             after = _snapshot(chain, after_src)

@@ -20,7 +20,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
+#include <thread>
 #include <new>
 #include <numeric>
 #include <vector>
@@ -2217,6 +2220,7 @@ struct dfq_cle_plan {
     bool fork = false;              // ranges on a concurrent graph branch (diagnostics DFQ_CLE_FORK=1)
     int64_t ri0 = 0, ri1 = 0;       // fused: each iteration's range tasks (the rest come from the rescales)
     int dev = 0;
+    struct CleAsync* async = nullptr;   // dfq_cle_plan_launch's worker and result
 #ifdef DFQ_DIAGNOSTICS
     std::vector<CleRel> h_rels;
     std::vector<CleTask> h_atasks;
@@ -2267,6 +2271,14 @@ struct CleDeviceCtx {
     // it instead of capturing and instantiating its own (~100 us).
     hipGraphExec_t gexec = nullptr;
     std::vector<char> gkey;
+    // asynchronous runs (dfq_cle_plan_launch): the signal word callers' streams
+    // wait on, its last generation, the launched plan not yet joined
+    void* sig = nullptr;
+    int sig_state = 0;                             // -1: the device cannot wait on a value
+    uint64_t gen = 0;
+    struct dfq_cle_plan* pending = nullptr;
+    hipEvent_t in_ev = nullptr;                    // the caller's producers, for the loop stream
+    struct CleWorker* worker = nullptr;            // drives launched runs
 };
 static CleDeviceCtx& cle_device_ctx(int dev) {
     static CleDeviceCtx ctx[64];
@@ -2276,14 +2288,22 @@ static CleDeviceCtx& cle_device_ctx(int dev) {
 // stream can take milliseconds the first time, so dfq_preload does it up front.
 static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
     hipError_t e = hipSuccess;
-    if (!ctx.st) e = hipStreamCreateWithFlags(&ctx.st, hipStreamNonBlocking);
+    if (!ctx.st) {   // high priority: a hardware queue of its own (see dfq_cle_plan_launch)
+        int least = 0, greatest = 0;
+        e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (ab_env("DFQ_CLE_PRIO_NORMAL")) greatest = 0;   // diagnostics A/B: a normal-priority loop stream
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx.st, hipStreamNonBlocking, greatest);
+    }
     if (e == hipSuccess && !ctx.h_state) e = hipHostMalloc(&ctx.h_state, 3 * sizeof(CleState));
     for (int i = 0; i < 2 && e == hipSuccess; ++i)
         if (!ctx.ev[i]) e = hipEventCreateWithFlags(&ctx.ev[i], hipEventDisableTiming);
+#ifdef DFQ_DIAGNOSTICS   // the range launch's graph branch (DFQ_CLE_FORK A/B only)
     if (e == hipSuccess && !ctx.side) e = hipStreamCreateWithFlags(&ctx.side, hipStreamNonBlocking);
+#endif
     for (int i = 0; i < 2 && e == hipSuccess; ++i)
         if (!ctx.fork[i]) e = hipEventCreateWithFlags(&ctx.fork[i], hipEventDisableTiming);
     if (e == hipSuccess && !ctx.pool_ev) e = hipEventCreateWithFlags(&ctx.pool_ev, hipEventDisableTiming);
+    if (e == hipSuccess && !ctx.in_ev) e = hipEventCreateWithFlags(&ctx.in_ev, hipEventDisableTiming);
     return e;
 }
 
@@ -3016,34 +3036,40 @@ static int32_t cle_persist_grid(dfq_cle_plan* p) {
 #endif
 }
 
-extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count, int32_t max_iters,
-                                int32_t* iterations, double* diffs, void* stream) {
-    if (!p || max_iters < 0) return DFQ_ERR_INVALID;
-    // The loop runs on the plan's own stream (graph capture needs a non-default
-    // stream): wait for the caller's producers first; the call is blocking.
-    const double ts0 = now_us();
-    DFQ_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-    const double ts1 = now_us();
-    int dev = 0;
-    DFQ_HIP_CHECK(hipGetDevice(&dev));
-    CleDeviceCtx& ctx = cle_device_ctx(dev);
-    std::lock_guard<std::mutex> lock(ctx.mu);
+// The context's history buffer for caps above the tables' kCleHistCap slots,
+// grown once (a launched run grows it before its caller's stream waits: hipFree
+// synchronises the whole device).
+static hipError_t cle_hist_ready(CleDeviceCtx& ctx, int32_t max_iters) {
+    if (max_iters + 1 <= kCleHistCap || ctx.hist_cap >= max_iters + 1) return hipSuccess;
+    (void)hipFree(ctx.d_hist);
+    ctx.d_hist = nullptr;
+    ctx.hist_cap = 0;
+    const hipError_t e = hipMalloc(&ctx.d_hist, sizeof(double) * (max_iters + 1));
+    if (e == hipSuccess) ctx.hist_cap = max_iters + 1;
+    return e;
+}
+
+// Device -> host copy ordered on the loop stream.  Never a blocking hipMemcpy
+// here: that runs on the null stream, which the caller of a launched run may be
+// holding behind its wait for this very loop (dfq_cle_plan_launch).
+static hipError_t cle_copy_back(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+    return e == hipSuccess ? hipStreamSynchronize(s) : e;
+}
+
+// The loop on the device context's stream; the caller holds ctx.mu and has
+// ordered the plan's producers before that stream.  iterations / hist: the run's
+// result (hist resized to the iterations run).
+static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, int32_t count, int32_t max_iters,
+                          int32_t* iterations, std::vector<double>* hist) {
     DFQ_HIP_CHECK(cle_ctx_ready(ctx));
-    if (cle_timing()) fprintf(stderr, "DFQ_CLE_TIMING run: caller sync %.1f us, context %.1f us\n", ts1 - ts0,
-                              now_us() - ts1);
     p->st = ctx.st;
     p->h_state = ctx.h_state;
     hipStream_t s = p->st;
     // the history: the tables' slots, or the context's buffer (grown once) for longer caps
     p->d_hist = p->d_hist_tables;
     if (max_iters + 1 > kCleHistCap) {
-        if (ctx.hist_cap < max_iters + 1) {
-            (void)hipFree(ctx.d_hist);
-            ctx.d_hist = nullptr;
-            ctx.hist_cap = 0;
-            DFQ_HIP_CHECK(hipMalloc(&ctx.d_hist, sizeof(double) * (max_iters + 1)));
-            ctx.hist_cap = max_iters + 1;
-        }
+        DFQ_HIP_CHECK(cle_hist_ready(ctx, max_iters));
         p->d_hist = ctx.d_hist;
     }
     CleState init{};
@@ -3111,8 +3137,11 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
             fprintf(stderr, "DFQ_CLE_TIMING run: persistent grid %d, loop %.1f us (%d iterations)\n",
                     p->persist_grid, now_us() - tl0, init.iters);
         if (iterations) *iterations = init.iters;
-        if (diffs && init.iters > 0)
-            DFQ_HIP_CHECK(hipMemcpy(diffs, p->d_hist, sizeof(double) * init.iters, hipMemcpyDeviceToHost));
+        if (hist) {
+            hist->assign((size_t)std::max(init.iters, 0), 0.0);
+            if (init.iters > 0)
+                DFQ_HIP_CHECK(cle_copy_back(hist->data(), p->d_hist, sizeof(double) * init.iters, s));
+        }
         return DFQ_OK;
     }
 #endif
@@ -3202,9 +3231,10 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
 #ifdef DFQ_DIAGNOSTICS
     if (d_tl) {   // per step: span, task durations, the slowest tasks
         std::vector<uint64_t> tl(4 * (size_t)n_at);
-        DFQ_HIP_CHECK(hipMemcpy(tl.data(), d_tl, sizeof(uint64_t) * tl.size(), hipMemcpyDeviceToHost));
+        DFQ_HIP_CHECK(cle_copy_back(tl.data(), d_tl, sizeof(uint64_t) * tl.size(), s));
         uint64_t* null_tl = nullptr;
-        DFQ_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_cle_tl), &null_tl, sizeof(null_tl)));
+        DFQ_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cle_tl), &null_tl, sizeof(null_tl), 0, hipMemcpyHostToDevice, s));
+        DFQ_HIP_CHECK(hipStreamSynchronize(s));
         (void)hipFree(d_tl);
         for (int32_t k = 0; k < p->steps; ++k) {
             const int64_t a0 = p->astep[k], a1 = p->astep[k + 1];
@@ -3261,7 +3291,7 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     }
     if (ab_env("DFQ_CLE_DEBUG")) {   // per-layer chunk sums of the last iteration run
         std::vector<float> part((size_t)p->slots * std::max(p->nl, 1));
-        DFQ_HIP_CHECK(hipMemcpy(part.data(), p->d_part, sizeof(float) * part.size(), hipMemcpyDeviceToHost));
+        DFQ_HIP_CHECK(cle_copy_back(part.data(), p->d_part, sizeof(float) * part.size(), s));
         for (int32_t l = 0; l < p->nl; ++l) {
             fprintf(stderr, "DFQ_CLE_DEBUG layer %d:", l);
             for (int t = 0; t < p->slots; ++t) fprintf(stderr, " %.9g", part[(size_t)p->slots * l + t]);
@@ -3269,8 +3299,209 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
         }
     }
     if (iterations) *iterations = fin.iters;
-    if (diffs && fin.iters > 0)
-        DFQ_HIP_CHECK(hipMemcpy(diffs, p->d_hist, sizeof(double) * fin.iters, hipMemcpyDeviceToHost));
+    if (hist) {
+        hist->assign((size_t)std::max(fin.iters, 0), 0.0);
+        if (fin.iters > 0)
+            DFQ_HIP_CHECK(cle_copy_back(hist->data(), p->d_hist, sizeof(double) * fin.iters, s));
+    }
+    return DFQ_OK;
+}
+
+extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count, int32_t max_iters,
+                                int32_t* iterations, double* diffs, void* stream) {
+    if (!p || max_iters < 0 || p->async) return DFQ_ERR_INVALID;   // a launched plan is joined instead
+    // The loop runs on the device context's stream: wait for the caller's
+    // producers first; the call is blocking.
+    const double ts0 = now_us();
+    DFQ_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    const double ts1 = now_us();
+    int dev = 0;
+    DFQ_HIP_CHECK(hipGetDevice(&dev));
+    CleDeviceCtx& ctx = cle_device_ctx(dev);
+    std::lock_guard<std::mutex> lock(ctx.mu);
+    if (cle_timing()) fprintf(stderr, "DFQ_CLE_TIMING run: caller sync %.1f us, context %.1f us\n", ts1 - ts0,
+                              now_us() - ts1);
+    std::vector<double> h;
+    const int rc = cle_run_locked(p, ctx, threshold, count, max_iters, iterations, diffs ? &h : nullptr);
+    if (rc == DFQ_OK && diffs && !h.empty()) std::memcpy(diffs, h.data(), sizeof(double) * h.size());
+    return rc;
+}
+
+// ---- asynchronous run (dfq_cle_plan_launch / _join) -------------------------
+// The loop needs the host between batches (the stop rule is read back), so a
+// worker thread drives it on the context's stream while the caller's thread goes
+// on enqueueing the next stages on its own stream.  That stream waits, in the
+// device's command processor, for a per-device signal word the worker writes
+// behind the loop's last launch (hipStreamWaitValue64 / hipStreamWriteValue64):
+// no host sync between the stages, and nothing of the caller's stream runs
+// before the loop is done.  The loop stream is a high-priority stream: it gets a
+// hardware queue of its own (queues are pooled per priority), so the caller's
+// waiting queue can never hold the loop's launches back.
+struct CleAsync {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false;
+    int rc = DFQ_OK;
+    int32_t iters = 0;
+    std::vector<double> hist;
+    char err[128] = {0};
+};
+
+// One long-lived worker thread per device context: a thread created per run paid
+// the HIP runtime's per-thread setup on every run.  Detached, never destroyed (a
+// process ends with it idle: wait() / destroy join every launched run first).
+struct CleWorker {
+    std::mutex m;
+    std::condition_variable cv;
+    std::function<void()> job;
+    bool has_job = false;
+};
+static void cle_worker_loop(CleWorker* w) {
+    for (;;) {
+        std::function<void()> j;
+        {
+            std::unique_lock<std::mutex> l(w->m);
+            w->cv.wait(l, [w] { return w->has_job; });
+            j = std::move(w->job);
+            w->has_job = false;
+        }
+        j();
+    }
+}
+
+// The context's signal word (lazily allocated as HIP signal memory); 0 when the
+// device cannot make a stream wait on a value (callers then run synchronously).
+static hipError_t cle_signal_ready(CleDeviceCtx& ctx, int dev) {
+    if (ctx.sig) return hipSuccess;
+    if (ctx.sig_state < 0) return hipErrorNotSupported;
+    int ok = 0;
+    hipError_t e = hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev);
+    if (e != hipSuccess || !ok) {
+        ctx.sig_state = -1;
+        return e != hipSuccess ? e : hipErrorNotSupported;
+    }
+    void* sig = nullptr;
+    if ((e = hipExtMallocWithFlags(&sig, sizeof(uint64_t), hipMallocSignalMemory)) != hipSuccess) {
+        ctx.sig_state = -1;
+        return e;
+    }
+    // generation 0, in stream order on the loop stream
+    if ((e = hipStreamWriteValue64(ctx.st, sig, 0, 0)) != hipSuccess || (e = hipStreamSynchronize(ctx.st)) != hipSuccess) {
+        (void)hipFree(sig);
+        ctx.sig_state = -1;
+        return e;
+    }
+    ctx.sig = sig;
+    ctx.gen = 0;
+    return hipSuccess;
+}
+
+static void cle_async_join(dfq_cle_plan* p) {
+    if (!p || !p->async) return;
+    CleAsync* a = p->async;
+    std::unique_lock<std::mutex> l(a->m);
+    a->cv.wait(l, [a] { return a->done; });
+}
+
+extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t count, int32_t max_iters,
+                                   void* stream) {
+    if (!p || max_iters < 0 || p->async) return DFQ_ERR_INVALID;
+    // Diagnostics A/B paths that allocate, free, capture or instantiate inside the
+    // loop (graph replay, the task timeline, the persistent loop) may synchronise
+    // the whole device -- behind a caller's stream that waits for the loop: they
+    // take the blocking run (the product library reads no switches).
+    {
+        const char* g = ab_env("DFQ_CLE_GRAPH");
+        if ((g && g[0] == '1') || ab_env("DFQ_CLE_TL") || ab_env("DFQ_CLE_PERSIST_BPC")) return DFQ_ERR_UNSUPPORTED;
+    }
+    hipStream_t caller = static_cast<hipStream_t>(stream);
+    CleDeviceCtx& ctx = cle_device_ctx(p->dev);
+    // one launched loop per device at a time: the signal's generations then
+    // complete in launch order
+    if (ctx.pending && ctx.pending != p) cle_async_join(ctx.pending);
+    ctx.pending = nullptr;
+    uint64_t gen = 0;
+    {
+        std::lock_guard<std::mutex> lock(ctx.mu);
+        DFQ_HIP_CHECK(hipSetDevice(p->dev));
+        DFQ_HIP_CHECK(cle_ctx_ready(ctx));
+        const hipError_t es = cle_signal_ready(ctx, p->dev);
+        if (es == hipErrorNotSupported) return DFQ_ERR_UNSUPPORTED;
+        DFQ_HIP_CHECK(es);
+        DFQ_HIP_CHECK(cle_hist_ready(ctx, max_iters));   // no hipFree in the worker
+        // the caller's producers before the loop; the caller's later work after it
+        DFQ_HIP_CHECK(hipEventRecord(ctx.in_ev, caller));
+        DFQ_HIP_CHECK(hipStreamWaitEvent(ctx.st, ctx.in_ev, 0));
+        gen = ctx.gen + 1;
+        DFQ_HIP_CHECK(hipStreamWaitValue64(caller, ctx.sig, gen, hipStreamWaitValueGte, ~0ull));
+        ctx.gen = gen;
+    }
+    // from here on the caller's stream is held until the signal reaches gen: every
+    // path below writes it
+    CleAsync* a = new (std::nothrow) CleAsync();
+    auto body = [p, &ctx, threshold, count, max_iters, gen](CleAsync* a) {
+        std::lock_guard<std::mutex> lock(ctx.mu);
+        int rc = DFQ_OK;
+        if (hipSetDevice(p->dev) != hipSuccess) {
+            rc = DFQ_ERR_HIP;
+        } else {
+            rc = cle_run_locked(p, ctx, threshold, count, max_iters, &a->iters, &a->hist);
+        }
+        if (rc == DFQ_ERR_HIP) {
+            const char* m = dfq_last_hip_error();
+            for (size_t i = 0; m && m[i] && i + 1 < sizeof(a->err); ++i) a->err[i] = m[i];
+        }
+        // release the caller's stream behind everything the loop enqueued
+        hipError_t e = hipStreamWriteValue64(ctx.st, ctx.sig, gen, 0);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx.st);
+        if (e != hipSuccess) {   // never expected; the caller's stream would wait forever
+            fprintf(stderr, "dfq_cle_plan_launch: releasing the caller's stream failed (%s)\n", hipGetErrorString(e));
+            if (rc == DFQ_OK) rc = DFQ_ERR_HIP;
+        }
+        {
+            std::lock_guard<std::mutex> l(a->m);
+            a->rc = rc;
+            a->done = true;
+        }
+        a->cv.notify_all();   // a is the joiner's from here on
+    };
+    if (!a) {   // no memory for the worker's record: run here, then release
+        CleAsync tmp;
+        body(&tmp);
+        return tmp.rc;
+    }
+    p->async = a;
+    ctx.pending = p;
+    bool posted = false;
+    try {
+        if (!ctx.worker) {
+            CleWorker* w = new CleWorker();
+            std::thread(cle_worker_loop, w).detach();
+            ctx.worker = w;
+        }
+        {
+            std::lock_guard<std::mutex> l(ctx.worker->m);
+            ctx.worker->job = [body, a] { body(a); };
+            ctx.worker->has_job = true;
+        }
+        ctx.worker->cv.notify_one();
+        posted = true;
+    } catch (...) {
+    }
+    if (!posted) body(a);   // no worker: run on this thread (blocking), which also releases
+    return DFQ_OK;
+}
+
+extern "C" int dfq_cle_plan_join(dfq_cle_plan* p, int32_t* iterations, double* diffs) {
+    if (!p || !p->async) return DFQ_ERR_INVALID;
+    cle_async_join(p);
+    CleDeviceCtx& ctx = cle_device_ctx(p->dev);
+    if (ctx.pending == p) ctx.pending = nullptr;
+    const CleAsync& a = *p->async;
+    if (a.rc == DFQ_ERR_HIP && a.err[0]) set_last_hip_error_text(a.err);
+    if (a.rc != DFQ_OK) return a.rc;
+    if (iterations) *iterations = a.iters;
+    if (diffs && !a.hist.empty()) std::memcpy(diffs, a.hist.data(), sizeof(double) * a.hist.size());
     return DFQ_OK;
 }
 
@@ -3293,6 +3524,13 @@ extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t
 
 extern "C" int dfq_cle_plan_destroy(dfq_cle_plan* p) {
     if (!p) return DFQ_OK;
+    if (p->async) {   // a launched run finishes first (its worker uses the plan)
+        cle_async_join(p);
+        CleDeviceCtx& ctx = cle_device_ctx(p->dev);
+        if (ctx.pending == p) ctx.pending = nullptr;
+        delete p->async;
+        p->async = nullptr;
+    }
     cle_plan_free(p);
     return DFQ_OK;
 }

@@ -437,6 +437,7 @@ __host__ __device__ inline float aten_outer_col_sum(const float* a, int64_t R, i
 // Host-side error plumbing shared by the translation units.
 namespace dfq {
 void set_last_hip_error(hipError_t e);
+void set_last_hip_error_text(const char* msg);
 // Stream-ordered host -> device upload of a host-built table (task lists, fold
 // jobs): `bytes` are copied into a pinned staging slot at once, the DMA is
 // enqueued on `s`, and the slot is reused only after an event recorded behind

@@ -15,6 +15,13 @@ void set_last_hip_error(hipError_t e) {
     for (; msg && msg[i] && i + 1 < sizeof(g_last_hip); ++i) g_last_hip[i] = msg[i];
     g_last_hip[i] = '\0';
 }
+// the calling thread's last HIP error text (a worker thread's error, reported by
+// the thread that joins it)
+void set_last_hip_error_text(const char* msg) {
+    size_t i = 0;
+    for (; msg && msg[i] && i + 1 < sizeof(g_last_hip); ++i) g_last_hip[i] = msg[i];
+    g_last_hip[i] = '\0';
+}
 
 // Pinned staging slots for stage_h2d, per device (an event belongs to the device
 // it was created on).  A slot is free once the event recorded behind its last DMA

@@ -34,9 +34,9 @@ from . import _lib, zoo
 from .bias_absorption import bias_absorption
 from .bias_correction import bias_correction
 from .clip_weight import clip_weight
-from .Cross_layer_equal import cross_layer_equalization
-from .utils.layer_transform import (merge_batchnorm, quantize_targ_layer, replace_op, restore_op, set_quant_minmax,
-                                    switch_layers)
+from .Cross_layer_equal import cross_layer_equalization, wait as cle_wait
+from .utils.layer_transform import (esum_source, merge_batchnorm, quantize_targ_layer, replace_op, restore_op,
+                                    set_quant_minmax, switch_layers)
 from .utils.quantize import QuantConv2d, QuantLinear, QuantMeasure, set_layer_bits
 from .utils.relation import create_relation
 from .utils.tracer import TorchTransformer
@@ -201,9 +201,10 @@ def main(argv=None):
     if args.correction:
         # main_dfq.py:231 passes visualize= to a signature without it (TypeError in the
         # reference); this driver calls the documented signature.
-        err = {k: v["esum"] for k, v in state.items()} if (state and args.bc_mode == "fused") else None
+        err = {k: esum_source(v) for k, v in state.items()} if (state and args.bc_mode == "fused") else None
         bias_correction(graph, bottoms, targ_layer, bits_weight=args.bits_weight, signed=args.symmetric,
                         error_sums=err)
+    cle_wait()   # the launched CLE loop's error, if any, surfaces here
     torch.cuda.synchronize()
     print(f"DFQ weight transforms took {time.perf_counter() - t0:.3f} s on {args.device}")
     if args.export and args.quantize and state and rank == 0:

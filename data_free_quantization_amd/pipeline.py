@@ -24,7 +24,7 @@ from . import Cross_layer_equal as cle
 from .bias_absorption import bias_absorption
 from .bias_correction import bias_correction
 from .clip_weight import clip_weight
-from .utils.layer_transform import merge_batchnorm, quantize_targ_layer
+from .utils.layer_transform import esum_source, merge_batchnorm, quantize_targ_layer
 from .utils.quantize import set_layer_bits
 from .utils.relation import create_relation
 
@@ -39,13 +39,16 @@ def run_dfq(model: nn.Module, graph, bottoms, targ, *, relu: bool = True, equali
     assert relu or relu == equalize, "must replace relu6 to relu while equalization"
     assert equalize or absorption == equalize, "must use absorption with equalize"
     t = timings if timings is not None else {}
+    timed = timings is not None   # per-stage times need a device sync around each stage
 
     def stage(name, fn, *a, **k):
-        torch.cuda.synchronize()
+        if timed:
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         out = fn(*a, **k)
-        torch.cuda.synchronize()
-        t[name] = time.perf_counter() - t0
+        if timed:
+            torch.cuda.synchronize()
+            t[name] = time.perf_counter() - t0
         if stage_hook:
             stage_hook(name)
         return out
@@ -71,7 +74,8 @@ def run_dfq(model: nn.Module, graph, bottoms, targ, *, relu: bool = True, equali
     if correction:
         err = None
         if bc_mode == "fused":
-            err = {k: v["esum"] for k, v in (state or {}).items()}
+            err = {k: esum_source(v) for k, v in (state or {}).items()}
         stage("bc", bias_correction, graph, bottoms, targ, bits_weight=bits_weight, signed=symmetric,
               error_sums=err)
+    cle.wait()   # a launched CLE loop's error surfaces here (its results are already ordered on the stream)
     return res

@@ -56,7 +56,7 @@ def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d], *, ranges: Optio
         return model
     # a layer feeding two BNs is folded twice in sequence by the reference: one
     # batch call per fold then, in graph order
-    if len({id(layer.weight) for _, layer in pairs}) < len(pairs):
+    if len({id(layer._parameters["weight"]) for _, layer in pairs}) < len(pairs):
         for pair in pairs:
             _fold_batch([pair], ranges)
     else:
@@ -275,6 +275,18 @@ class _StateEntry(Mapping):
 
     def __len__(self):
         return 5
+
+    def esum_ref(self):
+        """The E sums as (shared buffer, float offset, numel): no view made."""
+        _, f0, _, r, ne = self._span
+        return (self._f32, f0 + 2 * self._up(r), ne)
+
+
+def esum_source(entry):
+    """What bias_correction(error_sums=...) takes for one quantize state entry:
+    a (buffer, float offset, numel) ref when the entry has one, else its E tensor."""
+    ref = getattr(entry, "esum_ref", None)
+    return ref() if ref is not None else entry["esum"]
 
 
 def _quantize_targ_layer_sharded(graph, bit_weight, bits_bias, targ_type, *, granularity, symmetric, clip, state,

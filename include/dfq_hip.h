@@ -273,6 +273,17 @@ int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* ta
  * max_iters doubles, may be NULL) = the per-iteration diff (np.sum of the list). */
 int dfq_cle_plan_run(dfq_cle_plan* plan, double threshold, int32_t count, int32_t max_iters,
                      int32_t* iterations, double* diffs, void* stream);
+/* The same loop, asynchronous (a worker thread reads the stop rule back between
+ * batches): `stream`'s earlier work runs before the loop, and everything enqueued
+ * on `stream` after this call waits in the device until the loop is done -- the
+ * caller's thread goes on enqueueing the next stages meanwhile.  One launched
+ * plan per device at a time (a launch first joins the previous one).
+ * DFQ_ERR_UNSUPPORTED: the device cannot make a stream wait on a value (run
+ * dfq_cle_plan_run instead). */
+int dfq_cle_plan_launch(dfq_cle_plan* plan, double threshold, int32_t count, int32_t max_iters, void* stream);
+/* Waits for a launched run; its result as dfq_cle_plan_run's (diffs: room for
+ * max_iters doubles, may be NULL).  destroy also waits. */
+int dfq_cle_plan_join(dfq_cle_plan* plan, int32_t* iterations, double* diffs);
 /* chains = independent relation groups, steps = relations per chain (max),
  * launches = kernel launches per iteration (fused schedule: one range launch for
  * the whole iteration; DFQ_CLE_FUSED=0: one per step) */

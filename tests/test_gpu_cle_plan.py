@@ -272,3 +272,64 @@ def test_two_live_plans():
             assert torch.equal(a, b), k
         for a, b in zip(r0, r1):
             assert torch.equal(a.S, b.S)
+
+
+def _weights(g):
+    return {k: g[k].weight for k in g if type(g[k]) in (nn.Conv2d, nn.Linear)}
+
+
+@pytest.mark.parametrize("producer", [False, True])
+def test_async_launch_orders_the_callers_stream(producer, monkeypatch):
+    """dfq_cle_plan_launch: the call returns with the loop under way; work the
+    caller enqueues afterwards on its stream (here: clones of every weight, with no
+    wait and no sync in between) sees the loop's final weights, and work enqueued
+    before it (a producer rewriting the weights) is seen by the loop.  Results and
+    LAST_RUN are bit-identical with the blocking run."""
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    monkeypatch.setenv("DFQ_CLE_MODE", "device")
+    out = {}
+    for mode in (False, True):
+        monkeypatch.setattr(cle, "ASYNC", mode)
+        g, rels = _graph(3)
+        torch.cuda.synchronize()
+        if producer:   # in flight on the caller's stream when the loop is launched
+            for w in _weights(g).values():
+                w.data.mul_(1.25)   # (keeps the dead channel dead)
+        cle.cross_layer_equalization(g, rels, [nn.Conv2d, nn.Linear], Treshhold=2e-7, Count=20, Save_state=False)
+        clones = {k: w.detach().clone() for k, w in _weights(g).items()}   # enqueued behind the loop
+        if mode:
+            assert cle._PENDING is not None or cle.LAST_RUN._d   # launched (or already joined)
+        out[mode] = ({k: v.cpu() for k, v in clones.items()}, dict(cle.LAST_RUN), [r.S.cpu() for r in rels])
+    (wa, ra, sa), (wb, rb, sb) = out[False], out[True]
+    assert rb["launched"] and not ra["launched"]
+    assert ra["iterations"] == rb["iterations"]
+    np.testing.assert_array_equal(ra["diffs"], rb["diffs"])   # (NaN == NaN here)
+    for k in wa:
+        assert torch.equal(wa[k].view(torch.int32), wb[k].view(torch.int32)), k
+    for x, y in zip(sa, sb):
+        assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+
+
+def test_async_launches_back_to_back(monkeypatch):
+    """Two launched loops with no wait between them (the second call joins the
+    first), then a third on the same graph: each equals its blocking twin."""
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    monkeypatch.setenv("DFQ_CLE_MODE", "device")
+    res = {}
+    for mode in (False, True):
+        monkeypatch.setattr(cle, "ASYNC", mode)
+        g1, r1 = _graph(4)
+        g2, r2 = _graph(5)
+        cle.cross_layer_equalization(g1, r1, [nn.Conv2d, nn.Linear], Treshhold=2e-7, Count=20, Save_state=False)
+        cle.cross_layer_equalization(g2, r2, [nn.Conv2d, nn.Linear], Treshhold=2e-7, Count=20, Save_state=False)
+        n2 = cle.LAST_RUN["iterations"]
+        cle.cross_layer_equalization(g1, r1, [nn.Conv2d, nn.Linear], Treshhold=2e-7, Count=20, Save_state=False)
+        cle.wait()
+        res[mode] = ({k: w.detach().cpu() for k, w in _weights(g1).items()},
+                     {k: w.detach().cpu() for k, w in _weights(g2).items()}, n2, cle.LAST_RUN["diffs"])
+    a, b = res[False], res[True]
+    assert a[2] == b[2]
+    np.testing.assert_array_equal(a[3], b[3])
+    for da, db in ((a[0], b[0]), (a[1], b[1])):
+        for k in da:
+            assert torch.equal(da[k].view(torch.int32), db[k].view(torch.int32)), k
