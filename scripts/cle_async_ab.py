@@ -39,11 +39,21 @@ def once(name, staged):
     return total, (t["cle"] * 1e3 if staged else None), cle.LAST_RUN.get("host_ms")
 
 
+_orig = cle.cross_layer_equalization
+
+
+def _join_first(*a, **k):   # launched, then joined at once (the host idles during the loop)
+    _orig(*a, **k)
+    cle.wait()
+
+
+MODES = {"blocking": (False, _orig), "async": (True, _orig), "async_join_first": (True, _join_first)}
 for name in ("mobilenetv2", "resnet50"):
     res = {}
     for rep in range(5):
-        for mode in (False, True):
-            cle.ASYNC = mode
+        for mode, (asy, fn) in MODES.items():
+            cle.ASYNC = asy
+            cle.cross_layer_equalization = fn
             st_total, st_cle, host = once(name, True)
             e2e, _, _ = once(name, False)
             if rep:
@@ -53,5 +63,5 @@ for name in ("mobilenetv2", "resnet50"):
                 r["end_to_end"].append(e2e)
     out = {"tag": tag, "model": name}
     for mode, r in res.items():
-        out["async" if mode else "blocking"] = {k: round(statistics.median(v), 3) for k, v in r.items()}
+        out[mode] = {k: round(statistics.median(v), 3) for k, v in r.items()}
     print(json.dumps(out), flush=True)
