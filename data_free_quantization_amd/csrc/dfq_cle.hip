@@ -3327,6 +3327,26 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
     return rc;
 }
 
+namespace dfq {
+// The caller's stream gate of a launched loop: one lane polls the signal word
+// until the worker has written this run's generation behind the loop's last
+// launch, sleeping between polls.  A CP wait packet (hipStreamWaitValue64) in
+// the caller's queue measured 1.8x slower loops (MobileNetV2 CLE 2.73 -> 4.97 ms:
+// the polling packet holds up the dispatch of the loop's queue), a running
+// one-wave kernel costs nothing.  Bounded: past `limit` ticks of the 100 MHz
+// clock it returns (the worker then reports the run failed, see kCleGateSeconds),
+// so a lost release can never hang the queue.
+__global__ void __launch_bounds__(64) cle_caller_gate_kernel(const uint64_t* sig, uint64_t gen, uint64_t limit) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > limit) return;
+        __builtin_amdgcn_s_sleep(32);
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+}  // namespace dfq
+
 // ---- asynchronous run (dfq_cle_plan_launch / _join) -------------------------
 // The loop needs the host between batches (the stop rule is read back), so a
 // worker thread drives it on the context's stream while the caller's thread goes
@@ -3337,6 +3357,9 @@ extern "C" int dfq_cle_plan_run(dfq_cle_plan* p, double threshold, int32_t count
 // before the loop is done.  The loop stream is a high-priority stream: it gets a
 // hardware queue of its own (queues are pooled per priority), so the caller's
 // waiting queue can never hold the loop's launches back.
+// How long the caller's stream gate waits for a launched loop at most.
+static constexpr int kCleGateSeconds = 120;
+
 struct CleAsync {
     std::mutex m;
     std::condition_variable cv;
@@ -3433,13 +3456,24 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
         DFQ_HIP_CHECK(hipEventRecord(ctx.in_ev, caller));
         DFQ_HIP_CHECK(hipStreamWaitEvent(ctx.st, ctx.in_ev, 0));
         gen = ctx.gen + 1;
-        DFQ_HIP_CHECK(hipStreamWaitValue64(caller, ctx.sig, gen, hipStreamWaitValueGte, ~0ull));
+        // the caller's stream waits behind a gate kernel (cle_caller_gate_kernel);
+        // diagnostics A/Bs: DFQ_CLE_ASYNC_WAIT=value (the CP wait packet),
+        // DFQ_CLE_ASYNC_NOWAIT (no wait: timing only, for a caller that joins first)
+        const char* wv = ab_env("DFQ_CLE_ASYNC_WAIT");
+        if (wv && wv[0] == 'v') {
+            DFQ_HIP_CHECK(hipStreamWaitValue64(caller, ctx.sig, gen, hipStreamWaitValueGte, ~0ull));
+        } else if (!ab_env("DFQ_CLE_ASYNC_NOWAIT")) {
+            hipLaunchKernelGGL(cle_caller_gate_kernel, dim3(1), dim3(64), 0, caller,
+                               static_cast<const uint64_t*>(ctx.sig), gen, (uint64_t)kCleGateSeconds * 100000000ull);
+            DFQ_LAUNCH_CHECK();
+        }
         ctx.gen = gen;
     }
     // from here on the caller's stream is held until the signal reaches gen: every
     // path below writes it
     CleAsync* a = new (std::nothrow) CleAsync();
-    auto body = [p, &ctx, threshold, count, max_iters, gen](CleAsync* a) {
+    const double t_launch = now_us();
+    auto body = [p, &ctx, threshold, count, max_iters, gen, t_launch](CleAsync* a) {
         std::lock_guard<std::mutex> lock(ctx.mu);
         int rc = DFQ_OK;
         if (hipSetDevice(p->dev) != hipSuccess) {
@@ -3454,9 +3488,15 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
         // release the caller's stream behind everything the loop enqueued
         hipError_t e = hipStreamWriteValue64(ctx.st, ctx.sig, gen, 0);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx.st);
-        if (e != hipSuccess) {   // never expected; the caller's stream would wait forever
+        if (e != hipSuccess) {   // never expected; the gate gives up at its time limit
             fprintf(stderr, "dfq_cle_plan_launch: releasing the caller's stream failed (%s)\n", hipGetErrorString(e));
             if (rc == DFQ_OK) rc = DFQ_ERR_HIP;
+        }
+        if (rc == DFQ_OK && now_us() - t_launch > 0.9e6 * kCleGateSeconds) {   // the gate may have opened early
+            set_last_hip_error(hipErrorLaunchTimeOut);
+            const char* m = "CLE loop outlived the caller's stream gate";
+            for (size_t i = 0; m[i] && i + 1 < sizeof(a->err); ++i) a->err[i] = m[i];
+            rc = DFQ_ERR_HIP;
         }
         {
             std::lock_guard<std::mutex> l(a->m);

@@ -276,8 +276,10 @@ int dfq_cle_plan_run(dfq_cle_plan* plan, double threshold, int32_t count, int32_
 /* The same loop, asynchronous (a worker thread reads the stop rule back between
  * batches): `stream`'s earlier work runs before the loop, and everything enqueued
  * on `stream` after this call waits in the device until the loop is done -- the
- * caller's thread goes on enqueueing the next stages meanwhile.  One launched
- * plan per device at a time (a launch first joins the previous one).
+ * caller's thread goes on enqueueing the next stages meanwhile (the caller's
+ * stream waits behind a one-wave gate kernel that polls the library's signal
+ * word; it gives up after 120 s, and the join then reports the run failed).
+ * One launched plan per device at a time (a launch first joins the previous one).
  * DFQ_ERR_UNSUPPORTED: the device cannot make a stream wait on a value (run
  * dfq_cle_plan_run instead). */
 int dfq_cle_plan_launch(dfq_cle_plan* plan, double threshold, int32_t count, int32_t max_iters, void* stream);

@@ -8,6 +8,7 @@ import contextlib
 import io
 import json
 import logging
+import os
 import statistics
 import sys
 import time
@@ -48,6 +49,8 @@ def _join_first(*a, **k):   # launched, then joined at once (the host idles duri
 
 
 MODES = {"blocking": (False, _orig), "async": (True, _orig), "async_join_first": (True, _join_first)}
+if os.environ.get("DFQ_AB_MODES"):   # a subset (DFQ_CLE_ASYNC_NOWAIT runs join-first only)
+    MODES = {k: v for k, v in MODES.items() if k in os.environ["DFQ_AB_MODES"].split(",")}
 for name in ("mobilenetv2", "resnet50"):
     res = {}
     for rep in range(5):
