@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--no-parity", action="store_true",
                    help="skip the parity checks of the timed outputs (vs the C oracle) and of the MobileNetV2 "
                         "pipeline (vs the reference fixture)")
+    p.add_argument("--prewarm-ms", type=float, default=600.0,
+                   help="time-based pre-warm (ms of sweep steps) before the counted warm-up: a fresh lease starts "
+                        "at idle clocks (0 = none)")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r03.json"),
                    help="the committed rocprofv3 summary of this bench command (scripts/profile.sh + "
                         "scripts/summarize_profile.py): PMC traffic and the kernel's rocprof average")
@@ -96,6 +99,94 @@ def build_batch(model, dev, copies=0, bits=8, channel=True, sym=True, esum=True,
             items.append(allocate(w, bits=bits, per_channel=channel, symmetric=sym, khw=khw_of(w), want_esum=esum,
                                   clip=(-15.0, 15.0), pack_int4=pack))
     return items, shapes, per_copy, copies
+
+
+class Telemetry:
+    """GPU clocks, power and throttle state read in-process through the amdsmi
+    Python module (sysfs / driver queries, no HIP call), for the device this
+    process runs on (matched by PCI bus id).  Every read is best effort: a box
+    where amdsmi is missing or refuses a query reports None for that field."""
+
+    def __init__(self, dev):
+        self.handle, self.error = None, None
+        try:
+            import amdsmi
+            self.smi = amdsmi
+            amdsmi.amdsmi_init()
+            p = torch.cuda.get_device_properties(dev)
+            want = (int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+            for h in amdsmi.amdsmi_get_processor_handles():
+                bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)          # "dddd:bb:dd.f"
+                dom, bus, rest = bdf.split(":")
+                if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+                    self.handle = h
+                    break
+            if self.handle is None:
+                self.error = f"no amdsmi handle with PCI id {want}"
+        except Exception as e:   # amdsmi absent or not permitted on this box
+            self.error = f"{type(e).__name__}: {e}"
+
+    def sample(self, tag):
+        out = {"tag": tag, "t": round(time.perf_counter(), 4)}
+        if self.handle is None:
+            out["error"] = self.error
+            return out
+        smi = self.smi
+        try:
+            m = smi.amdsmi_get_gpu_metrics_info(self.handle)
+            for k in ("current_gfxclk", "current_uclk", "current_socclk", "average_gfxclk_frequency",
+                      "average_uclk_frequency", "average_socket_power", "current_socket_power",
+                      "average_umc_activity", "average_gfx_activity", "temperature_hotspot", "temperature_mem",
+                      "throttle_status", "indep_throttle_status", "gfxclk_lock_status"):
+                v = m.get(k)
+                if v is not None and v != "N/A":
+                    out[k] = v
+            g = m.get("current_gfxclks")
+            if isinstance(g, list):
+                g = [x for x in g if isinstance(x, int) and x < 0xFFFF]
+                if g:
+                    out["gfxclk_per_xcd"] = g
+        except Exception as e:
+            out["metrics_error"] = f"{type(e).__name__}: {e}"
+        for name, ct in (("sclk", "GFX"), ("mclk", "MEM"), ("fclk", "DF"), ("socclk", "SOC")):
+            try:
+                c = smi.amdsmi_get_clock_info(self.handle, getattr(smi.AmdSmiClkType, ct))
+                out[name] = {"clk": c["clk"], "min": c["min_clk"], "max": c["max_clk"],
+                             "deep_sleep": c["clk_deep_sleep"]}
+            except Exception:
+                pass
+        return out
+
+
+def steps_with_events(run, stream, n):
+    """Run ``run`` n times with a HIP event pair around each call on ``stream``;
+    returns the per-step device milliseconds (after one synchronize)."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in evs:
+        a.record(stream)
+        run()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in evs]
+
+
+def prewarm(run, stream, dev, ms_target):
+    """Time-based pre-warm before the counted warm-up: sweep steps until
+    ``ms_target`` milliseconds of wall time have passed, in batches of 8 with a
+    HIP event pair per step.  A fresh lease starts with the GPU at idle clocks;
+    the per-step series shows the ramp (first / last steps, and the mean of each
+    tenth of the run)."""
+    series = []
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms_target or not series:
+        series += steps_with_events(run, stream, 8)
+    wall = (time.perf_counter() - t0) * 1e3
+    k = max(1, len(series) // 10)
+    return {"ms_target": ms_target, "wall_ms": round(wall, 1), "steps": len(series),
+            "first_steps_ms": [round(x, 4) for x in series[:8]],
+            "last_steps_ms": [round(x, 4) for x in series[-8:]],
+            "tenths_mean_ms": [round(sum(series[i:i + k]) / len(series[i:i + k]), 4)
+                               for i in range(0, len(series), k)][:10]}
 
 
 def time_plan(plan, stream, dev, steps, warmup):
@@ -674,6 +765,8 @@ def main():
     args = parse()
     from data_free_quantization_amd import distributed as D
     world, rank, dev = D.init_from_env()
+    telemetry = Telemetry(dev)
+    tele_start = telemetry.sample("process_start")
     shapes = model_shapes(args.model)
     per_copy = sum(int(torch.Size(s).numel()) for s in shapes)
     copies = args.copies or max(1, -(-(2 << 30) // (4 * per_copy)))   # >= 2 GiB of fp32 weights in the list
@@ -713,23 +806,32 @@ def main():
         plan = SweepPlan(items)
         st = plan.stats
         run = lambda: plan.execute(stream)   # noqa: E731
-    for _ in range(args.warmup):
-        run()
+    tele = [telemetry.sample("before_prewarm")]
+    warm = prewarm(run, stream, dev, args.prewarm_ms) if args.prewarm_ms > 0 else None
+    tele.append(telemetry.sample("after_prewarm"))
+    warm_steps = steps_with_events(run, stream, args.warmup) if args.warmup > 0 else []
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    tele.append(telemetry.sample("before_timed"))
+    step_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
+    for a, b in step_ev:
+        a.record(stream)
         run()
+        b.record(stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
+    tele.append(telemetry.sample("after_timed"))
+    step_ms = [a.elapsed_time(b) for a, b in step_ev]
     dev_ms = ev0.elapsed_time(ev1)          # device time of this rank's K launches on this stream
     t_step = D.max_over_ranks(wall, dev) / args.steps
     weight_bytes = 4 * per_copy * copies    # the whole list, swept once per step by all ranks together
@@ -845,6 +947,18 @@ def main():
                                    f"{prof['source']}: separate rocprofv3 --pmc passes over this bench command, "
                                    "not measured in this run") if prof else None,
                 "profile": prof,
+            },
+            "timing": {
+                "prewarm": warm,
+                "warmup_step_ms": [round(x, 4) for x in warm_steps],
+                "step_ms": [round(x, 4) for x in step_ms],
+                "step_ms_min": round(min(step_ms), 4),
+                "step_ms_median": round(sorted(step_ms)[len(step_ms) // 2], 4),
+                "step_ms_max": round(max(step_ms), 4),
+                "note": "HIP events around each execute() on the launch stream (device ms); prewarm = the "
+                        "time-based sweep steps run before the counted warm-up (a fresh lease starts at idle "
+                        "clocks), not part of the timed steps",
+                "telemetry": [tele_start] + tele + [telemetry.sample("end_of_bench")],
             },
             "memory_pattern_probe": {
                 "lds_dma_GBs": probe_lds, "vgpr_stream_GBs": probe_stream,

@@ -364,12 +364,17 @@ class _NpSpy:
         return getattr(np, name)
 
 
-def pipeline(name: str, seed: int = 0, per_channel: bool = False, threads: int = 8, out: Path = None):
+def pipeline(name: str, seed: int = 0, per_channel: bool = False, threads: int = 8, out: Path = None,
+             bits_weight: int = 8, bits_bias: int = 8):
     """``threads``: torch's intra-op thread count for the run.  ATen splits two of the
     reference's fp32 reductions by it -- the CLE metric's torch.mean
     (Cross_layer_equal.py:107) and bias correction's view(-1, F).mean(0)
     (bias_correction.py:98-104,206-213) -- so the results depend on it;
-    pipeline_<name>.npz is the 8-thread run, pipeline_<name>_t<T>.npz the others."""
+    pipeline_<name>.npz is the 8-thread run, pipeline_<name>_t<T>.npz the others.
+    ``bits_weight`` != 8 (BASELINE configs[4], ResNet-50 W4): main_dfq.py:209-231 with
+    --bits_weight 4 -- set_layer_bits(graph, 4, 8, bits_bias), quantize_targ_layer(graph,
+    4, bits_bias), clip_weight([-15, 15]), bias_correction(bits_weight=4);
+    pipeline_<name>_w<bits>.npz."""
     t0 = time.time()
     torch.set_num_threads(threads)
     model = zoo.build(name, seed=seed, relu=True)
@@ -430,23 +435,30 @@ def pipeline(name: str, seed: int = 0, per_channel: bool = False, threads: int =
                     out[o] = ref_quantize(sl, 8, float(sl.min()), float(sl.max()), symmetric=sym)
                 hs.append(h(t2n(out)))
             P[f"{mode}8_wh"] = np.stack([np.frombuffer(bytes.fromhex(x), dtype=np.uint8) for x in hs])
+    if bits_weight != 8:   # main_dfq.py:209 (a host config step; no tensor changes on plain modules)
+        from utils.quantize import set_layer_bits as ref_slb
+        ref_slb(graph, bits_weight, 8, bits_bias, TARG)
     ref_merge_bn(model, graph, bottoms, TARG)
     snap("bn2", full_bias=True); snap_bn("bn2")
-    ref_qtl(graph, 8, 8, TARG)
+    ref_qtl(graph, bits_weight, bits_bias, TARG)
     snap("quant", full_bias=True)
     ref_clip(graph, [-15, 15], TARG)
     snap("clip", full_bias=True)
     try:
-        ref_bc.bias_correction(graph, bottoms, TARG, bits_weight=8)
+        ref_bc.bias_correction(graph, bottoms, TARG, bits_weight=bits_weight)
         P["bc_error"] = np.array("")
     except Exception as e:  # DeepLab: torch.cat of 2-D eps with 1-D expect (bias_correction.py:75)
         P["bc_error"] = np.array(f"{type(e).__name__}")
     snap("bc", full_bias=True); snap_bn("bc", full=True)
     stats["seconds"] = time.time() - t0
     stats["threads"] = threads
+    stats["bits_weight"], stats["bits_bias"] = bits_weight, bits_bias
     P["stats"] = np.array(json.dumps(stats))
+    P["bits"] = np.array([bits_weight, 8, bits_bias], dtype=np.int64)   # weight, activation, bias
     if out is None:
         out = HERE / (f"pipeline_{name}.npz" if threads == 8 else f"pipeline_{name}_t{threads}.npz")
+        if bits_weight != 8:
+            out = HERE / f"pipeline_{name}_w{bits_weight}.npz"
     np.savez_compressed(out, **P)
     torch.set_num_threads(8)
     print(name, "relations", len(res), "cle iters", len(spy.diffs), "bc", str(P["bc_error"]), stats)
@@ -558,7 +570,7 @@ def _record_op_calls(model, x):
     return rec
 
 
-def forward_logits(name: str, seed: int = 0):
+def forward_logits(name: str, seed: int = 0, bits_weight: int = 8):
     """The top-1 proxy: the reference's quantized forward after the
     main_dfq stage order (main_dfq.py:149-258) on a seeded synthetic batch.
 
@@ -608,14 +620,14 @@ def forward_logits(name: str, seed: int = 0):
     res = ref_create_relation(graph, bottoms, targ, delete_single=False)
     ref_cle.cross_layer_equalization(graph, res, targ, Save_state=False, Treshhold=2e-7)
     ref_absorb(graph, res, bottoms, N=3)
-    ref_slb(graph, 8, 8, 8, targ)
+    ref_slb(graph, bits_weight, 8, 8, targ)
     ref_merge_bn(model, graph, bottoms, targ)
-    ref_qtl(graph, 8, 8, targ)
+    ref_qtl(graph, bits_weight, 8, targ)
     ref_lt.set_quant_minmax(graph, bottoms, verbose=False)
     ref_clip(graph, [-15, 15], targ)
     correction = name != "deeplab"    # DeepLab: the reference's BC crashes on cat (bias_correction.py:75)
     if correction:
-        ref_bc.bias_correction(graph, bottoms, targ, bits_weight=8)
+        ref_bc.bias_correction(graph, bottoms, targ, bits_weight=bits_weight)
     model.eval()
     # merge_batchnorm left every folded BN an identity with eps = 0 (:277-281), which
     # torch >= 2 rejects in F.batch_norm (torch 1.1, the reference's pin, accepted it).
@@ -625,6 +637,7 @@ def forward_logits(name: str, seed: int = 0):
         if type(mod) == nn.BatchNorm2d and mod.eps == 0:
             mod.eps = float(torch.finfo(torch.float32).tiny)
     A = {"input_shape": np.array(FWD_INPUT[name], dtype=np.int64), "seed": np.array(FWD_SEED),
+         "bits": np.array([bits_weight, 8, 8], dtype=np.int64),   # weight, activation, bias
          "correction": np.array(correction), "op_names": np.array([c for _, c in names]),
          "op_keys": np.array([str(k) for k, _ in names])}
     name_of = {id(mod): n for n, mod in model.named_modules()}
@@ -663,7 +676,8 @@ def forward_logits(name: str, seed: int = 0):
         A[f"ops_layer_max{tag}"] = np.array([float(q.running_max) for q in lq], dtype=np.float32)
         A[f"ops_op_min{tag}"] = np.array([float(q.running_min) for q in oq], dtype=np.float32)
         A[f"ops_op_max{tag}"] = np.array([float(q.running_max) for q in oq], dtype=np.float32)
-    np.savez_compressed(HERE / f"forward_{name}.npz", **A)
+    np.savez_compressed(HERE / (f"forward_{name}.npz" if bits_weight == 8 else f"forward_{name}_w{bits_weight}a8.npz"),
+                        **A)
     d = lambda a, b: float(np.abs(A[a].astype(np.float64) - A[b]).max())   # noqa: E731
     print(name, "forward fixture:", len(names), "op nodes,", f"{time.time() - t0:.1f} s;",
           "mkldnn on/off max|d|: plain", d("plain", "plain_nomkldnn"), "ops", d("ops", "ops_nomkldnn"))
@@ -746,6 +760,10 @@ if __name__ == "__main__":
         for t in (1, 16):
             if f"{m}_t{t}" in which:
                 pipeline(m, threads=t)
+    if "resnet50_w4" in which:     # BASELINE configs[4]: ResNet-50 INT4 weights / INT8 acts, clip
+        pipeline("resnet50", bits_weight=4)
+    if "forward_resnet50_w4a8" in which:
+        forward_logits("resnet50", bits_weight=4)
     for m in ("mobilenetv2", "resnet50", "deeplab"):
         if "act" in which or f"act_{m}" in which:
             act_ranges(m)

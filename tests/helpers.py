@@ -57,9 +57,13 @@ def transform_cases():
     return z, json.loads(str(z["meta"]))
 
 
-def pipeline(name, threads=8):
+def pipeline(name, threads=8, bits_weight=8):
     """The reference's main_dfq stage order on the synthetic model, run with
-    ``threads`` torch intra-op threads (tests/golden/make_golden.py:pipeline)."""
+    ``threads`` torch intra-op threads (tests/golden/make_golden.py:pipeline);
+    ``bits_weight`` 4: the --bits_weight 4 run (pipeline_<name>_w4.npz, 8 threads)."""
+    if bits_weight != 8:
+        assert threads == 8, "the W4 fixtures are 8-thread runs"
+        return np.load(GOLDEN / f"pipeline_{name}_w{bits_weight}.npz", allow_pickle=False)
     f = f"pipeline_{name}.npz" if threads == 8 else f"pipeline_{name}_t{threads}.npz"
     return np.load(GOLDEN / f, allow_pickle=False)
 

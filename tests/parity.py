@@ -24,11 +24,13 @@ except ImportError:   # imported with tests/ itself on sys.path
 STAGES = ("bn1", "cle", "absorb", "bn2", "quant", "clip", "bc")
 
 
-def pipeline_mismatches(name: str = "mobilenetv2", threads: int = 8, device="cuda:0") -> dict:
+def pipeline_mismatches(name: str = "mobilenetv2", threads: int = 8, device="cuda:0", bits_weight: int = 8) -> dict:
     """Run run_dfq(bc_mode="reference") on zoo.build(name, seed=0, relu=True) and
     compare every stage with the reference fixture.  Tolerances are those of
     tests/test_gpu_pipeline.py: bit-exact except ResNet-50's post-absorption
-    biases before bias correction (the reference's MKL sgemv order: 1e-5)."""
+    biases before bias correction (the reference's MKL sgemv order: 1e-5).
+    ``bits_weight`` 4: main_dfq --bits_weight 4 (BASELINE configs[4]) against
+    pipeline_<name>_w4.npz."""
     import torch
     import torch.nn as nn
     from data_free_quantization_amd import _lib, zoo
@@ -36,7 +38,7 @@ def pipeline_mismatches(name: str = "mobilenetv2", threads: int = 8, device="cud
     from data_free_quantization_amd.pipeline import run_dfq
     from data_free_quantization_amd.utils.tracer import build_graph
     targ = (nn.Conv2d, nn.Linear)
-    P = pipeline(name, threads)
+    P = pipeline(name, threads, bits_weight)
     old_threads = _lib.REF_THREADS
     _lib.REF_THREADS = threads
     try:
@@ -44,7 +46,7 @@ def pipeline_mismatches(name: str = "mobilenetv2", threads: int = 8, device="cud
         g = build_graph(model, "positional")
         graph, bottoms = g.getGraph(), g.getBottoms()
         tkeys = [k for k in graph if type(graph[k]) in targ]
-        out = {"model": name, "ref_threads": threads, "targets": len(tkeys),
+        out = {"model": name, "ref_threads": threads, "bits_weight": bits_weight, "targets": len(tkeys),
                "target_keys_match": tkeys == list(P["targets"])}
         stage_bad = {}
         cle_info = {}
@@ -73,7 +75,8 @@ def pipeline_mismatches(name: str = "mobilenetv2", threads: int = 8, device="cud
         raised = None
         rels = None
         try:
-            rels = run_dfq(model, graph, bottoms, targ, bc_mode="reference", stage_hook=hook)
+            rels = run_dfq(model, graph, bottoms, targ, bc_mode="reference", stage_hook=hook,
+                           bits_weight=bits_weight, bits_bias=8)
         except RuntimeError as e:   # DeepLab: the reference's own cat-branch crash
             raised = str(e)
         torch.cuda.synchronize(device)

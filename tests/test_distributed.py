@@ -266,14 +266,35 @@ def test_sharded_sweep_rccl_world1():
         dist.destroy_process_group()
 
 
+def _configs4_specs():
+    """BASELINE configs[4]'s layer list: every ResNet-50 target layer, per-channel
+    asymmetric INT4 + clip [-15, 15], packed int4 codes (bench.SECONDARY's
+    "resnet50 per-ch asym INT4 + clip, packed int4 codes")."""
+    from data_free_quantization_amd import zoo
+    shapes = [tuple(m.weight.shape) for m in zoo.target_layers(zoo.MODELS["resnet50"]())]
+    return D.uniform_specs(shapes, bits=4, per_channel=True, symmetric=False, want_esum=False,
+                           clip=(-15.0, 15.0), pack_int4=True)
+
+
+def _configs4_weights(specs):
+    """Synthetic conv init of bench.synth_weight (N(0, sqrt(2 / (k*k*O))), Linear N(0, 0.01))."""
+    g = torch.Generator().manual_seed(9)
+    out = []
+    for s in specs:
+        shp = s.shape
+        std = (2.0 / (shp[2] * shp[3] * shp[0])) ** 0.5 if len(shp) == 4 else 0.01
+        out.append(torch.randn(shp, generator=g) * std)
+    return out
+
+
 def _gpu_worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        specs = _gpu_specs_mixed()
-        ws = _weights(9, [s.shape for s in specs])
-        sw = D.ShardedSweep(specs, device=torch.device("cuda:0"))
+        specs = _configs4_specs()
+        ws = _configs4_weights(specs)
+        sw = D.ShardedSweep(specs, replicate=True, device=torch.device("cuda:0"))
         if rank == 0:
             for i, w in enumerate(ws):
                 sw.weight(i).copy_(w)
@@ -281,11 +302,18 @@ def _gpu_worker(rank, world, port, outdir):
         sw.run()
         sw.gather("root")
         torch.cuda.synchronize()
-        ok = 0
-        for i, o in sw.result().items():
-            _check(o, ws[i], specs[i])
-            ok += 1
-        np.save(os.path.join(outdir, f"r{rank}.npy"), np.array([ok, len(sw.mine)]))
+        ok_root = 0
+        if rank == 0:   # rank 0 holds every layer's outputs after gather("root")
+            for i in range(len(specs)):
+                _check(sw.outputs(i), ws[i], specs[i])
+                ok_root += 1
+        sw.gather("all")
+        torch.cuda.synchronize()
+        ok_all = 0
+        for i in range(len(specs)):   # every rank holds every layer's outputs after gather("all")
+            _check(sw.outputs(i), ws[i], specs[i])
+            ok_all += 1
+        np.save(os.path.join(outdir, f"r{rank}.npy"), np.array([ok_root, ok_all, len(sw.mine)]))
         sw.destroy()
     finally:
         dist.destroy_process_group()
@@ -293,11 +321,14 @@ def _gpu_worker(rank, world, port, outdir):
 
 @pytest.mark.gpu
 def test_sharded_sweep_two_ranks_one_gpu(tmp_path):
-    """2-rank rehearsal on the one GPU (gloo between the processes): rank 0 holds
-    the layer list, scatters, both run the HIP sweep on their shard, rank 0
-    gathers; every layer bit-exact on rank 0."""
+    """2-rank rehearsal of BASELINE configs[4] on the one GPU (gloo between the
+    processes): the ResNet-50 INT4 + clip layer list (54 layers, 25.5 M weights),
+    LPT-sharded; rank 0 holds the list and scatters, both ranks run the HIP sweep
+    on their shard, then gather("root") (rank 0 checks every layer against the
+    oracle) and gather("all") (both ranks check every layer): bit-exact."""
     mp.spawn(_gpu_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    n = len(_gpu_specs_mixed())
+    n = len(_configs4_specs())
     r0, r1 = np.load(tmp_path / "r0.npy"), np.load(tmp_path / "r1.npy")
-    assert r0[0] == n
-    assert r1[0] == r1[1] and r0[1] + r1[1] == n
+    assert r0[0] == n and r1[0] == 0
+    assert r0[1] == n and r1[1] == n
+    assert r0[2] > 0 and r1[2] > 0 and r0[2] + r1[2] == n

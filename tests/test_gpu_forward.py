@@ -27,12 +27,17 @@ import torch
 
 pytestmark = pytest.mark.gpu
 GOLD = Path(__file__).parent / "golden"
-FLAGS = ["--relu", "--equalize", "--absorption", "--quantize", "--clip_weight", "--bits_weight", "8",
+FLAGS = ["--relu", "--equalize", "--absorption", "--quantize", "--clip_weight",
          "--bits_activation", "8", "--bits_bias", "8", "--bc_mode", "reference"]
-MODELS = {"mobilenetv2": ["--task", "cls", "--correction"],
-          "resnet50": ["--task", "cls", "--model", "resnet50", "--correction"],
-          "deeplab": ["--task", "seg"],   # the reference's BC crashes on DeepLab's cat (bias_correction.py:75)
-          "resnet18": ["--task", "cls", "--resnet", "--correction"]}
+# fixture name -> main_dfq flags (forward_<name>.npz)
+MODELS = {"mobilenetv2": ["--task", "cls", "--correction", "--bits_weight", "8"],
+          "resnet50": ["--task", "cls", "--model", "resnet50", "--correction", "--bits_weight", "8"],
+          # the reference's BC crashes on DeepLab's cat (bias_correction.py:75)
+          "deeplab": ["--task", "seg", "--bits_weight", "8"],
+          "resnet18": ["--task", "cls", "--resnet", "--correction", "--bits_weight", "8"],
+          # BASELINE configs[4]: INT4 weights / INT8 activations with clip (the
+          # QuantConv2d forward re-quantizes each weight at 4 bits, utils/quantize.py:225-238)
+          "resnet50_w4a8": ["--task", "cls", "--model", "resnet50", "--correction", "--bits_weight", "4"]}
 
 
 def _input(fx):

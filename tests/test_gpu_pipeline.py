@@ -93,6 +93,19 @@ def test_pipeline_matches_reference(name, cle_mode, threads, monkeypatch):
     assert not failures, failures
 
 
+def test_pipeline_w4_matches_reference():
+    """BASELINE configs[4] on one GPU: ResNet-50 through main_dfq's stage order at
+    --bits_weight 4 --bits_bias 8 with clip [-15, 15] and bias correction at 4 bits
+    (main_dfq.py:209-231) against the reference's own run
+    (tests/golden/pipeline_resnet50_w4.npz): every stage's weights and biases, the
+    CLE iterations and diffs, the relation scales."""
+    from tests.parity import pipeline_mismatches
+    r = pipeline_mismatches("resnet50", 8, "cuda:0", bits_weight=4)
+    print({k: v for k, v in r.items() if k != "stages"}, r["stages"])
+    assert r["mismatches"] == 0, r
+    assert set(r["stages"]) == {"bn1", "cle", "absorb", "bn2", "quant", "clip", "bc"}
+
+
 def test_per_channel_extension_matches_reference_slices():
     """Per-channel INT8 (sym and asym) of the post-absorption MobileNetV2 weights
     == the reference quantize() applied to every W[o] slice."""

@@ -57,3 +57,32 @@ def test_oracle_pipeline_matches_reference(name, threads):
         R.bias_correction(8, threads=threads)
         got = np.concatenate([R.B[k] for k in R.tkeys])
         assert np.array_equal(got, P["bc_bias"])   # ATen reduction order reproduced
+
+
+def test_oracle_pipeline_w4_matches_reference():
+    """BASELINE configs[4]'s arithmetic (ResNet-50, --bits_weight 4 --bits_bias 8,
+    clip [-15, 15], bias correction at 4 bits: main_dfq.py:209-231) against the
+    reference's own run (tests/golden/pipeline_resnet50_w4.npz).  At 4 bits the
+    re-quantization inside bias correction moves the weights (its range is the
+    quantized tensor's), so the corrections are not zero: 27,496 of 27,560
+    biases change in the reference run."""
+    P = pipeline("resnet50", bits_weight=4)
+    assert P["bits"].tolist() == [4, 8, 8]
+    m = zoo.build("resnet50", seed=0, relu=True)
+    g = build_graph(m, "positional")
+    R = OracleDFQ(g.getGraph(), g.getBottoms())
+    R.merge_bn()
+    R.cle(threads=8)
+    assert R.cle_diffs == list(P["cle_diffs"])
+    assert np.array_equal(_stage_hashes(R), P["cle_wh"])
+    R.absorb()
+    R.merge_bn()
+    assert np.array_equal(_stage_hashes(R), P["bn2_wh"])
+    R.quantize(4, 8)
+    assert np.array_equal(_stage_hashes(R), P["quant_wh"])
+    R.clip()
+    assert np.array_equal(_stage_hashes(R), P["clip_wh"])
+    R.bias_correction(4, threads=8)
+    got = np.concatenate([R.B[k] for k in R.tkeys])
+    assert (P["bc_bias"] != P["clip_bias"]).sum() > 27000
+    assert np.array_equal(got, P["bc_bias"])
