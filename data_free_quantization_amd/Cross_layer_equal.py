@@ -60,12 +60,17 @@ class _LastRun(MutableMapping):
 #: statistics of the last cross_layer_equalization call (extension, for tests/bench)
 LAST_RUN = _LastRun()
 
-#: Run the device loop asynchronously (dfq_cle_plan_launch): the call returns once
-#: the loop is under way, and whatever the caller enqueues on the current stream
-#: afterwards waits for it in the device -- the next stages' host work overlaps the
-#: loop.  ``wait()`` (or reading LAST_RUN) joins it; False: the blocking run.
-ASYNC = True
+#: Default of ``cross_layer_equalization(..., launch=None)``.  False (the
+#: reference's contract): the call blocks until the loop is done and raises its
+#: errors.  True: the device loop runs asynchronously (dfq_cle_plan_launch): the
+#: call returns once the loop is under way, and whatever the caller enqueues on the
+#: device's CURRENT stream afterwards waits for it in the device (work on any other
+#: stream is not ordered behind it) -- the next stages' host work overlaps the
+#: loop.  ``wait()`` (or reading LAST_RUN) joins it and raises its error.
+#: run_dfq and main_dfq opt in (launch=True) and call wait() at their end.
+ASYNC = False
 _PENDING = None   # (plan, workspace, host times) of the launched loop
+_ABANDONED = []   # (plan, workspace) of launched loops join gave up on: their worker may still use both
 
 
 def _layer_equalization(W1, W2, B1, Batnorm_weight=None, Batnorm_bias=None, s_min_max=(1e-8, 1e8), signed=False,
@@ -126,7 +131,7 @@ MAX_ITERS = int(os.environ.get("DFQ_CLE_MAX_ITERS", "100000"))
 
 
 def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8], Treshhold=2e-7, Count=20,
-                             signed=False, eps=0, Save_state=True):
+                             signed=False, eps=0, Save_state=True, *, launch=None):
     """Iterate the relations until the summed mean weight change is <= Treshhold
     or it stayed within 1e-9 for ``Count`` iterations (Cross_layer_equal.py:81-115).
 
@@ -134,7 +139,11 @@ def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8
     independent chains, the metric (fp32 torch.mean order + numpy's pairwise sum)
     and the stop rule evaluated by the GPU.  ``DFQ_CLE_MODE=host`` keeps the
     relation-by-relation host loop (one C call per relation, metric read back
-    every iteration) for comparison."""
+    every iteration) for comparison.
+
+    ``launch`` (extension, keyword-only; None: module ``ASYNC``, False by
+    default): True returns as soon as the loop is under way; only the device's
+    current stream is ordered behind it, and its errors surface at ``wait()``."""
     print("Cross layer equalization")
     if Save_state:
         warnings.warn("Save_state plots (ourplots.save_layer) are visualization, not part of the weight path; "
@@ -144,7 +153,8 @@ def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8
         if os.environ.get("DFQ_CLE_MODE", "device") == "host":
             _cle_host_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps)
         else:
-            _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps)
+            _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps,
+                             ASYNC if launch is None else bool(launch))
 
 
 _CLE_REL = np.dtype([("w1", "<u8"), ("w2", "<u8"), ("b1", "<u8"), ("bn_w", "<u8"), ("bn_b", "<u8"), ("s_acc", "<u8"),
@@ -240,8 +250,14 @@ def wait():
     iters = C.c_int32(0)
     hist = _hist_buffer()
     t0 = time.perf_counter()
+    rc = L.dfq_cle_plan_join(plan, C.byref(iters), hist)
+    if rc != _lib.DFQ_OK and "did not finish" in L.dfq_last_hip_error().decode():
+        # the loop is still running (the caller's stream stays held behind its
+        # gate): its plan and snapshot workspace must outlive it
+        _ABANDONED.append((plan, ws))
+        _lib.check(rc, "cross_layer_equalization (device loop)")
     try:
-        _lib.check(L.dfq_cle_plan_join(plan, C.byref(iters), hist), "cross_layer_equalization (device loop)")
+        _lib.check(rc, "cross_layer_equalization (device loop)")
         chains, steps, launches = C.c_int32(0), C.c_int32(0), C.c_int32(0)
         L.dfq_cle_plan_info(plan, C.byref(chains), C.byref(steps), C.byref(launches))
     finally:
@@ -257,22 +273,26 @@ def wait():
 
 
 def _at_exit():
+    """A launched loop nobody joined: join it; its failure must not end the
+    process with status 0 (the weights it was rescaling are not to be trusted)."""
     try:
         wait()
-    except Exception as e:   # noqa: BLE001 -- report, the interpreter is going down
-        warnings.warn(f"cross_layer_equalization: {e}")
+    except Exception as e:   # noqa: BLE001 -- the interpreter is going down
+        import sys
+        print(f"cross_layer_equalization (launched, never joined) failed: {e}", file=sys.stderr, flush=True)
+        os._exit(1)
 
 
 atexit.register(_at_exit)
 
 
-def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps):
+def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count, signed, eps, launch):
     global _PENDING
     wait()   # one launched loop at a time
     t0 = time.perf_counter()
     plan, ws, dev = _create_plan(graph, relations, Target_list, s_min_max, signed, eps)
     t2 = time.perf_counter()
-    if ASYNC:
+    if launch:
         L = _lib.load()
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         rc = L.dfq_cle_plan_launch(plan, float(Treshhold), int(Count), MAX_ITERS, stream)

@@ -36,8 +36,7 @@ EXPORTS = [
     "dfq_act_moments", "dfq_act_minmax", "dfq_act_affine",
 ]
 #: entry points only the diagnostics library exports (include/dfq_diag.h)
-DIAG_EXPORTS = ["dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline", "dfq_probe_grid_barrier",
-                "dfq_bc_chain_phases"]
+DIAG_EXPORTS = ["dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline"]
 DIAG_LIB_PATH = PKG / "libdfq_diag.so"
 
 
@@ -169,8 +168,6 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_probe_stream": ([P, P, P, P, I64, I32, P], C.c_int),
         "dfq_debug_timeline": ([P, I64], C.c_int),
         "dfq_probe_lds": ([P, P, P, P, I64, I32, I32, P], C.c_int),
-        "dfq_probe_grid_barrier": ([I32, I32, I32, P, P], C.c_int),
-        "dfq_bc_chain_phases": ([C.POINTER(BcOp), I32, I64, C.POINTER(I32), C.POINTER(I32)], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -199,23 +199,28 @@ class _Snapshot(Mapping):
         return len(self._spans)
 
 
-def _snapshot(chain, tensors):
+def _snapshot(chain, tensors, which=0, keys=None):
     """{name: t.clone()} (bias_correction.py:196,255 clone each bias) in one
     buffer, filled by COPY ops recorded in the chain, so the copies run in walk
-    order with the rest of the chain's work."""
+    order with the rest of the chain's work.  (``which`` / ``keys``: the
+    snapshot's symbolic names for a recorded walk.)"""
     if not tensors:
         return {}
     vals = list(tensors.values())
     _lib.require_device(*vals)
     flat = torch.empty(sum(t.numel() for t in vals), dtype=torch.float32, device=vals[0].device)
     spans, off = {}, 0
-    for name, t in tensors.items():
+    for i, (name, t) in enumerate(tensors.items()):
         n = t.numel()
-        chain.copy(t, flat, off)
+        chain.copy(t, flat, off, (_S_BIAS, keys[i], 0) if keys else _NULL, (_S_SNAP, which, 0))
         spans[name] = (off, t.shape, n)
         off += n
     return _Snapshot(flat, spans)
 
+
+# symbolic address spaces of a recorded walk (_WalkTemplate): (space, key, float offset)
+_S_NONE, _S_BN_W, _S_BN_B, _S_BIAS, _S_E, _S_SCRATCH, _S_SNAP = range(7)
+_NULL = (_S_NONE, 0, 0)
 
 _BC_OP = np.dtype([("kind", "<i4"), ("flag", "<i4"), ("a", "<u8"), ("b", "<u8"), ("out", "<u8"), ("out2", "<u8"),
                    ("n", "<i8"), ("i2", "<i8"), ("f", "<i8")])
@@ -235,77 +240,95 @@ class _BcChain:
     propagate).  Expectations and bias vectors live in scratch chunks allocated
     as the walk goes, so every ref ``(tensor, float offset)`` is a device address
     at once and the recorded ops can be flushed at any point: the walk flushes
-    every ``_FLUSH_OPS`` ops between layers (the GPU then overlaps the rest of
-    the Python walk) and before it raises, so the ops before an error take
-    effect, as in the reference."""
+    once ``_FLUSH_OPS`` ops are recorded, at a BN node right after its
+    propagate (so a layer's expect / apply / propagate group reaches the library
+    in one call, which runs it as one launch), and before it raises, so the ops
+    before an error take effect, as in the reference.  Ops are recorded as rows
+    of plain integers (device addresses computed once, at record time)."""
 
-    def __init__(self, dev):
+    def __init__(self, dev, record=False):
         self.dev = dev
         self.ops = []
         self.keep = []          # tensors the recorded ops point into
         self._chunk = None      # current scratch chunk
+        self._base = 0          # its device address
         self._fill = 0          # floats used in it
         self._chunks = []       # chunks the unflushed ops point into
+        # record=True: every op also as a symbolic row (_WalkTemplate) -- its
+        # addresses as (space, key, float offset) -- and the flush points
+        self.sym = [] if record else None
+        self.flushes = []
+        self._nchunk = -1       # ordinal of the current scratch chunk
+        self.chunk_fill = []    # floats used per scratch chunk
 
     def alloc(self, n):
-        """A 256-B aligned scratch slot of n floats."""
+        """A 256-B aligned scratch slot of n floats: (chunk, offset, address)."""
         need = -(-n // 64) * 64
         if self._chunk is None or self._fill + need > self._chunk.numel():
             self._chunk = torch.empty(max(need, _SCRATCH_CHUNK), dtype=torch.float32, device=self.dev)
+            self._base = self._chunk.data_ptr()
             self._chunks.append(self._chunk)
             self._fill = 0
+            self._nchunk += 1
+            self.chunk_fill.append(0)
         off = self._fill
         self._fill += need
-        return (self._chunk, off)
+        self.chunk_fill[self._nchunk] = self._fill
+        return (self._chunk, off, self._base + 4 * off, (_S_SCRATCH, self._nchunk, off))
 
     def extend_last(self, ref, size, n):
         """Grow the most recent slot ``ref`` ([size] floats) by n (torch.cat):
         in place when its chunk has room, else into a fresh slot that a COPY op
         fills with the size floats already written.  Returns the slot's ref."""
-        t, off = ref
+        t, off, addr = ref
         assert t is self._chunk and self._fill == off + -(-size // 64) * 64, "cat target is not the last slot"
         need = -(-(size + n) // 64) * 64
         if off + need <= t.numel():
             self._fill = off + need
             return ref
         new = self.alloc(size + n)
-        self.ops.append((_lib.DFQ_BC_OP_COPY, 0, ref, None, new, None, size, 0, 0))
+        self._op((_lib.DFQ_BC_OP_COPY, 0, addr, 0, new[2], 0, size, 0, 0), (ref[3], _NULL, new[3], _NULL))
         return new
 
-    @staticmethod
-    def _ptr(ref):
-        t, off = ref
-        return t.data_ptr() + 4 * off
+    def _op(self, row, syms):
+        self.ops.append(row)
+        if self.sym is not None:
+            self.sym.append((row, syms))
 
-    def expect(self, bn, relu, dst, accumulate):
+    def expect(self, bn, relu, dst, accumulate, bn_key=None):
         w, b = _buf(bn, "fake_weight"), _buf(bn, "fake_bias")
         _lib.require_device(w, b)
         self.keep += [w, b]
-        self.ops.append((_lib.DFQ_BC_OP_EXPECT, int(bool(relu)) | (int(accumulate) << 1), (w, 0), (b, 0), dst, None,
-                         b.numel(), 0, 0))
+        self._op((_lib.DFQ_BC_OP_EXPECT, int(bool(relu)) | (int(accumulate) << 1), w.data_ptr(),
+                  b.data_ptr(), dst[2], 0, b.numel(), 0, 0),
+                 ((_S_BN_W, bn_key, 0), (_S_BN_B, bn_key, 0), dst[3], _NULL))
 
-    def apply(self, E, o, i2, expect, f, bias, vec):
+    def apply(self, E, o, i2, expect, f, bias, vec, key=None):
         # E: a ref (tensor, float offset); vec: a scratch slot only this chain's propagate reads
-        self.keep += [E[0], bias]
-        self.ops.append((_lib.DFQ_BC_OP_APPLY, _lib.DFQ_BC_APPLY_VEC_SCRATCH, E, expect, (bias, 0), vec, o, i2, f))
+        e, eoff = E
+        self.keep += [e, bias]
+        self._op((_lib.DFQ_BC_OP_APPLY, _lib.DFQ_BC_APPLY_VEC_SCRATCH, e.data_ptr() + 4 * eoff, expect[2],
+                  bias.data_ptr(), vec[2], o, i2, f),
+                 ((_S_E, key, 0), expect[3], (_S_BIAS, key, 0), vec[3]))
 
-    def propagate(self, vec, numel, fake_b, f):
+    def propagate(self, vec, numel, fake_b, f, bn_key=None):
         _lib.require_device(fake_b)
         self.keep.append(fake_b)
-        self.ops.append((_lib.DFQ_BC_OP_PROPAGATE, _lib.REF_THREADS, vec, None, (fake_b, 0), None, numel, 0, f))
+        self._op((_lib.DFQ_BC_OP_PROPAGATE, _lib.REF_THREADS, vec[2], 0, fake_b.data_ptr(), 0, numel, 0, f),
+                 (vec[3], _NULL, (_S_BN_B, bn_key, 0), _NULL))
 
-    def copy(self, src, dst, off):   # src / dst validated by the caller (_snapshot)
+    def copy(self, src, dst, off, src_sym=_NULL, dst_sym=_NULL):   # src / dst validated by the caller
         self.keep += [src, dst]
-        self.ops.append((_lib.DFQ_BC_OP_COPY, 0, (src, 0), None, (dst, off), None, src.numel(), 0, 0))
+        self._op((_lib.DFQ_BC_OP_COPY, 0, src.data_ptr(), 0, dst.data_ptr() + 4 * off, 0, src.numel(), 0, 0),
+                 (src_sym, _NULL, (dst_sym[0], dst_sym[1], off), _NULL))
 
     def flush(self, stream):
         if not self.ops:
             return
-        ptr = lambda ref: 0 if ref is None else self._ptr(ref)   # noqa: E731
-        # the op table as a numpy record array (layout of _lib.BcOp), filled row-wise
-        # from plain tuples instead of ctypes field by field
-        arr = np.array([(kind, flag, ptr(a), ptr(b), ptr(out), ptr(out2), n, i2, f)
-                        for (kind, flag, a, b, out, out2, n, i2, f) in self.ops], dtype=_BC_OP)
+        if self.sym is not None:
+            self.flushes.append(len(self.sym))
+        # the op table as a numpy record array (layout of _lib.BcOp) from the rows of integers
+        arr = np.array(self.ops, dtype=_BC_OP)
         failed = C.c_int32(-1)
         rc = _lib.load().dfq_bc_chain(arr.ctypes.data_as(C.POINTER(_lib.BcOp)), len(self.ops), C.byref(failed),
                                       stream)
@@ -331,7 +354,9 @@ def _record_branches(chain, bn_branch):
                 chain.expect(layer, relu_attached, ref, False)
             elif connect_type == "cat":   # torch.cat([cum, e]): e lands right after cum
                 ref = chain.extend_last(ref, size, n)
-                chain.expect(layer, relu_attached, (ref[0], ref[1] + size), False)
+                sym = ref[3]
+                chain.expect(layer, relu_attached, (ref[0], ref[1] + size, ref[2] + 4 * size,
+                                                    (sym[0], sym[1], sym[2] + size)), False)
                 size += n
             else:                          # cum += e (in place)
                 if n != size:
@@ -416,6 +441,8 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                             raise RuntimeError(f"shape '[-1, {f}]' is invalid for input of size {numel}")
                         chain.propagate(vec, numel, fake_b, f)
                         bias_prev = None
+                        if len(chain.ops) >= _FLUSH_OPS:   # the device starts on what is recorded so far
+                            chain.flush(stream)
                     continue
                 if isinstance(node, torch.nn.ReLU) and bot[0] in bn_module:
                     relu_attached[bot[0]] = True
@@ -441,8 +468,6 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                     b = _param(layer, "bias")
                     if b is not None:
                         after_src[layer_name] = b
-                    if len(chain.ops) >= _FLUSH_OPS:   # the device starts on what is recorded so far
-                        chain.flush(stream)
             after = _snapshot(chain, after_src)
         finally:   # the ops recorded before an error still take effect, as in the reference
             if chain.ops:

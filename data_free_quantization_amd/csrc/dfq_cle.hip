@@ -687,13 +687,10 @@ __device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t 
 // on consecutive floats, khw independent loads per row in flight -- instead of
 // one thread per column walking its khw floats serially.
 constexpr int kTileMaxKhw = 9;   // 3x3 (and 2x2); larger kernels keep the per-column walk
-// Rows per position-parallel rescale tile (<= kColTileRows); the diagnostics
-// library takes DFQ_CLE_POS_ROWS for the A/B.
-constexpr int kPosTileMaxRows = 4;   // a position tile's rows: their loads are in flight together
-static int64_t cle_pos_tile_rows() {
-    const char* e = ab_env("DFQ_CLE_POS_ROWS");
-    return e && *e ? std::max<int64_t>(1, std::min<int64_t>(kColTileRows, atoll(e))) : kPosTileMaxRows;
-}
+// Rows per position-parallel rescale tile (<= kColTileRows): their loads are in
+// flight together (16-row tiles took ~70 us a task on ResNet-50's 3x3 layers,
+// 4-row tiles ~11 us: profiles/r03/cle_tl_*.log)
+constexpr int kPosTileMaxRows = 4;
 
 __device__ __forceinline__ bool tile_by_position(const CleRel& R, const CleTask& tk) {
     return R.khw2 > 1 && R.khw2 <= kTileMaxKhw && (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
@@ -873,27 +870,13 @@ __device__ __forceinline__ void cle_range_body(const CleRel* __restrict__ rels, 
 }
 
 // `next` = 1: the ranges of the NEXT iteration (launched after this iteration's
-// last rescale, fused into the metric-tile launch; see cle_loop_tiles_range_kernel)
+// last rescale, fused into the metric-tile launch; see cle_loop_tiles_fin_kernel)
 __global__ void __launch_bounds__(kThreads)
 cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
                       uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int next) {
     __shared__ float tl[2 * kThreads * kTileMaxKhw];
     if (st->done) return;
     cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + next) & 1, blockIdx.x, gridDim.x, tl);
-}
-
-// The next iteration's ranges as a launch of their own, on a graph branch that runs
-// CONCURRENTLY with the metric tiles (cle_loop_tiles_fin_kernel with no range
-// blocks): each kernel keeps its own LDS footprint (18 KB here, 35 KB for the
-// tiles), so the range blocks no longer take tile-sized LDS slots.  par: the
-// next iteration's parity from the launch argument -- the concurrent stop rule
-// advances st->iters; a block that sees st->done skips (no later iteration).
-__global__ void __launch_bounds__(kThreads)
-cle_loop_range_par_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
-                          uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int par) {
-    __shared__ float tl[2 * kThreads * kTileMaxKhw];
-    if (st->done) return;
-    cle_range_body(rels, tasks, t0, t1, rng, M, par, blockIdx.x, gridDim.x, tl);
 }
 
 // The scale of relation R for channel c (mins / maxs: the parity's range words).
@@ -1280,31 +1263,17 @@ cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict
                         blockIdx.x, gridDim.x, A);
 }
 
-#ifdef DFQ_DIAGNOSTICS
-// the same capped at 128 VGPRs for 4 waves per SIMD (A/B: DFQ_CLE_APPLY_OCC4=1;
-// it spills, and measured no faster: profiles/r03/cle_ab_aa.jsonl)
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
-cle_loop_apply_occ4_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
-                           uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
-                           float eps, double smin, double smax) {
-    __shared__ CleApplyLds A;
-    if (st->done) return;
-    cle_apply_body(rels, tasks, t0, t1, rng, M, st->iters & 1, st->iters == 0, is_signed, eps, smin, smax,
-                   blockIdx.x, gridDim.x, A);
-}
-#endif
-
 // The metric's fp32 sums (torch.mean's vectorized_inner_sum over one chunk) as a
 // fixed tree.  A chunk of len elements is 32 streams (s = 8k + l: 8 vector lanes x
 // ILP 4; stream element i is chunk element 32i + s) of sz = len/32 elements, each
 // a 4-level cascade with 16-element level-0 blocks (step 2^4 for every chunk below
 // 16M elements).  One level-1 group of all 32 streams is 8192 CONTIGUOUS elements:
-//   * cle_loop_diff_tiles_kernel: one workgroup per 8192-element tile stages
-//     |W - snap| in LDS (snap := W on the way), 512 threads-worth of level-0 block
-//     sums, then 32 level-1 sums -> b1buf; the chunk's remainder (partial group,
-//     level-0 tail, row_sum tail vectors, scalar tail) is one more "tail tile";
-//   * cle_loop_diff_combine_kernel: one wave per chunk finishes the cascade in
-//     ATen's order (level 2/3, a0 += a1 += a2 += a3, ILP, lanes, scalar tail).
+//   * cle_tiles_body: one workgroup per 8192-element tile: |W - snap| (snap := W
+//     on the way), 512 threads-worth of level-0 block sums, then 32 level-1 sums
+//     -> b1buf; the chunk's remainder (partial group, level-0 tail, row_sum tail
+//     vectors, scalar tail) is one more "tail tile";
+//   * cle_chunk_sum_with: one wave per chunk finishes the cascade in ATen's order
+//     (level 2/3, a0 += a1 += a2 += a3, ILP, lanes, scalar tail).
 constexpr int kCleTile = 8192;            // 32 streams x 16 x 16
 constexpr int kCleTailWords = 64;         // per chunk: 32 stream partials, 24 row-tail, 8 scalar-tail values
 
@@ -1443,35 +1412,6 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
 constexpr int kCleTilesLds = kCleTile + kCleTailWords + 512;
 constexpr int kCleRangeLds = 2 * kThreads * kTileMaxKhw;
 
-__global__ void __launch_bounds__(kThreads)
-cle_loop_diff_tiles_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
-                           const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t nunits,
-                           float* __restrict__ b1buf, float* __restrict__ tailbuf, const CleState* __restrict__ st) {
-    __shared__ float lds[kCleTilesLds];
-    if (st->done) return;
-    cle_tiles_body(layers, chunks, b1off, units, nunits, b1buf, tailbuf, blockIdx.x, gridDim.x, lds,
-                   lds + kCleTile + kCleTailWords);
-}
-
-// The metric tiles of this iteration and the range launch of the next one in ONE
-// launch (fused schedule): both only read the weights the iteration's last rescale
-// wrote.  Blocks [0, ntb) take tiles, the rest the range tasks (parity iters + 1;
-// its resets clear this iteration's words, no longer read).
-__global__ void __launch_bounds__(kThreads)
-cle_loop_tiles_range_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
-                            const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t nunits,
-                            float* __restrict__ b1buf, float* __restrict__ tailbuf, int64_t ntb,
-                            const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
-                            uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st) {
-    __shared__ float lds[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
-    if (st->done) return;
-    if ((int64_t)blockIdx.x < ntb)
-        cle_tiles_body(layers, chunks, b1off, units, nunits, b1buf, tailbuf, blockIdx.x, ntb, lds,
-                       lds + kCleTile + kCleTailWords);
-    else
-        cle_range_body(rels, tasks, t0, t1, rng, M, (st->iters + 1) & 1, blockIdx.x - ntb, gridDim.x - ntb, lds);
-}
-
 // One chunk's sum from its tiles' level-1 sums and tail words (one wave; the
 // result on lane 0): the rest of the cascade, the ILP and lane combines and the
 // scalar tail, in ATen's order.  Coherent loads: other blocks wrote b1 / tb.
@@ -1529,39 +1469,6 @@ __device__ __forceinline__ float cle_tiny_chunk_sum(const CleLayer* __restrict__
         sn[e] = x;
         return dd;
     }, ch.len);
-}
-
-// One wave per chunk: part[layer][t] = 0 + the chunk's sum.
-__device__ __forceinline__ void cle_combine_body(const CleLayer* __restrict__ layers,
-                                                 const CleChunk* __restrict__ chunks, int64_t nchunks,
-                                                 const int64_t* __restrict__ b1off, const float* __restrict__ b1buf,
-                                                 const float* __restrict__ tailbuf, float* __restrict__ part,
-                                                 int32_t S, int64_t blk, int64_t nblk) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = blk * (kThreads / 64) + (threadIdx.x >> 6);
-    const int64_t nwaves = nblk * (kThreads / 64);
-    for (int64_t k = wave; k < nchunks; k += nwaves) {
-        const CleChunk ch = chunks[k];
-        const int64_t len = ch.len;
-        float fa = 0.f;
-        if (len < 8) {   // tiny chunk: scalar row_sum (no tiles ran for it)
-            if (lane == 0) fa = cle_tiny_chunk_sum(layers, ch);
-        } else {   // a later launch than the tiles: plain loads see their stores
-            const float* b1 = b1buf + b1off[k];
-            const float* tb = tailbuf + k * kCleTailWords;
-            fa = cle_chunk_sum_with(ch, [&](int64_t i) { return b1[i]; }, [&](int64_t i) { return tb[i]; }, lane);
-        }
-        if (lane == 0) part[(int64_t)ch.layer * S + ch.t] = 0.f + fa;   // buffer[t] starts at 0
-    }
-}
-
-__global__ void __launch_bounds__(kThreads)
-cle_loop_diff_combine_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks, int64_t nchunks,
-                             const int64_t* __restrict__ b1off, const float* __restrict__ b1buf,
-                             const float* __restrict__ tailbuf, float* __restrict__ part, int32_t S,
-                             const CleState* __restrict__ st) {
-    if (st->done) return;
-    cle_combine_body(layers, chunks, nchunks, b1off, b1buf, tailbuf, part, S, blockIdx.x, gridDim.x);
 }
 
 // numpy pairwise float64 sum (identity 0 + pairwise_sum), as np.sum(diff_list).
@@ -1668,14 +1575,6 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
     }
 }
 
-__global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32_t nl, const float* __restrict__ part,
-                                      int32_t S, double* __restrict__ means, double* __restrict__ hist,
-                                      CleState* __restrict__ st) {
-    __shared__ double sm[1024];   // the per-layer means, read back by one thread
-    if (st->done) return;
-    cle_final_body(layers, nl, part, S, means, hist, st, sm);
-}
-
 // The metric tiles (+ the next iteration's ranges) with the chunk combine and the
 // stop rule folded in: the block that finishes a chunk's last tile sums that
 // chunk, and the block that finishes the last chunk runs the stop rule -- two
@@ -1687,26 +1586,17 @@ __global__ void cle_loop_final_kernel(const CleLayer* __restrict__ layers, int32
 // rule).  The words handed over (level-1 sums, chunk tails, chunk sums) are
 // written with agent-coherent stores (st_coh) and read with agent-coherent loads
 // (ld_coh), and the caller has drained its stores (s_waitcnt vmcnt(0)) first.
-//   ordered = 0 (product): the sc1 hand-off form MI355X_MICROARCH.md lists as
-//     valid (section "visibility", Valid forms, table row 1; cdna_hip_programming.md
-//     Guideline 16): every handed-off word stored sc1 and drained by every storing
-//     wave before ONE lane's agent-scope counter add (behind the workgroup
-//     barrier), the workgroup whose add came last told by the returned value, and
-//     every load of the words an sc1 load to registers issued after that add
-//     returned (the other waves after a workgroup barrier).  No L2 write-back.
-//   ordered = 1 (diagnostics DFQ_CLE_ORDERED=1): the memory model's ordering --
-//     release on every arrival, acquire in the winner.  Each release writes the
-//     arriving block's XCD L2 back (buffer_wbl2): measured +2.7 ms (+50 %) on the
-//     MobileNetV2 loop with the round-2 schedule, same results.
-__device__ __forceinline__ bool handoff_arrive(uint32_t* c, uint32_t target, int ordered) {
-    const uint32_t a = ordered ? __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
-                               : __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = a == target;
-    if (last && ordered) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the invalidate completes before the barrier
-    }
-    return last;
+// The sc1 hand-off form MI355X_MICROARCH.md lists as valid (section "visibility",
+// Valid forms, table row 1; cdna_hip_programming.md Guideline 16): every
+// handed-off word stored sc1 and drained by every storing wave before ONE lane's
+// agent-scope counter add (behind the workgroup barrier), the workgroup whose add
+// came last told by the returned value, and every load of the words an sc1 load to
+// registers issued after that add returned (the other waves after a workgroup
+// barrier).  No L2 write-back.  (The memory model's release / acquire form gave the
+// same results 50 % slower: each release writes the arriving block's XCD L2 back,
+// profiles/r03/cle_ab_d.jsonl.)
+__device__ __forceinline__ bool handoff_arrive(uint32_t* c, uint32_t target) {
+    return __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == target;
 }
 
 struct CleFin {
@@ -1716,7 +1606,6 @@ struct CleFin {
     double* hist;
     int64_t nchunks, nbig;   // all chunks / chunks with tiles (len >= 8)
     int32_t S, nl;
-    int32_t ordered;   // hand-off ordering (handoff_arrive)
 };
 
 __global__ void __launch_bounds__(kThreads)
@@ -1749,7 +1638,7 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
     auto arrive = [&](uint32_t* c, uint32_t members) -> bool {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) flag = handoff_arrive(c, round * members - 1u, F.ordered);
+        if (threadIdx.x == 0) flag = handoff_arrive(c, round * members - 1u);
         __syncthreads();
         return flag != 0;
     };
@@ -1764,9 +1653,17 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
-        cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
-                                   stage_part ? lds + 2048 : nullptr);
+        if (F.nl <= 128)   // numpy's pairwise sum over the layer means is one leaf
+            cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
+                                       stage_part ? lds + 2048 : nullptr);
+        else
+            cle_final_body<false, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st,
+                                        reinterpret_cast<double*>(lds), stage_part ? lds + 2048 : nullptr);
     };
+    if (F.nbig == 0) {   // no chunk has tiles (tiny or no target layers): one block finishes
+        if (blockIdx.x == 0) finish();
+        return;
+    }
     const uint32_t fin_members = (uint32_t)F.nbig;
     auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1) {
         if (!arrive(F.cnt + un.chunk, (uint32_t)(nb1 + 1))) return;   // not the chunk's last tile
@@ -1794,388 +1691,6 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
     cle_tiles_body(layers, chunks, b1off, units, nunits, b1buf, tailbuf, blockIdx.x, ntb, lds,
                    lds + kCleTile + kCleTailWords, hook);
 }
-
-// ---------------------------------------------------------------------------
-// Chain-grouped iteration: ONE launch per CLE iteration.  Chains commute (no
-// tensor in common), so each chain gets its own group of blocks, sized to its
-// bytes, that runs the chain's relations in order with group-local barriers
-// (none for a one-block group), then the chain's next-iteration ranges and the
-// metric tiles of the chain's layers; the launch's last arrival runs the stop
-// rule (as cle_loop_tiles_fin_kernel).  A short chain no longer waits for the
-// longest one at every step, and an iteration is one kernel boundary instead of
-// steps + 1.
-//
-// Group barriers are monotone arrival counters (one 128-B line per group; the
-// b-th barrier of the run completes at (b + 1) x members): agent-scope release
-// before arriving, acquire after the wait.  The blocks of a group must be
-// co-resident: the plan caps the grid at the CU count (one block per CU at most,
-// whatever else shares the GPU), and a wait that exceeds ~1 s flags st->error
-// (the host reports it) instead of hanging.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kCleBarrierSpins = 1u << 20;
-
-// Wait until the counter at w reaches target (wrap-safe); ~1 s without progress
-// flags st->error and gives up (a fault cannot hang the GPU).
-__device__ __forceinline__ bool cle_spin_until(const uint32_t* w, uint32_t target, CleState* st) {
-    uint32_t spins = 0;
-    while ((int32_t)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > kCleBarrierSpins) {
-            __hip_atomic_store(&st->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
-        }
-    }
-    return true;
-}
-
-struct CleGroup {
-    int32_t blk0, nblk;     // blocks [blk0, blk0 + nblk)
-    int32_t nsteps;         // relations in the chain (0: a group of layers no relation touches)
-    int32_t step_off;       // index of the chain's first step bound in CleGroups::abound
-    int64_t r0, r1;         // next-iteration range tasks (fused schedule)
-    int64_t u0, u1;         // metric units of the chain's layers
-};
-
-struct CleGroups {
-    const CleGroup* groups;
-    const int32_t* group_of_blk;
-    const int64_t* abound;  // per chain: nsteps + 1 bounds into the apply task table
-    const CleTask* atasks;
-    const CleTask* rtasks;
-    uint32_t* gbar;         // [group * 32]: arrival counters
-    int32_t sync_mode;      // cle_group_sync mode (0 in the product)
-};
-
-// mode 1 (diagnostics timing A/B only, DFQ_CLE_GSYNC_NOFENCE=1): no fences --
-// results may be stale, it prices the fences
-__device__ __forceinline__ bool cle_group_sync(uint32_t* ctr, uint32_t target, CleState* st, int* flag,
-                                               int mode = 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (mode == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        else __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int good = cle_spin_until(ctr, target, st) ? 1 : 0;
-        if (mode == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the invalidate completes before the barrier
-        }
-        if (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
-        *flag = good;
-    }
-    __syncthreads();
-    return *flag != 0;
-}
-
-union CleGroupLds {
-    float tiles[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
-    CleApplyLds apply;
-};
-
-__global__ void __launch_bounds__(kThreads)
-cle_loop_group_kernel(CleGroups Gs, const CleRel* __restrict__ rels, uint32_t* __restrict__ rng, int64_t M,
-                      int is_signed, float eps, double smin, double smax, const CleLayer* __restrict__ layers,
-                      const CleChunk* __restrict__ chunks, const int64_t* __restrict__ b1off,
-                      const CleUnit* __restrict__ units, float* __restrict__ b1buf, float* __restrict__ tailbuf,
-                      CleFin F, CleState* __restrict__ st) {
-    __shared__ CleGroupLds L;
-    __shared__ int flag;
-    // read before this block's final arrival; the stop rule (which advances them)
-    // runs after every block of the launch has arrived
-    if (st->done) return;
-    const int32_t it = st->iters;
-    const uint32_t round = (uint32_t)it + 1u;
-    const int par = it & 1;
-    const CleGroup G = Gs.groups[Gs.group_of_blk[blockIdx.x]];
-    const int64_t blk = (int64_t)blockIdx.x - G.blk0, nblk = G.nblk;
-    uint32_t* ctr = Gs.gbar + 32 * (int64_t)Gs.group_of_blk[blockIdx.x];
-    // barriers per iteration: between steps, and before the post phase
-    const uint32_t per_it = (uint32_t)G.nsteps;
-    uint32_t nb = per_it * (uint32_t)it;
-    bool ok = true;
-    for (int32_t k = 0; k < G.nsteps && ok; ++k) {
-        const int64_t a0 = Gs.abound[G.step_off + k], a1 = Gs.abound[G.step_off + k + 1];
-        cle_apply_body(rels, Gs.atasks, a0, a1, rng, M, par, it == 0, is_signed, eps, smin, smax, blk, nblk, L.apply);
-        if (nblk > 1) {
-            ok = cle_group_sync(ctr, (++nb) * (uint32_t)nblk, st, &flag, Gs.sync_mode);
-        } else {
-            __syncthreads();
-        }
-    }
-    if (ok) {
-        // the chain's weights are final for this iteration: the next iteration's
-        // ranges (parity it + 1; its resets clear this iteration's words, no
-        // longer read) and the metric tiles of the chain's layers
-        cle_range_body(rels, Gs.rtasks, G.r0, G.r1, rng, M, par ^ 1, blk, nblk, L.tiles);
-        __syncthreads();
-    }
-    auto arrive = [&](uint32_t* c, uint32_t members) -> bool {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) flag = handoff_arrive(c, round * members - 1u, F.ordered);
-        __syncthreads();
-        return flag != 0;
-    };
-    auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1) {
-        if (!arrive(F.cnt + un.chunk, (uint32_t)(nb1 + 1))) return;   // not the chunk's last tile
-        const float* gb1 = b1buf + b1off[un.chunk];
-        const float* gtb = tailbuf + (int64_t)un.chunk * kCleTailWords;
-        const int64_t nw = 32 * nb1;
-        const bool staged = nw + kCleTailWords <= kCleTile;
-        float* lds = L.tiles;
-        if (staged) {
-            for (int64_t i = threadIdx.x; i < nw; i += kThreads) lds[i] = ld_coh(gb1 + i);
-            if (threadIdx.x < kCleTailWords) lds[nw + threadIdx.x] = ld_coh(gtb + threadIdx.x);
-        }
-        __syncthreads();
-        if (threadIdx.x < 64) {
-            const float fa = staged ? cle_chunk_sum_with(ch, [&](int64_t i) { return lds[i]; },
-                                                         [&](int64_t i) { return lds[nw + i]; }, threadIdx.x)
-                                    : cle_chunk_sum(ch, gb1, gtb, threadIdx.x);
-            if (threadIdx.x == 0) st_coh(F.part + (int64_t)ch.layer * F.S + ch.t, 0.f + fa);
-        }
-        __syncthreads();   // LDS is reused by the next unit
-    };
-    if (ok)
-        cle_tiles_body(layers, chunks, b1off, units + G.u0, G.u1 - G.u0, b1buf, tailbuf, blk, nblk, L.tiles,
-                       L.tiles + kCleTile + kCleTailWords, hook);
-    // every block arrives once (after its chunk hand-offs): the last one runs the
-    // stop rule (a block that saw st->error still arrives, so nothing hangs)
-    if (arrive(F.cnt + F.nchunks, gridDim.x)) {
-        if (threadIdx.x == 0 && F.nchunks > F.nbig)   // tiny chunks exist (none in the zoo's models)
-            for (int64_t k = 0; k < F.nchunks; ++k) {
-                const CleChunk c2 = chunks[k];
-                if (c2.len < 8) st_coh(F.part + (int64_t)c2.layer * F.S + c2.t, 0.f + cle_tiny_chunk_sum(layers, c2));
-            }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
-        cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(L.tiles),
-                                   stage_part ? L.tiles + 2048 : nullptr);
-        if (threadIdx.x == 0 && __hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            st->done = 1;
-    }
-}
-
-// Grid-barrier words of the persistent loop (layout below); the plan's tables
-// reserve them in every build.
-constexpr int kCleMaxXcd = 16;
-constexpr int kCleRegBar = 64 + 32 * 3 * kCleMaxXcd;   // the registration barrier's two words
-constexpr int kCleBarWords = kCleRegBar + 64;
-
-// The persistent loop is a diagnostics-library A/B (measured slower, see
-// cle_persist_grid): the product build does not compile it.
-#ifdef DFQ_DIAGNOSTICS
-// ---------------------------------------------------------------------------
-// Persistent loop (fused schedule): ONE cooperative launch runs up to `batch`
-// whole iterations -- every chain step's rescale, the metric tiles with the next
-// iteration's ranges, the chunk combine and the stop rule -- separated by grid
-// barriers instead of kernel boundaries, and leaves as soon as the stop rule
-// says so.  The grid is co-resident (hipLaunchCooperativeKernel), so the barrier
-// cannot deadlock; a barrier that still waits ~1 s flags st->error and every
-// block leaves (the host turns that into an error), so a fault cannot hang.
-// ---------------------------------------------------------------------------
-constexpr int kClePersistMaxSteps = 32;
-
-struct ClePersist {
-    const CleRel* rels;
-    const CleTask* rtasks;
-    const CleTask* atasks;
-    const CleLayer* layers;
-    const CleChunk* chunks;
-    const int64_t* b1off;
-    const CleUnit* units;
-    float* b1;
-    float* tail;
-    uint32_t* rng;
-    float* part;
-    double* means;
-    double* hist;
-    CleState* st;
-    uint32_t* bar;       // {arrivals, generation}
-    int64_t M, nchunks, nunits, r0, r1;
-    int64_t astep[kClePersistMaxSteps + 1];
-    int32_t steps, nl, is_signed, batch, slots;
-    float eps;
-    double smin, smax;
-};
-
-// Sense-reversing grid barrier: agent-scope release (this block's writes, the
-// XCD's L2 written back) before arriving, acquire after leaving.
-__device__ __forceinline__ bool cle_grid_sync(uint32_t* bar, uint32_t nblk, CleState* st) {
-    __shared__ int ok;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int good = 1;
-        // one release (L2 write-back) per block: the arrival RMW; the generation is
-        // read before it (no later block can bump it until this one has arrived)
-        const uint32_t gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t arrived = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (arrived == nblk - 1) {
-            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(bar + 1, gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            uint32_t spins = 0;
-            // relaxed polls: an acquire load would invalidate the XCD's L2 on every
-            // poll under the blocks still working; one acquire fence after the wait
-            while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > kCleBarrierSpins) {
-                    __hip_atomic_store(&st->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    good = 0;
-                    break;
-                }
-            }
-        }
-        if (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other blocks' writes
-        ok = good;
-    }
-    __syncthreads();
-    return ok != 0;
-}
-
-// Two-level barrier: one L2 write-back and one L2 invalidate per XCD per barrier
-// (what a kernel boundary costs), instead of one per block.  The blocks of an
-// XCD meet at that XCD's counter (their stores are in its L2 once vmcnt drains);
-// the last one to arrive writes the XCD's L2 back (agent release), meets the
-// other XCDs' last arrivals at the global counter, invalidates the XCD's L2
-// (agent acquire) and releases its XCD's blocks, which then acquire too (their
-// CU's L1; the L2 has no stale lines left by then).
-// Counters only grow (arrival k of barrier b is the last one iff it equals
-// (b + 1) * members - 1), so nothing is reset between barriers.
-// Words (uint32, one 128-B line each): [0] global arrivals, [32] global
-// generation, [64 + 32 x] XCD x arrivals, [64 + 32 (16 + x)] XCD x generation,
-// [64 + 32 (32 + x)] XCD x block count (registration), [kCleRegBar] the
-// registration barrier.
-
-struct CleXcdSync {
-    uint32_t* bar;
-    uint32_t xcc;        // this block's XCD
-    uint32_t members;    // blocks on this XCD
-    uint32_t nxcd;       // XCDs holding blocks
-    uint32_t count;      // barriers passed by this block
-};
-
-__device__ __forceinline__ uint32_t xcc_id() {
-    uint32_t x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    return x & (kCleMaxXcd - 1);
-}
-
-__device__ __forceinline__ bool cle_grid_sync_xcd(CleXcdSync& S, CleState* st) {
-    __shared__ int ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores are in the XCD's L2
-    __syncthreads();
-    const uint32_t b = ++S.count;
-    if (threadIdx.x == 0) {
-        int good = 1;
-        uint32_t* xa = S.bar + 64 + 32 * S.xcc;
-        uint32_t* xg = S.bar + 64 + 32 * (kCleMaxXcd + S.xcc);
-        const uint32_t a = __hip_atomic_fetch_add(xa, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (a == b * S.members - 1) {   // the XCD's last arrival
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");      // this XCD's L2 -> memory
-            const uint32_t ga = __hip_atomic_fetch_add(S.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (ga == b * S.nxcd - 1)
-                __hip_atomic_store(S.bar + 32, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-                good = cle_spin_until(S.bar + 32, b, st);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");      // drop this XCD's stale L2 lines
-            __hip_atomic_store(xg, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            good = cle_spin_until(xg, b, st);
-            // this CU's L1 (a workgroup-scope invalidate is a no-op outside
-            // threadgroup-split mode, so the agent-scope acquire)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-        if (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
-        ok = good;
-    }
-    __syncthreads();
-    return ok != 0;
-}
-
-union ClePersistLds {
-    float tiles[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
-    CleApplyLds apply;
-    double fin[1024];
-};
-
-__global__ void __launch_bounds__(kThreads) cle_persist_kernel(ClePersist P) {
-    __shared__ ClePersistLds L;
-    __shared__ uint32_t reg[2];
-    const int64_t blk = blockIdx.x, nblk = gridDim.x;
-    // registration: which XCD this block runs on, and how many blocks each XCD
-    // holds (one plain barrier; the bar words are zeroed before the launch)
-    CleXcdSync S{P.bar, xcc_id(), 0, 0, 0};
-    if (threadIdx.x == 0)
-        __hip_atomic_fetch_add(P.bar + 64 + 32 * (2 * kCleMaxXcd + S.xcc), 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    if (!cle_grid_sync(P.bar + kCleRegBar, (uint32_t)nblk, P.st)) return;
-    if (threadIdx.x == 0) {
-        uint32_t nx = 0;
-        for (int x = 0; x < kCleMaxXcd; ++x)
-            nx += __hip_atomic_load(P.bar + 64 + 32 * (2 * kCleMaxXcd + x), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT) ? 1 : 0;
-        reg[0] = __hip_atomic_load(P.bar + 64 + 32 * (2 * kCleMaxXcd + S.xcc), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        reg[1] = nx;
-    }
-    __syncthreads();
-    S.members = reg[0];
-    S.nxcd = reg[1];
-    for (int32_t it = 0; it < P.batch; ++it) {
-        // read after the last barrier (or before the launch): the same values in every block
-        const int32_t done = __hip_atomic_load(&P.st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int32_t iters = __hip_atomic_load(&P.st->iters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done) return;
-        const int par = iters & 1;
-        for (int32_t k = 0; k < P.steps; ++k) {
-            cle_apply_body(P.rels, P.atasks, P.astep[k], P.astep[k + 1], P.rng, P.M, par, iters == 0, P.is_signed,
-                           P.eps, P.smin, P.smax, blk, nblk, L.apply);
-            if (!cle_grid_sync_xcd(S, P.st)) return;
-        }
-        // the metric tiles and the next iteration's ranges: both only read what the
-        // last rescale wrote
-        if (P.nchunks > 0)
-            cle_tiles_body(P.layers, P.chunks, P.b1off, P.units, P.nunits, P.b1, P.tail, blk, nblk, L.tiles,
-                           L.tiles + kCleTile + kCleTailWords);
-        cle_range_body(P.rels, P.rtasks, P.r0, P.r1, P.rng, P.M, par ^ 1, blk, nblk, L.tiles);
-        if (!cle_grid_sync_xcd(S, P.st)) return;
-        if (P.nchunks > 0) {
-            cle_combine_body(P.layers, P.chunks, P.nchunks, P.b1off, P.b1, P.tail, P.part, P.slots, blk, nblk);
-            if (!cle_grid_sync_xcd(S, P.st)) return;
-        }
-        if (blk == 0) cle_final_body<true>(P.layers, P.nl, P.part, P.slots, P.means, P.hist, P.st, L.fin);
-        if (!cle_grid_sync_xcd(S, P.st)) return;
-    }
-}
-
-// Diagnostics: the persistent loop's grid barrier alone (nbar barriers, no work).
-// mode 0: the two-level XCD barrier; 1: the flat barrier (every block releases).
-__global__ void __launch_bounds__(kThreads) cle_barrier_probe_kernel(uint32_t* bar, CleState* st, int32_t nbar,
-                                                                     int32_t mode) {
-    __shared__ uint32_t reg[2];
-    CleXcdSync S{bar, xcc_id(), 0, 0, 0};
-    if (threadIdx.x == 0)
-        __hip_atomic_fetch_add(bar + 64 + 32 * (2 * kCleMaxXcd + S.xcc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!cle_grid_sync(bar + kCleRegBar, gridDim.x, st)) return;
-    if (threadIdx.x == 0) {
-        uint32_t nx = 0;
-        for (int x = 0; x < kCleMaxXcd; ++x)
-            nx += __hip_atomic_load(bar + 64 + 32 * (2 * kCleMaxXcd + x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1 : 0;
-        reg[0] = __hip_atomic_load(bar + 64 + 32 * (2 * kCleMaxXcd + S.xcc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        reg[1] = nx;
-    }
-    __syncthreads();
-    S.members = reg[0];
-    S.nxcd = reg[1];
-    for (int32_t i = 0; i < nbar; ++i) {
-        const bool ok = mode == 0 ? cle_grid_sync_xcd(S, st) : cle_grid_sync(bar + kCleRegBar + 32, gridDim.x, st);
-        if (!ok) return;
-    }
-}
-#endif
 
 }  // namespace dfq
 
@@ -2212,28 +1727,16 @@ struct dfq_cle_plan {
     void* d_tables = nullptr;       // every device table above: ONE allocation (unless pooled)
     bool pooled = false;            // the tables live in the device context's pool
     void* d_snap_owned = nullptr;   // snapshots when the caller passed no workspace
-    uint32_t* d_bar = nullptr;      // persistent loop's grid barrier words
     uint32_t* d_cnt = nullptr;      // tiles_fin arrival counters [nchunks + 1]
-    bool fin_fused = false;         // combine + stop rule folded into the tiles launch
     int64_t nbig = 0;               // chunks with tiles
-    int32_t persist_grid = -1;      // cooperative grid of the persistent loop (0: not usable; -1: not sized)
-    bool fork = false;              // ranges on a concurrent graph branch (diagnostics DFQ_CLE_FORK=1)
     int64_t ri0 = 0, ri1 = 0;       // fused: each iteration's range tasks (the rest come from the rescales)
     int dev = 0;
     struct CleAsync* async = nullptr;   // dfq_cle_plan_launch's worker and result
+    bool abandoned = false;             // join gave up waiting for the launched loop
 #ifdef DFQ_DIAGNOSTICS
     std::vector<CleRel> h_rels;
     std::vector<CleTask> h_atasks;
 #endif
-    // chain-grouped schedule (cle_loop_group_kernel): one launch per iteration
-    bool grouped = false;
-    int32_t ngroups = 0, group_grid = 0;
-    CleGroup* d_groups = nullptr;
-    int32_t* d_gblk = nullptr;
-    int64_t* d_gbound = nullptr;
-    CleTask* d_gat = nullptr;
-    CleTask* d_grt = nullptr;
-    uint32_t* d_gbar = nullptr;     // group barrier counters [group * 32]
 };
 
 // DFQ_CLE_TIMING: host-side phase times of create / run / destroy on stderr.
@@ -2253,8 +1756,6 @@ struct CleDeviceCtx {
     hipStream_t st = nullptr;
     CleState* h_state = nullptr;   // pinned: [0] the run's state, [1..2] the batch readback slots
     hipEvent_t ev[2] = {nullptr, nullptr};
-    hipStream_t side = nullptr;                    // the range launch's graph branch
-    hipEvent_t fork[2] = {nullptr, nullptr};       // fork / join of that branch
     // Table pool: one plan at a time keeps its tables here (device + pinned upload
     // mirror), so a plan costs no hipMalloc / hipFree (hipFree waits for the whole
     // device) and its upload is an async DMA on the loop stream.
@@ -2266,11 +1767,6 @@ struct CleDeviceCtx {
     hipEvent_t pool_ev = nullptr;                  // behind the last upload from h_pool
     double* d_hist = nullptr;                      // histories longer than the tables' kCleHistCap
     int64_t hist_cap = 0;
-    // The last captured batch graph and the launch arguments it was captured with:
-    // a plan whose launches are identical (same pooled tables, same counts) reuses
-    // it instead of capturing and instantiating its own (~100 us).
-    hipGraphExec_t gexec = nullptr;
-    std::vector<char> gkey;
     // asynchronous runs (dfq_cle_plan_launch): the signal word callers' streams
     // wait on, its last generation, the launched plan not yet joined
     void* sig = nullptr;
@@ -2291,17 +1787,11 @@ static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
     if (!ctx.st) {   // high priority: a hardware queue of its own (see dfq_cle_plan_launch)
         int least = 0, greatest = 0;
         e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-        if (ab_env("DFQ_CLE_PRIO_NORMAL")) greatest = 0;   // diagnostics A/B: a normal-priority loop stream
         if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx.st, hipStreamNonBlocking, greatest);
     }
     if (e == hipSuccess && !ctx.h_state) e = hipHostMalloc(&ctx.h_state, 3 * sizeof(CleState));
     for (int i = 0; i < 2 && e == hipSuccess; ++i)
         if (!ctx.ev[i]) e = hipEventCreateWithFlags(&ctx.ev[i], hipEventDisableTiming);
-#ifdef DFQ_DIAGNOSTICS   // the range launch's graph branch (DFQ_CLE_FORK A/B only)
-    if (e == hipSuccess && !ctx.side) e = hipStreamCreateWithFlags(&ctx.side, hipStreamNonBlocking);
-#endif
-    for (int i = 0; i < 2 && e == hipSuccess; ++i)
-        if (!ctx.fork[i]) e = hipEventCreateWithFlags(&ctx.fork[i], hipEventDisableTiming);
     if (e == hipSuccess && !ctx.pool_ev) e = hipEventCreateWithFlags(&ctx.pool_ev, hipEventDisableTiming);
     if (e == hipSuccess && !ctx.in_ev) e = hipEventCreateWithFlags(&ctx.in_ev, hipEventDisableTiming);
     return e;
@@ -2443,7 +1933,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     // rescale and r's W1 rescale become ONE task (kApplyDwBoth), and r no longer
     // needs W1 range words.  MobileNetV2: 5 rescale launches per iteration -> 3.
     std::vector<int32_t> dw_next(n_rel, -1);
-    if (fused && !ab_env("DFQ_CLE_NO_DW_PAIRS")) {
+    if (fused) {
         for (int32_t r = 0; r < n_rel; ++r) {
             const int32_t q = w1_src[r];
             if (q < 0 || R[q].dw_prev >= 0 || dw_next[q] >= 0) continue;
@@ -2511,7 +2001,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             // KH*KW > 1 tiles go position-parallel, a row at a time: fewer rows per
             // task, more tasks in flight (ResNet-50's 3x3 W2 tiles: 16 rows took
             // ~70 us, DFQ_CLE_TL); 1x1 tiles keep kColTileRows (loads issued together)
-            const int64_t rows = (c.khw2 > 1 && c.khw2 <= kTileMaxKhw) ? cle_pos_tile_rows() : kColTileRows;
+            const int64_t rows = (c.khw2 > 1 && c.khw2 <= kTileMaxKhw) ? kPosTileMaxRows : kColTileRows;
             for (int64_t a = 0; a < c.o2; a += rows)
                 for (int64_t i0 = 0; i0 < c.i2; i0 += kThreads)
                     out.push_back({r, kApplyW2Tile, a, std::min<int64_t>(a + rows, c.o2), i0,
@@ -2536,8 +2026,6 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             if (w1_src[r] < 0 && R[r].dw_prev < 0) R[r].w1_self = 1;
             if (dw_next[r] >= 0) R[r].w2_self = 1;
         }
-        if (ab_env("DFQ_CLE_NO_SELF_RANGES"))
-            for (int32_t r = 0; r < n_rel; ++r) R[r].w1_self = R[r].w2_self = 0;
         ri0 = (int64_t)rt.size();
         for (int64_t t = rstep[0]; t < rstep[1]; ++t) {
             const CleTask tk = rt[t];
@@ -2600,121 +2088,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 for (int64_t g = 0; g <= nb1; ++g) units.push_back(CleUnit{ci, (int32_t)g});
         }
     }
-    // Chain-grouped schedule (cle_loop_group_kernel): one group of blocks per
-    // chain, plus one for the layers no relation touches; units reordered so each
-    // group's metric units are contiguous.
-    std::vector<CleGroup> groups;
-    std::vector<int32_t> group_of_blk;
-    std::vector<int64_t> gbound;
-    std::vector<CleTask> gat, grt;
-    // A diagnostics A/B (DFQ_CLE_GROUPS=1): measured 2.3x SLOWER than the step
-    // launches on MobileNetV2 (15.2 vs 6.6 ms; profiles/r03/cle_grouped.md) -- one
-    // block per CU exposes the rescale tasks' dependent latencies that the step
-    // launches hide behind 8 blocks per CU, fences or not.
-    const char* ge = ab_env("DFQ_CLE_GROUPS");
-    bool grouped = ge && ge[0] == '1' && fused && n_targets <= 128 && !units.empty() &&
-                   !ab_env("DFQ_CLE_UNFUSED_FIN");
-    if (grouped) {
-        std::vector<int32_t> chain_id(n_rel, -1), root_chain(n_rel, -1);
-        int32_t nch = 0;
-        for (int32_t r = 0; r < n_rel; ++r) {
-            const int32_t c = find(r);
-            if (root_chain[c] < 0) root_chain[c] = nch++;
-            chain_id[r] = root_chain[c];
-        }
-        std::vector<int32_t> layer_group(n_targets, nch);   // nch: no relation touches it
-        for (int32_t l = 0; l < n_targets; ++l)
-            for (int32_t r = 0; r < n_rel; ++r)
-                if (targets[l] == R[r].w1 || targets[l] == R[r].w2) layer_group[l] = chain_id[r];
-        const int32_t ngroups = nch + 1;
-        std::vector<double> work(ngroups, 0.0);
-        groups.assign(ngroups, CleGroup{});
-        for (int32_t c = 0; c < ngroups; ++c) {
-            CleGroup& g = groups[c];
-            g.step_off = (int32_t)gbound.size();
-            gbound.push_back((int64_t)gat.size());
-            g.r0 = (int64_t)grt.size();
-            for (int32_t r = 0; r < n_rel; ++r) {
-                if (chain_id[r] != c) continue;
-                apply_tasks(r, gat);
-                gbound.push_back((int64_t)gat.size());
-                g.nsteps += 1;
-                rout = &grt;
-                w1_range_tasks(r);
-                w2_range_tasks(r);
-                rout = &rt;
-                const CleRel& q = R[r];
-                work[c] += 8.0 * (double)(q.c1 * q.len1 + q.o2 * q.i2 * q.khw2) + 4.0 * (double)(q.o2 * q.i2 * q.khw2);
-            }
-            g.r1 = (int64_t)grt.size();
-        }
-        // units by group (stable: a chunk's units stay in tile order)
-        std::vector<CleUnit> sorted;
-        sorted.reserve(units.size());
-        for (int32_t c = 0; c < ngroups; ++c) {
-            groups[c].u0 = (int64_t)sorted.size();
-            for (const CleUnit& u : units)
-                if (layer_group[chunks[u.chunk].layer] == c) {
-                    sorted.push_back(u);
-                    work[c] += 12.0 * (double)std::min<int64_t>(kCleTile, chunks[u.chunk].len);
-                }
-            groups[c].u1 = (int64_t)sorted.size();
-        }
-        units.swap(sorted);
-        // blocks: at most one per CU (co-residency of every group), one at least per
-        // non-empty group, the rest in proportion to the group's bytes
-        int dev = 0, cus = 0;
-        int64_t budget = 256;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-            budget = cus;
-        if (const char* e = ab_env("DFQ_CLE_GROUP_GRID")) budget = std::max<int64_t>(1, atoll(e));
-        std::vector<int64_t> nb(ngroups, 0);
-        double wsum = 0.0;
-        int64_t used = 0;
-        for (int32_t c = 0; c < ngroups; ++c)
-            if (work[c] > 0.0 || groups[c].u1 > groups[c].u0) {
-                nb[c] = 1;
-                ++used;
-                wsum += work[c];
-            }
-        if (used == 0 || used > budget) {
-            grouped = false;
-        } else {
-            const int64_t spare = budget - used;
-            std::vector<std::pair<double, int32_t>> rem;
-            int64_t given = 0;
-            for (int32_t c = 0; c < ngroups; ++c) {
-                if (!nb[c] || wsum <= 0.0) continue;
-                const double want = spare * work[c] / wsum;
-                const int64_t k = (int64_t)want;
-                nb[c] += k;
-                given += k;
-                rem.push_back({want - (double)k, c});
-            }
-            std::sort(rem.begin(), rem.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
-            for (size_t i = 0; i < rem.size() && given < spare; ++i, ++given) nb[rem[i].second] += 1;
-            for (int32_t c = 0; c < ngroups; ++c) {
-                groups[c].blk0 = (int32_t)group_of_blk.size();
-                groups[c].nblk = (int32_t)nb[c];
-                for (int64_t b = 0; b < nb[c]; ++b) group_of_blk.push_back(c);
-            }
-        }
-    }
-    if (grouped && cle_timing())
-        for (size_t c = 0; c < groups.size(); ++c)
-            fprintf(stderr, "DFQ_CLE_TIMING group %zu: blocks %d, steps %d, apply tasks %lld, range tasks %lld, units %lld\n",
-                    c, groups[c].nblk, groups[c].nsteps,
-                    (long long)(gbound[groups[c].step_off + groups[c].nsteps] - gbound[groups[c].step_off]),
-                    (long long)(groups[c].r1 - groups[c].r0), (long long)(groups[c].u1 - groups[c].u0));
-    // measured SLOWER (MobileNetV2 CLE 7.7 vs 4.7 ms, profiles/r03/cle_ab_l.jsonl): a
-    // parallel graph branch's fork / join costs more than the LDS slots it frees,
-    // so it is a diagnostics A/B (DFQ_CLE_FORK=1)
-    p->fork = ab_env("DFQ_CLE_FORK") != nullptr;
     (void)hipGetDevice(&p->dev);
-    p->grouped = grouped;
-    p->ngroups = (int32_t)groups.size();
-    p->group_grid = (int32_t)group_of_blk.size();
     p->nunits = (int64_t)units.size();
     p->M = M;
     p->nl = n_targets;
@@ -2757,20 +2131,13 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_means = T.add<double>(n_targets);
     const int64_t o_state = T.add<CleState>(1);
     const int64_t o_hist = T.add<double>(kCleHistCap);
-    const int64_t o_bar = T.add<uint32_t>(kCleBarWords);
     const int64_t o_cnt = T.add<uint32_t>((int64_t)chunks.size() + 1);
-    const int64_t o_groups = T.add<CleGroup>((int64_t)groups.size());
-    const int64_t o_gblk = T.add<int32_t>((int64_t)group_of_blk.size());
-    const int64_t o_gbound = T.add<int64_t>((int64_t)gbound.size());
-    const int64_t o_gat = T.add<CleTask>((int64_t)gat.size());
-    const int64_t o_grt = T.add<CleTask>((int64_t)grt.size());
-    const int64_t o_gbar = T.add<uint32_t>(32 * (int64_t)std::max<size_t>(groups.size(), 1));
     const double tm0 = now_us();
     char* base = nullptr;
     char* hblob = nullptr;
     CleDeviceCtx& ctx = cle_device_ctx(p->dev);
     e = hipSuccess;   // a busy pool leaves it untouched: the private path follows
-    if (!grouped) {   // the pool (the diagnostics-only grouped tables take the private path)
+    {   // the pool
         std::lock_guard<std::mutex> lock(ctx.mu);
         if (!ctx.pool_busy && (e = cle_ctx_ready(ctx)) == hipSuccess &&
             (e = hipEventSynchronize(ctx.pool_ev)) == hipSuccess) {
@@ -2818,16 +2185,6 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     } else if ((e = hipMemcpy(base, hblob, host_bytes, hipMemcpyHostToDevice)) != hipSuccess) {
         return fail(e);
     }
-    if (grouped) {   // the group tables sit after the device-only buffers: one more copy
-        const int64_t g0 = o_groups, g1 = o_gbar;
-        std::vector<char> gblob(g1 - g0, 0);
-        auto gput = [&](int64_t off, const auto& v) {
-            if (!v.empty()) std::memcpy(gblob.data() + (off - g0), v.data(), sizeof(v[0]) * v.size());
-        };
-        gput(o_groups, groups); gput(o_gblk, group_of_blk); gput(o_gbound, gbound); gput(o_gat, gat);
-        gput(o_grt, grt);
-        if ((e = hipMemcpy(base + g0, gblob.data(), g1 - g0, hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
-    }
     if (cle_timing())
         fprintf(stderr, "DFQ_CLE_TIMING create: hipMalloc %lld B %.1f us, copy %lld B %.1f us\n", (long long)T.total,
                 tm1 - tm0, (long long)host_bytes, now_us() - tm1);
@@ -2845,65 +2202,15 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->d_means = reinterpret_cast<double*>(base + o_means);
     p->d_state = reinterpret_cast<CleState*>(base + o_state);
     p->d_hist = p->d_hist_tables = reinterpret_cast<double*>(base + o_hist);
-    p->d_bar = reinterpret_cast<uint32_t*>(base + o_bar);
     p->d_cnt = reinterpret_cast<uint32_t*>(base + o_cnt);
-    p->d_groups = reinterpret_cast<CleGroup*>(base + o_groups);
-    p->d_gblk = reinterpret_cast<int32_t*>(base + o_gblk);
-    p->d_gbound = reinterpret_cast<int64_t*>(base + o_gbound);
-    p->d_gat = reinterpret_cast<CleTask*>(base + o_gat);
-    p->d_grt = reinterpret_cast<CleTask*>(base + o_grt);
-    p->d_gbar = reinterpret_cast<uint32_t*>(base + o_gbar);
     for (const auto& c : chunks) p->nbig += c.len >= 8 ? 1 : 0;
-    p->fin_fused = p->nunits > 0 && p->nbig > 0 && n_targets <= 128 && !ab_env("DFQ_CLE_UNFUSED_FIN");
     *out = p;
     return DFQ_OK;
-}
-
-// Hand-off ordering of the tiles / stop-rule arrivals (handoff_arrive): the
-// ISA's (0) in the product, the memory model's release/acquire (1) as a
-// diagnostics A/B (DFQ_CLE_ORDERED=1).
-static int32_t cle_ordered() {
-    const char* e = ab_env("DFQ_CLE_ORDERED");
-    return (e && e[0] == '1') ? 1 : 0;
-}
-
-// Everything cle_enqueue_iteration passes to a launch (and the launch shapes): a
-// graph captured for one plan replays another exactly when these are equal.
-static std::vector<char> cle_graph_key(const dfq_cle_plan* p) {
-    std::vector<char> k;
-    auto add = [&](const auto& v) {
-        const char* c = reinterpret_cast<const char*>(&v);
-        k.insert(k.end(), c, c + sizeof(v));
-    };
-    add(p->dev); add(p->grouped); add(p->steps); add(p->fused); add(p->fin_fused); add(p->fork);
-    add(p->ri0); add(p->ri1); add(p->nunits); add(p->nchunks); add(p->nbig); add(p->M); add(p->slots); add(p->nl);
-    add(p->is_signed); add(p->eps); add(p->smin); add(p->smax); add(p->group_grid);
-    add(p->d_rels); add(p->d_rtasks); add(p->d_atasks); add(p->d_layers); add(p->d_chunks); add(p->d_rng);
-    add(p->d_part); add(p->d_means); add(p->d_hist); add(p->d_state); add(p->d_units); add(p->d_b1off); add(p->d_b1);
-    add(p->d_tail); add(p->d_cnt); add(p->d_groups); add(p->d_gblk); add(p->d_gbound); add(p->d_gat); add(p->d_grt);
-    add(p->d_gbar); add(p->st);
-    add(p->rstep.size());
-    for (int64_t x : p->rstep) add(x);
-    add(p->astep.size());
-    for (int64_t x : p->astep) add(x);
-    const char* nf = ab_env("DFQ_CLE_GSYNC_NOFENCE");
-    add(cle_ordered()); add((int)(nf && nf[0] == '1'));
-    return k;
 }
 
 // One CLE iteration's launches (steps, metric, stop rule) on stream s.
 // j: the iteration's position in its graph batch (its parity is j & 1).
 static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
-    if (p->grouped) {   // the whole iteration in one launch
-        const char* nf = ab_env("DFQ_CLE_GSYNC_NOFENCE");
-        CleGroups Gs{p->d_groups, p->d_gblk, p->d_gbound, p->d_gat, p->d_grt, p->d_gbar, (nf && nf[0] == '1') ? 1 : 0};
-        CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
-        hipLaunchKernelGGL(cle_loop_group_kernel, dim3(p->group_grid), dim3(kThreads), 0, s, Gs, p->d_rels, p->d_rng,
-                           p->M, p->is_signed, p->eps, p->smin, p->smax, p->d_layers, p->d_chunks, p->d_b1off,
-                           p->d_units, p->d_b1, p->d_tail, F, p->d_state);
-        DFQ_LAUNCH_CHECK();
-        return DFQ_OK;
-    }
     // grid caps: 2,048 / 4,096 blocks (caps of 128-1,024 measured 4-150 % slower on MobileNetV2)
     // step / tile grid caps (A/B: DFQ_CLE_STEP_GRID / DFQ_CLE_TILE_GRID, diagnostics library)
     static const int64_t kStepGrid = [] {
@@ -2927,9 +2234,6 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         }
         if (a1 > a0) {
             auto kern = p->step_pos[k] ? cle_loop_apply_kernel<true> : cle_loop_apply_kernel<false>;
-#ifdef DFQ_DIAGNOSTICS
-            if (ab_env("DFQ_CLE_APPLY_OCC4")) kern = cle_loop_apply_occ4_kernel;
-#endif
             hipLaunchKernelGGL(kern, dim3((int)std::min<int64_t>(a1 - a0, kStepGrid)), dim3(kThreads), 0, s,
                                p->d_rels, p->d_atasks, a0, a1, p->d_rng, p->M, p->d_state, p->is_signed, p->eps,
                                p->smin, p->smax);
@@ -2937,58 +2241,13 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         }
     }
     const int64_t nr = p->fused ? p->ri1 - p->ri0 : 0;   // next iteration's range tasks
-    const int64_t ntb = std::min<int64_t>(p->nunits, kTileGrid), nrb = std::min<int64_t>(nr, kStepGrid);
-    if (p->fin_fused && p->fork && nrb > 0) {
-        // tiles + chunk combine + stop rule on s; the next ranges on the side stream,
-        // concurrently (fork / join by events: captured as parallel graph branches)
-        CleDeviceCtx& ctx = cle_device_ctx(p->dev);
-        DFQ_HIP_CHECK(hipEventRecord(ctx.fork[0], s));
-        DFQ_HIP_CHECK(hipStreamWaitEvent(ctx.side, ctx.fork[0], 0));
-        hipLaunchKernelGGL(cle_loop_range_par_kernel, dim3((int)nrb), dim3(kThreads), 0, ctx.side, p->d_rels,
-                           p->d_rtasks, p->ri0, p->ri1, p->d_rng, p->M, p->d_state, (j + 1) & 1);
-        DFQ_LAUNCH_CHECK();
-        CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
-        hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)ntb), dim3(kThreads), 0, s, p->d_layers,
-                           p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
-                           p->d_rtasks, p->rstep[0], p->rstep[0], p->d_rng, p->M, F, p->d_state, (j + 1) & 1);
-        DFQ_LAUNCH_CHECK();
-        DFQ_HIP_CHECK(hipEventRecord(ctx.fork[1], ctx.side));
-        DFQ_HIP_CHECK(hipStreamWaitEvent(s, ctx.fork[1], 0));
-        return DFQ_OK;
-    }
-    if (p->fin_fused) {   // tiles (+ ranges) + chunk combine + stop rule: one launch
-        CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, cle_ordered()};
-        hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
-                           p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
-                           p->d_rtasks, p->ri0, p->fused ? p->ri1 : p->ri0, p->d_rng, p->M, F,
-                           p->d_state, (j + 1) & 1);
-        DFQ_LAUNCH_CHECK();
-        return DFQ_OK;
-    }
-    if (p->nchunks > 0 && ntb > 0 && nrb > 0) {
-        hipLaunchKernelGGL(cle_loop_tiles_range_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
-                           p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
-                           p->d_rtasks, p->ri0, p->ri1, p->d_rng, p->M, p->d_state);
-        DFQ_LAUNCH_CHECK();
-    } else if (nrb > 0) {
-        hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)nrb), dim3(kThreads), 0, s, p->d_rels, p->d_rtasks,
-                           p->ri0, p->ri1, p->d_rng, p->M, p->d_state, 1);
-        DFQ_LAUNCH_CHECK();
-    }
-    if (p->nchunks > 0) {
-        if (ntb > 0 && nrb == 0) {
-            hipLaunchKernelGGL(cle_loop_diff_tiles_kernel, dim3((int)ntb), dim3(kThreads),
-                               0, s, p->d_layers, p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail,
-                               p->d_state);
-            DFQ_LAUNCH_CHECK();
-        }
-        hipLaunchKernelGGL(cle_loop_diff_combine_kernel, dim3((int)ceil_div(p->nchunks, (int64_t)(kThreads / 64))),
-                           dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_b1off, p->d_b1, p->d_tail,
-                           p->d_part, p->slots, p->d_state);
-        DFQ_LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(cle_loop_final_kernel, dim3(1), dim3(kThreads), 0, s, p->d_layers, p->nl, p->d_part, p->slots,
-                       p->d_means, p->d_hist, p->d_state);
+    const int64_t ntb = std::max<int64_t>(1, std::min<int64_t>(p->nunits, kTileGrid));
+    const int64_t nrb = std::min<int64_t>(nr, kStepGrid);
+    // tiles (+ ranges) + chunk combine + stop rule: one launch
+    CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl};
+    hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
+                       p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
+                       p->d_rtasks, p->ri0, p->fused ? p->ri1 : p->ri0, p->d_rng, p->M, F, p->d_state, (j + 1) & 1);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }
@@ -2999,43 +2258,6 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
 // 3.97 with 8 and 16 (profiles/r03/cle_ab_q.jsonl).
 constexpr int32_t kCleBatch = 4;
 static_assert(kCleBatch % 2 == 0, "the tiles/range launch's parity argument assumes even batches");
-// Iterations per batch: kCleBatch; the diagnostics library takes DFQ_CLE_BATCH
-// (rounded up to even) for the A/B.
-static int32_t cle_batch() {
-    const char* e = ab_env("DFQ_CLE_BATCH");
-    const int32_t b = e && *e ? std::max(2, atoi(e)) : kCleBatch;
-    return b + (b & 1);
-}
-constexpr int32_t kClePersistBatch = 256;   // persistent loop: iterations per cooperative launch
-
-// The persistent loop's co-resident grid (0 = use the graph path).  Measured
-// slower than the graph path (profiles/r02/cle_persistent.md: MobileNetV2 CLE
-// 7.7-8.7 ms against 4.8; an empty grid barrier costs 4.4-6.5 us, no less than a
-// kernel boundary inside a graph, and the fused kernel holds 177 VGPRs, 2 waves
-// per SIMD), so it is a diagnostics-library A/B only: DFQ_CLE_PERSIST_BPC=<blocks
-// per CU> turns it on there; the product library never takes it.
-static int32_t cle_persist_grid(dfq_cle_plan* p) {
-#ifndef DFQ_DIAGNOSTICS
-    (void)p;
-    return 0;
-#else
-    if (p->persist_grid >= 0) return p->persist_grid;
-    p->persist_grid = 0;
-    int bpc = 0;
-    if (const char* e = ab_env("DFQ_CLE_PERSIST_BPC")) bpc = atoi(e);
-    if (bpc <= 0 || !p->fused || p->nchunks <= 0 || p->steps > kClePersistMaxSteps || p->nl > 128) return 0;
-    int dev = 0, cus = 0, coop = 0, occ = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess || !coop) return 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(cle_persist_kernel),
-                                                     kThreads, 0) != hipSuccess || occ <= 0)
-        return 0;
-    p->persist_grid = cus * std::min(bpc, occ);
-    return p->persist_grid;
-#endif
-}
-
 // The context's history buffer for caps above the tables' kCleHistCap slots,
 // grown once (a launched run grows it before its caller's stream waits: hipFree
 // synchronises the whole device).
@@ -3089,7 +2311,6 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     }
     DFQ_HIP_CHECK(hipMemsetAsync(p->d_part, 0, sizeof(float) * p->slots * std::max(p->nl, 1), s));
     DFQ_HIP_CHECK(hipMemsetAsync(p->d_cnt, 0, sizeof(uint32_t) * (p->nchunks + 1), s));
-    if (p->grouped) DFQ_HIP_CHECK(hipMemsetAsync(p->d_gbar, 0, sizeof(uint32_t) * 32 * p->ngroups, s));
     if (p->nchunks > 0) {
         hipLaunchKernelGGL(cle_loop_snap_kernel, dim3((int)std::min<int64_t>(std::max<int64_t>(p->nunits, 1), 4096)),
                            dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_units, p->nunits);
@@ -3102,57 +2323,11 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
                            p->d_state, 0);
         DFQ_LAUNCH_CHECK();
     }
-#ifdef DFQ_DIAGNOSTICS
-    // Persistent loop (fused schedule): one cooperative launch per kClePersistBatch
-    // iterations, the stop rule read back once per launch.
-    if (!init.done && cle_persist_grid(p) > 0) {
-        (void)0;
-        ClePersist P{};
-        P.rels = p->d_rels; P.rtasks = p->d_rtasks; P.atasks = p->d_atasks; P.layers = p->d_layers;
-        P.chunks = p->d_chunks; P.b1off = p->d_b1off; P.units = p->d_units; P.b1 = p->d_b1; P.tail = p->d_tail;
-        P.rng = p->d_rng; P.part = p->d_part; P.means = p->d_means; P.hist = p->d_hist; P.st = p->d_state;
-        P.bar = p->d_bar;
-        P.M = p->M; P.nchunks = p->nchunks; P.nunits = p->nunits; P.r0 = p->rstep[0]; P.r1 = p->rstep[1];
-        for (int32_t k = 0; k <= p->steps; ++k) P.astep[k] = p->astep[k];
-        P.steps = p->steps; P.nl = p->nl; P.is_signed = p->is_signed; P.eps = p->eps; P.slots = p->slots;
-        P.smin = p->smin; P.smax = p->smax;
-        const double tl0 = now_us();
-        int32_t launched = 0;
-        while (!init.done && launched < max_iters) {
-            P.batch = std::min<int32_t>(kClePersistBatch, max_iters - launched);
-            DFQ_HIP_CHECK(hipMemsetAsync(p->d_bar, 0, sizeof(uint32_t) * kCleBarWords, s));
-            void* args[] = {&P};
-            DFQ_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(cle_persist_kernel),
-                                                     dim3(p->persist_grid), dim3(kThreads), args, 0, s));
-            launched += P.batch;
-            DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
-            DFQ_HIP_CHECK(hipStreamSynchronize(s));
-            init = *p->h_state;
-            if (init.error) {
-                set_last_hip_error(hipErrorLaunchTimeOut);
-                return DFQ_ERR_HIP;
-            }
-        }
-        if (cle_timing())
-            fprintf(stderr, "DFQ_CLE_TIMING run: persistent grid %d, loop %.1f us (%d iterations)\n",
-                    p->persist_grid, now_us() - tl0, init.iters);
-        if (iterations) *iterations = init.iters;
-        if (hist) {
-            hist->assign((size_t)std::max(init.iters, 0), 0.0);
-            if (init.iters > 0)
-                DFQ_HIP_CHECK(cle_copy_back(hist->data(), p->d_hist, sizeof(double) * init.iters, s));
-        }
-        return DFQ_OK;
-    }
-#endif
     // Batches of `batch` iterations (kernels of finished runs return at once: the
-    // stop rule lives in d_state), enqueued launch by launch.  Replaying the batch
-    // as a captured HIP graph measured slower even with the capture cached (CLE
-    // on MobileNetV2 4.75 vs 4.51 ms, profiles/r03/cle_ab_p.jsonl): the graph is the
-    // diagnostics A/B DFQ_CLE_GRAPH=1.
-    const char* ge = ab_env("DFQ_CLE_GRAPH");
-    const bool use_graph = ge && ge[0] == '1';
-    const int32_t batch = cle_batch();
+    // stop rule lives in d_state), enqueued launch by launch.  (Replaying the batch
+    // as a captured HIP graph measured slower even with the capture cached: CLE on
+    // MobileNetV2 4.75 vs 4.51 ms, profiles/r03/cle_ab_p.jsonl.)
+    const int32_t batch = kCleBatch;
 #ifdef DFQ_DIAGNOSTICS
     uint64_t* d_tl = nullptr;   // DFQ_CLE_TL: per rescale task timestamps (cle_apply_body)
     const int64_t n_at = p->astep.empty() ? 0 : p->astep.back();
@@ -3163,49 +2338,18 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
         DFQ_HIP_CHECK(hipStreamSynchronize(s));
     }
 #endif
-    const double tc0 = now_us();
-    bool reused = false;
-    if (use_graph && !init.done) {
-        std::vector<char> key = cle_graph_key(p);
-        key.insert(key.end(), reinterpret_cast<const char*>(&batch), reinterpret_cast<const char*>(&batch + 1));
-        reused = ctx.gexec && key == ctx.gkey;
-        if (!reused) {
-            if (ctx.gexec) (void)hipGraphExecDestroy(ctx.gexec);
-            ctx.gexec = nullptr;
-            ctx.gkey.clear();
-            DFQ_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-            int rc = DFQ_OK;
-            for (int32_t it = 0; it < batch && rc == DFQ_OK; ++it) rc = cle_enqueue_iteration(p, s, it);
-            hipGraph_t g = nullptr;
-            const hipError_t ec = hipStreamEndCapture(s, &g);
-            if (rc != DFQ_OK) {
-                if (g) (void)hipGraphDestroy(g);
-                return rc;
-            }
-            DFQ_HIP_CHECK(ec);
-            const hipError_t ei = hipGraphInstantiate(&ctx.gexec, g, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(g);
-            if (ei != hipSuccess) ctx.gexec = nullptr;
-            DFQ_HIP_CHECK(ei);
-            ctx.gkey = std::move(key);
-        }
-    }
-    const double tc1 = now_us();
     // One batch in flight ahead of the stop-rule check: batch k + 1 is enqueued
     // before the host waits for batch k's state, so the readback and the check
     // overlap the GPU's next batch instead of idling it (round 2: ~31 us per
     // batch boundary).  A batch enqueued after convergence runs as no-ops (every
     // kernel returns at st->done).  Its state copy goes to the other pinned slot.
+    const double tc1 = now_us();
     int32_t launched = 0;
     int slot = 0;
     auto enqueue_batch = [&](int sl) -> int {
-        if (use_graph) {
-            DFQ_HIP_CHECK(hipGraphLaunch(ctx.gexec, s));
-        } else {
-            for (int32_t it = 0; it < batch; ++it) {
-                const int rc = cle_enqueue_iteration(p, s, it);
-                if (rc != DFQ_OK) return rc;
-            }
+        for (int32_t it = 0; it < batch; ++it) {
+            const int rc = cle_enqueue_iteration(p, s, it);
+            if (rc != DFQ_OK) return rc;
         }
         launched += batch;
         DFQ_HIP_CHECK(hipMemcpyAsync(ctx.h_state + 1 + sl, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
@@ -3226,8 +2370,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     }
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
     if (cle_timing())
-        fprintf(stderr, "DFQ_CLE_TIMING run: capture+instantiate %.1f us%s, loop %.1f us (%d iterations launched)\n",
-                tc1 - tc0, reused ? " (graph reused)" : "", now_us() - tc1, launched);
+        fprintf(stderr, "DFQ_CLE_TIMING run: loop %.1f us (%d iterations launched)\n", now_us() - tc1, launched);
 #ifdef DFQ_DIAGNOSTICS
     if (d_tl) {   // per step: span, task durations, the slowest tasks
         std::vector<uint64_t> tl(4 * (size_t)n_at);
@@ -3333,14 +2476,17 @@ namespace dfq {
 // launch, sleeping between polls.  A CP wait packet (hipStreamWaitValue64) in
 // the caller's queue measured 1.8x slower loops (MobileNetV2 CLE 2.73 -> 4.97 ms:
 // the polling packet holds up the dispatch of the loop's queue), a running
-// one-wave kernel costs nothing.  Bounded: past `limit` ticks of the 100 MHz
-// clock it returns (the worker then reports the run failed, see kCleGateSeconds),
-// so a lost release can never hang the queue.
+// one-wave kernel costs nothing.  Bounded and fail-closed: past `limit` ticks of
+// the 100 MHz clock (kCleGateSeconds: never reached by a loop that is running --
+// a MobileNetV2 loop takes milliseconds) it traps instead of returning.  The
+// queue faults and the process aborts, so nothing the caller queued behind the
+// loop (absorption, the second fold, quantize, bias correction) ever runs on
+// weights the loop may still be rescaling; a lost release cannot hang the queue.
 __global__ void __launch_bounds__(64) cle_caller_gate_kernel(const uint64_t* sig, uint64_t gen, uint64_t limit) {
     if (threadIdx.x != 0) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > limit) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > limit) __builtin_trap();
         __builtin_amdgcn_s_sleep(32);
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
@@ -3351,14 +2497,16 @@ __global__ void __launch_bounds__(64) cle_caller_gate_kernel(const uint64_t* sig
 // The loop needs the host between batches (the stop rule is read back), so a
 // worker thread drives it on the context's stream while the caller's thread goes
 // on enqueueing the next stages on its own stream.  That stream waits, in the
-// device's command processor, for a per-device signal word the worker writes
-// behind the loop's last launch (hipStreamWaitValue64 / hipStreamWriteValue64):
-// no host sync between the stages, and nothing of the caller's stream runs
-// before the loop is done.  The loop stream is a high-priority stream: it gets a
-// hardware queue of its own (queues are pooled per priority), so the caller's
-// waiting queue can never hold the loop's launches back.
-// How long the caller's stream gate waits for a launched loop at most.
+// device, behind the gate kernel for a per-device signal word the worker writes
+// behind the loop's last launch (hipStreamWriteValue64): no host sync between
+// the stages, and nothing of the caller's stream runs before the loop is done.
+// The loop stream is a high-priority stream: it gets a hardware queue of its own
+// (queues are pooled per priority), so the caller's waiting queue can never hold
+// the loop's launches back.
+// How long the caller's stream gate waits for a launched loop at most (it traps
+// after that), and how long join waits on the host (then it reports the loop lost).
 static constexpr int kCleGateSeconds = 120;
+static constexpr int kCleJoinSeconds = kCleGateSeconds + 30;
 
 struct CleAsync {
     std::mutex m;
@@ -3392,17 +2540,13 @@ static void cle_worker_loop(CleWorker* w) {
     }
 }
 
-// The context's signal word (lazily allocated as HIP signal memory); 0 when the
-// device cannot make a stream wait on a value (callers then run synchronously).
-static hipError_t cle_signal_ready(CleDeviceCtx& ctx, int dev) {
+// The context's signal word (lazily allocated as HIP signal memory: the gate
+// kernel polls it, the worker writes it with hipStreamWriteValue64); when it
+// cannot be allocated, callers run synchronously.
+static hipError_t cle_signal_ready(CleDeviceCtx& ctx) {
     if (ctx.sig) return hipSuccess;
     if (ctx.sig_state < 0) return hipErrorNotSupported;
-    int ok = 0;
-    hipError_t e = hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev);
-    if (e != hipSuccess || !ok) {
-        ctx.sig_state = -1;
-        return e != hipSuccess ? e : hipErrorNotSupported;
-    }
+    hipError_t e = hipSuccess;
     void* sig = nullptr;
     if ((e = hipExtMallocWithFlags(&sig, sizeof(uint64_t), hipMallocSignalMemory)) != hipSuccess) {
         ctx.sig_state = -1;
@@ -3419,24 +2563,26 @@ static hipError_t cle_signal_ready(CleDeviceCtx& ctx, int dev) {
     return hipSuccess;
 }
 
-static void cle_async_join(dfq_cle_plan* p) {
-    if (!p || !p->async) return;
+// Waits for a launched run; false when it has not finished within `seconds`
+// (< 0: no limit).
+static bool cle_async_join(dfq_cle_plan* p, double seconds = -1.0) {
+    if (!p || !p->async) return true;
     CleAsync* a = p->async;
     std::unique_lock<std::mutex> l(a->m);
-    a->cv.wait(l, [a] { return a->done; });
+    if (seconds < 0) {
+        a->cv.wait(l, [a] { return a->done; });
+        return true;
+    }
+    return a->cv.wait_for(l, std::chrono::duration<double>(seconds), [a] { return a->done; });
 }
 
 extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t count, int32_t max_iters,
                                    void* stream) {
     if (!p || max_iters < 0 || p->async) return DFQ_ERR_INVALID;
-    // Diagnostics A/B paths that allocate, free, capture or instantiate inside the
-    // loop (graph replay, the task timeline, the persistent loop) may synchronise
-    // the whole device -- behind a caller's stream that waits for the loop: they
-    // take the blocking run (the product library reads no switches).
-    {
-        const char* g = ab_env("DFQ_CLE_GRAPH");
-        if ((g && g[0] == '1') || ab_env("DFQ_CLE_TL") || ab_env("DFQ_CLE_PERSIST_BPC")) return DFQ_ERR_UNSUPPORTED;
-    }
+    // The diagnostics task timeline allocates and frees inside the loop, which may
+    // synchronise the whole device -- behind a caller's stream that waits for the
+    // loop: it takes the blocking run (the product library reads no switches).
+    if (ab_env("DFQ_CLE_TL")) return DFQ_ERR_UNSUPPORTED;
     hipStream_t caller = static_cast<hipStream_t>(stream);
     CleDeviceCtx& ctx = cle_device_ctx(p->dev);
     // one launched loop per device at a time: the signal's generations then
@@ -3448,7 +2594,7 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
         std::lock_guard<std::mutex> lock(ctx.mu);
         DFQ_HIP_CHECK(hipSetDevice(p->dev));
         DFQ_HIP_CHECK(cle_ctx_ready(ctx));
-        const hipError_t es = cle_signal_ready(ctx, p->dev);
+        const hipError_t es = cle_signal_ready(ctx);
         if (es == hipErrorNotSupported) return DFQ_ERR_UNSUPPORTED;
         DFQ_HIP_CHECK(es);
         DFQ_HIP_CHECK(cle_hist_ready(ctx, max_iters));   // no hipFree in the worker
@@ -3457,16 +2603,11 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
         DFQ_HIP_CHECK(hipStreamWaitEvent(ctx.st, ctx.in_ev, 0));
         gen = ctx.gen + 1;
         // the caller's stream waits behind a gate kernel (cle_caller_gate_kernel);
-        // diagnostics A/Bs: DFQ_CLE_ASYNC_WAIT=value (the CP wait packet),
-        // DFQ_CLE_ASYNC_NOWAIT (no wait: timing only, for a caller that joins first)
-        const char* wv = ab_env("DFQ_CLE_ASYNC_WAIT");
-        if (wv && wv[0] == 'v') {
-            DFQ_HIP_CHECK(hipStreamWaitValue64(caller, ctx.sig, gen, hipStreamWaitValueGte, ~0ull));
-        } else if (!ab_env("DFQ_CLE_ASYNC_NOWAIT")) {
-            hipLaunchKernelGGL(cle_caller_gate_kernel, dim3(1), dim3(64), 0, caller,
-                               static_cast<const uint64_t*>(ctx.sig), gen, (uint64_t)kCleGateSeconds * 100000000ull);
-            DFQ_LAUNCH_CHECK();
-        }
+        // a CP wait packet (hipStreamWaitValue64) there measured 1.8x slower loops
+        // (profiles/r03/async_ab/)
+        hipLaunchKernelGGL(cle_caller_gate_kernel, dim3(1), dim3(64), 0, caller,
+                           static_cast<const uint64_t*>(ctx.sig), gen, (uint64_t)kCleGateSeconds * 100000000ull);
+        DFQ_LAUNCH_CHECK();
         ctx.gen = gen;
     }
     // from here on the caller's stream is held until the signal reaches gen: every
@@ -3485,10 +2626,14 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
             const char* m = dfq_last_hip_error();
             for (size_t i = 0; m && m[i] && i + 1 < sizeof(a->err); ++i) a->err[i] = m[i];
         }
+#ifdef DFQ_DIAGNOSTICS   // tests of the held caller stream (test_gpu_cle_plan.py): a late release
+        if (const char* d = ab_env("DFQ_CLE_TEST_RELEASE_DELAY_MS"))
+            std::this_thread::sleep_for(std::chrono::milliseconds(atoi(d)));
+#endif
         // release the caller's stream behind everything the loop enqueued
         hipError_t e = hipStreamWriteValue64(ctx.st, ctx.sig, gen, 0);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx.st);
-        if (e != hipSuccess) {   // never expected; the gate gives up at its time limit
+        if (e != hipSuccess) {   // never expected; the gate traps at its time limit
             fprintf(stderr, "dfq_cle_plan_launch: releasing the caller's stream failed (%s)\n", hipGetErrorString(e));
             if (rc == DFQ_OK) rc = DFQ_ERR_HIP;
         }
@@ -3534,7 +2679,19 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
 
 extern "C" int dfq_cle_plan_join(dfq_cle_plan* p, int32_t* iterations, double* diffs) {
     if (!p || !p->async) return DFQ_ERR_INVALID;
-    cle_async_join(p);
+    if (p->abandoned) return DFQ_ERR_HIP;
+    double limit = kCleJoinSeconds;
+#ifdef DFQ_DIAGNOSTICS
+    if (const char* j = ab_env("DFQ_CLE_TEST_JOIN_LIMIT_MS")) limit = atoi(j) * 1e-3;
+#endif
+    if (!cle_async_join(p, limit)) {
+        // The loop has not finished: the caller's stream stays held behind the gate
+        // (which traps at its own limit); the plan stays with the worker, which may
+        // still use it (destroy leaves it alone).
+        p->abandoned = true;
+        set_last_hip_error_text("the launched CLE loop did not finish in time; the caller's stream stays held");
+        return DFQ_ERR_HIP;
+    }
     CleDeviceCtx& ctx = cle_device_ctx(p->dev);
     if (ctx.pending == p) ctx.pending = nullptr;
     const CleAsync& a = *p->async;
@@ -3549,21 +2706,15 @@ extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t
     if (!p) return DFQ_ERR_INVALID;
     if (chains) *chains = p->chains;
     if (steps) *steps = p->steps;
-    if (launches) {   // per iteration: range + rescale launches, then the metric (2) and the stop rule
-        if (p->grouped)
-            *launches = 1;
-        else if (p->fin_fused)   // rescales (+ per-step ranges), then tiles + ranges + combine + stop rule
-            *launches = (p->fused ? p->steps : 2 * p->steps) + 1 +
-                        ((p->fused && p->fork && p->ri1 > p->ri0) ? 1 : 0);   // + the concurrent ranges
-        else
-            *launches = (p->fused ? p->steps + ((p->nunits > 0 && p->nchunks > 0) ? 0 : 1) : 2 * p->steps) +
-                        (p->nunits > 0 ? 1 : 0) + (p->nchunks > 0 ? 1 : 0) + 1;
-    }
+    // per iteration: the rescale launches (+ per-step range launches when the
+    // schedule is not fused), then tiles + next ranges + chunk combine + stop rule
+    if (launches) *launches = (p->fused ? p->steps : 2 * p->steps) + 1;
     return DFQ_OK;
 }
 
 extern "C" int dfq_cle_plan_destroy(dfq_cle_plan* p) {
     if (!p) return DFQ_OK;
+    if (p->abandoned) return DFQ_OK;   // its worker may still run it: left to the worker (leaked)
     if (p->async) {   // a launched run finishes first (its worker uses the plan)
         cle_async_join(p);
         CleDeviceCtx& ctx = cle_device_ctx(p->dev);
@@ -3575,25 +2726,6 @@ extern "C" int dfq_cle_plan_destroy(dfq_cle_plan* p) {
     return DFQ_OK;
 }
 
-#ifdef DFQ_DIAGNOSTICS
-#include "dfq_diag.h"
-extern "C" int dfq_probe_grid_barrier(int32_t nbar, int32_t blocks_per_cu, int32_t mode, void* ws, void* stream) {
-    if (!ws || nbar < 0 || blocks_per_cu < 1) return DFQ_ERR_INVALID;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    int dev = 0, cus = 0, occ = 0;
-    DFQ_HIP_CHECK(hipGetDevice(&dev));
-    DFQ_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    DFQ_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(cle_barrier_probe_kernel),
-                                                               kThreads, 0));
-    uint32_t* bar = static_cast<uint32_t*>(ws);
-    CleState* st = reinterpret_cast<CleState*>(bar + kCleBarWords + 64);
-    DFQ_HIP_CHECK(hipMemsetAsync(ws, 0, sizeof(uint32_t) * (kCleBarWords + 64) + sizeof(CleState), s));
-    void* args[] = {&bar, &st, &nbar, &mode};
-    DFQ_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(cle_barrier_probe_kernel),
-                                             dim3(cus * std::min(blocks_per_cu, occ)), dim3(kThreads), args, 0, s));
-    return DFQ_OK;
-}
-#endif
 
 namespace dfq {
 hipError_t preload_cle() {   // see dfq_preload

@@ -190,186 +190,79 @@ bc_propagate_kernel(const float* __restrict__ bias_vec, int64_t nrows, int64_t f
     }
 }
 
-#ifdef DFQ_DIAGNOSTICS
-// ---------------------------------------------------------------------------
-// The bias-correction chain as ONE cooperative launch (dfq_bc_chain).  The walk
-// is a serial chain -- layer L's expectation reads the BN fake_bias that layer
-// L-1's propagate wrote -- of tiny vector ops (MobileNetV2: 173 launches of
-// 3-7 us each, 1.5 ms end to end).  Here the host cuts the op list into phases
-// with no cross-block dependency inside a phase; phases are separated by a grid
-// barrier.  Inside a phase:
-//   * every block computes each EXPECT vector into its own LDS slot (block 0
-//     also stores it), so the APPLY that reads it needs no barrier;
-//   * a PROPAGATE of the bias_vec an APPLY of the same phase produced recomputes
-//     each element as E + expect (the same single fp32 add) instead of reading
-//     what other blocks wrote;
-//   * two APPLYs of one bias give row r to the same wave (program order).
-// Everything a later phase reads is stored / loaded agent-coherent (st_coh /
-// ld_coh: the sc1 hand-off form, drained before the barrier's counter add).
-// ---------------------------------------------------------------------------
-constexpr int kBcChainThreads = 512;
-constexpr int kBcChainWaves = kBcChainThreads / 64;
-constexpr int kBcSlotFloats = 8192;        // LDS for one phase's expectation vectors
-constexpr int64_t kBcChainScratch = 1024;  // per-wave cascade scratch (b0s; b1s = /16)
-constexpr uint32_t kBcChainSpins = 1u << 21;
 
-struct BcDevOp {
-    int32_t kind, flag;
-    const float* a;
-    const float* b;
-    float* out;
-    float* out2;
-    int64_t n, i2, f, bcols;
-    int32_t lds_out;    // EXPECT: LDS slot of out
-    int32_t lds_prev;   // EXPECT accumulate: LDS slot of the running sum (-1: load out)
-    int32_t lds_b;      // APPLY: LDS slot of the expectation (-1: load b)
-    int32_t virt;       // PROPAGATE: index of the APPLY whose bias_vec it sums (-1: load a)
-    int64_t wbase;      // APPLY / PROPAGATE: global wave of row / column 0
-    uint32_t dmagic;    // APPLY: k / bcols as umulhi(k, dmagic) + k >> dshift (k < 2^31)
-    uint32_t dshift;
+
+// One target layer of the bias-correction walk in ONE launch: the op group
+// EXPECT+ -> APPLY (-> PROPAGATE) that dfq_bc_chain records per layer
+// (bias_correction.py:170-172,196-213,231-251).  Every block first evaluates the
+// layer's expectation vector (the branch's BN terms summed in op order) into
+// LDS; blocks [0, apply_blocks) then take the APPLY rows (bias += mean_j
+// (E (+) expect)[o, j], bias_vec written), the rest the PROPAGATE columns of
+// bias_vec.view(-1, F) -- recomputing each element fl(E + expect) instead of
+// reading what the apply blocks store, so the two run in the same launch.
+// Same per-element values and the same reduction trees as bc_expect_kernel /
+// bc_apply_kernel / bc_propagate_kernel: bit-identical, one dependent launch
+// per layer instead of three (MobileNetV2: 173 -> 55 launches).
+constexpr int kBcMaxTerms = 8;
+constexpr int64_t kBcMaxExpect = 4096;
+struct BcLayerJob {
+    const float* ew[kBcMaxTerms];
+    const float* eb[kBcMaxTerms];
+    int32_t relu[kBcMaxTerms];
+    int32_t nterms;
+    int32_t threads;            // PROPAGATE: the reference run's intra-op threads
+    float* expect_out;          // the EXPECT ops' slot (written by block 0, as they would)
+    int64_t f;                  // expect numel
+    const float* E;
+    int64_t o, i2, bcols;
+    float* bias;
+    float* vec;                 // APPLY's bias_vec (may be null)
+    float* fake_b;              // PROPAGATE target (null: no PROPAGATE in the group)
+    int64_t F, nrows;
+    int64_t apply_blocks;
 };
 
-// One op of a phase, by this block.  Each handler loads its op from the table
-// itself: a by-value op struct passed down went to the stack (scratch).
-struct BcLds {
-    float* slots;
-    float* b0s;
-    float* b1s;
-    int lane;
-    int64_t nw, gw;
-    __device__ int64_t first(int64_t wbase) const { return (gw - wbase + nw) % nw; }   // wbase in [0, nw)
-};
-
-__device__ __forceinline__ void bc_op_expect(const BcDevOp* __restrict__ opp, BcLds L) {
-    const BcDevOp op = *opp;
-    const int acc = (op.flag >> 1) & 1;
-    for (int64_t j = threadIdx.x; j < op.n; j += kBcChainThreads) {
-        float v = bc_expect_value(ld_coh(op.a + j), ld_coh(op.b + j), op.flag & 1);
-        if (acc) v = (op.lds_prev >= 0 ? L.slots[op.lds_prev + j] : ld_coh(op.out + j)) + v;
-        L.slots[op.lds_out + j] = v;
-        if (blockIdx.x == 0) st_coh(op.out + j, v);
+__global__ void __launch_bounds__(kThreads) bc_layer_kernel(BcLayerJob J) {
+    __shared__ float ex[kBcMaxExpect];
+    __shared__ float scratch[kThreads / 64][kBcScratch + kBcScratch / 16];
+    for (int64_t j = threadIdx.x; j < J.f; j += kThreads) {
+        float v = bc_expect_value(J.ew[0][j], J.eb[0][j], J.relu[0]);
+        for (int t = 1; t < J.nterms; ++t) v = v + bc_expect_value(J.ew[t][j], J.eb[t][j], J.relu[t]);
+        ex[j] = v;
+        if (blockIdx.x == 0) J.expect_out[j] = v;
     }
-}
-
-__device__ __forceinline__ void bc_op_apply(const BcDevOp* __restrict__ opp, BcLds L) {
-    const BcDevOp op = *opp;
-    const float* __restrict__ E = op.a;
-    const int64_t i2 = op.i2, f = op.f, bcols = op.bcols;
-    const int lane = L.lane;
-    for (int64_t r = L.first(op.wbase); r < op.n; r += L.nw) {
-        auto get = [&](int64_t j) {
-            const int64_t q = f > 1 ? j : 0;
-            return E[r * i2 + (i2 > 1 ? j : 0)] + (op.lds_b >= 0 ? L.slots[op.lds_b + q] : ld_coh(op.b + q));
-        };
-        if (op.out2)   // (nullptr here: scratch every reader recomputes, bc_chain_plan)
-            for (int64_t j = lane; j < bcols; j += 64) st_coh(op.out2 + r * bcols + j, get(j));
-        const float sum = wave_inner_sum(get, bcols, lane);
-        if (lane == 0) st_coh(op.out + r, ld_coh(op.out + r) + sum / (float)bcols);
-    }
-}
-
-template <typename Get>
-__device__ __forceinline__ void bc_column(const BcDevOp& op, const BcLds& L, int64_t nrows, int64_t c, Get get) {
-    const float sum = aten_outer_col_is_cascade(nrows, op.f, c, op.flag)
-                          ? wave_cascade(get, nrows, L.lane, L.b0s, L.b1s, kBcChainScratch)
-                          : wave_row_sum(get, nrows, L.lane, L.b0s, L.b1s, kBcChainScratch);
-    if (L.lane == 0) st_coh(op.out + c, ld_coh(op.out + c) + (-sum) / (float)nrows);
-}
-
-// bias_vec[k] of the APPLY `src`, recomputed: E[row, j] + expect[j]
-__device__ __forceinline__ void bc_op_propagate_virt(const BcDevOp* __restrict__ opp, const BcDevOp* __restrict__ srcp,
-                                                  BcLds L) {
-    const BcDevOp op = *opp, src = *srcp;
-    const int64_t F = op.f, nrows = op.n / F;
-    const float* __restrict__ E = src.a;
-    const uint32_t sb = (uint32_t)src.bcols;   // numel < 2^31 on this path (host)
-    const uint32_t si2 = (uint32_t)src.i2;
-    const uint32_t emask = src.i2 > 1 ? ~0u : 0u, xmask = src.f > 1 ? ~0u : 0u;
-    const float* ex = L.slots + src.lds_b;     // forwarded only from an LDS expectation (host)
-    const uint32_t Fu = (uint32_t)F;
-    for (int64_t c = L.first(op.wbase); c < F; c += L.nw)
-        bc_column(op, L, nrows, c, [&](int64_t r) {
-            const uint32_t kk = (uint32_t)r * Fu + (uint32_t)c;
-            const uint32_t row = (uint32_t)(((uint64_t)__umulhi(kk, src.dmagic) + kk) >> src.dshift);
-            const uint32_t j = kk - row * sb;
-            return E[row * si2 + (j & emask)] + ex[j & xmask];
-        });
-}
-
-__device__ __forceinline__ void bc_op_propagate(const BcDevOp* __restrict__ opp, BcLds L) {
-    const BcDevOp op = *opp;
-    const int64_t F = op.f, nrows = op.n / F;
-    for (int64_t c = L.first(op.wbase); c < F; c += L.nw)
-        bc_column(op, L, nrows, c, [&](int64_t r) { return ld_coh(op.a + r * F + c); });
-}
-
-// member wbase of a run of copies: block wbase mod grid copies all of it
-__device__ __forceinline__ void bc_op_copy(const BcDevOp* __restrict__ opp) {
-    const BcDevOp op = *opp;
-    if (op.wbase % gridDim.x != blockIdx.x) return;
-    for (int64_t i = threadIdx.x; i < op.n; i += kBcChainThreads) st_coh(op.out + i, ld_coh(op.a + i));
-}
-
-__global__ void __launch_bounds__(kBcChainThreads)
-bc_chain_kernel(const BcDevOp* __restrict__ ops, const int32_t* __restrict__ phase, int32_t nphase,
-                uint32_t* bar, int32_t* err, uint64_t* tl) {
-    __shared__ float slots[kBcSlotFloats];
-    __shared__ float scratch[kBcChainWaves][kBcChainScratch + kBcChainScratch / 16];
-    __shared__ int flag;
-    BcLds L;
-    L.slots = slots;
-    L.lane = threadIdx.x & 63;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    L.b0s = scratch[wv];
-    L.b1s = L.b0s + kBcChainScratch;
-    L.nw = (int64_t)gridDim.x * kBcChainWaves;
-    L.gw = (int64_t)blockIdx.x * kBcChainWaves + wv;
-    for (int32_t p = 0; p < nphase; ++p) {
-        for (int32_t k = phase[p]; k < phase[p + 1]; ++k) {
-            const int32_t kind = ops[k].kind;
-            if (kind == DFQ_BC_OP_EXPECT) {
-                // an accumulating expectation reads only its own threads' slot words:
-                // one block barrier after the run of expectations
-                bc_op_expect(ops + k, L);
-                if (k + 1 == phase[p + 1] || ops[k + 1].kind != DFQ_BC_OP_EXPECT) __syncthreads();
-            } else if (kind == DFQ_BC_OP_APPLY) {
-                bc_op_apply(ops + k, L);
-            } else if (kind == DFQ_BC_OP_PROPAGATE) {
-                const int32_t virt = ops[k].virt;
-                if (virt >= 0) bc_op_propagate_virt(ops + k, ops + virt, L);
-                else bc_op_propagate(ops + k, L);
-            } else {
-                bc_op_copy(ops + k);
-            }
+    const bool ebc = J.i2 > 1, xbc = J.f > 1;
+    if ((int64_t)blockIdx.x < J.apply_blocks) {
+        const int64_t wave = (int64_t)blockIdx.x * (kThreads / 64) + wv;
+        const int64_t nwaves = J.apply_blocks * (kThreads / 64);
+        for (int64_t r = wave; r < J.o; r += nwaves) {
+            auto get = [&](int64_t j) { return J.E[r * J.i2 + (ebc ? j : 0)] + ex[xbc ? j : 0]; };
+            if (J.vec)
+                for (int64_t j = lane; j < J.bcols; j += 64) J.vec[r * J.bcols + j] = get(j);
+            const float sum = wave_inner_sum(get, J.bcols, lane);
+            if (lane == 0) J.bias[r] = J.bias[r] + sum / (float)J.bcols;
         }
-        if (tl && blockIdx.x == 0 && threadIdx.x == 0) tl[2 * p] = __builtin_amdgcn_s_memrealtime();
-        if (p + 1 == nphase) break;
-        // grid barrier: every store of this phase has completed before the one add
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t target = (uint32_t)(p + 1) * gridDim.x;
-            int good = 1;
-            uint32_t spins = 0;
-            while ((int32_t)(__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > kBcChainSpins) {   // never expected (co-resident grid): report, do not hang
-                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    good = 0;
-                    break;
-                }
-            }
-            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
-            flag = good;
-        }
-        __syncthreads();
-        if (tl && blockIdx.x == 0 && threadIdx.x == 0) tl[2 * p + 1] = __builtin_amdgcn_s_memrealtime();
-        if (!flag) return;
+        return;
+    }
+    float* b0s = scratch[wv];
+    float* b1s = b0s + kBcScratch;
+    const int64_t wave = ((int64_t)blockIdx.x - J.apply_blocks) * (kThreads / 64) + wv;
+    const int64_t nwaves = ((int64_t)gridDim.x - J.apply_blocks) * (kThreads / 64);
+    for (int64_t c = wave; c < J.F; c += nwaves) {
+        auto get = [&](int64_t r) {
+            const int64_t idx = r * J.F + c;
+            const int64_t row = idx / J.bcols, j = idx - row * J.bcols;
+            return J.E[row * J.i2 + (ebc ? j : 0)] + ex[xbc ? j : 0];
+        };
+        const float sum = aten_outer_col_is_cascade(J.nrows, J.F, c, J.threads)
+                              ? wave_cascade(get, J.nrows, lane, b0s, b1s, kBcScratch)
+                              : wave_row_sum(get, J.nrows, lane, b0s, b1s, kBcScratch);
+        if (lane == 0) J.fake_b[c] = J.fake_b[c] + (-sum) / (float)J.nrows;
     }
 }
-#endif  // DFQ_DIAGNOSTICS
-
 
 // ---------------------------------------------------------------------------
 // Activation ranges from BN statistics: set_quant_minmax,
@@ -1096,434 +989,88 @@ __global__ void __launch_bounds__(256) copy_batch_kernel(CopyBatch b) {
         dst[i] = src[i];
 }
 
-#ifdef DFQ_DIAGNOSTICS
 namespace dfq {
 namespace {
-struct BcRange {
-    uintptr_t lo = 0, hi = 0;
+struct Span {
+    uintptr_t lo, hi;
 };
-BcRange bc_rng(const void* p, int64_t floats) {
+Span span(const void* p, int64_t floats) {
     const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
-    return BcRange{lo, lo + 4 * (uintptr_t)std::max<int64_t>(floats, 0)};
+    return Span{lo, lo + 4 * (uintptr_t)std::max<int64_t>(floats, 0)};
 }
-bool bc_ov(const BcRange& x, const BcRange& y) { return x.lo < x.hi && y.lo < y.hi && x.lo < y.hi && y.lo < x.hi; }
-bool bc_eq(const BcRange& x, const BcRange& y) { return x.lo == y.lo && x.hi == y.hi; }
-bool bc_in(const BcRange& x, const BcRange& y) { return y.lo <= x.lo && x.hi <= y.hi; }
-
-// Phases of a validated chain for bc_chain_kernel (rules at the kernel).
-// Returns 0, or -1: the chain does something this path does not forward (an op
-// that aliases itself, E written earlier in the chain, an expectation larger than
-// the LDS slots, 2^31+ elements) and runs as per-op launches instead; or k + 1:
-// retry with a phase break forced before op k (an accumulating expectation met a
-// conflict after its running sum's first term: that term moves to the new phase
-// with it -- 'add' branches whose second BN was just propagated into).
-int bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, const std::vector<char>& force,
-                    std::vector<BcDevOp>& dev, std::vector<int32_t>& phase) {
-    enum { kPlain, kSlot, kBias, kVec };
-    struct Wr {
-        BcRange r;
-        int kind;
-        int32_t op;   // index into dev
-    };
-    struct Slot {
-        BcRange r;
-        int32_t off;
-        bool read;   // an APPLY of this phase read it (a rewrite would change what a recompute sees)
-        int32_t src; // the op (index into ops) that started it
-    };
-    std::vector<Wr> wr;
-    std::vector<BcRange> rd;   // this phase's global reads
-    std::vector<Slot> slot, prev_slot;
-    int32_t top = 0;
-    int64_t wcur = 0;
-    dev.clear();
-    phase.assign(1, 0);
-    auto hits_wr = [&](const BcRange& r) {
-        for (const Wr& w : wr)
-            if (bc_ov(w.r, r)) return true;
-        return false;
-    };
-    auto hits_rd = [&](const BcRange& r) {
-        for (const BcRange& x : rd)
-            if (bc_ov(x, r)) return true;
-        return false;
-    };
-    auto find_slot = [&](const BcRange& r) -> Slot* {
-        for (Slot& s : slot)
-            if (bc_in(r, s.r)) return &s;
-        return nullptr;
-    };
-    constexpr int64_t kMax = (int64_t)1 << 31;
-    for (int32_t k = 0; k < n_ops; ++k) {
-        const dfq_bc_op& op = ops[k];
-        if ((op.kind == DFQ_BC_OP_EXPECT || op.kind == DFQ_BC_OP_COPY) && op.n == 0) continue;
-        if (force[k] && phase.back() != (int32_t)dev.size()) {
-            phase.push_back((int32_t)dev.size());
-            wr.clear(); rd.clear(); slot.clear();
-            top = 0;
-            wcur = 0;
-        }
-        BcDevOp d{};
-        d.kind = op.kind; d.flag = op.flag; d.a = op.a; d.b = op.b; d.out = op.out; d.out2 = op.out2;
-        d.n = op.n; d.i2 = op.i2; d.f = op.f;
-        d.lds_out = d.lds_prev = d.lds_b = d.virt = -1;
-        // this op's footprint
-        std::vector<BcRange> reads, writes;
-        BcRange rmw{};
-        if (op.kind == DFQ_BC_OP_EXPECT) {
-            if (op.n > kBcSlotFloats) return -1;
-            reads = {bc_rng(op.a, op.n), bc_rng(op.b, op.n)};
-            writes = {bc_rng(op.out, op.n)};
-        } else if (op.kind == DFQ_BC_OP_APPLY) {
-            d.bcols = (op.i2 == op.f || op.f == 1) ? op.i2 : op.f;
-            if (op.n * op.i2 >= kMax || op.n * d.bcols >= kMax) return -1;
-            // round-up magic for k / bcols: l = ceil(log2 bcols), m = 2^32 (2^l - bcols) / bcols + 1
-            uint32_t l = 0;
-            while (((uint64_t)1 << l) < (uint64_t)d.bcols) ++l;
-            d.dshift = l;
-            d.dmagic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - (uint64_t)d.bcols)) / (uint64_t)d.bcols + 1);
-            const BcRange E = bc_rng(op.a, op.n * op.i2);   // written by no op (bc_chain_plan checks)
-            reads = {E, bc_rng(op.b, op.f)};
-            rmw = bc_rng(op.out, op.n);
-            writes = {rmw};
-            if (op.out2) writes.push_back(bc_rng(op.out2, op.n * d.bcols));
-        } else if (op.kind == DFQ_BC_OP_PROPAGATE) {
-            if (op.n >= kMax) return -1;
-            reads = {bc_rng(op.a, op.n)};
-            rmw = bc_rng(op.out, op.f);
-            writes = {rmw};
-        } else {
-            reads = {bc_rng(op.a, op.n)};
-            writes = {bc_rng(op.out, op.n)};
-        }
-        for (const BcRange& w : writes) {   // an op that aliases itself
-            for (const BcRange& r : reads)
-                if (bc_ov(w, r)) return -1;
-            for (const BcRange& w2 : writes)
-                if (&w != &w2 && bc_ov(w, w2)) return -1;
-        }
-        // try to join the current phase; on a conflict start a new one and retry
-        for (int attempt = 0;; ++attempt) {
-            bool ok = true;
-            std::vector<BcRange> grd;   // global (non-forwarded) reads of this op
-            int64_t wb = -1;
-            if (op.kind == DFQ_BC_OP_EXPECT) {
-                const BcRange o = writes[0];
-                Slot* s = nullptr;
-                for (Slot& x : slot)
-                    if (bc_eq(x.r, o)) s = &x;
-                if ((op.flag >> 1) & 1) {
-                    // the running sum from another phase would be read by every block while
-                    // block 0 rewrites it: not forwarded
-                    if (!s && attempt > 0) {   // the first term stayed behind: move it here
-                        for (const Slot& x : prev_slot)
-                            if (bc_eq(x.r, o) && !force[x.src]) return x.src + 1;
-                        return -1;
-                    }
-                    if (s) d.lds_prev = s->off;
-                    else ok = false;
-                }
-                if (s && s->read) ok = false;
-                grd.push_back(reads[0]);
-                grd.push_back(reads[1]);
-                for (const BcRange& r : grd) ok = ok && !hits_wr(r);
-                // the write: the same slot again (accumulate) or a fresh one
-                for (const Wr& w : wr)
-                    if (bc_ov(w.r, o) && !(s && w.kind == kSlot && bc_eq(w.r, o))) ok = false;
-                ok = ok && !hits_rd(o);
-                if (ok) {
-                    if (s) d.lds_out = s->off;
-                    else if (top + op.n <= kBcSlotFloats) {
-                        d.lds_out = top;
-                        slot.push_back(Slot{o, top, false, k});
-                        top += (int32_t)((op.n + 15) / 16 * 16);
-                    } else ok = false;
-                }
-            } else if (op.kind == DFQ_BC_OP_APPLY) {
-                Slot* s = find_slot(reads[1]);
-                if (s) d.lds_b = s->off + (int32_t)((reads[1].lo - s->r.lo) / 4);
-                else grd.push_back(reads[1]);
-                grd.push_back(reads[0]);
-                for (const BcRange& r : grd) ok = ok && !hits_wr(r);
-                // bias: only an earlier APPLY of the same bias (same row owners)
-                for (const Wr& w : wr)
-                    if (bc_ov(w.r, rmw)) {
-                        if (w.kind == kBias && bc_eq(w.r, rmw)) wb = dev[w.op].wbase;
-                        else ok = false;
-                    }
-                ok = ok && !hits_rd(rmw);
-                if (writes.size() > 1) ok = ok && !hits_wr(writes[1]) && !hits_rd(writes[1]);
-                if (ok) {
-                    if (wb < 0) {
-                        wb = wcur;
-                        wcur = (wcur + op.n) % nw;
-                    }
-                    d.wbase = wb;   // (its bias read needs no entry: every writer checks the write list)
-                    if (s) s->read = true;
-                }
-            } else if (op.kind == DFQ_BC_OP_PROPAGATE) {
-                d.virt = -1;
-                for (const Wr& w : wr)   // the recompute takes the expectation from LDS
-                    if (w.kind == kVec && bc_eq(w.r, reads[0]) && dev[w.op].lds_b >= 0) d.virt = w.op;
-                if (d.virt < 0) {
-                    grd.push_back(reads[0]);
-                    ok = ok && !hits_wr(reads[0]);
-                } else {   // the recompute reads that APPLY's E (and its LDS expectation)
-                    grd.push_back(bc_rng(dev[d.virt].a, dev[d.virt].n * dev[d.virt].i2));
-                }
-                ok = ok && !hits_wr(rmw) && !hits_rd(rmw);
-                if (ok) {
-                    d.wbase = wcur;
-                    wcur = (wcur + op.f) % nw;
-                }
-            } else {
-                grd.push_back(reads[0]);
-                ok = !hits_wr(reads[0]) && !hits_wr(writes[0]) && !hits_rd(writes[0]);
-                // position in this phase's run of consecutive copies: run member j is
-                // block j mod grid's alone (the copies are independent)
-                if (ok) d.wbase = (!dev.empty() && phase.back() < (int32_t)dev.size() &&
-                                   dev.back().kind == DFQ_BC_OP_COPY) ? dev.back().wbase + 1 : 0;
-            }
-            if (ok) {
-                const int32_t me = (int32_t)dev.size();
-                for (const BcRange& r : grd) rd.push_back(r);
-                if (op.kind == DFQ_BC_OP_EXPECT) wr.push_back(Wr{writes[0], kSlot, me});
-                else if (op.kind == DFQ_BC_OP_APPLY) {
-                    wr.push_back(Wr{writes[0], kBias, me});
-                    if (writes.size() > 1) wr.push_back(Wr{writes[1], kVec, me});
-                } else wr.push_back(Wr{writes[0], kPlain, me});
-                dev.push_back(d);
-                break;
-            }
-            if (attempt > 0 || phase.back() == (int32_t)dev.size()) return -1;   // conflicts with nothing
-            phase.push_back((int32_t)dev.size());
-            prev_slot.swap(slot);
-            wr.clear(); rd.clear(); slot.clear();
-            top = 0;
-            wcur = 0;
-            d.lds_out = d.lds_prev = d.lds_b = d.virt = -1;
-        }
-    }
-    if (phase.back() != (int32_t)dev.size()) phase.push_back((int32_t)dev.size());
-    return dev.empty() ? -1 : 0;
-}
-
-// An APPLY whose bias_vec is chain scratch (DFQ_BC_APPLY_VEC_SCRATCH) and whose
-// every reader is a propagate that recomputes it (virt) writes no bias_vec.
-void bc_drop_scratch_vecs(std::vector<BcDevOp>& dev) {
-    const int32_t n = (int32_t)dev.size();
-    for (int32_t j = 0; j < n; ++j) {
-        BcDevOp& ap = dev[j];
-        if (ap.kind != DFQ_BC_OP_APPLY || !(ap.flag & DFQ_BC_APPLY_VEC_SCRATCH) || !ap.out2) continue;
-        const BcRange v = bc_rng(ap.out2, ap.n * ap.bcols);
-        bool read = false;
-        for (int32_t k = j + 1; k < n && !read; ++k) {
-            const BcDevOp& o = dev[k];
-            if (o.kind == DFQ_BC_OP_PROPAGATE && o.virt == j) continue;
-            const int64_t na = o.kind == DFQ_BC_OP_APPLY ? o.n * o.i2 : o.n;
-            const int64_t nb = o.kind == DFQ_BC_OP_APPLY ? o.f : o.n;
-            const int64_t no = o.kind == DFQ_BC_OP_PROPAGATE ? o.f : o.n;
-            read = bc_ov(v, bc_rng(o.a, na)) || (o.b && bc_ov(v, bc_rng(o.b, nb))) || bc_ov(v, bc_rng(o.out, no));
-        }
-        if (!read) ap.out2 = nullptr;
-    }
-}
-
-// The chain's phases, in one planner pass.  Before it, on the whole op list:
-//   * no APPLY's E may overlap anything an op writes (E is loaded without
-//     coherence): one sorted sweep instead of a check per pair;
-//   * the first term of every accumulated expectation ('add' branch) starts a
-//     phase, so its running sum never stays behind in an earlier phase.
-// A second pass with the one break the planner still asks for is the rare case.
-bool bc_chain_plan(const dfq_bc_op* ops, int32_t n_ops, int64_t nw, std::vector<BcDevOp>& dev,
-                   std::vector<int32_t>& phase) {
-    std::vector<std::pair<BcRange, int>> iv;   // (range, 0 = E / 1 = written)
-    std::vector<char> force(n_ops, 0);
-    for (int32_t k = 0; k < n_ops; ++k) {
-        const dfq_bc_op& op = ops[k];
-        switch (op.kind) {
-            case DFQ_BC_OP_EXPECT:
-                iv.push_back({bc_rng(op.out, op.n), 1});
-                if ((op.flag >> 1) & 1)   // its first term: the latest plain expectation into the same slot
-                    for (int32_t j = k - 1; j >= 0; --j)
-                        if (ops[j].kind == DFQ_BC_OP_EXPECT && ops[j].out == op.out) {
-                            if (!((ops[j].flag >> 1) & 1)) {
-                                force[j] = 1;
-                                break;
-                            }
-                        }
-                break;
-            case DFQ_BC_OP_APPLY: {
-                const int64_t bcols = (op.i2 == op.f || op.f == 1) ? op.i2 : op.f;
-                iv.push_back({bc_rng(op.a, op.n * op.i2), 0});
-                iv.push_back({bc_rng(op.out, op.n), 1});
-                if (op.out2) iv.push_back({bc_rng(op.out2, op.n * bcols), 1});
-                break;
-            }
-            case DFQ_BC_OP_PROPAGATE: iv.push_back({bc_rng(op.out, op.f), 1}); break;
-            default: iv.push_back({bc_rng(op.out, op.n), 1}); break;
-        }
-    }
-    std::sort(iv.begin(), iv.end(), [](const auto& x, const auto& y) { return x.first.lo < y.first.lo; });
-    uintptr_t hi_e = 0, hi_w = 0;   // furthest end of the E / written ranges seen so far
-    for (const auto& [r, w] : iv) {
-        if (r.lo == r.hi) continue;
-        if (w ? r.lo < hi_e : r.lo < hi_w) return false;   // an E overlaps a write
-        (w ? hi_w : hi_e) = std::max(w ? hi_w : hi_e, r.hi);
-    }
-    for (int pass = 0; pass < 4; ++pass) {
-        const int r = bc_chain_phases(ops, n_ops, nw, force, dev, phase);
-        if (r == 0) {
-            bc_drop_scratch_vecs(dev);
-            return true;
-        }
-        if (r < 0 || force[r - 1]) return false;
-        force[r - 1] = 1;
-    }
-    return false;
-}
-
-// Per-device state of the cooperative chain: the device table (op table, phase
-// offsets, barrier counter, error word) and its pinned mirror.  The call waits
-// for its launch, so one buffer per device serves every call.
-struct BcChainCtx {
-    std::mutex mu;
-    char* dbuf = nullptr;
-    char* hbuf = nullptr;
-    size_t cap = 0;
-    int grid = 0;      // default grid
-    int max_grid = 0;  // co-resident blocks (cooperative launch limit)
-};
-BcChainCtx& bc_chain_ctx(int dev) {
-    static std::mutex m;
-    static std::vector<BcChainCtx*> v;
-    std::lock_guard<std::mutex> lk(m);
-    if ((int)v.size() <= dev) v.resize(dev + 1, nullptr);
-    if (!v[dev]) v[dev] = new BcChainCtx();
-    return *v[dev];
-}
-
-constexpr int kBcNotEligible = 1;   // internal: run the per-op launches
-double bc_now_us() {
-    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
-int bc_chain_coop(const dfq_bc_op* ops, int32_t n_ops, hipStream_t s) {
-    const bool timing = ab_env("DFQ_BC_TIMING") != nullptr;   // diagnostics: host phase times on stderr
-    const double t0 = timing ? bc_now_us() : 0.0;
-    int dev = 0;
-    DFQ_HIP_CHECK(hipStreamGetDevice(s, &dev));
-    BcChainCtx& ctx = bc_chain_ctx(dev);
-    std::lock_guard<std::mutex> lock(ctx.mu);
-    if (ctx.grid == 0) {   // blocks that can be co-resident, capped: the phases are latency-bound
-        int cus = 0, per = 0;
-        DFQ_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        DFQ_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per, reinterpret_cast<const void*>(bc_chain_kernel), kBcChainThreads, 0));
-        ctx.max_grid = std::max(1, cus * per);
-        ctx.grid = std::min(ctx.max_grid, 64);
-    }
-    int grid = ctx.grid;
-    if (const char* g = ab_env("DFQ_BC_GRID")) grid = std::max(1, std::min(ctx.max_grid, atoi(g)));
-    std::vector<BcDevOp> dv;
-    std::vector<int32_t> ph;
-    if (!bc_chain_plan(ops, n_ops, (int64_t)grid * kBcChainWaves, dv, ph)) return kBcNotEligible;
-    const double t1 = timing ? bc_now_us() : 0.0;
-    const int32_t nphase = (int32_t)ph.size() - 1;
-    auto up256 = [](size_t b) { return (b + 255) / 256 * 256; };
-    const size_t o_ph = up256(sizeof(BcDevOp) * dv.size());
-    const size_t o_bar = o_ph + up256(sizeof(int32_t) * ph.size());
-    // diagnostics DFQ_BC_TIMELINE=1: block 0's 100 MHz clock at each phase end and
-    // barrier exit, printed per phase to stderr after the call
-    const bool timeline = ab_env("DFQ_BC_TIMELINE") != nullptr;
-    const size_t o_tl = o_bar + 256;
-    const size_t need = o_tl + (timeline ? sizeof(uint64_t) * 2 * (size_t)nphase : 0);
-    if (ctx.cap < need) {
-        if (ctx.dbuf) (void)hipFree(ctx.dbuf);
-        if (ctx.hbuf) (void)hipHostFree(ctx.hbuf);
-        ctx.dbuf = ctx.hbuf = nullptr;
-        ctx.cap = 0;
-        const size_t cap = std::max<size_t>(need * 2, 64 << 10);
-        DFQ_HIP_CHECK(hipMalloc(&ctx.dbuf, cap));
-        DFQ_HIP_CHECK(hipHostMalloc(&ctx.hbuf, cap, hipHostMallocDefault));
-        ctx.cap = cap;
-    }
-    std::memcpy(ctx.hbuf, dv.data(), sizeof(BcDevOp) * dv.size());
-    std::memcpy(ctx.hbuf + o_ph, ph.data(), sizeof(int32_t) * ph.size());
-    std::memset(ctx.hbuf + o_bar, 0, 256);   // barrier counter, error word
-    DFQ_HIP_CHECK(hipMemcpyAsync(ctx.dbuf, ctx.hbuf, need, hipMemcpyHostToDevice, s));
-    const BcDevOp* d_ops = reinterpret_cast<const BcDevOp*>(ctx.dbuf);
-    const int32_t* d_ph = reinterpret_cast<const int32_t*>(ctx.dbuf + o_ph);
-    uint32_t* d_bar = reinterpret_cast<uint32_t*>(ctx.dbuf + o_bar);
-    int32_t* d_err = reinterpret_cast<int32_t*>(ctx.dbuf + o_bar + 128);
-    uint64_t* d_tl = timeline ? reinterpret_cast<uint64_t*>(ctx.dbuf + o_tl) : nullptr;
-    // A plain launch: hipLaunchCooperativeKernel measured ~1 ms of launch overhead
-    // per call (MobileNetV2 BC stage 2.70 vs 2.13 ms with a 1.07 ms kernel,
-    // profiles/r03/bc_ab_q.jsonl).  The grid (<= 64 blocks, one per CU by its LDS
-    // and VGPRs, at most the occupancy limit) fits on the device at once, so every
-    // block becomes resident even beside other work (the spinning ones hold <= 64
-    // CUs); a barrier that still waits ~1 s reports an error instead of hanging.
-    const char* cl = ab_env("DFQ_BC_COOPLAUNCH");   // diagnostics A/B: the cooperative launch
-    if (cl && cl[0] == '1') {
-        void* args[] = {&d_ops, &d_ph, const_cast<int32_t*>(&nphase), &d_bar, &d_err, &d_tl};
-        DFQ_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(bc_chain_kernel), dim3(grid),
-                                                 dim3(kBcChainThreads), args, 0, s));
-    } else {
-        hipLaunchKernelGGL(bc_chain_kernel, dim3(grid), dim3(kBcChainThreads), 0, s, d_ops, d_ph, nphase, d_bar, d_err,
-                           d_tl);
-        DFQ_LAUNCH_CHECK();
-    }
-    int32_t* h_err = reinterpret_cast<int32_t*>(ctx.hbuf + o_bar + 128);
-    DFQ_HIP_CHECK(hipMemcpyAsync(h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    const double t2 = timing ? bc_now_us() : 0.0;
-    DFQ_HIP_CHECK(hipStreamSynchronize(s));
-    if (timing)
-        fprintf(stderr, "DFQ_BC_TIMING ops %d phases %d grid %d: plan %.1f us, upload+launch %.1f us, wait %.1f us\n",
-                n_ops, nphase, grid, t1 - t0, t2 - t1, bc_now_us() - t2);
-    if (*h_err) {
-        set_last_hip_error(hipErrorLaunchTimeOut);
-        return DFQ_ERR_HIP;
-    }
-    if (timeline) {
-        std::vector<uint64_t> t(2 * (size_t)nphase);
-        DFQ_HIP_CHECK(hipMemcpy(t.data(), d_tl, sizeof(uint64_t) * t.size(), hipMemcpyDeviceToHost));
-        uint64_t prev = 0;
-        for (int32_t q = 0; q < nphase; ++q) {
-            std::string kinds;
-            for (int32_t k = ph[q]; k < ph[q + 1]; ++k) kinds += "EAPC"[dv[k].kind];
-            const double work = q == 0 ? 0.0 : (double)(t[2 * q] - prev) * 0.01;
-            const double bar = q + 1 < nphase ? (double)(t[2 * q + 1] - t[2 * q]) * 0.01 : 0.0;
-            fprintf(stderr, "DFQ_BC_TIMELINE phase %d ops %s work %.2f us barrier %.2f us\n", q, kinds.c_str(), work,
-                    bar);
-            prev = t[2 * q + 1];
-        }
-    }
-    return DFQ_OK;
-}
+bool overlap(const Span& x, const Span& y) { return x.lo < x.hi && y.lo < y.hi && x.lo < y.hi && y.lo < x.hi; }
 }  // namespace
-}  // namespace dfq
 
-#include "dfq_diag.h"
-extern "C" int dfq_bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t waves, int32_t* n_phases,
-                                   int32_t* op_phase) {
-    if (n_ops < 0 || (n_ops > 0 && !ops) || waves < 1) return DFQ_ERR_INVALID;
-    std::vector<dfq::BcDevOp> dv;
-    std::vector<int32_t> ph;
-    if (!dfq::bc_chain_plan(ops, n_ops, waves, dv, ph)) return 1;
-    if (n_phases) *n_phases = (int32_t)ph.size() - 1;
-    if (op_phase) {   // dev ops are the non-empty ops in order
-        int32_t j = 0, p = 0;
-        for (int32_t k = 0; k < n_ops; ++k) {
-            const bool empty = (ops[k].kind == DFQ_BC_OP_EXPECT || ops[k].kind == DFQ_BC_OP_COPY) && ops[k].n == 0;
-            if (empty) { op_phase[k] = -1; continue; }
-            while (p + 1 < (int32_t)ph.size() && ph[p + 1] <= j) ++p;
-            op_phase[k] = p;
-            ++j;
-        }
+// ops[k..] as one layer group for bc_layer_kernel: EXPECT (plain) [+ EXPECT
+// (accumulate) ...] into one slot, the APPLY reading that slot, and optionally
+// the PROPAGATE of that APPLY's bias_vec right after it.  Returns the ops used,
+// or 0 (the ops then run one launch each).  Fused only when no op of the group
+// writes what another one reads (the launch has no order inside it).
+int32_t bc_layer_group(const dfq_bc_op* ops, int32_t n_ops, int32_t k, BcLayerJob& J) {
+    const dfq_bc_op& e0 = ops[k];
+    if (e0.kind != DFQ_BC_OP_EXPECT || (e0.flag & 2) || e0.n <= 0 || e0.n > kBcMaxExpect) return 0;
+    int32_t m = k;
+    J.nterms = 0;
+    while (m < n_ops && ops[m].kind == DFQ_BC_OP_EXPECT && ops[m].out == e0.out && ops[m].n == e0.n &&
+           (m == k || (ops[m].flag & 2))) {
+        if (J.nterms == kBcMaxTerms) return 0;
+        J.ew[J.nterms] = ops[m].a;
+        J.eb[J.nterms] = ops[m].b;
+        J.relu[J.nterms] = ops[m].flag & 1;
+        ++J.nterms;
+        ++m;
     }
-    return DFQ_OK;
+    if (m >= n_ops) return 0;
+    const dfq_bc_op& ap = ops[m];
+    if (ap.kind != DFQ_BC_OP_APPLY || ap.b != e0.out || ap.f != e0.n) return 0;
+    if (!(ap.i2 == ap.f || ap.f == 1 || ap.i2 == 1)) return 0;   // the launches report the shape error
+    J.f = e0.n;
+    J.expect_out = e0.out;
+    J.E = ap.a;
+    J.o = ap.n;
+    J.i2 = ap.i2;
+    J.bcols = (ap.i2 == ap.f || ap.f == 1) ? ap.i2 : ap.f;
+    J.bias = ap.out;
+    J.vec = ap.out2;
+    J.apply_blocks = std::min<int64_t>(ceil_div(J.o, (int64_t)4), 2048);
+    int32_t used = m - k + 1;
+    const dfq_bc_op* pr = (m + 1 < n_ops) ? &ops[m + 1] : nullptr;
+    if (pr && pr->kind == DFQ_BC_OP_PROPAGATE && ap.out2 && pr->a == ap.out2 && pr->n == J.o * J.bcols &&
+        pr->f > 0 && pr->n % pr->f == 0 && pr->flag >= 1) {
+        J.fake_b = pr->out;
+        J.F = pr->f;
+        J.nrows = pr->n / pr->f;
+        J.threads = pr->flag;
+        ++used;
+    }
+    // hazards: what the group writes (slot, bias, bias_vec, fake_b) vs what it reads
+    // (BN stats, E) -- and the writes among themselves
+    std::vector<Span> rd, wr;
+    for (int t = 0; t < J.nterms; ++t) {
+        rd.push_back(span(J.ew[t], J.f));
+        rd.push_back(span(J.eb[t], J.f));
+    }
+    rd.push_back(span(J.E, J.o * (J.i2 > 1 ? J.i2 : 1)));
+    rd.push_back(span(J.bias, J.o));   // bias[r] = bias[r] + ...
+    wr.push_back(span(J.expect_out, J.f));
+    wr.push_back(span(J.bias, J.o));
+    if (J.vec) wr.push_back(span(J.vec, J.o * J.bcols));
+    if (J.fake_b) {
+        wr.push_back(span(J.fake_b, J.F));
+        rd.push_back(span(J.fake_b, J.F));
+    }
+    for (size_t a = 0; a < wr.size(); ++a) {
+        for (size_t b = 0; b < rd.size(); ++b) {
+            const bool same = (a == 1 && b == rd.size() - (J.fake_b ? 2 : 1)) ||        // bias vs bias
+                              (J.fake_b && a == wr.size() - 1 && b == rd.size() - 1);   // fake_b vs fake_b
+            if (!same && overlap(wr[a], rd[b])) return 0;
+        }
+        for (size_t b = a + 1; b < wr.size(); ++b)
+            if (overlap(wr[a], wr[b])) return 0;
+    }
+    return used;
 }
-#endif
+}  // namespace dfq
 
 extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed_op, void* stream) {
     if (failed_op) *failed_op = -1;
@@ -1558,17 +1105,25 @@ extern "C" int dfq_bc_chain(const dfq_bc_op* ops, int32_t n_ops, int32_t* failed
         }
     }
     if (n_ops == 0) return DFQ_OK;
-#ifdef DFQ_DIAGNOSTICS
-    // The one-launch chain (bc_chain_kernel): bit-identical, measured slower than
-    // these per-op launches, so a diagnostics A/B: DFQ_BC_CHAIN=coop.
-    if (const char* ev = dfq::ab_env("DFQ_BC_CHAIN"); ev && std::strcmp(ev, "coop") == 0) {
-        const int crc = dfq::bc_chain_coop(ops, n_ops, static_cast<hipStream_t>(stream));
-        if (crc != dfq::kBcNotEligible) return crc;
-    }
-#endif
     for (int32_t k = 0; k < n_ops; ++k) {
         const dfq_bc_op& op = ops[k];
         int rc = DFQ_OK;
+        if (op.kind == DFQ_BC_OP_EXPECT) {   // a layer's EXPECT+ -> APPLY (-> PROPAGATE) group: one launch
+            dfq::BcLayerJob J{};
+            const int32_t used = dfq::bc_layer_group(ops, n_ops, k, J);
+            if (used > 0) {
+                const int64_t pb = J.fake_b ? std::min<int64_t>(ceil_div(J.F, (int64_t)4), 2048) : 0;
+                hipLaunchKernelGGL(dfq::bc_layer_kernel, dim3((int)(J.apply_blocks + pb)), dim3(kThreads), 0,
+                                   static_cast<hipStream_t>(stream), J);
+                const hipError_t e = hipGetLastError();
+                if (e != hipSuccess) {
+                    dfq::set_last_hip_error(e);
+                    return fail(k, DFQ_ERR_HIP);
+                }
+                k += used - 1;
+                continue;
+            }
+        }
         if (op.kind == DFQ_BC_OP_COPY) {   // this copy and the ones right after it: one launch
             CopyBatch b{};
             int cnt = 0;

@@ -182,7 +182,7 @@ def main(argv=None):
     res = []
     if args.equalize:
         res = create_relation(graph, bottoms, targ_layer, delete_single=False)
-        cross_layer_equalization(graph, res, targ_layer, Save_state=False, Treshhold=2e-7)
+        cross_layer_equalization(graph, res, targ_layer, Save_state=False, Treshhold=2e-7, launch=True)
     if args.absorption:
         bias_absorption(graph, res, bottoms, N=3, visualize=args.visualize)
     state = {} if (args.bc_mode == "fused" or args.export) else None

@@ -57,7 +57,9 @@ def run_dfq(model: nn.Module, graph, bottoms, targ, *, relu: bool = True, equali
     res = []
     if equalize:
         res = stage("relations", create_relation, graph, bottoms, targ, delete_single=False)
-        stage("cle", cle.cross_layer_equalization, graph, res, targ, Save_state=False, Treshhold=2e-7)
+        # launched: the next stages' host work overlaps the device loop (their kernels
+        # are ordered behind it on the current stream); wait() below joins it
+        stage("cle", cle.cross_layer_equalization, graph, res, targ, Save_state=False, Treshhold=2e-7, launch=True)
     if absorption:
         stage("absorb", bias_absorption, graph, res, bottoms, N=3)
     state = {} if (correction and bc_mode == "fused") else None

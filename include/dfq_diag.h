@@ -37,18 +37,6 @@ int dfq_debug_timeline(void* buf, int64_t cap);
 int dfq_probe_lds(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t copy_only,
                   int32_t blocks, void* stream);
 
-/* The persistent CLE loop's grid barrier alone: nbar barriers on a cooperative
- * grid of blocks_per_cu blocks per CU (capped by occupancy), mode 0 = two-level
- * (one L2 write-back per XCD), 1 = flat (every block releases).  ws: >= 8 KB of
- * device memory (zeroed on the stream). */
-int dfq_probe_grid_barrier(int32_t nbar, int32_t blocks_per_cu, int32_t mode, void* ws, void* stream);
-
-/* The phases dfq_bc_chain's cooperative path would run `ops` in, for a grid of
- * `waves` waves (host only, no device call): *n_phases, and per op (n_ops
- * entries) its phase or -1 when skipped.  Returns 0, or 1 when the chain would
- * take the per-op launches instead. */
-int dfq_bc_chain_phases(const dfq_bc_op* ops, int32_t n_ops, int64_t waves, int32_t* n_phases, int32_t* op_phase);
-
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }

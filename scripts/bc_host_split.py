@@ -1,7 +1,7 @@
 """Where the bias-correction stage's time goes (MobileNetV2 / ResNet-50, warm,
 fused BC): the Python walk that records the chain vs the dfq_bc_chain call
 (_BcChain.flush), per configuration of the diagnostics switches in argv
-(DFQ_BC_CHAIN=launches etc. come from the environment)."""
+(diagnostics switches come from the environment)."""
 import contextlib
 import io
 import json
@@ -59,5 +59,5 @@ for model in ("mobilenetv2", "resnet50"):
             res.append((acc["stage"] * 1e3, acc["flush"] * 1e3))
     res.sort()
     st, fl = res[len(res) // 2]
-    print(json.dumps({"model": model, "chain": os.environ.get("DFQ_BC_CHAIN", "launches"), "stage_ms": round(st, 3),
+    print(json.dumps({"model": model, "stage_ms": round(st, 3),
                       "flush_ms": round(fl, 3), "walk_ms": round(st - fl, 3)}), flush=True)

@@ -3,7 +3,7 @@ time of run_dfq (per-channel sym INT8, fused BC) on MobileNetV2 and ResNet-50,
 median of ``--reps`` warm runs per configuration, interleaved; every
 configuration also checked against the reference fixture once.
 
-  python scripts/cle_ab.py [--reps 7] [--configs grouped,tiles_fin,...]
+  python scripts/cle_ab.py [--reps 7] [--configs tiles_fin,unfused_steps,...]
 """
 import argparse
 import contextlib
@@ -20,26 +20,12 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
-SWITCHES = ("DFQ_CLE_UNFUSED_FIN", "DFQ_CLE_GROUPS", "DFQ_CLE_GROUP_GRID", "DFQ_CLE_ORDERED", "DFQ_CLE_GSYNC_NOFENCE",
-            "DFQ_CLE_NO_DW_PAIRS", "DFQ_CLE_FORK", "DFQ_CLE_NO_SELF_RANGES", "DFQ_CLE_GRAPH",
-            "DFQ_CLE_BATCH", "DFQ_CLE_APPLY_OCC4",
-            "DFQ_CLE_POS_ROWS")
+SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID")
 CONFIGS = {
-    "tiles_fin": {},                                       # the product (eager batches of 4)
-    "no_dw_pairs": {"DFQ_CLE_NO_DW_PAIRS": "1"},           # round-2 steps: one launch per relation
-    "fork": {"DFQ_CLE_FORK": "1"},                         # next ranges on a concurrent graph branch
-    "no_self_ranges": {"DFQ_CLE_NO_SELF_RANGES": "1"},     # every next range from a range task
-    "apply_occ4": {"DFQ_CLE_APPLY_OCC4": "1"},              # rescale kernel capped at 128 VGPRs (4 waves / SIMD)
-    "pos_rows16": {"DFQ_CLE_POS_ROWS": "16"},               # 3x3 rescale tiles of 16 rows (round 2)
-    "graph": {"DFQ_CLE_GRAPH": "1"},                       # each batch replayed as a (cached) HIP graph
-    "batch8": {"DFQ_CLE_BATCH": "8"},
-    "batch2": {"DFQ_CLE_BATCH": "2"},
-    "tiles_fin_ordered": {"DFQ_CLE_ORDERED": "1"},
-    "grouped": {"DFQ_CLE_GROUPS": "1"},
-    "grouped_ordered": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_ORDERED": "1"},
-    "grouped_512": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_GROUP_GRID": "512"},
-    "grouped_nofence": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_GSYNC_NOFENCE": "1"},   # timing only: stale results
-    "grouped_nofence_1024": {"DFQ_CLE_GROUPS": "1", "DFQ_CLE_GSYNC_NOFENCE": "1", "DFQ_CLE_GROUP_GRID": "1024"},
+    "tiles_fin": {},                                # the product
+    "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
+    "tile_grid_1024": {"DFQ_CLE_TILE_GRID": "1024"},
+    "step_grid_1024": {"DFQ_CLE_STEP_GRID": "1024"},
 }
 
 
