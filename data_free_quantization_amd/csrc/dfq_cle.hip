@@ -24,6 +24,7 @@
 #include <functional>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <new>
 #include <numeric>
 #include <vector>
@@ -870,7 +871,7 @@ __device__ __forceinline__ void cle_range_body(const CleRel* __restrict__ rels, 
 }
 
 // `next` = 1: the ranges of the NEXT iteration (launched after this iteration's
-// last rescale, fused into the metric-tile launch; see cle_loop_tiles_fin_kernel)
+// last rescale, fused into the metric-tile launch; see cle_loop_step_kernel)
 __global__ void __launch_bounds__(kThreads)
 cle_loop_range_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
                       uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int next) {
@@ -1252,17 +1253,6 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
     }
 }
 
-template <bool POS>
-__global__ void __launch_bounds__(kThreads)
-cle_loop_apply_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
-                      uint32_t* __restrict__ rng, int64_t M, const CleState* __restrict__ st, int is_signed,
-                      float eps, double smin, double smax) {
-    __shared__ CleApplyLds A;
-    if (st->done) return;
-    cle_apply_body<POS>(rels, tasks, t0, t1, rng, M, st->iters & 1, st->iters == 0, is_signed, eps, smin, smax,
-                        blockIdx.x, gridDim.x, A);
-}
-
 // The metric's fp32 sums (torch.mean's vectorized_inner_sum over one chunk) as a
 // fixed tree.  A chunk of len elements is 32 streams (s = 8k + l: 8 vector lanes x
 // ILP 4; stream element i is chunk element 32i + s) of sz = len/32 elements, each
@@ -1491,21 +1481,25 @@ __device__ __forceinline__ double np_pairwise_leaf(const double* x, int64_t n) {
     return res;
 }
 
-__device__ double np_pairwise(const double* a, int64_t n) {
-    // numpy's recursion (blocks of <= 128 with 8 accumulators; split at n/2
-    // rounded down to a multiple of 8) as an explicit post-order walk; a single
-    // leaf (every model here: <= 128 target layers) skips the frame stack.
+// numpy's recursion (blocks of <= 128 with 8 accumulators; split at n/2 rounded
+// down to a multiple of 8) as an explicit post-order walk on one thread; a single
+// leaf (every model here: <= 128 target layers) skips the frame stack.  The
+// stack (kNpFrames frames) lives in the caller's LDS (`stack`: >= kNpStackFloats
+// floats, 8-B aligned), so the kernel needs no scratch memory.
+struct NpFrame {
+    int64_t o, n;
+    int64_t state;
+};
+constexpr int kNpFrames = 48;
+constexpr int kNpStackFloats = kNpFrames * (int)(sizeof(NpFrame) + sizeof(double)) / 4;
+__device__ double np_pairwise(const double* a, int64_t n, float* stack) {
     if (n <= 128) return 0. + np_pairwise_leaf(a, n);
-    struct Frame {
-        int64_t o, n;
-        int state;
-    };
-    Frame fr[48];
-    double acc[48];
+    NpFrame* fr = reinterpret_cast<NpFrame*>(stack);
+    double* acc = reinterpret_cast<double*>(fr + kNpFrames);
     int fp = 0, ap = 0;
     fr[fp++] = {0, n, 0};
     while (fp > 0) {
-        Frame& f = fr[fp - 1];
+        NpFrame& f = fr[fp - 1];
         if (f.n <= 128) {
             acc[ap++] = np_pairwise_leaf(a + f.o, f.n);
             --fp;
@@ -1513,7 +1507,7 @@ __device__ double np_pairwise(const double* a, int64_t n) {
             int64_t n2 = f.n / 2;
             n2 -= n2 % 8;
             f.state = 1;
-            const Frame left{f.o, n2, 0}, right{f.o + n2, f.n - n2, 0};
+            const NpFrame left{f.o, n2, 0}, right{f.o + n2, f.n - n2, 0};
             fr[fp++] = right;   // evaluated second
             fr[fp++] = left;    // evaluated first
         } else {
@@ -1536,7 +1530,7 @@ template <bool kLeafOnly = false, bool kCoherent = false>
 __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ layers, int32_t nl,
                                                const float* __restrict__ part, int32_t S, double* __restrict__ means,
                                                double* __restrict__ hist, CleState* __restrict__ st, double* sm,
-                                               float* part_lds = nullptr) {
+                                               float* part_lds = nullptr, float* np_stack = nullptr) {
     if (part_lds) {   // every chunk sum in one parallel pass of coherent loads
         for (int64_t i = threadIdx.x; i < (int64_t)nl * S; i += blockDim.x)
             part_lds[i] = kCoherent ? ld_coh(part + i) : part[i];
@@ -1559,7 +1553,7 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         if constexpr (kLeafOnly) {
             dt = nl > 0 ? 0. + np_pairwise_leaf(m, nl) : 0.0;
         } else {
-            dt = nl > 0 ? np_pairwise(m, nl) : 0.0;
+            dt = nl > 0 ? np_pairwise(m, nl, np_stack) : 0.0;
         }
         const int it = st->iters;
         hist[it] = dt;
@@ -1606,33 +1600,64 @@ struct CleFin {
     double* hist;
     int64_t nchunks, nbig;   // all chunks / chunks with tiles (len >= 8)
     int32_t S, nl;
+    int32_t last;            // the iteration's last launch
 };
 
-__global__ void __launch_bounds__(kThreads)
-cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
-                          const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t nunits,
-                          float* __restrict__ b1buf, float* __restrict__ tailbuf, int64_t ntb,
-                          const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks, int64_t t0, int64_t t1,
-                          uint32_t* __restrict__ rng, int64_t M, CleFin F, CleState* __restrict__ st,
-                          int32_t par_next) {
-    __shared__ float lds[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
+// The launches of one iteration.  Launch k < steps runs the rescale tasks of
+// chain step k (blocks [0, nab)); every launch also runs the metric tiles
+// (blocks [nab, nab + ntb)) and the next iteration's range tasks (the rest) of
+// the tensors that are final once the steps before it have run -- a tensor no
+// later step touches is measured and ranged in the launch right after its last
+// rescale, where the step's latency-bound rescale tasks leave the chip idle,
+// instead of all of them after the last step.  The last launch (k = steps, no
+// rescale blocks) takes the last step's tensors and, through the arrival
+// counters, the chunk combine and the stop rule: every chunk of an iteration
+// arrives before its last launch ends, and some chunk always arrives in it (its
+// last step's tensors), so the stop rule runs there, after every rescale.
+//
+// The stop rule (last arrival, last launch) advances st->iters and may set
+// st->done while range blocks of the same launch are still being dispatched, so
+// range blocks take the next iteration's parity from the launch argument
+// (iteration i of a batch of kCleBatch, an even count, from a batch start that
+// is a multiple of it: parity (i + 1) & 1), never from st->iters; a range block
+// that starts after the stop rule said "done" skips its tasks (no later
+// iteration reads them).  Rescale and tile blocks read st->iters before the
+// stop rule can run (the rescale blocks of an earlier launch; the tile blocks
+// before their arrival).
+static_assert(kCleTilesLds - kCleTile >= kNpStackFloats, "np_pairwise's frame stack after the tile area");
+union CleStepLds {
+    CleApplyLds apply;
+    float tiles[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
+};
+
+// POS = false (no position-parallel 3x3 rescale tiles): capped at 128 VGPRs,
+// 4 waves per SIMD like the rescale body alone
+template <bool POS>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(POS ? 1 : 4)))
+cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ atasks, int64_t a0, int64_t a1,
+                     int64_t nab, uint32_t* __restrict__ rng, int64_t M, int is_signed, float eps, double smin,
+                     double smax, const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
+                     const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t u0, int64_t u1,
+                     int64_t ntb, float* __restrict__ b1buf, float* __restrict__ tailbuf,
+                     const CleTask* __restrict__ rtasks, int64_t r0, int64_t r1, CleFin F,
+                     CleState* __restrict__ st, int32_t par_next) {
+    __shared__ CleStepLds L;
     __shared__ int flag;
-    // The stop rule (last chunk winner, this launch) advances st->iters and may set
-    // st->done while range blocks of the same launch are still being dispatched, so
-    // the range blocks take the next iteration's parity from the launch argument
-    // (iteration i of a graph batch of kCleBatch, an even count, from a batch start
-    // that is a multiple of it: parity (i + 1) & 1), never from st->iters.  A range
-    // block that starts after the stop rule said "done" skips its tasks: no later
-    // iteration reads them.  Tile blocks read st->iters before their arrival, and
-    // every tile block has arrived before the stop rule runs.
     if (st->done) return;
-    const int64_t nrb = (int64_t)gridDim.x - ntb;
-    if ((int64_t)blockIdx.x >= ntb) {
-        cle_range_body(rels, tasks, t0, t1, rng, M, par_next, blockIdx.x - ntb, nrb, lds);
+    const int64_t blk = blockIdx.x;
+    if (blk < nab) {   // this step's rescale tasks
+        cle_apply_body<POS>(rels, atasks, a0, a1, rng, M, st->iters & 1, st->iters == 0, is_signed, eps, smin, smax,
+                            blk, nab, L.apply);
         return;
     }
+    if (blk >= nab + ntb) {   // the next iteration's ranges of the tensors final by now
+        cle_range_body(rels, rtasks, r0, r1, rng, M, par_next, blk - nab - ntb, (int64_t)gridDim.x - nab - ntb,
+                       L.tiles);
+        return;
+    }
+    float* lds = L.tiles;
     const uint32_t round = (uint32_t)st->iters + 1u;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && (int32_t)(round & 1u) != par_next)   // never expected
+    if (blk == nab && threadIdx.x == 0 && (int32_t)(round & 1u) != par_next)   // never expected
         __hip_atomic_store(&st->error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // Arrival on counter c (handoff_arrive); returns whether this block arrived last.
     auto arrive = [&](uint32_t* c, uint32_t members) -> bool {
@@ -1642,8 +1667,8 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
         __syncthreads();
         return flag != 0;
     };
-    // The last arrival of the launch: tiny chunks' sums, then the per-layer means,
-    // the history and the stop rule.
+    // The last arrival of the iteration: tiny chunks' sums, then the per-layer
+    // means, the history and the stop rule.
     auto finish = [&]() {
         if (threadIdx.x == 0 && F.nchunks > F.nbig)   // tiny chunks exist (none in the zoo's models)
             for (int64_t k = 0; k < F.nchunks; ++k) {
@@ -1656,12 +1681,13 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
         if (F.nl <= 128)   // numpy's pairwise sum over the layer means is one leaf
             cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
                                        stage_part ? lds + 2048 : nullptr);
-        else
+        else   // the frame stack after the metric tile area (free: this block's units are done)
             cle_final_body<false, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st,
-                                        reinterpret_cast<double*>(lds), stage_part ? lds + 2048 : nullptr);
+                                        reinterpret_cast<double*>(lds), stage_part ? lds + 2048 : nullptr,
+                                        lds + kCleTile);
     };
-    if (F.nbig == 0) {   // no chunk has tiles (tiny or no target layers): one block finishes
-        if (blockIdx.x == 0) finish();
+    if (F.nbig == 0) {   // no chunk has tiles (tiny or no target layers): the last launch's one block finishes
+        if (blk == nab && F.last) finish();
         return;
     }
     const uint32_t fin_members = (uint32_t)F.nbig;
@@ -1686,9 +1712,9 @@ cle_loop_tiles_fin_kernel(const CleLayer* __restrict__ layers, const CleChunk* _
                 if (threadIdx.x == 0) st_coh(F.part + (int64_t)ch.layer * F.S + ch.t, 0.f + fa);
             }
         }
-        if (arrive(F.cnt + F.nchunks, fin_members)) finish();   // the launch's last arrival
+        if (arrive(F.cnt + F.nchunks, fin_members)) finish();   // the iteration's last arrival
     };
-    cle_tiles_body(layers, chunks, b1off, units, nunits, b1buf, tailbuf, blockIdx.x, ntb, lds,
+    cle_tiles_body(layers, chunks, b1off, units + u0, u1 - u0, b1buf, tailbuf, blk - nab, ntb, lds,
                    lds + kCleTile + kCleTailWords, hook);
 }
 
@@ -1730,6 +1756,7 @@ struct dfq_cle_plan {
     uint32_t* d_cnt = nullptr;      // tiles_fin arrival counters [nchunks + 1]
     int64_t nbig = 0;               // chunks with tiles
     int64_t ri0 = 0, ri1 = 0;       // fused: each iteration's range tasks (the rest come from the rescales)
+    std::vector<int64_t> ulaunch, rlaunch;   // per launch k = 0..steps: units / range tasks [v[k], v[k + 1])
     int dev = 0;
     struct CleAsync* async = nullptr;   // dfq_cle_plan_launch's worker and result
     bool abandoned = false;             // join gave up waiting for the launched loop
@@ -2044,6 +2071,22 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             }
             apply_tasks(r, at);
         }
+        // The step's slowest tasks first (its span is the last task's end): W2 row
+        // tiles (strided columns, their loads and stores a row at a time), then the
+        // depthwise pairs, W1 rows, contiguous W2 channels, and the per-channel
+        // vectors (profiles/r03/cle_tl_*.log: tile tasks started up to 10 us into
+        // a step and ran ~10 us)
+        auto prio = [](int32_t kind) {
+            switch (kind) {
+                case kApplyW2Tile: return 0;
+                case kApplyDwBoth: return 1;
+                case kApplyW1: return 2;
+                case kApplyW2Contig: return 3;
+                default: return 4;
+            }
+        };
+        std::stable_sort(at.begin() + astep.back(), at.end(),
+                         [&](const CleTask& x, const CleTask& y) { return prio(x.kind) < prio(y.kind); });
         if (!fused) rstep.push_back((int64_t)rt.size());
         astep.push_back((int64_t)at.size());
     }
@@ -2088,7 +2131,64 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 for (int64_t g = 0; g <= nb1; ++g) units.push_back(CleUnit{ci, (int32_t)g});
         }
     }
+    // Each metric unit and each next-iteration range task runs in the launch right
+    // after the last step that rescales its tensor (cle_loop_step_kernel): launch
+    // k <= steps; resets of a relation's words after that relation's own step.
+    // The unfused schedule keeps them all in the last launch.
+    std::vector<int64_t> ulaunch(steps + 2, 0), rlaunch(steps + 2, 0);
+    {
+        std::vector<int32_t> last_step(n_targets, -1);
+        std::unordered_map<const float*, int32_t> layer_of;
+        for (int32_t l = 0; l < n_targets; ++l) layer_of[targets[l]] = l;
+        auto touch = [&](const float* w, int32_t k) {
+            auto it = layer_of.find(w);
+            if (it != layer_of.end()) last_step[it->second] = std::max(last_step[it->second], k);
+        };
+        for (int32_t r = 0; r < n_rel; ++r) {
+            touch(R[r].w1, step_of[r]);
+            touch(R[r].w2, step_of[r]);
+        }
+        auto launch_of_w = [&](const float* w) -> int32_t {
+            if (!fused) return steps;
+            auto it = layer_of.find(w);
+            int32_t k = 0;
+            for (int32_t r = 0; r < n_rel; ++r)   // a tensor that is no target: after its relations' steps
+                if (R[r].w1 == w || R[r].w2 == w) k = std::max(k, step_of[r] + 1);
+            if (it != layer_of.end()) k = std::max(k, last_step[it->second] + 1);
+            return std::min(k, steps);
+        };
+        std::vector<std::vector<CleUnit>> ub(steps + 1);
+        for (const CleUnit& u : units) {
+            const int32_t l = chunks[u.chunk].layer;
+            ub[fused ? std::min(last_step[l] + 1, steps) : steps].push_back(u);
+        }
+        units.clear();
+        for (int32_t k = 0; k <= steps; ++k) {
+            ulaunch[k] = (int64_t)units.size();
+            units.insert(units.end(), ub[k].begin(), ub[k].end());
+        }
+        ulaunch[steps + 1] = (int64_t)units.size();
+        std::vector<std::vector<CleTask>> rb(steps + 1);
+        for (int64_t t = ri0; t < ri1; ++t) {
+            const CleTask tk = rt[t];
+            const CleRel& q = R[tk.rel];
+            int32_t k;
+            if (tk.kind == kRangeW1) k = launch_of_w(q.w1);
+            else if (tk.kind == kRangeW2Contig || tk.kind == kRangeW2Tile) k = launch_of_w(q.w2);
+            else k = fused ? std::min(step_of[tk.rel] + 1, steps) : steps;   // resets: after the relation's step
+            rb[k].push_back(tk);
+        }
+        rt.resize(ri0);
+        for (int32_t k = 0; k <= steps; ++k) {
+            rlaunch[k] = (int64_t)rt.size();
+            rt.insert(rt.end(), rb[k].begin(), rb[k].end());
+        }
+        rlaunch[steps + 1] = (int64_t)rt.size();
+        ri1 = (int64_t)rt.size();
+    }
     (void)hipGetDevice(&p->dev);
+    p->ulaunch = ulaunch;
+    p->rlaunch = rlaunch;
     p->nunits = (int64_t)units.size();
     p->M = M;
     p->nl = n_targets;
@@ -2221,34 +2321,34 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         const char* e = ab_env("DFQ_CLE_TILE_GRID");
         return e && *e ? std::max<int64_t>(1, atoll(e)) : int64_t(4096);
     }();
-    // fused schedule: this iteration's ranges were taken at the end of the previous
-    // one (or by plan_run before the first); the next iteration's ride with the tiles
-    for (int32_t k = 0; k < p->steps; ++k) {
-        const int64_t r0 = p->fused ? 0 : p->rstep[k];
-        const int64_t r1 = p->fused ? 0 : p->rstep[k + 1];
-        const int64_t a0 = p->astep[k], a1 = p->astep[k + 1];
-        if (r1 > r0) {
-            hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(r1 - r0, kStepGrid)), dim3(kThreads), 0, s,
-                               p->d_rels, p->d_rtasks, r0, r1, p->d_rng, p->M, p->d_state, 0);
+    // fused schedule: this iteration's ranges were taken during the previous one
+    // (or by plan_run before the first); the next iteration's ride with the
+    // launches after their tensors' last rescale (cle_loop_step_kernel)
+    CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, 0};
+    for (int32_t k = 0; k <= p->steps; ++k) {
+        const bool last = k == p->steps;
+        const int64_t a0 = last ? 0 : p->astep[k], a1 = last ? 0 : p->astep[k + 1];
+        if (!last && !p->fused && p->rstep[k + 1] > p->rstep[k]) {   // unfused: this step's ranges first
+            hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(p->rstep[k + 1] - p->rstep[k], kStepGrid)),
+                               dim3(kThreads), 0, s, p->d_rels, p->d_rtasks, p->rstep[k], p->rstep[k + 1], p->d_rng,
+                               p->M, p->d_state, 0);
             DFQ_LAUNCH_CHECK();
         }
-        if (a1 > a0) {
-            auto kern = p->step_pos[k] ? cle_loop_apply_kernel<true> : cle_loop_apply_kernel<false>;
-            hipLaunchKernelGGL(kern, dim3((int)std::min<int64_t>(a1 - a0, kStepGrid)), dim3(kThreads), 0, s,
-                               p->d_rels, p->d_atasks, a0, a1, p->d_rng, p->M, p->d_state, p->is_signed, p->eps,
-                               p->smin, p->smax);
-            DFQ_LAUNCH_CHECK();
-        }
+        const int64_t u0 = p->ulaunch[k], u1 = p->ulaunch[k + 1];
+        const int64_t r0 = p->fused ? p->rlaunch[k] : 0, r1 = p->fused ? p->rlaunch[k + 1] : 0;
+        const int64_t nab = std::min<int64_t>(a1 - a0, kStepGrid);
+        int64_t ntb = std::min<int64_t>(u1 - u0, kTileGrid);
+        if (last) ntb = std::max<int64_t>(ntb, 1);   // the stop rule's block when no chunk has tiles
+        const int64_t nrb = std::min<int64_t>(r1 - r0, kStepGrid);
+        if (nab + ntb + nrb == 0) continue;
+        F.last = last ? 1 : 0;
+        auto kern = (!last && p->step_pos[k]) ? cle_loop_step_kernel<true> : cle_loop_step_kernel<false>;
+        hipLaunchKernelGGL(kern, dim3((int)(nab + ntb + nrb)), dim3(kThreads), 0, s, p->d_rels, p->d_atasks, a0, a1, nab,
+                           p->d_rng, p->M, p->is_signed, p->eps, p->smin, p->smax, p->d_layers, p->d_chunks,
+                           p->d_b1off, p->d_units, u0, u1, ntb, p->d_b1, p->d_tail, p->d_rtasks, r0, r1, F, p->d_state,
+                           (j + 1) & 1);
+        DFQ_LAUNCH_CHECK();
     }
-    const int64_t nr = p->fused ? p->ri1 - p->ri0 : 0;   // next iteration's range tasks
-    const int64_t ntb = std::max<int64_t>(1, std::min<int64_t>(p->nunits, kTileGrid));
-    const int64_t nrb = std::min<int64_t>(nr, kStepGrid);
-    // tiles (+ ranges) + chunk combine + stop rule: one launch
-    CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl};
-    hipLaunchKernelGGL(cle_loop_tiles_fin_kernel, dim3((int)(ntb + nrb)), dim3(kThreads), 0, s, p->d_layers,
-                       p->d_chunks, p->d_b1off, p->d_units, p->nunits, p->d_b1, p->d_tail, ntb, p->d_rels,
-                       p->d_rtasks, p->ri0, p->fused ? p->ri1 : p->ri0, p->d_rng, p->M, F, p->d_state, (j + 1) & 1);
-    DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }
 
@@ -2738,9 +2838,8 @@ hipError_t preload_cle() {   // see dfq_preload
         if ((e0 = cle_ctx_ready(ctx)) != hipSuccess) return e0;
     }
     hipFuncAttributes a;
-    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_apply_kernel<true>));
-    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_apply_kernel<false>));
-    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_tiles_fin_kernel));
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_step_kernel<true>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_step_kernel<false>));
     return e;
 }
 }  // namespace dfq
