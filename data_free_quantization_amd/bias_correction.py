@@ -14,6 +14,7 @@ The arithmetic is HIP:
 from __future__ import annotations
 
 import ctypes as C
+from collections import OrderedDict
 from collections.abc import Mapping
 import logging
 
@@ -347,27 +348,27 @@ def _record_branches(chain, bn_branch):
     res = {}
     for key, branch in bn_branch.items():
         ref, size, connect_type = None, 0, None
-        for layer, relu_attached, connect_type in branch:
+        for layer, relu_attached, connect_type, bn_key in branch:
             n = _buf(layer, "fake_bias").numel()
             if ref is None:
                 ref, size = chain.alloc(n), n
-                chain.expect(layer, relu_attached, ref, False)
+                chain.expect(layer, relu_attached, ref, False, bn_key)
             elif connect_type == "cat":   # torch.cat([cum, e]): e lands right after cum
                 ref = chain.extend_last(ref, size, n)
                 sym = ref[3]
                 chain.expect(layer, relu_attached, (ref[0], ref[1] + size, ref[2] + 4 * size,
-                                                    (sym[0], sym[1], sym[2] + size)), False)
+                                                    (sym[0], sym[1], sym[2] + size)), False, bn_key)
                 size += n
             else:                          # cum += e (in place)
                 if n != size:
                     raise RuntimeError(f"output with shape [{size}] doesn't match the broadcast shape [{n}]"
                                        if n != 1 else "a one-channel BN expectation broadcast is not supported")
-                chain.expect(layer, relu_attached, ref, True)
+                chain.expect(layer, relu_attached, ref, True, bn_key)
         res[key] = (connect_type, ref, size)
     return res
 
 
-def _record_apply(chain, layer, E, o, i2, connect_type, expect, f):
+def _record_apply(chain, layer, E, o, i2, connect_type, expect, f, key=None):
     """_apply_bias_correction_E's checks, then one chain op; returns the bias_vec
     ref and its numel (kept for the next BN)."""
     if connect_type == "cat":
@@ -382,8 +383,133 @@ def _record_apply(chain, layer, E, o, i2, connect_type, expect, f):
         raise ValueError("Bias correction shape mismatch that cannot be handled automatically.")
     _lib.require_device(E[0], bias)
     vec = chain.alloc(o * bcols)
-    chain.apply(E, o, i2, expect, f, bias, vec)
+    chain.apply(E, o, i2, expect, f, bias, vec, key)
     return vec, o * bcols
+
+
+#: compiled walks (_WalkTemplate) by the graph's structure, most recent last
+_TEMPLATES = OrderedDict()
+_TEMPLATE_CAP = 8
+
+
+def _structure(graph, bottoms, targ_type, bn_type, signed, bits_weight, error_sums):
+    """Everything the walk's control flow and op fields depend on (the graph's
+    keys, node types, bottoms, the shapes of targets / biases / BN statistics /
+    error sums), as a hashable signature; plus the per-node tensors a replay
+    takes addresses from.  The walk never reads a tensor value."""
+    nodes = {}
+    shp = []
+    keys = list(graph.keys())
+    for i, v in enumerate(graph.values()):
+        t = type(v)
+        if isinstance(v, bn_type):
+            fw, fb = _buf(v, "fake_weight"), _buf(v, "fake_bias")
+            nodes[i] = (fw, fb)
+            shp.append((i, 0, fw.shape, fb.shape))
+        elif isinstance(v, targ_type) and t is not str:
+            w, b = _param(v, "weight"), _param(v, "bias")
+            pre = error_sums.get(keys[i])
+            n = -1 if pre is None else (pre.numel() if isinstance(pre, torch.Tensor) else pre[2])
+            nodes[i] = (b, pre)
+            shp.append((i, 1, w.shape, None if b is None else b.shape, n))
+    sig = (tuple(keys), tuple(map(type, graph.values())), tuple(bottoms.keys()),
+           tuple(None if v is None else tuple(v) for v in bottoms.values()), targ_type, bn_type, bool(signed),
+           int(bits_weight), _lib.REF_THREADS, tuple(shp))
+    return sig, nodes
+
+
+class _WalkTemplate:
+    """A recorded walk (record=True chain): its ops with symbolic addresses, the
+    warnings it logged and the before / after snapshot layouts.  ``replay`` binds
+    the addresses of another graph of the same structure and enqueues every op in
+    one dfq_bc_chain call."""
+
+    def __init__(self, chain, warnings_, before, after):
+        # the recording as it is; the tables are built at the first replay, so a
+        # walk that is never replayed costs only its recording
+        self.warnings = list(warnings_)
+        self.before = (dict(before._spans), before._flat.numel()) if before else None
+        self.after = (dict(after._spans), after._flat.numel()) if after else None
+        self._raw = (chain.sym, list(chain.chunk_fill))
+        self.static = None
+
+    def _build(self):
+        sym, chunk_fill = self._raw
+        self.static = np.array([(row[0], row[1], row[6], row[7], row[8]) for row, _ in sym], dtype=np.int64)
+        # scratch chunks -> one buffer; symbolic slots -> indices into an address vector
+        cbase, tot = [], 0
+        for fill in chunk_fill:
+            cbase.append(tot)
+            tot += fill
+        self.scratch = tot
+        slots = {}          # (space, key) -> index; 0 = null
+        self.slot_keys = [(_S_NONE, 0)]
+        idx = np.zeros((len(sym), 4), dtype=np.int64)
+        off = np.zeros((len(sym), 4), dtype=np.int64)
+        for k, (_, syms) in enumerate(sym):
+            for j, (space, key, o) in enumerate(syms):
+                if space == _S_NONE:
+                    continue
+                if space == _S_SCRATCH:
+                    key, o = 0, cbase[key] + o
+                sk = (space, key)
+                if sk not in slots:
+                    slots[sk] = len(self.slot_keys)
+                    self.slot_keys.append(sk)
+                idx[k, j], off[k, j] = slots[sk], o
+        self.idx, self.off = idx, off
+        self._raw = None
+
+    def replay(self, nodes, dev, stream):
+        if self.static is None:
+            self._build()
+        for m in self.warnings:
+            logger.warning(m)
+        scratch = torch.empty(max(self.scratch, 1), dtype=torch.float32, device=dev)
+        flats = [None, None]
+        for w, snap in enumerate((self.before, self.after)):
+            if snap is not None:
+                flats[w] = torch.empty(snap[1], dtype=torch.float32, device=dev)
+        addr = [0] * len(self.slot_keys)
+        used = []
+        for i, (space, key) in enumerate(self.slot_keys):
+            if space == _S_NONE:
+                continue
+            if space == _S_SCRATCH:
+                addr[i] = scratch.data_ptr()
+                continue
+            if space == _S_SNAP:
+                addr[i] = flats[key].data_ptr()
+                continue
+            if space in (_S_BN_W, _S_BN_B):
+                t = nodes[key][0 if space == _S_BN_W else 1]
+            elif space == _S_BIAS:
+                t = nodes[key][0]
+            else:   # _S_E: a tensor or a (buffer, float offset, numel) ref
+                pre = nodes[key][1]
+                if isinstance(pre, torch.Tensor):
+                    t = pre
+                else:
+                    t = pre[0]
+                    addr[i] = 4 * pre[1]
+            used.append(t)
+            addr[i] += t.data_ptr()
+        _lib.require_device(*used)
+        a = np.array(addr, dtype=np.int64)[self.idx] + 4 * self.off
+        a[self.idx == 0] = 0
+        arr = np.empty(len(self.static), dtype=_BC_OP)
+        arr["kind"], arr["flag"] = self.static[:, 0], self.static[:, 1]
+        arr["n"], arr["i2"], arr["f"] = self.static[:, 2], self.static[:, 3], self.static[:, 4]
+        for j, name in enumerate(("a", "b", "out", "out2")):
+            arr[name] = a[:, j].astype(np.uint64)
+        if len(arr):
+            failed = C.c_int32(-1)
+            rc = _lib.load().dfq_bc_chain(arr.ctypes.data_as(C.POINTER(_lib.BcOp)), len(arr), C.byref(failed), stream)
+            _lib.check(rc, f"dfq_bc_chain (op {failed.value})", RuntimeError)
+            scratch.record_stream(torch.cuda.current_stream(dev))
+        before = _Snapshot(flats[0], self.before[0]) if self.before else {}
+        after = _Snapshot(flats[1], self.after[0]) if self.after else {}
+        return before, after
 
 
 def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.BatchNorm2d, signed=False, *,
@@ -398,7 +524,26 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
     assert isinstance(bottoms, dict), "Expected 'bottoms' to be a dictionary."
     assert isinstance(targ_type, (type, tuple)), "Expected 'targ_type' to be a type or tuple of types."
     logger.info("Starting bias correction...")
-    bn_module, relu_attached = {}, {}
+    # A graph of a structure walked before replays the compiled walk: the walk's
+    # control flow and every op's fields depend on the structure only (keys, node
+    # types, bottoms, shapes), never on a tensor value; the addresses are bound
+    # afresh.  Only fused-mode walks (error sums given) are compiled: the other
+    # mode quantizes each weight inside the walk.
+    sig = nodes = None
+    if error_sums is not None:
+        sig, nodes = _structure(graph, bottoms, targ_type, bn_type, signed, bits_weight, error_sums)
+        tpl = _TEMPLATES.get(sig)
+        if tpl is not None:
+            _TEMPLATES.move_to_end(sig)
+            dev = next((t.device for v in nodes.values() for t in v if isinstance(t, torch.Tensor)), None)
+            if dev is None:
+                dev = torch.device("cuda", torch.cuda.current_device())
+            with torch.no_grad():
+                res = tpl.replay(nodes, dev, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+            logger.info("Bias correction completed.")
+            return res
+    warned = []
+    bn_module, relu_attached, bn_key = {}, {}, {}
     bias_prev = None        # device bias_vec of the last corrected layer (negated when used)
     bias = None             # persists across layers like the reference's local
     before, after = {}, {}
@@ -414,14 +559,16 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                 b = _param(l, "bias")
                 if b is not None:
                     biases[f"layer_{i}"] = b   # read through data_ptr only (no .data view)
-        chain = _BcChain(next(iter(biases.values())).device if biases else torch.device("cuda"))
-        before = _snapshot(chain, biases)
+        chain = _BcChain(next(iter(biases.values())).device if biases else torch.device("cuda"),
+                         record=sig is not None)
+        before = _snapshot(chain, biases, 0, [int(k[6:]) for k in biases])
         stream = None
         try:
             for idx_layer, layer in enumerate(graph.values()):
                 layer_name = f"layer_{idx_layer}"
                 if idx_layer not in bottoms:
-                    logger.warning(f"Layer index {idx_layer} not found in bottoms")
+                    warned.append(f"Layer index {idx_layer} not found in bottoms")
+                    logger.warning(warned[-1])
                     continue
                 bot = bottoms[idx_layer]
                 if bot is None or bot[0] == "Data":
@@ -429,6 +576,7 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                 node = graph[idx_layer]
                 if isinstance(node, bn_type):
                     bn_module[idx_layer] = node
+                    bn_key[id(node)] = idx_layer
                     relu_attached[idx_layer] = False
                     if bias_prev is not None:
                         vec, numel = bias_prev
@@ -439,7 +587,7 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                             raise RuntimeError("output with shape [{}] doesn't match the broadcast shape".format(f))
                         if numel % f:
                             raise RuntimeError(f"shape '[-1, {f}]' is invalid for input of size {numel}")
-                        chain.propagate(vec, numel, fake_b, f)
+                        chain.propagate(vec, numel, fake_b, f, idx_layer)
                         bias_prev = None
                         if len(chain.ops) >= _FLUSH_OPS:   # the device starts on what is recorded so far
                             chain.flush(stream)
@@ -447,7 +595,10 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                 if isinstance(node, torch.nn.ReLU) and bot[0] in bn_module:
                     relu_attached[bot[0]] = True
                 if isinstance(node, targ_type):
-                    bn_list, relu_list, type_list, _ = find_prev_bn(bn_module, relu_attached, graph, bottoms, bot[:])
+                    bn_list, relu_list, type_list, no_bn = find_prev_bn(bn_module, relu_attached, graph, bottoms,
+                                                                        bot[:])
+                    if no_bn:   # find_prev_bn printed a warning: not a walk to replay silently
+                        sig = None
                     pre = None if error_sums is None else error_sums.get(keys[idx_layer])
                     E, o, i2 = _error_sums(_param(node, "weight"), bits_weight, signed, pre)
                     if stream is None:
@@ -455,10 +606,11 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                         chain.dev = E[0].device
                     branches = {}
                     for j, (bn_layer, bid) in enumerate(bn_list):
-                        branches.setdefault(bid[0], []).append((bn_layer, relu_list[j], type_list[j]))
+                        branches.setdefault(bid[0], []).append((bn_layer, relu_list[j], type_list[j],
+                                                                bn_key.get(id(bn_layer))))
                     for connect_type, expect, f in _record_branches(chain, branches).values():
                         try:
-                            bias = _record_apply(chain, node, E, o, i2, connect_type, expect, f)
+                            bias = _record_apply(chain, node, E, o, i2, connect_type, expect, f, idx_layer)
                         except ValueError as e:
                             logger.error(f"Error in applying bias correction: {e}")
                             raise
@@ -468,9 +620,13 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                     b = _param(layer, "bias")
                     if b is not None:
                         after_src[layer_name] = b
-            after = _snapshot(chain, after_src)
+            after = _snapshot(chain, after_src, 1, [int(k[6:]) for k in after_src])
         finally:   # the ops recorded before an error still take effect, as in the reference
             if chain.ops:
                 chain.flush(stream if stream is not None else _lib.stream_of(next(iter(biases.values()))))
+    if sig is not None and all(isinstance(k, int) for k in bn_key.values()):
+        _TEMPLATES[sig] = _WalkTemplate(chain, warned, before, after)
+        if len(_TEMPLATES) > _TEMPLATE_CAP:
+            _TEMPLATES.popitem(last=False)
     logger.info("Bias correction completed.")
     return before, after
