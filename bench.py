@@ -189,8 +189,15 @@ def prewarm(run, stream, dev, ms_target):
                                for i in range(0, len(series), k)][:10]}
 
 
-def time_plan(plan, stream, dev, steps, warmup):
-    """Device ms per execute() of ``plan`` (all its launches; HIP events on its stream)."""
+def time_plan(plan, stream, dev, steps, warmup, prewarm_ms=100.0):
+    """Device ms per execute() of ``plan`` (all its launches; HIP events on its stream),
+    after ``prewarm_ms`` of wall time of executes (the GPU idles between legs) and
+    ``warmup`` more."""
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < prewarm_ms:
+        for _ in range(4):
+            plan.execute(stream)
+        torch.cuda.synchronize(dev)
     for _ in range(warmup):
         plan.execute(stream)
     torch.cuda.synchronize(dev)

@@ -2162,29 +2162,39 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             const int32_t l = chunks[u.chunk].layer;
             ub[fused ? std::min(last_step[l] + 1, steps) : steps].push_back(u);
         }
+        // the stop rule runs at the iteration's last arrival, which must come in the
+        // last launch (after every rescale): if no unit landed there (the last
+        // step's tensors are all tiny), every unit goes there
+        if (ub[steps].empty())
+            for (int32_t k = 0; k < steps; ++k) {
+                ub[steps].insert(ub[steps].end(), ub[k].begin(), ub[k].end());
+                ub[k].clear();
+            }
         units.clear();
         for (int32_t k = 0; k <= steps; ++k) {
             ulaunch[k] = (int64_t)units.size();
             units.insert(units.end(), ub[k].begin(), ub[k].end());
         }
         ulaunch[steps + 1] = (int64_t)units.size();
-        std::vector<std::vector<CleTask>> rb(steps + 1);
-        for (int64_t t = ri0; t < ri1; ++t) {
-            const CleTask tk = rt[t];
-            const CleRel& q = R[tk.rel];
-            int32_t k;
-            if (tk.kind == kRangeW1) k = launch_of_w(q.w1);
-            else if (tk.kind == kRangeW2Contig || tk.kind == kRangeW2Tile) k = launch_of_w(q.w2);
-            else k = fused ? std::min(step_of[tk.rel] + 1, steps) : steps;   // resets: after the relation's step
-            rb[k].push_back(tk);
+        if (fused) {   // (the unfused schedule's range tasks are per step: rstep)
+            std::vector<std::vector<CleTask>> rb(steps + 1);
+            for (int64_t t = ri0; t < ri1; ++t) {
+                const CleTask tk = rt[t];
+                const CleRel& q = R[tk.rel];
+                int32_t k;
+                if (tk.kind == kRangeW1) k = launch_of_w(q.w1);
+                else if (tk.kind == kRangeW2Contig || tk.kind == kRangeW2Tile) k = launch_of_w(q.w2);
+                else k = std::min(step_of[tk.rel] + 1, steps);   // resets: after the relation's own step
+                rb[k].push_back(tk);
+            }
+            rt.resize(ri0);
+            for (int32_t k = 0; k <= steps; ++k) {
+                rlaunch[k] = (int64_t)rt.size();
+                rt.insert(rt.end(), rb[k].begin(), rb[k].end());
+            }
+            rlaunch[steps + 1] = (int64_t)rt.size();
+            ri1 = (int64_t)rt.size();
         }
-        rt.resize(ri0);
-        for (int32_t k = 0; k <= steps; ++k) {
-            rlaunch[k] = (int64_t)rt.size();
-            rt.insert(rt.end(), rb[k].begin(), rb[k].end());
-        }
-        rlaunch[steps + 1] = (int64_t)rt.size();
-        ri1 = (int64_t)rt.size();
     }
     (void)hipGetDevice(&p->dev);
     p->ulaunch = ulaunch;

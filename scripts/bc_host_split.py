@@ -1,7 +1,7 @@
 """Where the bias-correction stage's time goes (MobileNetV2 / ResNet-50, warm,
-fused BC): the Python walk that records the chain vs the dfq_bc_chain call
-(_BcChain.flush), per configuration of the diagnostics switches in argv
-(diagnostics switches come from the environment)."""
+fused BC): the Python walk that records the chain vs the dfq_bc_chain calls
+(_BcChain.flush, each followed by a device sync here), for the live walk and for
+the compiled walk's replay (bias_correction._TEMPLATES)."""
 import contextlib
 import io
 import json
@@ -47,17 +47,20 @@ def bc(*a, **k):
 BC._BcChain.flush = flush
 pipeline.bias_correction = bc
 for model in ("mobilenetv2", "resnet50"):
-    res = []
-    for rep in range(5):
-        acc.clear()
-        m = zoo.build(model, seed=0, relu=True).cuda()
-        g = build_graph(m, "positional")
-        with contextlib.redirect_stdout(io.StringIO()):
-            pipeline.run_dfq(m, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel",
-                             symmetric=True, bc_mode="fused")
-        if rep:
-            res.append((acc["stage"] * 1e3, acc["flush"] * 1e3))
-    res.sort()
-    st, fl = res[len(res) // 2]
-    print(json.dumps({"model": model, "stage_ms": round(st, 3),
-                      "flush_ms": round(fl, 3), "walk_ms": round(st - fl, 3)}), flush=True)
+    for mode in ("live", "replay"):   # live: the walk recorded each time; replay: the compiled walk
+        res = []
+        for rep in range(6):
+            acc.clear()
+            if mode == "live":
+                BC._TEMPLATES.clear()
+            m = zoo.build(model, seed=0, relu=True).cuda()
+            g = build_graph(m, "positional")
+            with contextlib.redirect_stdout(io.StringIO()):
+                pipeline.run_dfq(m, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel",
+                                 symmetric=True, bc_mode="fused")
+            if rep:
+                res.append((acc["stage"] * 1e3, acc.get("flush", 0.0) * 1e3))
+        res.sort()
+        st, fl = res[len(res) // 2]
+        print(json.dumps({"model": model, "mode": mode, "stage_ms": round(st, 3),
+                          "flush_ms": round(fl, 3), "walk_ms": round(st - fl, 3)}), flush=True)
