@@ -66,8 +66,9 @@ constexpr Variant kVariants[] = {
     {1024, 64, false},    // 12: variant 9 with the generic E sums (fewer VGPRs)
     {2048, 64, false},    // 13: variant 6 + per-task timestamps (diagnostics: dfq_debug_timeline)
     {2048, 64, false},    // 14: variant 6 with the IEEE divide on every element (round-2 arithmetic)
+    {2048, 64, false},    // 15: variant 6 with the generic quantize loop (flags tested per float4; round 3)
 };
-constexpr int kNumVariants = 15;
+constexpr int kNumVariants = 16;
 // DevTask.nrows <= kGroupTag: a row-group piece of R = kGroupTag - nrows + 1 rows
 constexpr int kGroupTag = -64;
 constexpr int kGroupMaxRows = 16;
@@ -233,6 +234,107 @@ __device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTas
     }
 }
 
+
+// The VEC quantize loop with the task's output set fixed at compile time (clip,
+// code format, error-sum form): straight-line per-float4 bodies without the
+// generic loop's per-iteration flag branches, clamps as v_med3 (no operand
+// canonicalisation: fminf / fmaxf on values the compiler cannot prove canonical
+// cost a v_max x, x each), byte codes by v_cvt_pk_u8_f32 (q is integral and in
+// [qmin, qmax]: exact; symmetric codes offset by 128 and flipped back by one
+// xor), stores addressed from the task's uniform base pointers.  Bit-identical
+// with the generic loop (same per-element operation sequence: the med3 clamp
+// equals fminf(fmaxf(.)) for qmin <= qmax and non-NaN inputs).
+// CB: 0 no codes, 1 int8 / uint8, 2 int16, 3 packed int4.  EM: 0 no error sums,
+// 1 E stored (KH*KW = 1), 2 eps back to LDS (KH*KW > 1).
+template <bool CLIP, int CB, int EM, bool NT>
+__device__ __forceinline__ void quant_vec4(const DevTensor& T, int n, int64_t base, float* data, const float* ls,
+                                           const float* lmn, const QParams& pc, bool whole, int eoff, int lane,
+                                           float qmin, float qmax, bool sym) {
+    const int nj = n >> 2;
+    float* dq = T.dst + base;
+    const float clo = T.clip_lo, chi = T.clip_hi;
+    const float inv_len = T.inv_len;
+    const float coff = sym ? 128.f : 0.f;
+    const uint32_t cflip = sym ? 0x80808080u : 0u;
+#pragma unroll 2
+    for (int j = lane; j < nj; j += kWave) {
+        const float4 xv = reinterpret_cast<const float4*>(data)[j];
+        float s = pc.s, mn = pc.mn;
+        if (whole) {   // one row per float4 (4 | len, 4 | goff)
+            int r = (int)(((float)(4 * j + eoff) + 0.5f) * inv_len);
+            r = min(r, 63);
+            s = ls[r];
+            mn = lmn[r];
+        }
+        const float negmn = whole ? -mn : pc.negmn;
+        const float rs = __builtin_amdgcn_rcpf(s);
+        float t[4] = {(xv.x + negmn) * rs, (xv.y + negmn) * rs, (xv.z + negmn) * rs, (xv.w + negmn) * rs};
+        bool need[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            t[k] = __builtin_amdgcn_fmed3f(t[k], qmin, qmax);
+            const float d = __builtin_amdgcn_fractf(t[k]) - 0.5f;
+            need[k] = !(fabsf(d) > fabsf(t[k]) * 0x1p-20f);
+        }
+        if (__builtin_amdgcn_ballot_w64(need[0] | need[1] | need[2] | need[3])) {   // wave-uniform, rare
+            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (need[k]) t[k] = __builtin_amdgcn_fmed3f((xs[k] + negmn) / s, qmin, qmax);
+        }
+        float q[4], y[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            q[k] = rintf(t[k]);
+            y[k] = q[k] * s;
+            y[k] = y[k] + mn;
+            if constexpr (CLIP) y[k] = __builtin_amdgcn_fmed3f(y[k], clo, chi);
+        }
+        st<NT>(reinterpret_cast<float4*>(dq) + j, make_float4(y[0], y[1], y[2], y[3]));
+        if constexpr (CB == 1) {
+            uint32_t c = __builtin_amdgcn_cvt_pk_u8_f32(q[0] + coff, 0, 0u);
+            c = __builtin_amdgcn_cvt_pk_u8_f32(q[1] + coff, 1, c);
+            c = __builtin_amdgcn_cvt_pk_u8_f32(q[2] + coff, 2, c);
+            c = __builtin_amdgcn_cvt_pk_u8_f32(q[3] + coff, 3, c);
+            st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, c ^ cflip);
+        } else if constexpr (CB == 3) {   // DFQ_PACK_INT4: 4 codes -> 2 bytes (base % 4 == 0)
+            const uint32_t c = ((uint32_t)(int)q[0] & 0xFu) | (((uint32_t)(int)q[1] & 0xFu) << 4) |
+                               (((uint32_t)(int)q[2] & 0xFu) << 8) | (((uint32_t)(int)q[3] & 0xFu) << 12);
+            st<NT>(reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(T.codes) + base / 2) + j, (uint16_t)c);
+        } else if constexpr (CB == 2) {
+            const uint64_t c = ((uint64_t)(uint16_t)(int)q[0]) | ((uint64_t)(uint16_t)(int)q[1] << 16) |
+                               ((uint64_t)(uint16_t)(int)q[2] << 32) | ((uint64_t)(uint16_t)(int)q[3] << 48);
+            st<NT>(reinterpret_cast<uint64_t*>(static_cast<uint16_t*>(T.codes) + base) + j, c);
+        }
+        if constexpr (EM != 0) {
+            const float4 ev = make_float4(y[0] - xv.x, y[1] - xv.y, y[2] - xv.z, y[3] - xv.w);
+            if constexpr (EM == 1) st<NT>(reinterpret_cast<float4*>(T.esum + base) + j, ev);
+            else reinterpret_cast<float4*>(data)[j] = ev;
+        }
+    }
+}
+
+template <bool CLIP, int CB, bool NT>
+__device__ __forceinline__ void quant_vec4_e(int em, const DevTensor& T, int n, int64_t base, float* data,
+                                             const float* ls, const float* lmn, const QParams& pc, bool whole,
+                                             int eoff, int lane, float qmin, float qmax, bool sym) {
+    if (em == 0) quant_vec4<CLIP, CB, 0, NT>(T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
+    else if (em == 1) quant_vec4<CLIP, CB, 1, NT>(T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
+    else quant_vec4<CLIP, CB, 2, NT>(T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
+}
+
+template <bool CLIP, bool NT>
+__device__ __forceinline__ void quant_vec4_c(int cb, int em, const DevTensor& T, int n, int64_t base, float* data,
+                                             const float* ls, const float* lmn, const QParams& pc, bool whole,
+                                             int eoff, int lane, float qmin, float qmax, bool sym) {
+    switch (cb) {
+        case 0: quant_vec4_e<CLIP, 0, NT>(em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym); break;
+        case 1: quant_vec4_e<CLIP, 1, NT>(em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym); break;
+        case 2: quant_vec4_e<CLIP, 2, NT>(em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym); break;
+        default: quant_vec4_e<CLIP, 3, NT>(em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
+    }
+}
+
 // Steps 2-4 on a chunk that has landed in ``data``.
 // ESPEC: compile-time KH*KW error sums -- 2: 3x3/5x5/7x7/2x2, 1: 3x3, 0: none
 // goff >= 0: a row-group piece whose per-row parameters are already in ls / lmn
@@ -241,7 +343,7 @@ __device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTas
 // SCREEN: the screened reciprocal quantize (qdq_screen, the IEEE divide only near a
 // rounding boundary); false: the IEEE divide for every element (round-2 arithmetic,
 // diagnostics variant 14).  Bit-identical results.
-template <int MAXROWS, bool VEC, bool NT = false, int ESPEC = 2, bool SCREEN = true>
+template <int MAXROWS, bool VEC, bool NT = false, int ESPEC = 2, bool SCREEN = true, bool FAST = true>
 __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& task, float* data, float* ls,
                                              float* lmn, const uint32_t* __restrict__ slot_min,
                                              const uint32_t* __restrict__ slot_max, int lane, float bmn = 0.f,
@@ -379,7 +481,8 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         return y;
     };
 
-    if constexpr (VEC) {
+    // the generic VEC loop: every output flag tested per float4
+    auto vec_generic = [&]() {
         const int nj = n >> 2;
 #pragma unroll 2
         for (int j = lane; j < nj; j += kWave) {
@@ -410,6 +513,19 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
                 else reinterpret_cast<float4*>(data)[j] = ev;
             }
         }
+    };
+    if constexpr (VEC) {
+        bool done = false;
+        if constexpr (SCREEN && FAST && MAXROWS == 64) {
+            if (T.dst && (!clip || T.clip_lo <= T.clip_hi)) {   // one compile-time body per (clip, codes, E form)
+                const int cb = !T.codes ? 0 : (T.code_bytes == 1 ? 1 : (T.code_bytes == 0 ? 3 : 2));
+                const int em = !want_e ? 0 : (khw == 1 ? 1 : 2);
+                if (clip) quant_vec4_c<true, NT>(cb, em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
+                else quant_vec4_c<false, NT>(cb, em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
+                done = true;
+            }
+        }
+        if (!done) vec_generic();
     } else if (T.codes && T.code_bytes == 0) {
         // packed nibbles on the scalar path: the task starts at an even element
         // (build()), so even lanes own a byte and take the odd neighbour's code by
@@ -491,7 +607,8 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
 __device__ uint64_t* g_timeline = nullptr;
 __device__ int64_t g_timeline_cap = 0;
 
-template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false, int ESPEC = 2, bool TL = false, bool SCREEN = true>
+template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false, int ESPEC = 2, bool TL = false, bool SCREEN = true,
+          bool FAST = true>
 __global__ void __launch_bounds__(kBlockThreads)
 sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restrict__ tasks, int64_t ntasks,
                   const uint32_t* __restrict__ slot_min, const uint32_t* __restrict__ slot_max) {
@@ -616,11 +733,11 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                 block_lds_sync();   // the slots are rewritten by the next task
             }
             if (T.vec4)
-                compute_task<MAXROWS, true, NT, ESPEC, SCREEN>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx,
-                                                       goff);
+                compute_task<MAXROWS, true, NT, ESPEC, SCREEN, FAST>(T, task, wl, ls, lmn, slot_min, slot_max, lane,
+                                                                     bmn, bmx, goff);
             else
-                compute_task<MAXROWS, false, NT, ESPEC, SCREEN>(T, task, wl, ls, lmn, slot_min, slot_max, lane, bmn, bmx,
-                                                        goff);
+                compute_task<MAXROWS, false, NT, ESPEC, SCREEN, FAST>(T, task, wl, ls, lmn, slot_min, slot_max, lane,
+                                                                      bmn, bmx, goff);
             if constexpr (TL) {
                 if (lane == 0 && t < g_timeline_cap) {
                     uint32_t hw;
@@ -1003,6 +1120,7 @@ static MainKernel main_kernel(int variant) {
         case 12: return sweep_main_kernel<DFQ_V(12), true, 0>;
         case 13: return sweep_main_kernel<DFQ_V(13), true, 1, true>;
         case 14: return sweep_main_kernel<DFQ_V(14), true, 1, false, false>;
+        case 15: return sweep_main_kernel<DFQ_V(15), true, 1, false, true, false>;
         default: return sweep_main_kernel<DFQ_V(0)>;
     }
 #endif
