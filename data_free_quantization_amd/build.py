@@ -16,7 +16,7 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libdfq_hip.so"
-SOURCES = ["dfq_lib.hip", "dfq_sweep.hip", "dfq_transform.hip", "dfq_cle.hip"]
+SOURCES = ["dfq_lib.hip", "dfq_sweep.hip", "dfq_transform.hip", "dfq_cle.hip", "dfq_cle_relation.hip"]
 # Diagnostics build (bench.py's ceiling probes, scripts/ A/B runs): the same
 # sources with -DDFQ_DIAGNOSTICS (the sweep's A/B variants and environment
 # switches) plus the probes (include/dfq_diag.h).  Never loaded by the product path.
@@ -53,7 +53,7 @@ def _stale(out: Path, deps) -> bool:
 
 
 def _build_one(out: Path, sources, defines, force: bool, verbose: bool) -> Path:
-    deps = [CSRC / s for s in sources] + [CSRC / "dfq_common.h", ROOT / "include" / "dfq_hip.h",
+    deps = [CSRC / s for s in sources] + [CSRC / "dfq_common.h", CSRC / "dfq_cle_common.h", ROOT / "include" / "dfq_hip.h",
                                           ROOT / "include" / "dfq_diag.h", EXPORTS, Path(__file__)]
     if not force and not _stale(out, deps):
         return out
