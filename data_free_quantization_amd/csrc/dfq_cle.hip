@@ -1137,7 +1137,8 @@ template <bool kLeafOnly = false, bool kCoherent = false>
 __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ layers, int32_t nl,
                                                const float* __restrict__ part, int32_t S, double* __restrict__ means,
                                                double* __restrict__ hist, CleState* __restrict__ st, double* sm,
-                                               float* part_lds = nullptr, float* np_stack = nullptr) {
+                                               float* part_lds = nullptr, float* np_stack = nullptr,
+                                               uint32_t* hflag = nullptr) {
     if (part_lds) {   // every chunk sum in one parallel pass of coherent loads
         for (int64_t i = threadIdx.x; i < (int64_t)nl * S; i += blockDim.x)
             part_lds[i] = kCoherent ? ld_coh(part + i) : part[i];
@@ -1172,7 +1173,14 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
             st->iter_count += 1;
         }
         const bool cont = (st->diff > st->thr) && (st->iter_count < st->count);
-        st->done = (!cont || st->iters >= st->max_iters) ? 1 : 0;
+        const int done = (!cont || st->iters >= st->max_iters) ? 1 : 0;
+        st->done = done;
+        // the host's copy of the stop rule (pinned host memory; a system-scope
+        // vector store): the loop's host side reads it instead of copying the
+        // state back after every batch on the loop stream
+        if (hflag)
+            __hip_atomic_store(hflag, ((uint32_t)(it + 1) << 1) | (uint32_t)done, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1208,6 +1216,7 @@ struct CleFin {
     int64_t nchunks, nbig;   // all chunks / chunks with tiles (len >= 8)
     int32_t S, nl;
     int32_t last;            // the iteration's last launch
+    uint32_t* hflag;         // pinned host word: (iterations << 1) | done, or null
 };
 
 // The launches of one iteration.  Launch k < steps runs the rescale tasks of
@@ -1287,11 +1296,11 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
         if (F.nl <= 128)   // numpy's pairwise sum over the layer means is one leaf
             cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
-                                       stage_part ? lds + 2048 : nullptr);
+                                       stage_part ? lds + 2048 : nullptr, nullptr, F.hflag);
         else   // the frame stack after the metric tile area (free: this block's units are done)
             cle_final_body<false, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st,
                                         reinterpret_cast<double*>(lds), stage_part ? lds + 2048 : nullptr,
-                                        lds + kCleTile);
+                                        lds + kCleTile, F.hflag);
     };
     if (F.nbig == 0) {   // no chunk has tiles (tiny or no target layers): the last launch's one block finishes
         if (blk == nab && F.last) finish();
@@ -1343,6 +1352,7 @@ struct dfq_cle_plan {
     double* d_hist_tables = nullptr;
     CleState* d_state = nullptr;
     CleState* h_state = nullptr;    // pinned (the device context's, set by run)
+    uint32_t* d_flag = nullptr;     // the stop rule's host word (the device context's, set by run)
     hipStream_t st = nullptr;       // the loop's stream (the device context's)
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
     std::vector<char> step_pos;          // per step: position-parallel W2 tiles (the POS rescale kernel)
@@ -1389,6 +1399,8 @@ struct CleDeviceCtx {
     std::mutex mu;
     hipStream_t st = nullptr;
     CleState* h_state = nullptr;   // pinned: [0] the run's state, [1..2] the batch readback slots
+    uint32_t* h_flag = nullptr;    // pinned, written by the stop rule: (iterations << 1) | done
+    uint32_t* d_flag = nullptr;    // its device address
     hipEvent_t ev[2] = {nullptr, nullptr};
     // Table pool: one plan at a time keeps its tables here (device + pinned upload
     // mirror), so a plan costs no hipMalloc / hipFree (hipFree waits for the whole
@@ -1424,6 +1436,10 @@ static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
         if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx.st, hipStreamNonBlocking, greatest);
     }
     if (e == hipSuccess && !ctx.h_state) e = hipHostMalloc(&ctx.h_state, 3 * sizeof(CleState));
+    if (e == hipSuccess && !ctx.h_flag) {
+        e = hipHostMalloc(&ctx.h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx.d_flag), ctx.h_flag, 0);
+    }
     for (int i = 0; i < 2 && e == hipSuccess; ++i)
         if (!ctx.ev[i]) e = hipEventCreateWithFlags(&ctx.ev[i], hipEventDisableTiming);
     if (e == hipSuccess && !ctx.pool_ev) e = hipEventCreateWithFlags(&ctx.pool_ev, hipEventDisableTiming);
@@ -1941,7 +1957,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     // fused schedule: this iteration's ranges were taken during the previous one
     // (or by plan_run before the first); the next iteration's ride with the
     // launches after their tensors' last rescale (cle_loop_step_kernel)
-    CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, 0};
+    CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, 0, p->d_flag};
     for (int32_t k = 0; k <= p->steps; ++k) {
         const bool last = k == p->steps;
         const int64_t a0 = last ? 0 : p->astep[k], a1 = last ? 0 : p->astep[k + 1];
@@ -2004,6 +2020,8 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     DFQ_HIP_CHECK(cle_ctx_ready(ctx));
     p->st = ctx.st;
     p->h_state = ctx.h_state;
+    *ctx.h_flag = 0;   // (no kernel of this context's stream is running: the caller holds ctx.mu)
+    p->d_flag = ctx.d_flag;
     hipStream_t s = p->st;
     // the history: the tables' slots, or the context's buffer (grown once) for longer caps
     p->d_hist = p->d_hist_tables;
@@ -2056,10 +2074,14 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     }
 #endif
     // One batch in flight ahead of the stop-rule check: batch k + 1 is enqueued
-    // before the host waits for batch k's state, so the readback and the check
-    // overlap the GPU's next batch instead of idling it (round 2: ~31 us per
-    // batch boundary).  A batch enqueued after convergence runs as no-ops (every
-    // kernel returns at st->done).  Its state copy goes to the other pinned slot.
+    // before the host waits for batch k, so the check overlaps the GPU's next
+    // batch instead of idling it (round 2: ~31 us per batch boundary).  A batch
+    // enqueued after convergence runs as no-ops (every kernel returns at
+    // st->done).  The stop rule writes its outcome into pinned host memory
+    // (ctx.h_flag), so nothing but the event sits between two batches on the
+    // loop stream (diagnostics DFQ_CLE_STATE_COPY=1: a state copy per batch
+    // instead, into the other pinned slot).
+    const bool copy_state = ab_env("DFQ_CLE_STATE_COPY") != nullptr;
     const double tc1 = now_us();
     int32_t launched = 0;
     int slot = 0;
@@ -2069,7 +2091,8 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             if (rc != DFQ_OK) return rc;
         }
         launched += batch;
-        DFQ_HIP_CHECK(hipMemcpyAsync(ctx.h_state + 1 + sl, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
+        if (copy_state)
+            DFQ_HIP_CHECK(hipMemcpyAsync(ctx.h_state + 1 + sl, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
         DFQ_HIP_CHECK(hipEventRecord(ctx.ev[sl], s));
         return DFQ_OK;
     };
@@ -2080,8 +2103,9 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             const bool more = launched < max_iters;
             if (more && (rc = enqueue_batch(slot ^ 1)) != DFQ_OK) return rc;
             DFQ_HIP_CHECK(hipEventSynchronize(ctx.ev[slot]));
-            init = ctx.h_state[1 + slot];
-            if (init.done || !more) break;
+            const bool done = copy_state ? ctx.h_state[1 + slot].done != 0
+                                         : (__atomic_load_n(ctx.h_flag, __ATOMIC_ACQUIRE) & 1u) != 0;
+            if (done || !more) break;
             slot ^= 1;
         }
     }
