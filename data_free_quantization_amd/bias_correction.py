@@ -281,11 +281,12 @@ class _BcChain:
         """Grow the most recent slot ``ref`` ([size] floats) by n (torch.cat):
         in place when its chunk has room, else into a fresh slot that a COPY op
         fills with the size floats already written.  Returns the slot's ref."""
-        t, off, addr = ref
+        t, off, addr, _ = ref
         assert t is self._chunk and self._fill == off + -(-size // 64) * 64, "cat target is not the last slot"
         need = -(-(size + n) // 64) * 64
         if off + need <= t.numel():
             self._fill = off + need
+            self.chunk_fill[self._nchunk] = self._fill
             return ref
         new = self.alloc(size + n)
         self._op((_lib.DFQ_BC_OP_COPY, 0, addr, 0, new[2], 0, size, 0, 0), (ref[3], _NULL, new[3], _NULL))

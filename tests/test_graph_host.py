@@ -186,3 +186,24 @@ def test_export_dequantize_u16_codes(tmp_path):
     meta["symmetric"] = True       # symmetric int16 stays signed
     y = export.dequantize(meta, "k", {"codes": codes, "scale": s, "zero": torch.tensor([0.0])})
     assert torch.equal(y, codes.float() * 0.5)
+
+
+def test_bc_chain_scratch_slot_growth_on_cpu():
+    """The walk's torch.cat of expectations (DeepLab's concat branches) grows the
+    last scratch slot: in place while its chunk has room, else into a fresh slot
+    filled by a COPY op; a recorded walk keeps each chunk's fill for its replay
+    (symbolic refs are 4-tuples: tensor, float offset, address, symbol)."""
+    import torch
+    from data_free_quantization_amd import _lib
+    from data_free_quantization_amd import bias_correction as bc
+    ch = bc._BcChain(torch.device("cpu"), record=True)
+    ref = ch.alloc(100)
+    assert len(ref) == 4 and ref[3] == (bc._S_SCRATCH, 0, 0)
+    assert ch.extend_last(ref, 100, 50) is ref and ch.chunk_fill == [192]
+    big = ch.alloc(bc._SCRATCH_CHUNK - 256)
+    new = ch.extend_last(big, bc._SCRATCH_CHUNK - 256, 128)
+    assert new[0] is not big[0] and new[3] == (bc._S_SCRATCH, 1, 0)
+    kind, _, src, _, dst, _, n = ch.ops[-1][:7]
+    assert kind == _lib.DFQ_BC_OP_COPY and (src, dst, n) == (big[2], new[2], bc._SCRATCH_CHUNK - 256)
+    assert ch.sym[-1][1][0] == big[3] and ch.sym[-1][1][2] == new[3]
+    assert ch.chunk_fill == [bc._SCRATCH_CHUNK - 64, bc._SCRATCH_CHUNK - 128]
