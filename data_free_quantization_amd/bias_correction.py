@@ -393,27 +393,39 @@ _TEMPLATES = OrderedDict()
 _TEMPLATE_CAP = 8
 
 
+#: node kind per (module type, targ_type, bn_type): 1 BN, 2 target layer, 0 other
+_KINDS = {}
+
+
 def _structure(graph, bottoms, targ_type, bn_type, signed, bits_weight, error_sums):
     """Everything the walk's control flow and op fields depend on (the graph's
     keys, node types, bottoms, the shapes of targets / biases / BN statistics /
-    error sums), as a hashable signature; plus the per-node tensors a replay
-    takes addresses from.  The walk never reads a tensor value."""
+    error sums), as a hashable signature of flat tuples (cheap to hash and to
+    compare); plus the per-node tensors a replay takes addresses from.  The walk
+    never reads a tensor value."""
     nodes = {}
     shp = []
-    keys = list(graph.keys())
-    for i, v in enumerate(graph.values()):
-        t = type(v)
-        if isinstance(v, bn_type):
+    kinds = _KINDS
+    keys = tuple(graph.keys())
+    vals = list(graph.values())
+    types = tuple(map(type, vals))
+    for i, v in enumerate(vals):
+        t = types[i]
+        k = kinds.get((t, targ_type, bn_type))
+        if k is None:
+            k = kinds[(t, targ_type, bn_type)] = (1 if issubclass(t, bn_type) else
+                                                  2 if issubclass(t, targ_type) and t is not str else 0)
+        if k == 1:
             fw, fb = _buf(v, "fake_weight"), _buf(v, "fake_bias")
             nodes[i] = (fw, fb)
-            shp.append((i, 0, fw.shape, fb.shape))
-        elif isinstance(v, targ_type) and t is not str:
+            shp += (i, -1, *fw.shape, -2, *fb.shape)
+        elif k == 2:
             w, b = _param(v, "weight"), _param(v, "bias")
             pre = error_sums.get(keys[i])
-            n = -1 if pre is None else (pre.numel() if isinstance(pre, torch.Tensor) else pre[2])
             nodes[i] = (b, pre)
-            shp.append((i, 1, w.shape, None if b is None else b.shape, n))
-    sig = (tuple(keys), tuple(map(type, graph.values())), tuple(bottoms.keys()),
+            shp += (i, -3, *w.shape, -4, *(() if b is None else b.shape), -5 if b is None else -6,
+                    -1 if pre is None else (pre.numel() if isinstance(pre, torch.Tensor) else pre[2]))
+    sig = (keys, types, tuple(bottoms.keys()),
            tuple(None if v is None else tuple(v) for v in bottoms.values()), targ_type, bn_type, bool(signed),
            int(bits_weight), _lib.REF_THREADS, tuple(shp))
     return sig, nodes
