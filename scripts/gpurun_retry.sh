@@ -4,7 +4,7 @@
 # failure reported before the command started.  A command that ran and failed is
 # never resubmitted.  usage: scripts/gpurun_retry.sh <log> <timeout> <command>
 log=$1; to=$2; shift 2
-for attempt in 1 2 3 4 5 6 7 8; do
+for attempt in $(seq 1 ${ATTEMPTS:-8}); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$@" > "$log" 2>&1
   rc=$?
   if [ $rc -eq 3 ] || grep -q "backing off\|status=transient" "$log"; then
