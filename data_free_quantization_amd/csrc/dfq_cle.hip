@@ -1138,7 +1138,8 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
                                                const float* __restrict__ part, int32_t S, double* __restrict__ means,
                                                double* __restrict__ hist, CleState* __restrict__ st, double* sm,
                                                float* part_lds = nullptr, float* np_stack = nullptr,
-                                               uint32_t* hflag = nullptr) {
+                                               uint32_t* hflag = nullptr, uint64_t* sig = nullptr,
+                                               uint64_t gen = 0) {
     if (part_lds) {   // every chunk sum in one parallel pass of coherent loads
         for (int64_t i = threadIdx.x; i < (int64_t)nl * S; i += blockDim.x)
             part_lds[i] = kCoherent ? ld_coh(part + i) : part[i];
@@ -1181,6 +1182,14 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         if (hflag)
             __hip_atomic_store(hflag, ((uint32_t)(it + 1) << 1) | (uint32_t)done, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
+        // A launched run: the caller's stream is released here, at convergence,
+        // instead of behind the host's check and the no-op batch enqueued ahead of
+        // it.  Every rescale ran in an earlier launch of the stream (complete, its
+        // writes released at its end); what this launch's remaining blocks write
+        // (next-iteration range words) is the loop's own.  Not after a flagged
+        // error: the worker then fails the run and the gate stays shut.
+        if (done && sig && __hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            __hip_atomic_store(sig, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1217,6 +1226,8 @@ struct CleFin {
     int32_t S, nl;
     int32_t last;            // the iteration's last launch
     uint32_t* hflag;         // pinned host word: (iterations << 1) | done, or null
+    uint64_t* sig;           // a launched run: the caller's gate word and the generation
+    uint64_t gen;            // that releases it at convergence (else null)
 };
 
 // The launches of one iteration.  Launch k < steps runs the rescale tasks of
@@ -1296,11 +1307,11 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
         if (F.nl <= 128)   // numpy's pairwise sum over the layer means is one leaf
             cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
-                                       stage_part ? lds + 2048 : nullptr, nullptr, F.hflag);
+                                       stage_part ? lds + 2048 : nullptr, nullptr, F.hflag, F.sig, F.gen);
         else   // the frame stack after the metric tile area (free: this block's units are done)
             cle_final_body<false, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st,
                                         reinterpret_cast<double*>(lds), stage_part ? lds + 2048 : nullptr,
-                                        lds + kCleTile, F.hflag);
+                                        lds + kCleTile, F.hflag, F.sig, F.gen);
     };
     if (F.nbig == 0) {   // no chunk has tiles (tiny or no target layers): the last launch's one block finishes
         if (blk == nab && F.last) finish();
@@ -1353,6 +1364,8 @@ struct dfq_cle_plan {
     CleState* d_state = nullptr;
     CleState* h_state = nullptr;    // pinned (the device context's, set by run)
     uint32_t* d_flag = nullptr;     // the stop rule's host word (the device context's, set by run)
+    uint64_t* d_sig = nullptr;      // a launched run: the caller's gate word and its generation
+    uint64_t gen = 0;
     hipStream_t st = nullptr;       // the loop's stream (the device context's)
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
     std::vector<char> step_pos;          // per step: position-parallel W2 tiles (the POS rescale kernel)
@@ -1957,7 +1970,8 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     // fused schedule: this iteration's ranges were taken during the previous one
     // (or by plan_run before the first); the next iteration's ride with the
     // launches after their tensors' last rescale (cle_loop_step_kernel)
-    CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, 0, p->d_flag};
+    CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, 0, p->d_flag,
+             p->d_sig, p->gen};
     for (int32_t k = 0; k <= p->steps; ++k) {
         const bool last = k == p->steps;
         const int64_t a0 = last ? 0 : p->astep[k], a1 = last ? 0 : p->astep[k + 1];
@@ -2398,6 +2412,9 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
     }
     p->async = a;
     ctx.pending = p;
+    p->d_sig = static_cast<uint64_t*>(ctx.sig);   // the stop rule opens the gate at convergence
+    p->gen = gen;
+    if (ab_env("DFQ_CLE_HOST_RELEASE")) p->d_sig = nullptr;   // diagnostics: the worker's release only
     bool posted = false;
     try {
         if (!ctx.worker) {

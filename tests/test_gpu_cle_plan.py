@@ -5,6 +5,7 @@ dead channel, a relation without BN stats, a layer shared by two relations in
 one chain and a large layer (multi-chunk metric).  Weights, biases, BN fake
 stats, Relation.S, iteration count and every per-iteration diff: bit-exact."""
 import os
+import time
 from collections import OrderedDict
 
 import numpy as np
@@ -304,6 +305,7 @@ def test_async_join_watchdog_keeps_callers_stream_held(monkeypatch):
     monkeypatch.setenv("DFQ_CLE_MODE", "device")
     monkeypatch.setenv("DFQ_CLE_TEST_RELEASE_DELAY_MS", "2500")
     monkeypatch.setenv("DFQ_CLE_TEST_JOIN_LIMIT_MS", "200")
+    monkeypatch.setenv("DFQ_CLE_HOST_RELEASE", "1")   # a loop that has not converged: no release from the stop rule
     g, rels = _graph(3)
     torch.cuda.synchronize()
     marker = torch.zeros(1, device=DEV)
@@ -315,3 +317,29 @@ def test_async_join_watchdog_keeps_callers_stream_held(monkeypatch):
     assert not torch.cuda.current_stream().query()   # still held: the downstream work has not run
     torch.cuda.synchronize()                 # the delayed release arrives, then it runs
     assert marker.item() == 1.0
+
+
+def test_async_caller_released_at_convergence(monkeypatch):
+    """The stop rule opens the caller's gate when the loop converges, before the
+    worker's own release (delayed here by 2.5 s): the work queued behind the loop
+    runs, sees the final weights, and LAST_RUN still comes from the join."""
+    from data_free_quantization_amd import _lib
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    monkeypatch.setattr(_lib, "_LIB", _lib.load_diag())
+    monkeypatch.setenv("DFQ_CLE_MODE", "device")
+    g0, r0 = _graph(3)
+    cle.cross_layer_equalization(g0, r0, [nn.Conv2d, nn.Linear], Treshhold=2e-7, Save_state=False, launch=False)
+    ref = {k: w.detach().clone() for k, w in _weights(g0).items()}
+    monkeypatch.setenv("DFQ_CLE_TEST_RELEASE_DELAY_MS", "2500")
+    g, rels = _graph(3)
+    torch.cuda.synchronize()
+    cle.cross_layer_equalization(g, rels, [nn.Conv2d, nn.Linear], Treshhold=2e-7, Save_state=False, launch=True)
+    t0 = time.perf_counter()
+    clones = {k: w.detach().clone() for k, w in _weights(g).items()}   # queued behind the loop
+    torch.cuda.current_stream().synchronize()
+    assert time.perf_counter() - t0 < 2.0       # released by the device, not by the delayed worker
+    assert cle._PENDING is not None             # the worker has not finished
+    for k in ref:
+        assert torch.equal(ref[k].view(torch.int32), clones[k].view(torch.int32)), k
+    cle.wait()
+    assert cle.LAST_RUN["launched"]
