@@ -1,5 +1,6 @@
 """CLE loop schedules A/B in one process (diagnostics library): the CLE stage
-time of run_dfq (per-channel sym INT8, fused BC) on MobileNetV2 and ResNet-50,
+time of run_dfq (per-channel sym INT8, fused BC) and its end-to-end time (no
+sync between stages) on MobileNetV2 and ResNet-50,
 median of ``--reps`` warm runs per configuration, interleaved; every
 configuration also checked against the reference fixture once.
 
@@ -20,13 +21,14 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
-SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_STATE_COPY")
+SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_STATE_COPY", "DFQ_CLE_HOST_RELEASE")
 CONFIGS = {
     "tiles_fin": {},                                # the product
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
     "tile_grid_1024": {"DFQ_CLE_TILE_GRID": "1024"},
     "step_grid_1024": {"DFQ_CLE_STEP_GRID": "1024"},
     "state_copy": {"DFQ_CLE_STATE_COPY": "1"},      # a state copy per batch on the loop stream
+    "host_release": {"DFQ_CLE_HOST_RELEASE": "1"},  # launched runs: the worker's release only
 }
 
 
@@ -53,6 +55,7 @@ def main():
         os.environ.update(CONFIGS[tag])
 
     res = {(t, m): [] for t in cfgs for m in models}
+    e2e = {(t, m): [] for t in cfgs for m in models}
     host = {(t, m): [] for t in cfgs for m in models}
     info = {}
     for t in cfgs:   # parity + warm-up
@@ -75,11 +78,23 @@ def main():
                 torch.cuda.synchronize(dev)
                 res[(t, m)].append(tm["cle"] * 1e3)
                 host[(t, m)].append(cle.LAST_RUN.get("host_ms", {}))
+                # end to end as main_dfq runs it: no sync between the stages
+                model = zoo.build(m, seed=0, relu=True).to(dev)
+                g = build_graph(model, "positional")
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                with contextlib.redirect_stdout(io.StringIO()):
+                    run_dfq(model, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel",
+                            symmetric=True, bc_mode="fused")
+                torch.cuda.synchronize(dev)
+                e2e[(t, m)].append((time.perf_counter() - t0) * 1e3)
     for t in cfgs:
         for m in models:
             v = res[(t, m)]
             print(json.dumps({"config": t, "model": m, "cle_ms_median": round(statistics.median(v), 3),
-                              "cle_ms_min": round(min(v), 3), **info[(t, m)],
+                              "cle_ms_min": round(min(v), 3),
+                              "e2e_ms_median": round(statistics.median(e2e[(t, m)]), 3),
+                              "e2e_ms_min": round(min(e2e[(t, m)]), 3), **info[(t, m)],
                               "host_ms_median": {k: round(statistics.median(h[k] for h in host[(t, m)]), 3)
                                                  for k in (host[(t, m)][0] if host[(t, m)] else {})}}), flush=True)
 
