@@ -1772,6 +1772,8 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     // k <= steps; resets of a relation's words after that relation's own step.
     // The unfused schedule keeps them all in the last launch.
     std::vector<int64_t> ulaunch(steps + 2, 0), rlaunch(steps + 2, 0);
+    // diagnostics A/B: round 3's placement, every tile and range task in the last launch
+    const bool tiles_last = ab_env("DFQ_CLE_TILES_LAST") != nullptr;
     {
         std::vector<int32_t> last_step(n_targets, -1);
         std::unordered_map<const float*, int32_t> layer_of;
@@ -1785,7 +1787,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             touch(R[r].w2, step_of[r]);
         }
         auto launch_of_w = [&](const float* w) -> int32_t {
-            if (!fused) return steps;
+            if (!fused || tiles_last) return steps;
             auto it = layer_of.find(w);
             int32_t k = 0;
             for (int32_t r = 0; r < n_rel; ++r)   // a tensor that is no target: after its relations' steps
@@ -1796,7 +1798,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         std::vector<std::vector<CleUnit>> ub(steps + 1);
         for (const CleUnit& u : units) {
             const int32_t l = chunks[u.chunk].layer;
-            ub[fused ? std::min(last_step[l] + 1, steps) : steps].push_back(u);
+            ub[(fused && !tiles_last) ? std::min(last_step[l] + 1, steps) : steps].push_back(u);
         }
         // the stop rule runs at the iteration's last arrival, which must come in the
         // last launch (after every rescale): if no unit landed there (the last
@@ -1820,7 +1822,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 int32_t k;
                 if (tk.kind == kRangeW1) k = launch_of_w(q.w1);
                 else if (tk.kind == kRangeW2Contig || tk.kind == kRangeW2Tile) k = launch_of_w(q.w2);
-                else k = std::min(step_of[tk.rel] + 1, steps);   // resets: after the relation's own step
+                else k = tiles_last ? steps : std::min(step_of[tk.rel] + 1, steps);   // resets: after the relation's own step
                 rb[k].push_back(tk);
             }
             rt.resize(ri0);
