@@ -69,7 +69,7 @@ constexpr Variant kVariants[] = {
     {2048, 64, false},    // 15: variant 6 with the generic quantize loop (flags tested per float4; round 3)
 };
 constexpr int kNumVariants = 16;
-// DevTask.nrows <= kGroupTag: a row-group piece of R = kGroupTag - nrows + 1 rows
+// HostTask / DevTask .nrows <= kGroupTag: a row-group piece of R = kGroupTag - nrows + 1 rows
 constexpr int kGroupTag = -64;
 constexpr int kGroupMaxRows = 16;
 #ifndef DFQ_DEFAULT_VARIANT   // compile-time override for side-by-side A/B builds (scripts/ab_variant_libs.py)
@@ -101,7 +101,12 @@ struct alignas(16) DevTensor {
     const uint32_t* range_enc;   // DFQ_DEVICE_RANGE
 };
 
-struct alignas(16) DevTask {
+// A wave task as the host builds it (HostTask) and as the kernels read it
+// (DevTask): the device record carries the address of its first element and the
+// tensor's 16-B-vector flag, so a wave issues the task's LDS-DMA as soon as the
+// record has landed, while the tensor's 128-B descriptor is still on its way
+// (one dependent scalar round trip off every task's critical path).
+struct HostTask {
     int64_t elem_start;  // first element (tensor-relative)
     int32_t tensor;
     int32_t n;           // elements in the task
@@ -110,6 +115,17 @@ struct alignas(16) DevTask {
     int32_t slot;        // workspace (min,max) slot for pieces, -1 = given range
     int32_t first;       // this piece writes scale/zero for its slot
 };
+struct alignas(16) DevTask {
+    const float* src;    // T.src + elem_start
+    int32_t tensor;
+    int32_t n;
+    int32_t row0;
+    int32_t nrows;
+    int32_t slot;
+    int32_t flags;       // bit 0: first (as HostTask); bit 1: T.vec4
+};
+static_assert(sizeof(DevTask) == 32, "one 32-B scalar load per task record");
+__device__ __forceinline__ int64_t task_elem_start(const DevTask& k, const DevTensor& T) { return k.src - T.src; }
 
 // Per-wave LDS image: [NB buffers of CHUNK floats][MAXROWS scales][MAXROWS mins],
 // carved out of ONE __shared__ array (a second __shared__ object next to an
@@ -184,10 +200,9 @@ sweep_reduce_kernel(const DevTensor* __restrict__ tensors, const DevTask* __rest
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     for (int64_t t = wave0; t < ntasks; t += nwaves) {
         const DevTask task = tasks[t];
-        const DevTensor& T = tensors[task.tensor];
-        const float* src = T.src + task.elem_start;
+        const float* src = task.src;
         float vmin = INFINITY, vmax = -INFINITY;
-        if (T.vec4) {
+        if (task.flags & 2) {
             const int nj = task.n >> 2;
 #pragma unroll 8
             for (int j = lane; j < nj; j += kWave) {
@@ -217,10 +232,10 @@ sweep_reduce_kernel(const DevTensor* __restrict__ tensors, const DevTask* __rest
 // ---------------------------------------------------------------------------
 // Issue the task's HBM -> LDS DMA (all loads in flight; no wait).
 template <bool NT = false>
-__device__ __forceinline__ void issue_task_load(const DevTensor& T, const DevTask& task, float* data, int lane) {
-    const float* src = T.src + task.elem_start;
+__device__ __forceinline__ void issue_task_load(const DevTask& task, float* data, int lane) {
+    const float* src = task.src;
     const int n = task.n;
-    if (T.vec4) {
+    if (task.flags & 2) {
         const int nj = n >> 2;
         for (int m = 0; m * kWave < nj; ++m) {
             const int j = lane + m * kWave;
@@ -412,7 +427,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
             mx = dec_ord(T.range_enc[1]);
         }
         pc = make_qparams(mn, mx, T.bits, sym, T.flags, T.given_min, T.given_max);
-        if (task.first && lane == 0) {
+        if ((task.flags & 1) && lane == 0) {
             const int64_t row_g = (T.mode == DFQ_CHANNEL_ASYM || T.mode == DFQ_CHANNEL_SYM) ? task.row0 : 0;
             if (T.scale) st<false>(T.scale + row_g, pc.s);
             if (T.zero) st<false>(T.zero + row_g, pc.mn);
@@ -426,7 +441,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
     const int khw = T.khw;
     const float qmin = sym ? -(float)(1 << (T.bits - 1)) : 0.f;
     const float qmax = sym ? (float)((1 << (T.bits - 1)) - 1) : (float)((1 << T.bits) - 1);
-    const int64_t base = task.elem_start;
+    const int64_t base = task_elem_start(task, T);
 
     auto params_for = [&](int e) -> QParams {
         if (!whole) return pc;
@@ -628,8 +643,8 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
         for (int64_t t = wave0; t < ntasks; t += nwaves) {
             uint64_t tl0 = 0, tl1 = 0;
             if constexpr (TL) tl0 = wall_clock64();
+            issue_task_load<NT>(task, wl, lane);   // needs only the task record
             const DevTensor T = tensors[task.tensor];
-            issue_task_load<NT>(T, task, wl, lane);
             DevTask next = task;   // next record's scalar load overlaps this task
             if (t + nwaves < ntasks) next = tasks[t + nwaves];
             vm_wait_all();
@@ -644,7 +659,7 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                 // the rows its piece touches, a second barrier, then its row parameters.
                 const int R = kGroupTag - task.nrows + 1;
                 const int len = (int)T.row_len;
-                const int g0 = (int)(task.elem_start - (int64_t)task.row0 * len);   // piece offset in the group
+                const int g0 = (int)(task_elem_start(task, T) - (int64_t)task.row0 * len);   // piece offset in the group
                 const int rf = g0 / len;
                 const int rl = task.n > 0 ? (g0 + task.n - 1) / len : rf - 1;
                 for (int r = 0; r < R; ++r) {
@@ -760,7 +775,7 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
         int64_t t = wave0;
         if (t < ntasks) {
             const DevTask task = tasks[t];
-            issue_task_load<NT>(tensors[task.tensor], task, wl, lane);
+            issue_task_load<NT>(task, wl, lane);
         }
         for (; t < ntasks; t += nwaves) {
             const DevTask task = tasks[t];
@@ -770,7 +785,7 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
             const int64_t tn = t + nwaves;
             if (tn < ntasks) {
                 const DevTask nt = tasks[tn];
-                issue_task_load<NT>(tensors[nt.tensor], nt, wl + (cur ^ 1) * CHUNK, lane);
+                issue_task_load<NT>(nt, wl + (cur ^ 1) * CHUNK, lane);
             }
             float* data = wl + cur * CHUNK;
             if (T.vec4) compute_task<MAXROWS, true, NT, ESPEC, SCREEN>(T, task, data, ls, lmn, slot_min, slot_max, lane);
@@ -803,10 +818,10 @@ static int validate(const dfq_tensor_desc& d) {
 
 struct Built {
     std::vector<DevTensor> tensors;
-    std::vector<DevTask> reduce;
-    std::vector<DevTask> blockrow;   // groups of kWavesPerBlock, placed first in the main list
-    std::vector<DevTask> main;       // block rows, then tasks needing no reduce, then slot pieces
-    std::vector<DevTask> slotted;    // slot pieces, in reduce order (appended to main at the end)
+    std::vector<HostTask> reduce;
+    std::vector<HostTask> blockrow;   // groups of kWavesPerBlock, placed first in the main list
+    std::vector<HostTask> main;       // block rows, then tasks needing no reduce, then slot pieces
+    std::vector<HostTask> slotted;    // slot pieces, in reduce order (appended to main at the end)
     // slabs of the two-pass (reduce -> quantize) work: reduce[rslab[k], rslab[k+1]) and
     // the main list's slot pieces [mslab[k], mslab[k+1]) (offsets into `slotted`)
     std::vector<int64_t> rslab, mslab;
@@ -886,9 +901,9 @@ static int64_t reduce_span() {
     const char* e = ab_env("DFQ_SWEEP_REDUCE_SPAN");
     return (e && *e) ? std::max<int64_t>(1, atoll(e)) : 16384;
 }
-static void push_reduce(std::vector<DevTask>& R, const DevTask& k, int64_t span) {
+static void push_reduce(std::vector<HostTask>& R, const HostTask& k, int64_t span) {
     if (!R.empty()) {
-        DevTask& p = R.back();
+        HostTask& p = R.back();
         if (p.slot == k.slot && p.tensor == k.tensor && p.elem_start + p.n == k.elem_start &&
             (int64_t)p.n + k.n <= span) {
             p.n += k.n;
@@ -990,7 +1005,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                 const int64_t piece = ceil_div(ceil_div(tot, grp_unit), (int64_t)kWavesPerBlock) * grp_unit;
                 for (int i = 0; i < kWavesPerBlock; ++i) {
                     const int64_t off = std::min<int64_t>((int64_t)i * piece, tot);
-                    DevTask k{};
+                    HostTask k{};
                     k.tensor = ti; k.slot = -1; k.first = 0;
                     k.nrows = kGroupTag - (int32_t)(R - 1);
                     k.row0 = (int32_t)r0;
@@ -1016,7 +1031,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                 for (int i = 0; i < kWavesPerBlock; ++i) {
                     const int64_t r = r0 + i / gs;
                     const int64_t off = (int64_t)(i % gs) * bpl;
-                    DevTask k{};
+                    HostTask k{};
                     k.tensor = ti; k.nrows = -gs; k.slot = -1;
                     if (r < nr) {
                         k.elem_start = r * blen + std::min<int64_t>(off, blen);
@@ -1037,7 +1052,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
             if (packed && (d.row_len & 1) && rpt > 1) rpt &= ~int64_t(1);   // even task starts
             for (int64_t r = 0; r < d.rows; r += rpt) {
                 const int64_t nr = std::min<int64_t>(rpt, d.rows - r);
-                DevTask k{};
+                HostTask k{};
                 k.elem_start = r * d.row_len; k.tensor = ti; k.n = (int32_t)(nr * d.row_len);
                 k.row0 = (int32_t)r; k.nrows = (int32_t)nr; k.slot = -1; k.first = 0;
                 B.main.push_back(k);
@@ -1048,7 +1063,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
             for (int64_t r = 0; r < d.rows; ++r) {
                 const int64_t slot = B.slots++;
                 for (int64_t off = 0; off < d.row_len; off += plen) {
-                    DevTask k{};
+                    HostTask k{};
                     k.elem_start = r * d.row_len + off; k.tensor = ti;
                     k.n = (int32_t)std::min<int64_t>(plen, d.row_len - off);
                     k.row0 = (int32_t)r; k.nrows = 0; k.slot = (int32_t)slot; k.first = (off == 0);
@@ -1063,7 +1078,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                 slab_used += 4 * total;
             }
             for (int64_t off = 0; off < total; off += plen) {
-                DevTask k{};
+                HostTask k{};
                 k.elem_start = off; k.tensor = ti; k.n = (int32_t)std::min<int64_t>(plen, total - off);
                 k.row0 = 0; k.nrows = 0; k.slot = (int32_t)slot; k.first = (off == 0);
                 if (!given) {
@@ -1083,6 +1098,18 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
     B.main.insert(B.main.end(), B.slotted.begin(), B.slotted.end());
     shuffle_quads(B);
     return DFQ_OK;
+}
+
+// The device form of a task list (DevTask: the first element's address, the
+// tensor's vector flag) into `out`.
+static void put_tasks(const std::vector<HostTask>& h, const std::vector<DevTensor>& T, char* out) {
+    DevTask* d = reinterpret_cast<DevTask*>(out);
+    for (size_t i = 0; i < h.size(); ++i) {
+        const HostTask& k = h[i];
+        const DevTensor& t = T[k.tensor];
+        d[i] = DevTask{t.src + k.elem_start, k.tensor, k.n, k.row0, k.nrows, k.slot,
+                       (k.first ? 1 : 0) | (t.vec4 ? 2 : 0)};
+    }
 }
 
 static int variant_from_env() {
@@ -1237,9 +1264,8 @@ static int sweep_plan_create_impl(const dfq_tensor_desc* descs, int32_t n, void*
     if (e == hipSuccess) {
         std::vector<char> blob(Lo.o_slots, 0);   // the host-built tables
         if (n > 0) std::memcpy(blob.data() + Lo.o_tensors, B.tensors.data(), sizeof(DevTensor) * n);
-        if (!B.reduce.empty())
-            std::memcpy(blob.data() + Lo.o_reduce, B.reduce.data(), sizeof(DevTask) * B.reduce.size());
-        if (!B.main.empty()) std::memcpy(blob.data() + Lo.o_main, B.main.data(), sizeof(DevTask) * B.main.size());
+        put_tasks(B.reduce, B.tensors, blob.data() + Lo.o_reduce);
+        put_tasks(B.main, B.tensors, blob.data() + Lo.o_main);
         if (ws) {   // stream-ordered: pinned staging, no host synchronisation
             e = stage_h2d(base, blob.data(), Lo.o_slots, stream);
         } else {
@@ -1419,8 +1445,8 @@ extern "C" int dfq_quantize_tensor(const dfq_tensor_desc* d, void* ws, size_t ws
         const size_t tb = om + sizeof(DevTask) * B.main.size() - ot;
         std::vector<char> blob(tb, 0);
         std::memcpy(blob.data(), B.tensors.data(), sizeof(DevTensor));
-        if (!B.reduce.empty()) std::memcpy(blob.data() + (orr - ot), B.reduce.data(), sizeof(DevTask) * B.reduce.size());
-        if (!B.main.empty()) std::memcpy(blob.data() + (om - ot), B.main.data(), sizeof(DevTask) * B.main.size());
+        put_tasks(B.reduce, B.tensors, blob.data() + (orr - ot));
+        put_tasks(B.main, B.tensors, blob.data() + (om - ot));
         DFQ_HIP_CHECK(stage_h2d(dt, blob.data(), tb, s));
     }
     if (!B.reduce.empty()) {
