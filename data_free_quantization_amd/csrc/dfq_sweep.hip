@@ -822,9 +822,6 @@ struct Built {
     std::vector<HostTask> blockrow;   // groups of kWavesPerBlock, placed first in the main list
     std::vector<HostTask> main;       // block rows, then tasks needing no reduce, then slot pieces
     std::vector<HostTask> slotted;    // slot pieces, in reduce order (appended to main at the end)
-    // slabs of the two-pass (reduce -> quantize) work: reduce[rslab[k], rslab[k+1]) and
-    // the main list's slot pieces [mslab[k], mslab[k+1]) (offsets into `slotted`)
-    std::vector<int64_t> rslab, mslab;
     int64_t slots = 0;
     int64_t elems = 0;
     int64_t algo_bytes = 0;
@@ -857,7 +854,7 @@ static int piece_len(int khw, bool vec4, int chunk, bool packed = false) {
     return p > 0 ? p : -1;
 }
 
-// A/B and diagnostics switches (DFQ_SWEEP_VARIANT / _SLAB_MB / _REDUCE_SPAN /
+// A/B and diagnostics switches (DFQ_SWEEP_VARIANT / _REDUCE_SPAN /
 // _SHUFFLE / _BLOCKS_PER_CU) are read only by the diagnostics library
 // (libdfq_diag.so, -DDFQ_DIAGNOSTICS); the product library runs the measured
 // defaults whatever the environment says.
@@ -879,20 +876,11 @@ static bool blockrow_enabled() {
     return !(e && e[0] == '0');
 }
 
-// DFQ_SWEEP_SLAB_MB: split the two-pass (reduce -> quantize) tensors into slabs of
-// about this many MB, each reduced and quantized back to back, so the second read
-// of a slab can still hit the 256 MB Infinity Cache (0: one slab).
-// Two-pass ranges can be pipelined in slabs of this many bytes of inputs (see
-// dfq_sweep_plan_execute): the quantize pass of slab k re-reads its inputs while
-// they are still in the 256 MB Infinity Cache.  Measured slower at every slab
-// size (profiles/r02/ab_slab.json: 16-256 MB slabs on two streams 1.34-3.9 ms per
-// step against 1.11 for the two passes back to back), so the product runs one
-// slab; DFQ_SWEEP_SLAB_MB sets the size in the diagnostics library.
-constexpr int64_t kSlabBytes = 0;
-static int64_t slab_bytes() {
-    const char* e = ab_env("DFQ_SWEEP_SLAB_MB");
-    return (e && *e) ? (int64_t)atoll(e) << 20 : kSlabBytes;
-}
+// Two-pass ranges pipelined in slabs (the quantize pass of slab k re-reading its
+// inputs while they are still in the 256 MB Infinity Cache, on two streams) were
+// measured slower at every slab size (profiles/r02/ab_slab.json: 16-256 MB slabs
+// 1.34-3.9 ms per step against 1.11 for the two passes back to back) and deleted
+// in round 4.
 
 // Reduce-launch tasks: consecutive pieces of one range merged up to `span`
 // elements per wave task (fewer same-address atomics, longer read streams).
@@ -915,11 +903,10 @@ static void push_reduce(std::vector<HostTask>& R, const HostTask& k, int64_t spa
 
 // DFQ_SWEEP_SHUFFLE=<seed> (A/B): visit the main list's 4-task units (one
 // workgroup's grid-stride step; block-row groups stay whole) in a seeded random
-// order instead of list order.  Only for single-slab plans (slab ranges index
-// the list).
+// order instead of list order.
 static void shuffle_quads(Built& B) {
     const char* e = ab_env("DFQ_SWEEP_SHUFFLE");
-    if (!e || !*e || B.mslab.size() > 2) return;
+    if (!e || !*e) return;
     const int64_t units = (int64_t)B.main.size() / kWavesPerBlock;
     if (units < 2) return;
     uint64_t x = (uint64_t)atoll(e) * 0x9E3779B97F4A7C15ull + 1;
@@ -935,17 +922,6 @@ static void shuffle_quads(Built& B) {
 static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Variant& V) {
     const int64_t rspan = reduce_span();
     const bool use_blockrow = blockrow_enabled();
-    const int64_t slab = slab_bytes();
-    int64_t slab_used = 0;
-    B.rslab.assign(1, 0);
-    B.mslab.assign(1, 0);
-    auto close_slab_if_full = [&](int64_t next_bytes) {
-        if (slab > 0 && slab_used > 0 && slab_used + next_bytes > slab) {
-            B.rslab.push_back((int64_t)B.reduce.size());
-            B.mslab.push_back((int64_t)B.slotted.size());
-            slab_used = 0;
-        }
-    };
     const int kChunk = V.chunk, kMaxRows = V.max_rows;
     for (int32_t ti = 0; ti < n; ++ti) {
         const dfq_tensor_desc& d = descs[ti];
@@ -1058,8 +1034,6 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
                 B.main.push_back(k);
             }
         } else if (channel) {   // long rows: one slot per row
-            close_slab_if_full(4 * total);
-            slab_used += 4 * total;
             for (int64_t r = 0; r < d.rows; ++r) {
                 const int64_t slot = B.slots++;
                 for (int64_t off = 0; off < d.row_len; off += plen) {
@@ -1073,10 +1047,6 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
             }
         } else {                // tensor modes: one slot per tensor (none for a given range)
             const int64_t slot = given ? -1 : B.slots++;
-            if (!given) {
-                close_slab_if_full(4 * total);
-                slab_used += 4 * total;
-            }
             for (int64_t off = 0; off < total; off += plen) {
                 HostTask k{};
                 k.elem_start = off; k.tensor = ti; k.n = (int32_t)std::min<int64_t>(plen, total - off);
@@ -1090,12 +1060,8 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
             }
         }
     }
-    B.rslab.push_back((int64_t)B.reduce.size());
-    B.mslab.push_back((int64_t)B.slotted.size());
     B.main.insert(B.main.begin(), B.blockrow.begin(), B.blockrow.end());
-    const int64_t base = (int64_t)B.main.size();   // slot pieces follow the single-pass tasks
-    for (auto& m : B.mslab) m += base;
-    B.main.insert(B.main.end(), B.slotted.begin(), B.slotted.end());
+    B.main.insert(B.main.end(), B.slotted.begin(), B.slotted.end());   // slot pieces after the single-pass tasks
     shuffle_quads(B);
     return DFQ_OK;
 }
@@ -1192,14 +1158,6 @@ struct dfq_sweep_plan {
     uint32_t* d_slots = nullptr;   // [slots] mins then [slots] maxs
     void* d_owned = nullptr;       // the tables' allocation when no workspace was given
     int64_t n_reduce = 0, n_main = 0, n_slots = 0, n_tensors = 0, n_elems = 0, algo_bytes = 0;
-    std::vector<int64_t> rslab, mslab;   // slab boundaries (Built)
-    // slab pipeline: reduce launches on `aux`, quantize launches on the caller's
-    // stream, each quantize slab waiting for its reduce (ev_r) and each reduce
-    // waiting for the quantize two slabs back (ev_m: the reduce stream stays at
-    // most two slabs ahead, so the re-reads hit the Infinity Cache)
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_fork = nullptr;
-    std::vector<hipEvent_t> ev_r, ev_m;
 };
 
 namespace dfq {
@@ -1249,8 +1207,6 @@ static int sweep_plan_create_impl(const dfq_tensor_desc* descs, int32_t n, void*
     p->n_tensors = n;
     p->n_elems = B.elems;
     p->algo_bytes = B.algo_bytes;
-    p->rslab = B.rslab;
-    p->mslab = B.mslab;
     hipError_t e = hipSuccess;
     char* base = static_cast<char*>(ws);
     if (!base) {
@@ -1299,64 +1255,16 @@ extern "C" int dfq_sweep_plan_execute(dfq_sweep_plan* p, void* stream) {
         DFQ_HIP_CHECK(hipMemsetAsync(p->d_slots, 0xFF, sizeof(uint32_t) * p->n_slots, s));
         DFQ_HIP_CHECK(hipMemsetAsync(p->d_slots + p->n_slots, 0x00, sizeof(uint32_t) * p->n_slots, s));
     }
-    const size_t nslab = p->rslab.size() - 1;
-    if (nslab <= 1) {   // one reduce launch over every slot piece, then one main launch
-        if (p->n_reduce > 0) {
-            hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for(p->n_reduce)), dim3(kBlockThreads), 0, s,
-                               p->d_tensors, p->d_reduce, p->n_reduce, p->d_slots, p->d_slots + p->n_slots);
-            DFQ_LAUNCH_CHECK();
-        }
-        if (p->n_main > 0) {
-            launch_main(p->variant, grid_for_variant(p->n_main, p->variant), s, p->d_tensors, p->d_main, p->n_main,
-                        p->d_slots, p->d_slots + p->n_slots);
-            DFQ_LAUNCH_CHECK();
-        }
-        return DFQ_OK;
-    }
-    // slabs, two streams: the single-pass tasks, then quantize slab k as soon as
-    // reduce slab k (running ahead on the plan's aux stream) has its ranges
-    if (!p->aux) {
-        int dev = 0;
-        DFQ_HIP_CHECK(hipStreamGetDevice(s, &dev));
-        int cur = 0;
-        DFQ_HIP_CHECK(hipGetDevice(&cur));
-        if (cur != dev) DFQ_HIP_CHECK(hipSetDevice(dev));
-        hipError_t e = hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming);
-        p->ev_r.assign(nslab, nullptr);
-        p->ev_m.assign(nslab, nullptr);
-        for (size_t k = 0; k < nslab && e == hipSuccess; ++k) {
-            e = hipEventCreateWithFlags(&p->ev_r[k], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_m[k], hipEventDisableTiming);
-        }
-        if (cur != dev) (void)hipSetDevice(cur);
-        DFQ_HIP_CHECK(e);
-    }
-    DFQ_HIP_CHECK(hipEventRecord(p->ev_fork, s));   // after the slot initialisation
-    DFQ_HIP_CHECK(hipStreamWaitEvent(p->aux, p->ev_fork, 0));
-    const int64_t single = p->mslab[0];   // blockrow + whole-row tasks: no range needed
-    if (single > 0) {
-        launch_main(p->variant, grid_for_variant(single, p->variant), s, p->d_tensors, p->d_main, single, p->d_slots,
-                    p->d_slots + p->n_slots);
+    // one reduce launch over every slot piece, then one main launch
+    if (p->n_reduce > 0) {
+        hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for(p->n_reduce)), dim3(kBlockThreads), 0, s, p->d_tensors,
+                           p->d_reduce, p->n_reduce, p->d_slots, p->d_slots + p->n_slots);
         DFQ_LAUNCH_CHECK();
     }
-    for (size_t k = 0; k < nslab; ++k) {
-        const int64_t r0 = p->rslab[k], r1 = p->rslab[k + 1];
-        if (k >= 2) DFQ_HIP_CHECK(hipStreamWaitEvent(p->aux, p->ev_m[k - 2], 0));
-        if (r1 > r0) {
-            hipLaunchKernelGGL(sweep_reduce_kernel, dim3(grid_for(r1 - r0)), dim3(kBlockThreads), 0, p->aux,
-                               p->d_tensors, p->d_reduce + r0, r1 - r0, p->d_slots, p->d_slots + p->n_slots);
-            DFQ_LAUNCH_CHECK();
-        }
-        DFQ_HIP_CHECK(hipEventRecord(p->ev_r[k], p->aux));
-        DFQ_HIP_CHECK(hipStreamWaitEvent(s, p->ev_r[k], 0));
-        const int64_t m0 = p->mslab[k], m1 = p->mslab[k + 1];
-        if (m1 > m0) {
-            launch_main(p->variant, grid_for_variant(m1 - m0, p->variant), s, p->d_tensors, p->d_main + m0, m1 - m0,
-                        p->d_slots, p->d_slots + p->n_slots);
-            DFQ_LAUNCH_CHECK();
-        }
-        DFQ_HIP_CHECK(hipEventRecord(p->ev_m[k], s));
+    if (p->n_main > 0) {
+        launch_main(p->variant, grid_for_variant(p->n_main, p->variant), s, p->d_tensors, p->d_main, p->n_main,
+                    p->d_slots, p->d_slots + p->n_slots);
+        DFQ_LAUNCH_CHECK();
     }
     return DFQ_OK;
 }
@@ -1368,15 +1276,7 @@ extern "C" int dfq_sweep_plan_stats(const dfq_sweep_plan* p, dfq_sweep_stats* st
     st->n_tasks_reduce = p->n_reduce;
     st->n_tasks_main = p->n_main;
     st->algo_bytes = p->algo_bytes;
-    if (p->rslab.size() > 2) {
-        int32_t l = 0;
-        l = p->mslab[0] > 0 ? 1 : 0;
-        for (size_t k = 0; k + 1 < p->rslab.size(); ++k)
-            l += (p->rslab[k + 1] > p->rslab[k] ? 1 : 0) + ((p->mslab[k + 1] > p->mslab[k]) ? 1 : 0);
-        st->launches = l;
-    } else {
-        st->launches = (p->n_reduce > 0 ? 1 : 0) + (p->n_main > 0 ? 1 : 0);
-    }
+    st->launches = (p->n_reduce > 0 ? 1 : 0) + (p->n_main > 0 ? 1 : 0);
     st->grid_blocks = p->n_main > 0 ? grid_for_variant(p->n_main, p->variant) : 0;
     st->variant = p->variant;
     return DFQ_OK;
@@ -1384,13 +1284,6 @@ extern "C" int dfq_sweep_plan_stats(const dfq_sweep_plan* p, dfq_sweep_stats* st
 
 extern "C" int dfq_sweep_plan_destroy(dfq_sweep_plan* p) {
     if (!p) return DFQ_OK;
-    if (p->aux) {
-        (void)hipStreamSynchronize(p->aux);
-        for (auto e : p->ev_r) (void)hipEventDestroy(e);
-        for (auto e : p->ev_m) (void)hipEventDestroy(e);
-        (void)hipEventDestroy(p->ev_fork);
-        (void)hipStreamDestroy(p->aux);
-    }
     (void)hipFree(p->d_owned);   // NULL for workspace-backed plans
     delete p;
     return DFQ_OK;

@@ -150,7 +150,7 @@ typedef struct dfq_sweep_stats {
     int64_t n_tasks_reduce;   /* wave tasks of the range-reduction launch (0 = launch skipped) */
     int64_t n_tasks_main;     /* wave tasks of the quantize launch */
     int64_t algo_bytes;       /* algorithmic HBM bytes of one execute */
-    int32_t launches;         /* kernel launches per execute (1, 2, or 2 per slab under DFQ_SWEEP_SLAB_MB) */
+    int32_t launches;         /* kernel launches per execute (1, or 2 with a reduce pass) */
     int32_t grid_blocks;      /* blocks of the quantize launch */
     int32_t variant;          /* kernel variant (env DFQ_SWEEP_VARIANT at create) */
     int32_t reserved;
