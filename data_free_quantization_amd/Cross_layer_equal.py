@@ -182,8 +182,9 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
     targets = [v._parameters["weight"] for v in graph.values() if type(v) in tl]
     n = len(relations)
     rows = []
+    fresh = []   # relations whose S the loop creates: views of one allocation, carved below
     for rel in relations:
-        first, second, bn_idx = rel.get_idxs()
+        first, second, bn_idx = rel.layer_first, rel.layer_second, rel.bn_idx
         l1, l2 = graph[first], graph[second]
         p1 = l1._parameters
         if p1.get("bias") is None:   # :93-94
@@ -195,11 +196,17 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
         _lib.require_device(W1, W2, B1, bnw, bnb)
         init = rel.S is None
         if init:
-            rel.S = torch.empty(W1.size(0), dtype=torch.float32, device=W1.device)
+            fresh.append((len(rows), rel, W1))
         s1, s2 = W1.shape, W2.shape
-        rows.append((W1.data_ptr(), W2.data_ptr(), B1.data_ptr(), 0 if bnw is None else bnw.data_ptr(),
-                     0 if bnb is None else bnb.data_ptr(), rel.S.data_ptr(), s1[0], W1.numel() // s1[0], s2[0], s2[1],
-                     W2.numel() // (s2[0] * s2[1]), 1 if init else 0, 0))
+        rows.append([W1.data_ptr(), W2.data_ptr(), B1.data_ptr(), 0 if bnw is None else bnw.data_ptr(),
+                     0 if bnb is None else bnb.data_ptr(), 0 if init else rel.S.data_ptr(), s1[0],
+                     W1.numel() // s1[0], s2[0], s2[1], W2.numel() // (s2[0] * s2[1]), 1 if init else 0, 0])
+    if fresh:   # one allocation for every new Relation.S (a torch.empty per relation cost ~7 us each)
+        flat = torch.empty(sum(w.size(0) for _, _, w in fresh), dtype=torch.float32, device=fresh[0][2].device)
+        for (j, rel, w), v in zip(fresh, torch.split(flat, [w.size(0) for _, _, w in fresh])):
+            rel.S = v
+            rows[j][5] = v.data_ptr()
+    rows = [tuple(r) for r in rows]
     # the descriptor table as a numpy record array (layout of _lib.CleRel), one row per
     # relation from plain tuples instead of ctypes field by field
     tab = np.array(rows if rows else [(0,) * 13], dtype=_CLE_REL)
