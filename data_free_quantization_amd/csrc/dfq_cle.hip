@@ -4,8 +4,8 @@
 // tensors they touch) and the k-th relation of every chain runs in one launch;
 // the per-iteration metric sum_l mean|W_l - W_l_prev| (fp32 torch.mean in ATen's
 // reduction order, then numpy's pairwise float64 sum) and the stop rule are
-// evaluated on the device.  The host enqueues iterations in batches and reads
-// the state back.  One relation at a time: dfq_cle_relation.hip.
+// evaluated on the device.  The host enqueues iterations and polls the stop
+// rule's word in pinned memory.  One relation at a time: dfq_cle_relation.hip.
 // fp32 arithmetic is ordered exactly as the reference's torch CPU ops.
 #include "dfq_cle_common.h"
 
@@ -88,7 +88,7 @@ struct CleState {
     int32_t done;
     int32_t count;       // Count
     int32_t max_iters;
-    int32_t error;       // persistent loop: a grid barrier timed out (never expected)
+    int32_t error;       // 2: a tile block saw an unexpected iteration parity (never expected)
 };
 
 constexpr int kCleW1RowsPerTask = 4;       // one wave per row
@@ -1177,14 +1177,14 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         const int done = (!cont || st->iters >= st->max_iters) ? 1 : 0;
         st->done = done;
         // the host's copy of the stop rule (pinned host memory; a system-scope
-        // vector store): the loop's host side reads it instead of copying the
-        // state back after every batch on the loop stream
+        // vector store): the loop's host side polls it to enqueue the next
+        // iteration or stop (cle_run_locked)
         if (hflag)
             __hip_atomic_store(hflag, ((uint32_t)(it + 1) << 1) | (uint32_t)done, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         // A launched run: the caller's stream is released here, at convergence,
-        // instead of behind the host's check and the no-op batch enqueued ahead of
-        // it.  Every rescale ran in an earlier launch of the stream (complete, its
+        // instead of behind the host's check and the no-op iteration enqueued
+        // ahead of it.  Every rescale ran in an earlier launch of the stream (complete, its
         // writes released at its end); what this launch's remaining blocks write
         // (next-iteration range words) is the loop's own.  Not after a flagged
         // error: the worker then fails the run and the gate stays shut.
@@ -1245,8 +1245,7 @@ struct CleFin {
 // The stop rule (last arrival, last launch) advances st->iters and may set
 // st->done while range blocks of the same launch are still being dispatched, so
 // range blocks take the next iteration's parity from the launch argument
-// (iteration i of a batch of kCleBatch, an even count, from a batch start that
-// is a multiple of it: parity (i + 1) & 1), never from st->iters; a range block
+// (iteration i of the run: parity (i + 1) & 1), never from st->iters; a range block
 // that starts after the stop rule said "done" skips its tasks (no later
 // iteration reads them).  Rescale and tile blocks read st->iters before the
 // stop rule can run (the rescale blocks of an earlier launch; the tile blocks
@@ -1411,10 +1410,9 @@ static double now_us() {
 struct CleDeviceCtx {
     std::mutex mu;
     hipStream_t st = nullptr;
-    CleState* h_state = nullptr;   // pinned: [0] the run's state, [1..2] the batch readback slots
+    CleState* h_state = nullptr;   // pinned: the run's state
     uint32_t* h_flag = nullptr;    // pinned, written by the stop rule: (iterations << 1) | done
     uint32_t* d_flag = nullptr;    // its device address
-    hipEvent_t ev[2] = {nullptr, nullptr};
     // Table pool: one plan at a time keeps its tables here (device + pinned upload
     // mirror), so a plan costs no hipMalloc / hipFree (hipFree waits for the whole
     // device) and its upload is an async DMA on the loop stream.
@@ -1448,13 +1446,11 @@ static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
         e = hipDeviceGetStreamPriorityRange(&least, &greatest);
         if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx.st, hipStreamNonBlocking, greatest);
     }
-    if (e == hipSuccess && !ctx.h_state) e = hipHostMalloc(&ctx.h_state, 3 * sizeof(CleState));
+    if (e == hipSuccess && !ctx.h_state) e = hipHostMalloc(&ctx.h_state, sizeof(CleState));
     if (e == hipSuccess && !ctx.h_flag) {
         e = hipHostMalloc(&ctx.h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx.d_flag), ctx.h_flag, 0);
     }
-    for (int i = 0; i < 2 && e == hipSuccess; ++i)
-        if (!ctx.ev[i]) e = hipEventCreateWithFlags(&ctx.ev[i], hipEventDisableTiming);
     if (e == hipSuccess && !ctx.pool_ev) e = hipEventCreateWithFlags(&ctx.pool_ev, hipEventDisableTiming);
     if (e == hipSuccess && !ctx.in_ev) e = hipEventCreateWithFlags(&ctx.in_ev, hipEventDisableTiming);
     return e;
@@ -1957,7 +1953,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
 }
 
 // One CLE iteration's launches (steps, metric, stop rule) on stream s.
-// j: the iteration's position in its graph batch (its parity is j & 1).
+// j: the iteration's index in the run (its parity is j & 1).
 static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     // grid caps: 2,048 / 4,096 blocks (caps of 128-1,024 measured 4-150 % slower on MobileNetV2)
     // step / tile grid caps (A/B: DFQ_CLE_STEP_GRID / DFQ_CLE_TILE_GRID, diagnostics library)
@@ -2001,12 +1997,12 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     return DFQ_OK;
 }
 
-// Iterations enqueued between state read-backs (even: see par_next).  4: the
-// batch after convergence (enqueued ahead of the check) runs as no-op launches,
-// and smaller batches waste fewer of them -- CLE on MobileNetV2 3.88 ms with 4,
-// 3.97 with 8 and 16 (profiles/r03/cle_ab_q.jsonl).
-constexpr int32_t kCleBatch = 4;
-static_assert(kCleBatch % 2 == 0, "the tiles/range launch's parity argument assumes even batches");
+// Iterations the host keeps enqueued behind the running one.  Whatever is queued
+// when the loop converges runs as no-op launches (every block returns at
+// st->done), and a no-op launch of a full-size grid still costs ~9 us
+// (profiles/r04/cle_trace_*): round 3's batches of 4 iterations, one batch
+// ahead, wasted 16-28 of them per run.
+constexpr int32_t kCleAhead = 1;
 // The context's history buffer for caps above the tables' kCleHistCap slots,
 // grown once (a launched run grows it before its caller's stream waits: hipFree
 // synchronises the whole device).
@@ -2074,11 +2070,6 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
                            p->d_state, 0);
         DFQ_LAUNCH_CHECK();
     }
-    // Batches of `batch` iterations (kernels of finished runs return at once: the
-    // stop rule lives in d_state), enqueued launch by launch.  (Replaying the batch
-    // as a captured HIP graph measured slower even with the capture cached: CLE on
-    // MobileNetV2 4.75 vs 4.51 ms, profiles/r03/cle_ab_p.jsonl.)
-    const int32_t batch = kCleBatch;
 #ifdef DFQ_DIAGNOSTICS
     uint64_t* d_tl = nullptr;   // DFQ_CLE_TL: per rescale task timestamps (cle_apply_body)
     const int64_t n_at = p->astep.empty() ? 0 : p->astep.back();
@@ -2089,40 +2080,32 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
         DFQ_HIP_CHECK(hipStreamSynchronize(s));
     }
 #endif
-    // One batch in flight ahead of the stop-rule check: batch k + 1 is enqueued
-    // before the host waits for batch k, so the check overlaps the GPU's next
-    // batch instead of idling it (round 2: ~31 us per batch boundary).  A batch
-    // enqueued after convergence runs as no-ops (every kernel returns at
-    // st->done).  The stop rule writes its outcome into pinned host memory
-    // (ctx.h_flag), so nothing but the event sits between two batches on the
-    // loop stream (diagnostics DFQ_CLE_STATE_COPY=1: a state copy per batch
-    // instead, into the other pinned slot).
-    const bool copy_state = ab_env("DFQ_CLE_STATE_COPY") != nullptr;
+    // Iteration by iteration, kCleAhead of them queued behind the running one: the
+    // stop rule writes (iterations << 1) | done into pinned host memory
+    // (ctx.h_flag, a system-scope store), and this thread polls that word -- no
+    // event, copy or host round trip sits between two iterations on the loop
+    // stream, and at convergence at most kCleAhead iterations are left to run as
+    // no-ops.  (Round 3 enqueued batches of 4 iterations a batch ahead and read
+    // the state back per batch; replaying a batch as a captured HIP graph
+    // measured slower, profiles/r03/cle_ab_p.jsonl.)  A stream that drains
+    // without the word saying done (a kernel error) ends the polling; the final
+    // state read below decides.
     const double tc1 = now_us();
     int32_t launched = 0;
-    int slot = 0;
-    auto enqueue_batch = [&](int sl) -> int {
-        for (int32_t it = 0; it < batch; ++it) {
-            const int rc = cle_enqueue_iteration(p, s, it);
-            if (rc != DFQ_OK) return rc;
-        }
-        launched += batch;
-        if (copy_state)
-            DFQ_HIP_CHECK(hipMemcpyAsync(ctx.h_state + 1 + sl, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
-        DFQ_HIP_CHECK(hipEventRecord(ctx.ev[sl], s));
-        return DFQ_OK;
-    };
     if (!init.done) {
-        int rc = enqueue_batch(slot);
-        if (rc != DFQ_OK) return rc;
+        int64_t polls = 0;
         for (;;) {
-            const bool more = launched < max_iters;
-            if (more && (rc = enqueue_batch(slot ^ 1)) != DFQ_OK) return rc;
-            DFQ_HIP_CHECK(hipEventSynchronize(ctx.ev[slot]));
-            const bool done = copy_state ? ctx.h_state[1 + slot].done != 0
-                                         : (__atomic_load_n(ctx.h_flag, __ATOMIC_ACQUIRE) & 1u) != 0;
-            if (done || !more) break;
-            slot ^= 1;
+            const uint32_t f = __atomic_load_n(ctx.h_flag, __ATOMIC_ACQUIRE);
+            if (f & 1u) break;
+            const int32_t ran = (int32_t)(f >> 1);
+            if (launched < max_iters && launched - ran <= kCleAhead) {
+                const int rc = cle_enqueue_iteration(p, s, launched);
+                if (rc != DFQ_OK) return rc;
+                ++launched;
+                continue;
+            }
+            if ((++polls & 255) == 0 && hipStreamQuery(s) != hipErrorNotReady) break;
+            __builtin_ia32_pause();
         }
     }
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
@@ -2181,11 +2164,11 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
         }
     }
 #endif
-    // the final state (a speculative batch after convergence changed nothing)
+    // the final state (a no-op iteration after convergence changed nothing)
     DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
     const CleState fin = *p->h_state;
-    if (fin.error) {   // a group barrier gave up (blocks not co-resident): never expected
+    if (fin.error) {   // a range block saw the wrong parity: never expected
         set_last_hip_error(hipErrorLaunchTimeOut);
         return DFQ_ERR_HIP;
     }
@@ -2251,7 +2234,7 @@ __global__ void __launch_bounds__(64) cle_caller_gate_kernel(const uint64_t* sig
 }  // namespace dfq
 
 // ---- asynchronous run (dfq_cle_plan_launch / _join) -------------------------
-// The loop needs the host between batches (the stop rule is read back), so a
+// The loop needs the host between iterations (it polls the stop rule), so a
 // worker thread drives it on the context's stream while the caller's thread goes
 // on enqueueing the next stages on its own stream.  That stream waits, in the
 // device, behind the gate kernel for a per-device signal word the worker writes

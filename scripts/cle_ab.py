@@ -21,14 +21,13 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
-SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_STATE_COPY", "DFQ_CLE_HOST_RELEASE",
+SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_HOST_RELEASE",
             "DFQ_CLE_TILES_LAST")
 CONFIGS = {
     "tiles_fin": {},                                # the product
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
     "tile_grid_1024": {"DFQ_CLE_TILE_GRID": "1024"},
     "step_grid_1024": {"DFQ_CLE_STEP_GRID": "1024"},
-    "state_copy": {"DFQ_CLE_STATE_COPY": "1"},      # a state copy per batch on the loop stream
     "host_release": {"DFQ_CLE_HOST_RELEASE": "1"},  # launched runs: the worker's release only
     "tiles_last": {"DFQ_CLE_TILES_LAST": "1"},      # round 3's placement: all tiles / ranges in the last launch
 }

@@ -13,7 +13,9 @@ for m in ${MODELS:-mobilenetv2 resnet50}; do
       python3 "$GRAFT_REPO_ROOT/scripts/cle_ab.py" --configs tiles_fin --models "$m" --reps 2 \
       > "$GRAFT_REPO_ROOT/$out/cle_ab_$m.log" 2>&1 || { echo "trace $m failed rc=$?"; tail -20 "$GRAFT_REPO_ROOT/$out/cle_ab_$m.log"; exit 1; }
   f=$(find "$GRAFT_REPO_ROOT/$out/kt_$m" -name "*kernel_trace.csv" | head -1)
-  python3 "$GRAFT_REPO_ROOT/scripts/cle_trace_summary.py" "$f" > "$GRAFT_REPO_ROOT/$out/summary_$m.txt" 2>&1
+  read L N < <(python3 -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(d['launches'], d['iterations'])" "$GRAFT_REPO_ROOT/$out/cle_ab_$m.log")
+  python3 "$GRAFT_REPO_ROOT/scripts/cle_trace_summary.py" "$f" --launches "$L" --iterations "$N" \
+      --csv "$GRAFT_REPO_ROOT/$out/loop_$m.csv" > "$GRAFT_REPO_ROOT/$out/summary_$m.txt" 2>&1
   cat "$GRAFT_REPO_ROOT/$out/summary_$m.txt"
-  rm -f "$f"   # keep the summary, not the multi-MB trace
+  rm -f "$f"   # keep the summary and the loop's dispatches, not the multi-MB trace
 done

@@ -1,59 +1,75 @@
 """CLE loop kernel timeline from a rocprofv3 ``--kernel-trace --output-format
-csv`` run: the last run of consecutive ``cle_loop_*`` dispatches (one device
-loop), per kernel kind the calls and mean / median duration, the gaps between
-dispatches, and the span per iteration (tiles/stop-rule launch to the next).
+csv`` run: the last device loop (the dispatches of the loop's kernels after the
+last ``cle_loop_snap_kernel``; the caller's kernels that run beside a launched
+loop are skipped), per launch position of an iteration the median duration and
+the gap before it, the span per iteration, and the no-op launches after
+convergence.  ``--launches`` is the loop's launches per iteration and
+``--iterations`` its iteration count (both in the cle_ab line); ``--csv``
+writes the loop's dispatches (small) for later reading.
 
-  python scripts/cle_trace_summary.py <kernel_trace.csv> [--iterations N]
+  python scripts/cle_trace_summary.py <kernel_trace.csv> --launches 4 --iterations 44 [--csv out.csv]
 """
+import argparse
 import csv
 import statistics
-import sys
 
 
-def main(path, iters=None):
-    rows = list(csv.DictReader(open(path)))
-    if not rows:
-        print("empty trace")
-        return
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--launches", type=int, required=True)
+    ap.add_argument("--iterations", type=int, required=True)
+    ap.add_argument("--csv")
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
     k = lambda r, *names: next(r[n] for n in names if n in r)   # noqa: E731
     ev = []
     for r in rows:
         ev.append((int(k(r, "Start_Timestamp", "start")), int(k(r, "End_Timestamp", "end")),
-                   k(r, "Kernel_Name", "kernel_name"), int(k(r, "Grid_Size_X", "Grid_Size", "grid_size") or 0),
-                   int(k(r, "Workgroup_Size_X", "Workgroup_Size", "workgroup_size") or 1)))
+                   k(r, "Kernel_Name", "kernel_name").split("(")[0].replace("dfq::", "").replace("void ", ""),
+                   int(k(r, "Grid_Size_X", "Grid_Size", "grid_size") or 0) //
+                   max(1, int(k(r, "Workgroup_Size_X", "Workgroup_Size", "workgroup_size") or 1))))
     ev.sort()
-    # the last maximal run of CLE loop kernels (gate / snapshot kernels included)
-    is_cle = lambda name: "cle_loop" in name or "cle_caller_gate" in name   # noqa: E731
-    end = max(i for i, e in enumerate(ev) if is_cle(e[2]))
-    start = end
-    while start > 0 and is_cle(ev[start - 1][2]):
-        start -= 1
-    run = [e for e in ev[start:end + 1] if "cle_caller_gate" not in e[2]]
-    kinds = {}
-    for i, (s, e, name, g, w) in enumerate(run):
-        short = name.split("(")[0].replace("dfq::", "")
-        if "apply" in short:
-            short += f"[grid {g // max(w, 1)}]"
-        d = kinds.setdefault(short, {"dur": [], "gap": []})
-        d["dur"].append((e - s) / 1e3)
-        if i:
-            d["gap"].append((s - run[i - 1][1]) / 1e3)
-    print(f"CLE run: {len(run)} dispatches, span {(run[-1][1] - run[0][0]) / 1e3:.1f} us")
-    print(f"{'kernel':60s} {'calls':>6s} {'mean_us':>8s} {'med_us':>8s} {'gap_med':>8s}")
-    for n, d in kinds.items():
-        print(f"{n[:60]:60s} {len(d['dur']):6d} {statistics.mean(d['dur']):8.2f} {statistics.median(d['dur']):8.2f} "
-              f"{statistics.median(d['gap']) if d['gap'] else 0:8.2f}")
-    tiles = [i for i, e in enumerate(run) if "tiles_fin" in e[2]]
-    if len(tiles) > 2:
-        per = [(run[b][1] - run[a][1]) / 1e3 for a, b in zip(tiles, tiles[1:])]
-        print(f"per iteration (tiles end to tiles end): median {statistics.median(per):.2f} us, "
-              f"min {min(per):.2f}, max {max(per):.2f}, iterations {len(per) + 1}")
-        mid = tiles[len(tiles) // 2]
-        prev = tiles[len(tiles) // 2 - 1]
-        print("one iteration (middle of the loop):")
-        for s, e, name, g, w in run[prev + 1:mid + 1]:
-            print(f"  {name.split('(')[0].replace('dfq::', '')[:50]:50s} dur {(e - s) / 1e3:7.2f} us  grid {g // max(w, 1)}")
+    snaps = [i for i, e in enumerate(ev) if "cle_loop_snap" in e[2]]
+    if not snaps:
+        print("no CLE loop in the trace")
+        return
+    run = [e for e in ev[snaps[-1]:] if "cle_loop" in e[2]]
+    steps = [e for e in run if "cle_loop_step" in e[2]]
+    L, N = a.launches, a.iterations
+    it = [steps[i * L:(i + 1) * L] for i in range(N)]
+    noop = steps[N * L:]
+    print(f"CLE loop: {len(run)} dispatches ({len(steps)} step launches: {N} iterations x {L} + {len(noop)} no-op), "
+          f"span {(run[-1][1] - run[0][0]) / 1e3:.1f} us")
+    print(f"{'position':>8s} {'kernel':34s} {'grid_med':>8s} {'dur_med':>8s} {'dur_min':>8s} {'gap_med':>8s}")
+    prev_end = {}
+    for p in range(L):
+        d = [(x[p][1] - x[p][0]) / 1e3 for x in it if len(x) == L]
+        g = []
+        for i, x in enumerate(it):
+            if len(x) != L:
+                continue
+            before = x[p - 1][1] if p else (it[i - 1][-1][1] if i and len(it[i - 1]) == L else None)
+            if before is not None:
+                g.append((x[p][0] - before) / 1e3)
+        grid = statistics.median([x[p][3] for x in it if len(x) == L])
+        print(f"{p:8d} {it[0][p][2][:34]:34s} {grid:8.0f} {statistics.median(d):8.2f} {min(d):8.2f} "
+              f"{statistics.median(g) if g else 0:8.2f}")
+    span = [(x[-1][1] - x[0][0]) / 1e3 for x in it if len(x) == L]
+    per = [(it[i][-1][1] - it[i - 1][-1][1]) / 1e3 for i in range(1, N) if len(it[i]) == L]
+    print(f"per iteration: launches span median {statistics.median(span):.2f} us; end to end median "
+          f"{statistics.median(per):.2f} us (min {min(per):.2f}, max {max(per):.2f})")
+    if noop:
+        print(f"no-op launches after convergence: {len(noop)}, {sum((e[1] - e[0]) for e in noop) / 1e3:.1f} us busy, "
+              f"last ends {(noop[-1][1] - it[-1][-1][1]) / 1e3:.1f} us after the last iteration")
+    if a.csv:
+        with open(a.csv, "w") as f:
+            w = csv.writer(f)
+            w.writerow(["start_ns", "end_ns", "kernel", "grid"])
+            t0 = run[0][0]
+            for e in run:
+                w.writerow([e[0] - t0, e[1] - t0, e[2], e[3]])
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main()
