@@ -84,7 +84,7 @@ for model in ("mobilenetv2", "resnet50"):
             g = build_graph(m, "positional")
             with contextlib.redirect_stdout(io.StringIO()):
                 pipeline.run_dfq(m, g.getGraph(), g.getBottoms(), (nn.Conv2d, nn.Linear), granularity="channel",
-                                 symmetric=True, bc_mode="fused")
+                                 symmetric=True, bc_mode="fused", timings={})
             if rep:
                 res.append((acc["stage"] * 1e3, acc.get("flush", 0.0) * 1e3, acc.get("structure", 0.0) * 1e3,
                             acc.get("replay_host", 0.0) * 1e3, acc.get("replay_device_tail", 0.0) * 1e3))

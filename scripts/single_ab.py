@@ -1,5 +1,6 @@
 """Single-model sweep latency per kernel variant: one weight set,
-per-channel sym INT8 + codes + clip + BC sums, device us per execute (diagnostic).
+per-channel sym INT8 + codes + clip + BC sums, device us per execute from HIP
+graph replays (a Python execute() alone costs more than one small sweep).
 usage: python scripts/single_ab.py [variants...]   (env DFQ_SWEEP_BLOCKS_PER_CU applies)"""
 import os
 os.environ.setdefault("DFQ_LIB", "diag")   # A/B variants, switches and probes: libdfq_diag.so
@@ -23,7 +24,8 @@ for model in ("mobilenetv2", "resnet50", "deeplab"):
     for v in variants:
         os.environ["DFQ_SWEEP_VARIANT"] = str(v)
         plan = SweepPlan(items)
-        ms = bench.time_plan(plan, stream, dev, 200, 20)
+        bench.time_plan(plan, stream, dev, 20, 5)                 # warm (host-paced rate: not reported)
+        ms = bench.time_plan_graph(plan, dev)                      # kernel-to-kernel (HIP graph replays)
         row[f"v{v}"] = round(ms * 1e3, 2)
         row[f"v{v}_grid"] = plan.stats["grid_blocks"]
         plan.destroy()
