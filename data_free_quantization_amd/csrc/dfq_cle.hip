@@ -542,7 +542,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
         const uint64_t tl_start = tl_on ? __builtin_amdgcn_s_memrealtime() : 0;
         uint64_t tl_sub = 0;   // position tiles: phase ends (10 ns ticks after start, 16 bits each)
 #define DFQ_CLE_TL_MARK(k) \
-        if (tl_on) tl_sub |= ((__builtin_amdgcn_s_memrealtime() - tl_start) & 0xffffull) << (16 * (k));
+        if (tl_on) tl_sub |= (1ull << 63) | (((__builtin_amdgcn_s_memrealtime() - tl_start) & 0xffffull) << (16 * (k)));
 #else
 #define DFQ_CLE_TL_MARK(k)
 #endif
@@ -756,6 +756,9 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                             y = v[j] * inv;
                             R.w2[(tk.a + j) * rowlen + i] = y;
                         }
+                        if (j == 0) {   // the column's loads and its scale have landed
+                            DFQ_CLE_TL_MARK(0)
+                        }
                         float a = act ? y : INFINITY, b = act ? y : -INFINITY;
                         cle_wave_minmax(a, b);
                         if (lane == 0) {
@@ -764,6 +767,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                         }
                     }
                 }
+                DFQ_CLE_TL_MARK(1)   // every row stored and reduced
             } else {
                 int64_t g_prev = -1;
                 float inv = 0.f;
@@ -793,6 +797,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                 }
             }
             __syncthreads();
+            DFQ_CLE_TL_MARK(2)
             if (threadIdx.x < tk.b - tk.a) {
                 const int j = threadIdx.x;
                 float a = red[0][0][j], b = red[1][0][j];
@@ -816,9 +821,12 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                         if (tk.a + j < tk.b) v[j] = R.w2[(tk.a + j) * rowlen + i];
                     const float inv = cle_rel_scale(rels, R, mins, maxs, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin,
                                                 smax).inv;
+                    R.w2[tk.a * rowlen + i] = v[0] * inv;
+                    DFQ_CLE_TL_MARK(0)   // the column's loads and its scale have landed
 #pragma unroll
-                    for (int j = 0; j < kColTileRows; ++j)
+                    for (int j = 1; j < kColTileRows; ++j)
                         if (tk.a + j < tk.b) R.w2[(tk.a + j) * rowlen + i] = v[j] * inv;
+                    DFQ_CLE_TL_MARK(1)
                     continue;
                 }
                 int64_t g_prev = -1;
@@ -2145,11 +2153,11 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
                 fprintf(stderr, " [%.2f us kind %d rel %d n %lld c1 %lld o2 %lld i2 %lld khw2 %lld o2g %lld fuse %d cols %lld",
                         d[i].first, (int)(m & 255), rel, (long long)(m >> 24), (long long)q.c1, (long long)q.o2,
                         (long long)q.i2, (long long)q.khw2, (long long)q.o2g, q.fuse_next, (long long)(tk.c1 - tk.c0));
-                if (q.khw2 > 1) {
-                    const uint64_t sub = tl[4 * d[i].second + 2];
-                    fprintf(stderr, " scales %.2f inv_pos %.2f rows %.2f", (double)(sub & 0xffff) * 0.01,
-                            (double)((sub >> 16) & 0xffff) * 0.01, (double)((sub >> 32) & 0xffff) * 0.01);
-                }
+                const uint64_t sub = tl[4 * d[i].second + 2];
+                if (sub >> 63)   // phase marks (us after the task's start)
+                    fprintf(stderr, q.khw2 > 1 ? " scales %.2f inv_pos %.2f rows %.2f" : " landed %.2f rows %.2f barrier %.2f",
+                            (double)(sub & 0xffff) * 0.01, (double)((sub >> 16) & 0xffff) * 0.01,
+                            (double)((sub >> 32) & 0xffff) * 0.01);
                 fprintf(stderr, "]");
             }
             // start-time histogram: when the tasks began relative to the first
