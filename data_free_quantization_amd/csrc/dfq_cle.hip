@@ -1804,8 +1804,13 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     // k <= steps; resets of a relation's words after that relation's own step.
     // The unfused schedule keeps them all in the last launch.
     std::vector<int64_t> ulaunch(steps + 2, 0), rlaunch(steps + 2, 0);
-    // diagnostics A/B: round 3's placement, every tile and range task in the last launch
-    const bool tiles_last = ab_env("DFQ_CLE_TILES_LAST") != nullptr;
+    // Every metric tile and next-iteration range task goes to the last launch (after
+    // the last step): placing each tensor's tiles and ranges in the launch right
+    // after its last rescale (diagnostics DFQ_CLE_TILES_EARLY=1) measured slower on
+    // every box -- MobileNetV2 CLE 3.89 vs 3.65 ms, ResNet-50 2.69 vs 2.62
+    // (profiles/r04/cle_ab_r04g.jsonl): beside the step's latency-bound rescale
+    // tasks they lengthen the chain's critical path.
+    const bool tiles_last = ab_env("DFQ_CLE_TILES_EARLY") == nullptr;
     {
         std::vector<int32_t> last_step(n_targets, -1);
         std::unordered_map<const float*, int32_t> layer_of;

@@ -3,7 +3,7 @@
  *
  * libdfq_diag.so is the product library (every dfq_hip.h entry point) built with
  * -DDFQ_DIAGNOSTICS: it also carries the sweep's A/B kernel variants and
- * environment switches (DFQ_SWEEP_VARIANT, DFQ_CLE_FUSED, DFQ_CLE_TILES_LAST, ...)
+ * environment switches (DFQ_SWEEP_VARIANT, DFQ_CLE_FUSED, DFQ_CLE_TILES_EARLY, ...)
  * and the probes below, which bench.py and scripts/ use to measure the ceiling
  * of the sweep's memory pattern.  None of this is part of the reference
  * interface; libdfq_hip.so exports none of it.
