@@ -1702,8 +1702,11 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                     out.push_back({r, kApplyW2Tile, a, std::min<int64_t>(a + rows, c.o2), i0,
                                    std::min<int64_t>(i0 + kThreads, c.i2)});
         }
-        for (int64_t a = 0; a < c.c1; a += kCleChansPerTask)
-            out.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kCleChansPerTask, c.c1), 0, 0});
+        // one channel per thread: each channel's scale is a chain of dependent loads
+        // and fp32 divides, and 1,024-channel tasks (4 channels a thread, one after
+        // the other) were the slowest of their steps (6-9 us, DFQ_CLE_TL)
+        for (int64_t a = 0; a < c.c1; a += kThreads)
+            out.push_back({r, kApplyChannels, a, std::min<int64_t>(a + kThreads, c.c1), 0, 0});
     };
     int64_t ri0 = 0, ri1 = 0;
     if (fused) {
@@ -1740,16 +1743,16 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             apply_tasks(r, at);
         }
         // The step's slowest tasks first (its span is the last task's end): W2 row
-        // tiles (strided columns, their loads and stores a row at a time), then the
-        // depthwise pairs, W1 rows, contiguous W2 channels, and the per-channel
-        // vectors (profiles/r03/cle_tl_*.log: tile tasks started up to 10 us into
-        // a step and ran ~10 us)
+        // tiles (strided columns, their loads and stores a row at a time), the
+        // per-channel vectors (each a chain of dependent loads), then the depthwise
+        // pairs, W1 rows and contiguous W2 channels (profiles/r03/cle_tl_*.log: tile
+        // tasks started up to 10 us into a step and ran ~10 us)
         auto prio = [](int32_t kind) {
             switch (kind) {
                 case kApplyW2Tile: return 0;
-                case kApplyDwBoth: return 1;
-                case kApplyW1: return 2;
-                case kApplyW2Contig: return 3;
+                case kApplyChannels: return 1;
+                case kApplyDwBoth: return 2;
+                case kApplyW1: return 3;
                 default: return 4;
             }
         };
