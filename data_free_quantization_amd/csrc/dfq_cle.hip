@@ -1814,6 +1814,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     // (profiles/r04/cle_ab_r04g.jsonl): beside the step's latency-bound rescale
     // tasks they lengthen the chain's critical path.
     const bool tiles_last = ab_env("DFQ_CLE_TILES_EARLY") == nullptr;
+    const bool ranges_last = ab_env("DFQ_CLE_RANGES_EARLY") == nullptr;   // the same A/B for the range tasks alone
     {
         std::vector<int32_t> last_step(n_targets, -1);
         std::unordered_map<const float*, int32_t> layer_of;
@@ -1827,7 +1828,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             touch(R[r].w2, step_of[r]);
         }
         auto launch_of_w = [&](const float* w) -> int32_t {
-            if (!fused || tiles_last) return steps;
+            if (!fused || ranges_last) return steps;
             auto it = layer_of.find(w);
             int32_t k = 0;
             for (int32_t r = 0; r < n_rel; ++r)   // a tensor that is no target: after its relations' steps
@@ -1862,7 +1863,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 int32_t k;
                 if (tk.kind == kRangeW1) k = launch_of_w(q.w1);
                 else if (tk.kind == kRangeW2Contig || tk.kind == kRangeW2Tile) k = launch_of_w(q.w2);
-                else k = tiles_last ? steps : std::min(step_of[tk.rel] + 1, steps);   // resets: after the relation's own step
+                else k = ranges_last ? steps : std::min(step_of[tk.rel] + 1, steps);   // resets: after the relation's own step
                 rb[k].push_back(tk);
             }
             rt.resize(ri0);

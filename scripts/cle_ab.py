@@ -22,14 +22,16 @@ sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_HOST_RELEASE",
-            "DFQ_CLE_TILES_EARLY")
+            "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY")
 CONFIGS = {
     "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
     "tile_grid_1024": {"DFQ_CLE_TILE_GRID": "1024"},
     "step_grid_1024": {"DFQ_CLE_STEP_GRID": "1024"},
     "host_release": {"DFQ_CLE_HOST_RELEASE": "1"},  # launched runs: the worker's release only
-    "tiles_early": {"DFQ_CLE_TILES_EARLY": "1"},    # each tensor's tiles / ranges right after its last rescale
+    "tiles_early": {"DFQ_CLE_TILES_EARLY": "1", "DFQ_CLE_RANGES_EARLY": "1"},   # each tensor's tiles / ranges right after its last rescale
+    "ranges_early": {"DFQ_CLE_RANGES_EARLY": "1"},  # only the range tasks early
+    "units_early": {"DFQ_CLE_TILES_EARLY": "1"},    # only the metric tiles early
 }
 
 

@@ -42,12 +42,12 @@ import json, os, sys
 sys.path.insert(0, os.environ["DFQ_ROOT"])
 from tests.parity import pipeline_mismatches
 from data_free_quantization_amd import Cross_layer_equal as cle
-SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_TILES_EARLY")
+SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY")
 CONFIGS = {
     "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches (graphs the fused schedule rejects)
     "tile_grid_64": {"DFQ_CLE_TILE_GRID": "64"},    # few tile blocks: each walks many metric units
-    "tiles_early": {"DFQ_CLE_TILES_EARLY": "1"},    # each tensor's tiles / ranges right after its last rescale
+    "tiles_early": {"DFQ_CLE_TILES_EARLY": "1", "DFQ_CLE_RANGES_EARLY": "1"},   # tiles / ranges after each tensor's last rescale
 }
 out = []
 for tag, env in CONFIGS.items():
