@@ -73,7 +73,7 @@ BC._BcChain.flush = flush
 BC._WalkTemplate.replay = replay
 BC._structure = structure
 pipeline.bias_correction = bc
-for model in ("mobilenetv2", "resnet50"):
+for model in (sys.argv[1:] or ["mobilenetv2", "resnet50"]):
     for mode in ("live", "replay"):   # live: the walk recorded each time; replay: the compiled walk
         res = []
         for rep in range(6):
