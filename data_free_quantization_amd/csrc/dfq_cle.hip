@@ -1175,7 +1175,7 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
                                                double* __restrict__ hist, CleState* __restrict__ st, double* sm,
                                                float* part_lds = nullptr, float* np_stack = nullptr,
                                                uint32_t* hflag = nullptr, uint64_t* sig = nullptr,
-                                               uint64_t gen = 0) {
+                                               uint64_t gen = 0, int flag_every = 0) {
     if (part_lds) {   // every chunk sum in one parallel pass of coherent loads
         for (int64_t i = threadIdx.x; i < (int64_t)nl * S; i += blockDim.x)
             part_lds[i] = kCoherent ? ld_coh(part + i) : part[i];
@@ -1213,9 +1213,12 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         const int done = (!cont || st->iters >= st->max_iters) ? 1 : 0;
         st->done = done;
         // the host's copy of the stop rule (pinned host memory; a system-scope
-        // vector store): the loop's host side polls it to enqueue the next
-        // iteration or stop (cle_run_locked)
-        if (hflag)
+        // vector store), written when the loop stops: the loop's host side polls it
+        // (cle_run_locked).  Written every iteration (diagnostics
+        // DFQ_CLE_FLAG_EVERY=1, the host pacing itself by it), each store to host
+        // memory held the launch's end back: a 6 us gap before every iteration's
+        // first launch (profiles/r04/r04h, cle_trace).
+        if (hflag && (done || flag_every))
             __hip_atomic_store(hflag, ((uint32_t)(it + 1) << 1) | (uint32_t)done, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         // A launched run: the caller's stream is released here, at convergence,
@@ -1264,6 +1267,7 @@ struct CleFin {
     uint32_t* hflag;         // pinned host word: (iterations << 1) | done, or null
     uint64_t* sig;           // a launched run: the caller's gate word and the generation
     uint64_t gen;            // that releases it at convergence (else null)
+    int32_t flag_every;      // hflag written every iteration (diagnostics), else at the stop
 };
 
 // The launches of one iteration.  Launch k < steps runs the rescale tasks of
@@ -1342,11 +1346,12 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
         if (F.nl <= 128)   // numpy's pairwise sum over the layer means is one leaf
             cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
-                                       stage_part ? lds + 2048 : nullptr, nullptr, F.hflag, F.sig, F.gen);
+                                       stage_part ? lds + 2048 : nullptr, nullptr, F.hflag, F.sig, F.gen,
+                                       F.flag_every);
         else   // the frame stack after the metric tile area (free: this block's units are done)
             cle_final_body<false, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st,
                                         reinterpret_cast<double*>(lds), stage_part ? lds + 2048 : nullptr,
-                                        lds + kCleTile, F.hflag, F.sig, F.gen);
+                                        lds + kCleTile, F.hflag, F.sig, F.gen, F.flag_every);
     };
     if (F.nbig == 0) {   // no chunk has tiles (tiny or no target layers): the last launch's one block finishes
         if (blk == nab && F.last) finish();
@@ -1401,6 +1406,7 @@ struct dfq_cle_plan {
     uint32_t* d_flag = nullptr;     // the stop rule's host word (the device context's, set by run)
     uint64_t* d_sig = nullptr;      // a launched run: the caller's gate word and its generation
     uint64_t gen = 0;
+    int32_t flag_every = 0;         // the stop rule's host word every iteration (diagnostics)
     hipStream_t st = nullptr;       // the loop's stream (the device context's)
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
     std::vector<char> step_pos;          // per step: position-parallel W2 tiles (the POS rescale kernel)
@@ -1449,6 +1455,7 @@ struct CleDeviceCtx {
     CleState* h_state = nullptr;   // pinned: the run's state
     uint32_t* h_flag = nullptr;    // pinned, written by the stop rule: (iterations << 1) | done
     uint32_t* d_flag = nullptr;    // its device address
+    hipEvent_t iev[4] = {};        // behind each iteration in flight (the host's pacing)
     // Table pool: one plan at a time keeps its tables here (device + pinned upload
     // mirror), so a plan costs no hipMalloc / hipFree (hipFree waits for the whole
     // device) and its upload is an async DMA on the loop stream.
@@ -1487,6 +1494,8 @@ static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
         e = hipHostMalloc(&ctx.h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx.d_flag), ctx.h_flag, 0);
     }
+    for (int i = 0; i < 4 && e == hipSuccess; ++i)
+        if (!ctx.iev[i]) e = hipEventCreateWithFlags(&ctx.iev[i], hipEventDisableTiming);
     if (e == hipSuccess && !ctx.pool_ev) e = hipEventCreateWithFlags(&ctx.pool_ev, hipEventDisableTiming);
     if (e == hipSuccess && !ctx.in_ev) e = hipEventCreateWithFlags(&ctx.in_ev, hipEventDisableTiming);
     return e;
@@ -2014,7 +2023,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     // (or by plan_run before the first); the next iteration's ride with the
     // launches after their tensors' last rescale (cle_loop_step_kernel)
     CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, 0, p->d_flag,
-             p->d_sig, p->gen};
+             p->d_sig, p->gen, p->flag_every};
     for (int32_t k = 0; k <= p->steps; ++k) {
         const bool last = k == p->steps;
         const int64_t a0 = last ? 0 : p->astep[k], a1 = last ? 0 : p->astep[k + 1];
@@ -2125,27 +2134,35 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
         DFQ_HIP_CHECK(hipStreamSynchronize(s));
     }
 #endif
-    // Iteration by iteration, kCleAhead of them queued behind the running one: the
-    // stop rule writes (iterations << 1) | done into pinned host memory
+    // Iteration by iteration, kCleAhead of them queued behind the running one (an
+    // event behind each iteration paces this thread); the stop rule writes
+    // (iterations << 1) | done into pinned host memory when the loop stops
     // (ctx.h_flag, a system-scope store), and this thread polls that word -- no
-    // event, copy or host round trip sits between two iterations on the loop
-    // stream, and at convergence at most kCleAhead iterations are left to run as
-    // no-ops.  (Round 3 enqueued batches of 4 iterations a batch ahead and read
+    // copy or host round trip sits between two iterations on the loop stream, and
+    // at convergence at most kCleAhead iterations are left to run as no-ops.  (Round 3 enqueued batches of 4 iterations a batch ahead and read
     // the state back per batch; replaying a batch as a captured HIP graph
     // measured slower, profiles/r03/cle_ab_p.jsonl.)  A stream that drains
     // without the word saying done (a kernel error) ends the polling; the final
     // state read below decides.
     const double tc1 = now_us();
     int32_t launched = 0;
+    p->flag_every = ab_env("DFQ_CLE_FLAG_EVERY") != nullptr;
+    static_assert(kCleAhead + 1 < 4, "one pacing event per iteration in flight");
     if (!init.done) {
         int64_t polls = 0;
+        int32_t ran = 0;   // iterations known complete (the pacing events)
         for (;;) {
             const uint32_t f = __atomic_load_n(ctx.h_flag, __ATOMIC_ACQUIRE);
             if (f & 1u) break;
-            const int32_t ran = (int32_t)(f >> 1);
+            if (p->flag_every) {
+                ran = (int32_t)(f >> 1);
+            } else {
+                while (ran < launched && hipEventQuery(ctx.iev[ran & 3]) == hipSuccess) ++ran;
+            }
             if (launched < max_iters && launched - ran <= kCleAhead) {
                 const int rc = cle_enqueue_iteration(p, s, launched);
                 if (rc != DFQ_OK) return rc;
+                if (!p->flag_every) DFQ_HIP_CHECK(hipEventRecord(ctx.iev[launched & 3], s));
                 ++launched;
                 continue;
             }

@@ -22,7 +22,8 @@ sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_HOST_RELEASE",
-            "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY")
+            "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY",
+            "DFQ_CLE_FLAG_EVERY")
 CONFIGS = {
     "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
@@ -32,6 +33,7 @@ CONFIGS = {
     "tiles_early": {"DFQ_CLE_TILES_EARLY": "1", "DFQ_CLE_RANGES_EARLY": "1"},   # each tensor's tiles / ranges right after its last rescale
     "ranges_early": {"DFQ_CLE_RANGES_EARLY": "1"},  # only the range tasks early
     "units_early": {"DFQ_CLE_TILES_EARLY": "1"},    # only the metric tiles early
+    "flag_every": {"DFQ_CLE_FLAG_EVERY": "1"},      # the stop rule's host word every iteration (the host paces by it)
 }
 
 
