@@ -336,7 +336,8 @@ __device__ inline float wave_row_sum(Get get, int64_t size, int lane, float* b0s
 }
 
 // aten_inner_sum by one wave when every stream is short: lanes 0..31 each run one
-// of the 32 (vector lane, ILP) cascades sequentially; the combine follows on lane 0.
+// of the 32 (vector lane, ILP) cascades sequentially; every lane then runs the
+// combine (the same value on every lane).
 template <typename Get>
 __device__ inline float wave_inner_sum(Get get, int64_t n, int lane) {
     float r = 0.f;
@@ -352,22 +353,19 @@ __device__ inline float wave_inner_sum(Get get, int64_t n, int lane) {
         if (k == 0)
             for (int64_t v = 4 * sz; v < vs; ++v) p += get(8 * v + l);   // row_sum tail into p0
     }
-    float ps[32];
-#pragma unroll
-    for (int s = 0; s < 32; ++s) ps[s] = __shfl(p, s, 64);
-    if (lane == 0) {
-        float fa = 0.f;
-        for (int64_t e = 8 * vs; e < n; ++e) fa += get(e);
-        for (int l = 0; l < 8; ++l) {
-            float p0 = ps[l];
-            p0 += ps[l + 8];
-            p0 += ps[l + 16];
-            p0 += ps[l + 24];
-            fa += p0;
-        }
-        r = fa;
+    // the combine on every lane from the 32 partials read lane by lane (readlane:
+    // uniform values, no 32-register array, no LDS permute per partial)
+    auto rl = [&](int s) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), s)); };
+    float fa = 0.f;
+    for (int64_t e = 8 * vs; e < n; ++e) fa += get(e);
+    for (int l = 0; l < 8; ++l) {
+        float p0 = rl(l);
+        p0 += rl(l + 8);
+        p0 += rl(l + 16);
+        p0 += rl(l + 24);
+        fa += p0;
     }
-    return __shfl(r, 0, 64);
+    return fa;
 }
 
 // Agent-coherent fp32 store / load (sc1: no stale copy in another XCD's L2), for

@@ -222,9 +222,17 @@ struct BcLayerJob {
     int64_t apply_blocks;
 };
 
+// Rows / columns of at most kBcStage values are first staged into LDS by all 64
+// lanes of the wave (independent loads in flight together), then summed in
+// ATen's order from LDS: the order's lane-serial parts (cascade tails, the
+// 32-stream inner sums) read LDS instead of issuing one dependent global load
+// per element (a 96-row propagate column took ~50 us that way, DFQ trace
+// profiles/r04/r04i_bc).
+constexpr int64_t kBcStage = 2048;
 __global__ void __launch_bounds__(kThreads) bc_layer_kernel(BcLayerJob J) {
     __shared__ float ex[kBcMaxExpect];
     __shared__ float scratch[kThreads / 64][kBcScratch + kBcScratch / 16];
+    __shared__ float stage[kThreads / 64][kBcStage];
     for (int64_t j = threadIdx.x; j < J.f; j += kThreads) {
         float v = bc_expect_value(J.ew[0][j], J.eb[0][j], J.relu[0]);
         for (int t = 1; t < J.nterms; ++t) v = v + bc_expect_value(J.ew[t][j], J.eb[t][j], J.relu[t]);
@@ -238,11 +246,17 @@ __global__ void __launch_bounds__(kThreads) bc_layer_kernel(BcLayerJob J) {
     if ((int64_t)blockIdx.x < J.apply_blocks) {
         const int64_t wave = (int64_t)blockIdx.x * (kThreads / 64) + wv;
         const int64_t nwaves = J.apply_blocks * (kThreads / 64);
+        float* rowv = stage[wv];
         for (int64_t r = wave; r < J.o; r += nwaves) {
             auto get = [&](int64_t j) { return J.E[r * J.i2 + (ebc ? j : 0)] + ex[xbc ? j : 0]; };
-            if (J.vec)
-                for (int64_t j = lane; j < J.bcols; j += 64) J.vec[r * J.bcols + j] = get(j);
-            const float sum = wave_inner_sum(get, J.bcols, lane);
+            for (int64_t j = lane; j < J.bcols; j += 64) {   // bcols <= kBcStage (bc_layer_group)
+                const float v = get(j);
+                rowv[j] = v;
+                if (J.vec) J.vec[r * J.bcols + j] = v;
+            }
+            wave_lds_sync();
+            const float sum = wave_inner_sum([&](int64_t j) { return rowv[j]; }, J.bcols, lane);
+            wave_lds_sync();   // rowv is rewritten by the next row
             if (lane == 0) J.bias[r] = J.bias[r] + sum / (float)J.bcols;
         }
         return;
@@ -251,15 +265,20 @@ __global__ void __launch_bounds__(kThreads) bc_layer_kernel(BcLayerJob J) {
     float* b1s = b0s + kBcScratch;
     const int64_t wave = ((int64_t)blockIdx.x - J.apply_blocks) * (kThreads / 64) + wv;
     const int64_t nwaves = ((int64_t)gridDim.x - J.apply_blocks) * (kThreads / 64);
+    float* colv = stage[wv];
     for (int64_t c = wave; c < J.F; c += nwaves) {
-        auto get = [&](int64_t r) {
-            const int64_t idx = r * J.F + c;
-            const int64_t row = idx / J.bcols, j = idx - row * J.bcols;
-            return J.E[row * J.i2 + (ebc ? j : 0)] + ex[xbc ? j : 0];
+        auto get = [&](int64_t r) {   // 32-bit index math: o * bcols < 2^31 (bc_layer_group)
+            const uint32_t idx = (uint32_t)r * (uint32_t)J.F + (uint32_t)c;
+            const uint32_t row = idx / (uint32_t)J.bcols, j = idx - row * (uint32_t)J.bcols;
+            return J.E[(int64_t)row * J.i2 + (ebc ? j : 0)] + ex[xbc ? j : 0];
         };
-        const float sum = aten_outer_col_is_cascade(J.nrows, J.F, c, J.threads)
-                              ? wave_cascade(get, J.nrows, lane, b0s, b1s, kBcScratch)
-                              : wave_row_sum(get, J.nrows, lane, b0s, b1s, kBcScratch);
+        const bool cascade = aten_outer_col_is_cascade(J.nrows, J.F, c, J.threads);
+        for (int64_t r = lane; r < J.nrows; r += 64) colv[r] = get(r);   // nrows <= kBcStage (bc_layer_group)
+        wave_lds_sync();
+        auto lds = [&](int64_t r) { return colv[r]; };
+        const float sum = cascade ? wave_cascade(lds, J.nrows, lane, b0s, b1s, kBcScratch)
+                                  : wave_row_sum(lds, J.nrows, lane, b0s, b1s, kBcScratch);
+        wave_lds_sync();   // colv is rewritten by the next column
         if (lane == 0) J.fake_b[c] = J.fake_b[c] + (-sum) / (float)J.nrows;
     }
 }
@@ -1030,13 +1049,16 @@ int32_t bc_layer_group(const dfq_bc_op* ops, int32_t n_ops, int32_t k, BcLayerJo
     J.o = ap.n;
     J.i2 = ap.i2;
     J.bcols = (ap.i2 == ap.f || ap.f == 1) ? ap.i2 : ap.f;
+    // the kernel stages a row / column in LDS and indexes bias_vec in 32 bits;
+    // larger ones take the per-op launches
+    if (J.bcols > kBcStage || J.o * J.bcols >= (int64_t(1) << 31)) return 0;
     J.bias = ap.out;
     J.vec = ap.out2;
     J.apply_blocks = std::min<int64_t>(ceil_div(J.o, (int64_t)4), 2048);
     int32_t used = m - k + 1;
     const dfq_bc_op* pr = (m + 1 < n_ops) ? &ops[m + 1] : nullptr;
     if (pr && pr->kind == DFQ_BC_OP_PROPAGATE && ap.out2 && pr->a == ap.out2 && pr->n == J.o * J.bcols &&
-        pr->f > 0 && pr->n % pr->f == 0 && pr->flag >= 1) {
+        pr->f > 0 && pr->n % pr->f == 0 && pr->flag >= 1 && pr->n / pr->f <= kBcStage) {
         J.fake_b = pr->out;
         J.F = pr->f;
         J.nrows = pr->n / pr->f;

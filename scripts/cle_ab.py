@@ -23,7 +23,7 @@ os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_HOST_RELEASE",
             "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY",
-            "DFQ_CLE_FLAG_EVERY")
+            "DFQ_CLE_FLAG_EVERY", "CLE_AB_BLOCKING")
 CONFIGS = {
     "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
@@ -34,6 +34,7 @@ CONFIGS = {
     "ranges_early": {"DFQ_CLE_RANGES_EARLY": "1"},  # only the range tasks early
     "units_early": {"DFQ_CLE_TILES_EARLY": "1"},    # only the metric tiles early
     "flag_every": {"DFQ_CLE_FLAG_EVERY": "1"},      # the stop rule's host word every iteration (the host paces by it)
+    "blocking": {"CLE_AB_BLOCKING": "1"},           # run_dfq's CLE blocking (no caller gate beside the loop)
 }
 
 
@@ -54,10 +55,18 @@ def main():
     cfgs = a.configs.split(",")
     models = a.models.split(",")
 
+    import data_free_quantization_amd.pipeline as pipeline_mod
+    cle_call = cle.cross_layer_equalization
+
+    def blocking_cle(*args, **kw):
+        kw["launch"] = False
+        return cle_call(*args, **kw)
+
     def use(tag):
         for k in SWITCHES:
             os.environ.pop(k, None)
         os.environ.update(CONFIGS[tag])
+        pipeline_mod.cle.cross_layer_equalization = blocking_cle if os.environ.get("CLE_AB_BLOCKING") else cle_call
 
     res = {(t, m): [] for t in cfgs for m in models}
     e2e = {(t, m): [] for t in cfgs for m in models}
