@@ -401,14 +401,16 @@ def _structure(graph, bottoms, targ_type, bn_type, signed, bits_weight, error_su
     """Everything the walk's control flow and op fields depend on (the graph's
     keys, node types, bottoms, the shapes of targets / biases / BN statistics /
     error sums), as a hashable signature of flat tuples (cheap to hash and to
-    compare); plus the per-node tensors a replay takes addresses from.  The walk
-    never reads a tensor value."""
-    nodes = {}
+    compare); plus what a replay takes addresses from: per node index two device
+    addresses (BN: fake_weight, fake_bias; target layer: bias, E) and the tensors
+    behind them.  The walk never reads a tensor value."""
     shp = []
     kinds = _KINDS
     keys = tuple(graph.keys())
     vals = list(graph.values())
     types = tuple(map(type, vals))
+    ptrs = [(0, 0)] * len(vals)
+    tensors = []
     for i, v in enumerate(vals):
         t = types[i]
         k = kinds.get((t, targ_type, bn_type))
@@ -417,18 +419,29 @@ def _structure(graph, bottoms, targ_type, bn_type, signed, bits_weight, error_su
                                                   2 if issubclass(t, targ_type) and t is not str else 0)
         if k == 1:
             fw, fb = _buf(v, "fake_weight"), _buf(v, "fake_bias")
-            nodes[i] = (fw, fb)
+            ptrs[i] = (fw.data_ptr(), fb.data_ptr())
+            tensors += (fw, fb)
             shp += (i, -1, *fw.shape, -2, *fb.shape)
         elif k == 2:
             w, b = _param(v, "weight"), _param(v, "bias")
             pre = error_sums.get(keys[i])
-            nodes[i] = (b, pre)
+            if pre is None:
+                e = 0
+            elif isinstance(pre, torch.Tensor):   # E itself, or a (buffer, float offset, numel) ref
+                e = pre.data_ptr()
+                tensors.append(pre)
+            else:
+                e = pre[0].data_ptr() + 4 * pre[1]
+                tensors.append(pre[0])
+            if b is not None:
+                tensors.append(b)
+            ptrs[i] = (0 if b is None else b.data_ptr(), e)
             shp += (i, -3, *w.shape, -4, *(() if b is None else b.shape), -5 if b is None else -6,
                     -1 if pre is None else (pre.numel() if isinstance(pre, torch.Tensor) else pre[2]))
     sig = (keys, types, tuple(bottoms.keys()),
            tuple(None if v is None else tuple(v) for v in bottoms.values()), targ_type, bn_type, bool(signed),
            int(bits_weight), _lib.REF_THREADS, tuple(shp))
-    return sig, nodes
+    return sig, (np.array(ptrs, dtype=np.int64), tensors)
 
 
 class _WalkTemplate:
@@ -454,9 +467,13 @@ class _WalkTemplate:
         for fill in chunk_fill:
             cbase.append(tot)
             tot += fill
-        self.scratch = tot
+        self.scratch = -(-tot // 64) * 64
+        snap = [0 if x is None else -(-x[1] // 64) * 64 for x in (self.before, self.after)]
+        # one device allocation per replay: [scratch | before snapshot | after snapshot]
+        self.snap_off = (self.scratch, self.scratch + snap[0])
+        self.alloc = max(self.scratch + snap[0] + snap[1], 1)
         slots = {}          # (space, key) -> index; 0 = null
-        self.slot_keys = [(_S_NONE, 0)]
+        keys = [(_S_NONE, 0)]
         idx = np.zeros((len(sym), 4), dtype=np.int64)
         off = np.zeros((len(sym), 4), dtype=np.int64)
         for k, (_, syms) in enumerate(sym):
@@ -467,48 +484,35 @@ class _WalkTemplate:
                     key, o = 0, cbase[key] + o
                 sk = (space, key)
                 if sk not in slots:
-                    slots[sk] = len(self.slot_keys)
-                    self.slot_keys.append(sk)
+                    slots[sk] = len(keys)
+                    keys.append(sk)
                 idx[k, j], off[k, j] = slots[sk], o
         self.idx, self.off = idx, off
+        # per slot: the node index and the field of _structure's address table
+        # (BN weight / bias; bias / E), or a float offset into the replay's allocation
+        self.slot_node = np.array([key if sp in (_S_BN_W, _S_BN_B, _S_BIAS, _S_E) else 0 for sp, key in keys],
+                                  dtype=np.int64)
+        self.slot_field = np.array([1 if sp in (_S_BN_B, _S_E) else 0 for sp, _ in keys], dtype=np.int64)
+        self.slot_tab = np.array([sp in (_S_BN_W, _S_BN_B, _S_BIAS, _S_E) for sp, _ in keys])
+        self.slot_local = np.array([0 if sp == _S_SCRATCH else self.snap_off[key] if sp == _S_SNAP else -1
+                                    for sp, key in keys], dtype=np.int64)
         self._raw = None
 
-    def replay(self, nodes, dev, stream):
+    def replay(self, where, dev, stream):
         if self.static is None:
             self._build()
         for m in self.warnings:
             logger.warning(m)
-        scratch = torch.empty(max(self.scratch, 1), dtype=torch.float32, device=dev)
-        flats = [None, None]
-        for w, snap in enumerate((self.before, self.after)):
-            if snap is not None:
-                flats[w] = torch.empty(snap[1], dtype=torch.float32, device=dev)
-        addr = [0] * len(self.slot_keys)
-        used = []
-        for i, (space, key) in enumerate(self.slot_keys):
-            if space == _S_NONE:
-                continue
-            if space == _S_SCRATCH:
-                addr[i] = scratch.data_ptr()
-                continue
-            if space == _S_SNAP:
-                addr[i] = flats[key].data_ptr()
-                continue
-            if space in (_S_BN_W, _S_BN_B):
-                t = nodes[key][0 if space == _S_BN_W else 1]
-            elif space == _S_BIAS:
-                t = nodes[key][0]
-            else:   # _S_E: a tensor or a (buffer, float offset, numel) ref
-                pre = nodes[key][1]
-                if isinstance(pre, torch.Tensor):
-                    t = pre
-                else:
-                    t = pre[0]
-                    addr[i] = 4 * pre[1]
-            used.append(t)
-            addr[i] += t.data_ptr()
-        _lib.require_device(*used)
-        a = np.array(addr, dtype=np.int64)[self.idx] + 4 * self.off
+        ptrs, tensors = where
+        _lib.require_device(*tensors)
+        buf = torch.empty(self.alloc, dtype=torch.float32, device=dev)
+        base = np.zeros(len(self.slot_node), dtype=np.int64)
+        base[self.slot_tab] = ptrs[self.slot_node[self.slot_tab], self.slot_field[self.slot_tab]]
+        if not base[self.slot_tab].all():   # a tensor the recorded walk used is missing here
+            raise RuntimeError("bias_correction: an error sum the compiled walk reads is missing")
+        loc = self.slot_local >= 0
+        base[loc] = buf.data_ptr() + 4 * self.slot_local[loc]
+        a = base[self.idx] + 4 * self.off
         a[self.idx == 0] = 0
         arr = np.empty(len(self.static), dtype=_BC_OP)
         arr["kind"], arr["flag"] = self.static[:, 0], self.static[:, 1]
@@ -519,9 +523,9 @@ class _WalkTemplate:
             failed = C.c_int32(-1)
             rc = _lib.load().dfq_bc_chain(arr.ctypes.data_as(C.POINTER(_lib.BcOp)), len(arr), C.byref(failed), stream)
             _lib.check(rc, f"dfq_bc_chain (op {failed.value})", RuntimeError)
-            scratch.record_stream(torch.cuda.current_stream(dev))
-        before = _Snapshot(flats[0], self.before[0]) if self.before else {}
-        after = _Snapshot(flats[1], self.after[0]) if self.after else {}
+            buf.record_stream(torch.cuda.current_stream(dev))
+        before = _Snapshot(buf[self.snap_off[0]:self.snap_off[0] + self.before[1]], self.before[0]) if self.before else {}
+        after = _Snapshot(buf[self.snap_off[1]:self.snap_off[1] + self.after[1]], self.after[0]) if self.after else {}
         return before, after
 
 
@@ -542,17 +546,15 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
     # types, bottoms, shapes), never on a tensor value; the addresses are bound
     # afresh.  Only fused-mode walks (error sums given) are compiled: the other
     # mode quantizes each weight inside the walk.
-    sig = nodes = None
+    sig = where = None
     if error_sums is not None:
-        sig, nodes = _structure(graph, bottoms, targ_type, bn_type, signed, bits_weight, error_sums)
+        sig, where = _structure(graph, bottoms, targ_type, bn_type, signed, bits_weight, error_sums)
         tpl = _TEMPLATES.get(sig)
         if tpl is not None:
             _TEMPLATES.move_to_end(sig)
-            dev = next((t.device for v in nodes.values() for t in v if isinstance(t, torch.Tensor)), None)
-            if dev is None:
-                dev = torch.device("cuda", torch.cuda.current_device())
+            dev = where[1][0].device if where[1] else torch.device("cuda", torch.cuda.current_device())
             with torch.no_grad():
-                res = tpl.replay(nodes, dev, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+                res = tpl.replay(where, dev, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
             logger.info("Bias correction completed.")
             return res
     warned = []

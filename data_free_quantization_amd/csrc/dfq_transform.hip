@@ -1067,27 +1067,29 @@ int32_t bc_layer_group(const dfq_bc_op* ops, int32_t n_ops, int32_t k, BcLayerJo
     }
     // hazards: what the group writes (slot, bias, bias_vec, fake_b) vs what it reads
     // (BN stats, E) -- and the writes among themselves
-    std::vector<Span> rd, wr;
+    // (fixed-size span lists: this runs once per layer on the host, between launches)
+    Span rd[2 * kBcMaxTerms + 3], wr[4];
+    int nr = 0, nw = 0;
     for (int t = 0; t < J.nterms; ++t) {
-        rd.push_back(span(J.ew[t], J.f));
-        rd.push_back(span(J.eb[t], J.f));
+        rd[nr++] = span(J.ew[t], J.f);
+        rd[nr++] = span(J.eb[t], J.f);
     }
-    rd.push_back(span(J.E, J.o * (J.i2 > 1 ? J.i2 : 1)));
-    rd.push_back(span(J.bias, J.o));   // bias[r] = bias[r] + ...
-    wr.push_back(span(J.expect_out, J.f));
-    wr.push_back(span(J.bias, J.o));
-    if (J.vec) wr.push_back(span(J.vec, J.o * J.bcols));
+    rd[nr++] = span(J.E, J.o * (J.i2 > 1 ? J.i2 : 1));
+    rd[nr++] = span(J.bias, J.o);   // bias[r] = bias[r] + ...
+    wr[nw++] = span(J.expect_out, J.f);
+    wr[nw++] = span(J.bias, J.o);
+    if (J.vec) wr[nw++] = span(J.vec, J.o * J.bcols);
     if (J.fake_b) {
-        wr.push_back(span(J.fake_b, J.F));
-        rd.push_back(span(J.fake_b, J.F));
+        wr[nw++] = span(J.fake_b, J.F);
+        rd[nr++] = span(J.fake_b, J.F);
     }
-    for (size_t a = 0; a < wr.size(); ++a) {
-        for (size_t b = 0; b < rd.size(); ++b) {
-            const bool same = (a == 1 && b == rd.size() - (J.fake_b ? 2 : 1)) ||        // bias vs bias
-                              (J.fake_b && a == wr.size() - 1 && b == rd.size() - 1);   // fake_b vs fake_b
+    for (int a = 0; a < nw; ++a) {
+        for (int b = 0; b < nr; ++b) {
+            const bool same = (a == 1 && b == nr - (J.fake_b ? 2 : 1)) ||        // bias vs bias
+                              (J.fake_b && a == nw - 1 && b == nr - 1);   // fake_b vs fake_b
             if (!same && overlap(wr[a], rd[b])) return 0;
         }
-        for (size_t b = a + 1; b < wr.size(); ++b)
+        for (int b = a + 1; b < nw; ++b)
             if (overlap(wr[a], wr[b])) return 0;
     }
     return used;
