@@ -1548,6 +1548,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                                    dfq_cle_plan** out) {
     if (!out || n_rel < 0 || n_targets < 0 || (n_rel > 0 && !rels) || (n_targets > 0 && (!targets || !target_n)))
         return DFQ_ERR_INVALID;
+    const double tc0 = now_us();
     const int64_t need_ws = dfq_cle_plan_ws_bytes(target_n, n_targets);
     if (need_ws < 0) return DFQ_ERR_INVALID;
     if (ws && (ws_bytes < need_ws || reinterpret_cast<uintptr_t>(ws) % 256 != 0)) return DFQ_ERR_INVALID;
@@ -1987,8 +1988,8 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         return fail(e);
     }
     if (cle_timing())
-        fprintf(stderr, "DFQ_CLE_TIMING create: hipMalloc %lld B %.1f us, copy %lld B %.1f us\n", (long long)T.total,
-                tm1 - tm0, (long long)host_bytes, now_us() - tm1);
+        fprintf(stderr, "DFQ_CLE_TIMING create: plan %.1f us, tables %lld B %.1f us, copy %lld B %.1f us\n",
+                tm0 - tc0, (long long)T.total, tm1 - tm0, (long long)host_bytes, now_us() - tm1);
     p->d_rels = reinterpret_cast<CleRel*>(base + o_rels);
     p->d_rtasks = reinterpret_cast<CleTask*>(base + o_rt);
     p->d_atasks = reinterpret_cast<CleTask*>(base + o_at);
@@ -2396,6 +2397,7 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
     if (ab_env("DFQ_CLE_TL")) return DFQ_ERR_UNSUPPORTED;
     hipStream_t caller = static_cast<hipStream_t>(stream);
     CleDeviceCtx& ctx = cle_device_ctx(p->dev);
+    const double tl0 = now_us();
     // one launched loop per device at a time: the signal's generations then
     // complete in launch order
     if (ctx.pending && ctx.pending != p) cle_async_join(ctx.pending);
@@ -2421,6 +2423,7 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
         DFQ_LAUNCH_CHECK();
         ctx.gen = gen;
     }
+    if (cle_timing()) fprintf(stderr, "DFQ_CLE_TIMING launch: gate and order %.1f us\n", now_us() - tl0);
     // from here on the caller's stream is held until the signal reaches gen: every
     // path below writes it
     CleAsync* a = new (std::nothrow) CleAsync();
