@@ -2232,6 +2232,24 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             std::sort(st.begin(), st.end());
             for (double q : {0.1, 0.5, 0.9, 0.99, 1.0})
                 if (!st.empty()) fprintf(stderr, " p%.0f %.2f", q * 100, st[std::min(st.size() - 1, (size_t)(q * st.size()))]);
+            // per task kind: count, mean / max duration, mean start
+            fprintf(stderr, "\nDFQ_CLE_TL step %d kinds:", k);
+            for (int kind = 0; kind < 8; ++kind) {
+                int64_t cnt = 0;
+                double sum = 0, mx = 0, s0 = 0;
+                for (int64_t t = a0; t < a1; ++t) {
+                    const uint64_t* r = &tl[4 * t];
+                    if (!r[0] || (int)(r[3] & 255) != kind) continue;
+                    const double us = (double)(r[1] - r[0]) * 0.01;
+                    ++cnt;
+                    sum += us;
+                    mx = std::max(mx, us);
+                    s0 += (double)(r[0] - t_lo) * 0.01;
+                }
+                if (cnt)
+                    fprintf(stderr, " [kind %d: %lld tasks, mean %.2f max %.2f us, start mean %.2f]", kind,
+                            (long long)cnt, sum / cnt, mx, s0 / cnt);
+            }
             fprintf(stderr, "\n");
         }
     }
