@@ -519,6 +519,10 @@ struct CleApplyLds {
 // DFQ_CLE_TL (diagnostics): per rescale task of one steady-state iteration,
 // {start, end} in s_memrealtime ticks (100 MHz) and the block's XCC / CU ids.
 __device__ uint64_t* g_cle_tl = nullptr;
+// ... and per block of the iteration's last launch (tiles / ranges / stop rule):
+// {start, end, role (1 tile, 2 range), 0}; slot kCleTl2Fin: the stop rule's {start, end}
+__device__ uint64_t* g_cle_tl2 = nullptr;
+constexpr int kCleTl2Fin = 8192;
 #endif
 
 // POS: the step has position-parallel (KH*KW > 1) W2 tiles; without them the
@@ -1319,9 +1323,24 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
                             blk, nab, L.apply);
         return;
     }
+#ifdef DFQ_DIAGNOSTICS
+    const bool tl2 = F.last && g_cle_tl2 != nullptr && blk < kCleTl2Fin;
+    const uint64_t tl2_start = tl2 ? __builtin_amdgcn_s_memrealtime() : 0;
+    auto tl2_rec = [&](int role) {
+        if (tl2 && threadIdx.x == 0) {
+            uint64_t* r = g_cle_tl2 + 4 * blk;
+            r[0] = tl2_start;
+            r[1] = __builtin_amdgcn_s_memrealtime();
+            r[2] = (uint64_t)role;
+        }
+    };
+#else
+    auto tl2_rec = [](int) {};
+#endif
     if (blk >= nab + ntb) {   // the next iteration's ranges of the tensors final by now
         cle_range_body(rels, rtasks, r0, r1, rng, M, par_next, blk - nab - ntb, (int64_t)gridDim.x - nab - ntb,
                        L.tiles);
+        tl2_rec(2);
         return;
     }
     float* lds = L.tiles;
@@ -1339,6 +1358,9 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
     // The last arrival of the iteration: tiny chunks' sums, then the per-layer
     // means, the history and the stop rule.
     auto finish = [&]() {
+#ifdef DFQ_DIAGNOSTICS
+        const uint64_t tf0 = __builtin_amdgcn_s_memrealtime();
+#endif
         if (threadIdx.x == 0 && F.nchunks > F.nbig)   // tiny chunks exist (none in the zoo's models)
             for (int64_t k = 0; k < F.nchunks; ++k) {
                 const CleChunk c2 = chunks[k];
@@ -1355,6 +1377,13 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
             cle_final_body<false, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st,
                                         reinterpret_cast<double*>(lds), stage_part ? lds + 2048 : nullptr,
                                         lds + kCleTile, F.hflag, F.sig, F.gen, F.flag_every);
+#ifdef DFQ_DIAGNOSTICS
+        if (tl2 && threadIdx.x == 0) {
+            uint64_t* r = g_cle_tl2 + 4 * kCleTl2Fin;
+            r[0] = tf0;
+            r[1] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
     };
     if (F.nbig == 0) {   // no chunk has tiles (tiny or no target layers): the last launch's one block finishes
         if (blk == nab && F.last) finish();
@@ -1386,6 +1415,7 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
     };
     cle_tiles_body<decltype(hook), NTS>(layers, chunks, b1off, units + u0, u1 - u0, b1buf, tailbuf, blk - nab, ntb, lds,
                    lds + kCleTile + kCleTailWords, hook);
+    tl2_rec(1);
 }
 
 }  // namespace dfq
@@ -2136,11 +2166,16 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     }
 #ifdef DFQ_DIAGNOSTICS
     uint64_t* d_tl = nullptr;   // DFQ_CLE_TL: per rescale task timestamps (cle_apply_body)
+    uint64_t* d_tl2 = nullptr;  // ... and per block of the last launch
     const int64_t n_at = p->astep.empty() ? 0 : p->astep.back();
+    const size_t n_tl2 = 4 * (size_t)(kCleTl2Fin + 1);
     if (ab_env("DFQ_CLE_TL") && n_at > 0) {
         DFQ_HIP_CHECK(hipMalloc(&d_tl, sizeof(uint64_t) * 4 * n_at));
         DFQ_HIP_CHECK(hipMemsetAsync(d_tl, 0, sizeof(uint64_t) * 4 * n_at, s));
         DFQ_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cle_tl), &d_tl, sizeof(d_tl), 0, hipMemcpyHostToDevice, s));
+        DFQ_HIP_CHECK(hipMalloc(&d_tl2, sizeof(uint64_t) * n_tl2));
+        DFQ_HIP_CHECK(hipMemsetAsync(d_tl2, 0, sizeof(uint64_t) * n_tl2, s));
+        DFQ_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cle_tl2), &d_tl2, sizeof(d_tl2), 0, hipMemcpyHostToDevice, s));
         DFQ_HIP_CHECK(hipStreamSynchronize(s));
     }
 #endif
@@ -2189,6 +2224,39 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
         DFQ_HIP_CHECK(cle_copy_back(tl.data(), d_tl, sizeof(uint64_t) * tl.size(), s));
         uint64_t* null_tl = nullptr;
         DFQ_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cle_tl), &null_tl, sizeof(null_tl), 0, hipMemcpyHostToDevice, s));
+        std::vector<uint64_t> tl2(n_tl2);
+        DFQ_HIP_CHECK(cle_copy_back(tl2.data(), d_tl2, sizeof(uint64_t) * n_tl2, s));
+        DFQ_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cle_tl2), &null_tl, sizeof(null_tl), 0, hipMemcpyHostToDevice, s));
+        DFQ_HIP_CHECK(hipStreamSynchronize(s));
+        (void)hipFree(d_tl2);
+        {   // the last launch: per role, when blocks started / ended (us after the first start)
+            uint64_t t0 = ~0ull;
+            for (int b = 0; b < kCleTl2Fin; ++b)
+                if (tl2[4 * b]) t0 = std::min(t0, tl2[4 * b]);
+            fprintf(stderr, "DFQ_CLE_TL last launch:");
+            for (int role = 1; role <= 2; ++role) {
+                std::vector<double> st, en, du;
+                for (int b = 0; b < kCleTl2Fin; ++b) {
+                    const uint64_t* r = &tl2[4 * b];
+                    if (!r[0] || (int)r[2] != role) continue;
+                    st.push_back((double)(r[0] - t0) * 0.01);
+                    en.push_back((double)(r[1] - t0) * 0.01);
+                    du.push_back((double)(r[1] - r[0]) * 0.01);
+                }
+                if (st.empty()) continue;
+                std::sort(st.begin(), st.end());
+                std::sort(en.begin(), en.end());
+                double m = 0;
+                for (double x : du) m += x;
+                fprintf(stderr, " [%s: %zu blocks, start p50 %.2f max %.2f, end p50 %.2f max %.2f, dur mean %.2f]",
+                        role == 1 ? "tiles" : "ranges", st.size(), st[st.size() / 2], st.back(), en[en.size() / 2],
+                        en.back(), m / du.size());
+            }
+            const uint64_t* f = &tl2[4 * kCleTl2Fin];
+            if (f[0] && t0 != ~0ull)
+                fprintf(stderr, " [stop rule: %.2f - %.2f]", (double)(f[0] - t0) * 0.01, (double)(f[1] - t0) * 0.01);
+            fprintf(stderr, "\n");
+        }
         DFQ_HIP_CHECK(hipStreamSynchronize(s));
         (void)hipFree(d_tl);
         for (int32_t k = 0; k < p->steps; ++k) {
