@@ -2192,7 +2192,11 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     const double tc1 = now_us();
     int32_t launched = 0;
     p->flag_every = ab_env("DFQ_CLE_FLAG_EVERY") != nullptr;
-    static_assert(kCleAhead + 1 < 4, "one pacing event per iteration in flight");
+    // diagnostics A/B: once the queue is down to kCleAhead iterations, top it up by
+    // `burst` (the host's enqueue then meets fewer iteration boundaries)
+    int32_t burst = 1;
+    if (const char* b = ab_env("DFQ_CLE_BURST")) burst = std::max(1, std::min(2, atoi(b)));   // <= 3 in flight: 4 events
+    int32_t fill = 0;   // iterations still to enqueue in the current burst
     if (!init.done) {
         int64_t polls = 0;
         int32_t ran = 0;   // iterations known complete (the pacing events)
@@ -2204,11 +2208,13 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             } else {
                 while (ran < launched && hipEventQuery(ctx.iev[ran & 3]) == hipSuccess) ++ran;
             }
-            if (launched < max_iters && launched - ran <= kCleAhead) {
+            if (launched < max_iters && (fill > 0 || launched - ran <= kCleAhead)) {
+                if (fill == 0) fill = burst;
                 const int rc = cle_enqueue_iteration(p, s, launched);
                 if (rc != DFQ_OK) return rc;
                 if (!p->flag_every) DFQ_HIP_CHECK(hipEventRecord(ctx.iev[launched & 3], s));
                 ++launched;
+                --fill;
                 continue;
             }
             if ((++polls & 255) == 0 && hipStreamQuery(s) != hipErrorNotReady) break;
