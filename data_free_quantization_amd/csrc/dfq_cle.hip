@@ -1183,6 +1183,13 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
                                                float* part_lds = nullptr, float* np_stack = nullptr,
                                                uint32_t* hflag = nullptr, uint64_t* sig = nullptr,
                                                uint64_t gen = 0, int flag_every = 0) {
+    // The stop rule's state, read up front in one batch of independent loads (they
+    // land while the chunk sums are staged): read field by field between the
+    // stores below, they were ~5 dependent round trips of a serial 7.6 us stop
+    // rule (DFQ_CLE_TL, the last launch's block timeline).  Nothing else writes
+    // the state during this launch.
+    CleState s0{};
+    if (threadIdx.x == 0) s0 = *st;
     if (part_lds) {   // every chunk sum in one parallel pass of coherent loads
         for (int64_t i = threadIdx.x; i < (int64_t)nl * S; i += blockDim.x)
             part_lds[i] = kCoherent ? ld_coh(part + i) : part[i];
@@ -1207,24 +1214,26 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         } else {
             dt = nl > 0 ? np_pairwise(m, nl, np_stack) : 0.0;
         }
-        const int it = st->iters;
+        const int it = s0.iters;
         hist[it] = dt;
-        st->iters = it + 1;
-        if (fabs(st->diff - dt) > 1e-9) {
-            st->iter_count = 0;
-            st->diff = dt;
+        int ic = s0.iter_count;
+        double diff = s0.diff;
+        if (fabs(diff - dt) > 1e-9) {
+            ic = 0;
+            diff = dt;
         } else {
-            st->iter_count += 1;
+            ic += 1;
         }
-        const bool cont = (st->diff > st->thr) && (st->iter_count < st->count);
-        const int done = (!cont || st->iters >= st->max_iters) ? 1 : 0;
+        const bool cont = (diff > s0.thr) && (ic < s0.count);
+        const int done = (!cont || it + 1 >= s0.max_iters) ? 1 : 0;
+        st->iters = it + 1;
+        st->iter_count = ic;
+        st->diff = diff;
         st->done = done;
         // the host's copy of the stop rule (pinned host memory; a system-scope
         // vector store), written when the loop stops: the loop's host side polls it
-        // (cle_run_locked).  Written every iteration (diagnostics
-        // DFQ_CLE_FLAG_EVERY=1, the host pacing itself by it), each store to host
-        // memory held the launch's end back: a 6 us gap before every iteration's
-        // first launch (profiles/r04/r04h, cle_trace).
+        // (cle_run_locked).  (Written every iteration instead, DFQ_CLE_FLAG_EVERY=1,
+        // it measured the same.)
         if (hflag && (done || flag_every))
             __hip_atomic_store(hflag, ((uint32_t)(it + 1) << 1) | (uint32_t)done, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
