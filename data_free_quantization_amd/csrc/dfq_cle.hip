@@ -1053,8 +1053,8 @@ constexpr int kCleTilesLds = kCleTile + kCleTailWords + 512;
 constexpr int kCleRangeLds = 2 * kThreads * kTileMaxKhw;
 
 // One chunk's sum from its tiles' level-1 sums and tail words (one wave; the
-// result on lane 0): the rest of the cascade, the ILP and lane combines and the
-// scalar tail, in ATen's order.  Coherent loads: other blocks wrote b1 / tb.
+// result on every lane): the rest of the cascade, the ILP and lane combines and
+// the scalar tail, in ATen's order.  Coherent loads: other blocks wrote b1 / tb.
 template <class LdB1, class LdTb>
 __device__ __forceinline__ float cle_chunk_sum_with(const CleChunk& ch, LdB1&& b1, LdTb&& tb, int lane) {
     const int64_t len = ch.len;
@@ -1075,20 +1075,18 @@ __device__ __forceinline__ float cle_chunk_sum_with(const CleChunk& ch, LdB1&& b
         p += a2p;
         p += a3;
     }
-    float ps[32];
-#pragma unroll
-    for (int s = 0; s < 32; ++s) ps[s] = __shfl(p, s, 64);
-    if (lane == 0) {
-        for (int64_t e = 0; e < len - 8 * vs; ++e) fa += tb(56 + e);   // scalar tail first
-        const int64_t nv = vs - 4 * sz;
-        for (int l = 0; l < 8; ++l) {
-            float p0 = ps[l];
-            for (int64_t v = 0; v < nv; ++v) p0 += tb(32 + v * 8 + l);   // row_sum tail into p0
-            p0 += ps[l + 8];
-            p0 += ps[l + 16];
-            p0 += ps[l + 24];
-            fa += p0;
-        }
+    // the combine on every lane, the 32 stream partials read by readlane (uniform
+    // values: no 32-register array, no LDS permute per partial)
+    auto ps = [&](int s) { return rl_f(p, s); };
+    for (int64_t e = 0; e < len - 8 * vs; ++e) fa += tb(56 + e);   // scalar tail first
+    const int64_t nv = vs - 4 * sz;
+    for (int l = 0; l < 8; ++l) {
+        float p0 = ps(l);
+        for (int64_t v = 0; v < nv; ++v) p0 += tb(32 + v * 8 + l);   // row_sum tail into p0
+        p0 += ps(l + 8);
+        p0 += ps(l + 16);
+        p0 += ps(l + 24);
+        fa += p0;
     }
     return fa;
 }
