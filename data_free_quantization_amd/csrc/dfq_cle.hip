@@ -945,12 +945,18 @@ __global__ void cle_loop_snap_kernel(const CleLayer* __restrict__ layers, const 
 // Metric tiles taken by blocks blk, blk + nblk, ... (d: kCleTile + kCleTailWords
 // floats of LDS, b0: 512).
 struct CleNoUnitHook {
-    __device__ void operator()(const CleUnit&, const CleChunk&, int64_t) const {}
+    template <class Flush>
+    __device__ void operator()(const CleUnit&, const CleChunk&, int64_t, Flush flush) const { flush(); }
 };
 
-// hook(unit, chunk, nb1) runs after each unit (LDS free again).  NT: the snapshot
-// stores non-temporal (diagnostics A/B, DFQ_CLE_SNAP_NT)
-template <class Hook = CleNoUnitHook, bool NT = false>
+// hook(unit, chunk, nb1, flush) runs after each unit (LDS free again) and calls
+// flush() once the unit's hand-off has arrived: a full tile's snapshot stores
+// (snap := W) are issued there, so they no longer sit in front of the arrival's
+// vmcnt(0) drain, and its 32 W values per thread stay live only across the
+// arrival (not across the chunk combine or the stop rule).  NT: the snapshot
+// stores non-temporal (diagnostics A/B, DFQ_CLE_SNAP_NT); !DEFER: the snapshot
+// stores before the arrival (diagnostics A/B, DFQ_CLE_SNAP_EARLY)
+template <class Hook = CleNoUnitHook, bool NT = false, bool DEFER = true>
 __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
                                                const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units,
                                                int64_t nunits, float* __restrict__ b1buf, float* __restrict__ tailbuf,
@@ -967,13 +973,14 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
         const bool full = un.tile < nb1;
         const int64_t e0 = (int64_t)un.tile * kCleTile;
         const int64_t cnt = full ? kCleTile : len - e0;
+        float xs[2][16];   // a full tile's W values: snap := W after the hand-off (below)
         if (full) {
             // level 0 straight from the loads: thread t owns (block m, stream s) for
             // q = t and t + 256; its 16 elements 32 (16 m + j) + s sit at stride 32,
             // so each load instruction covers whole 128-B lines across the lanes,
             // and the 16-term sum runs in ATen's order in registers (32 loads in
             // flight per thread, no LDS staging of |W - W_prev|)
-            float xs[2][16], ys[2][16];
+            float ys[2][16];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int q = tid + h * kThreads;
@@ -987,15 +994,18 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int q = tid + h * kThreads;
-                const int64_t base = e0 + 32 * (16 * (q >> 5)) + (q & 31);
                 float a = 0.f;
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    a += fabsf(xs[h][j] - ys[h][j]);
-                    if constexpr (NT) __builtin_nontemporal_store(xs[h][j], &sn[base + 32 * j]);
-                    else sn[base + 32 * j] = xs[h][j];
-                }
+                for (int j = 0; j < 16; ++j) a += fabsf(xs[h][j] - ys[h][j]);
                 b0[q] = a;   // b0[m * 32 + s]
+            }
+            if constexpr (!DEFER) {   // diagnostics A/B (DFQ_CLE_SNAP_EARLY): the snapshot before the arrival
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    float* ps = sn + e0 + 32 * (16 * ((tid + h * kThreads) >> 5)) + (tid & 31);
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) ps[32 * j] = xs[h][j];
+                }
             }
             __syncthreads();
             if (tid < 32) {   // level 1
@@ -1045,7 +1055,20 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
             }
         }
         __syncthreads();   // LDS reused by the next unit
-        hook(un, ch, nb1);
+        hook(un, ch, nb1, [&]() {   // snap := W of a full tile (read again only after the launch boundary)
+            if (!DEFER || !full) return;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int q = tid + h * kThreads;
+                float* ps = sn + e0 + 32 * (16 * (q >> 5)) + (q & 31);
+                asm volatile("" : "+v"(ps));   // a fresh address: not the loads' 16 addresses kept live
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    if constexpr (NT) __builtin_nontemporal_store(xs[h][j], ps + 32 * j);
+                    else ps[32 * j] = xs[h][j];
+                }
+            }
+        });
     }
 }
 
@@ -1312,7 +1335,7 @@ union CleStepLds {
 
 // POS = false (no position-parallel 3x3 rescale tiles): capped at 128 VGPRs,
 // 4 waves per SIMD like the rescale body alone
-template <bool POS, bool NTS = false>
+template <bool POS, bool NTS = false, bool DEFER = true>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(POS ? 1 : 4)))
 cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ atasks, int64_t a0, int64_t a1,
                      int64_t nab, uint32_t* __restrict__ rng, int64_t M, int is_signed, float eps, double smin,
@@ -1397,8 +1420,10 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         return;
     }
     const uint32_t fin_members = (uint32_t)F.nbig;
-    auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1) {
-        if (!arrive(F.cnt + un.chunk, (uint32_t)(nb1 + 1))) return;   // not the chunk's last tile
+    auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1, auto flush) {
+        const bool last_tile = arrive(F.cnt + un.chunk, (uint32_t)(nb1 + 1));
+        flush();
+        if (!last_tile) return;   // not the chunk's last tile
         {
             // the chunk's level-1 sums and tail words in one parallel pass of coherent
             // loads into LDS (free again: the unit is done), then one wave sums them
@@ -1420,7 +1445,7 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         }
         if (arrive(F.cnt + F.nchunks, fin_members)) finish();   // the iteration's last arrival
     };
-    cle_tiles_body<decltype(hook), NTS>(layers, chunks, b1off, units + u0, u1 - u0, b1buf, tailbuf, blk - nab, ntb, lds,
+    cle_tiles_body<decltype(hook), NTS, DEFER>(layers, chunks, b1off, units + u0, u1 - u0, b1buf, tailbuf, blk - nab, ntb, lds,
                    lds + kCleTile + kCleTailWords, hook);
     tl2_rec(1);
 }
@@ -2084,8 +2109,12 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         F.last = last ? 1 : 0;
 #ifdef DFQ_DIAGNOSTICS
         static const bool snap_nt = ab_env("DFQ_CLE_SNAP_NT") != nullptr;   // A/B: non-temporal snapshot stores
-        auto kern = (!last && p->step_pos[k]) ? (snap_nt ? cle_loop_step_kernel<true, true> : cle_loop_step_kernel<true>)
-                                              : (snap_nt ? cle_loop_step_kernel<false, true> : cle_loop_step_kernel<false>);
+        static const bool snap_early = ab_env("DFQ_CLE_SNAP_EARLY") != nullptr;   // A/B: snapshot before the arrival
+        auto kern = (!last && p->step_pos[k])
+                        ? (snap_nt ? cle_loop_step_kernel<true, true>
+                                   : snap_early ? cle_loop_step_kernel<true, false, false> : cle_loop_step_kernel<true>)
+                        : (snap_nt ? cle_loop_step_kernel<false, true>
+                                   : snap_early ? cle_loop_step_kernel<false, false, false> : cle_loop_step_kernel<false>);
 #else
         auto kern = (!last && p->step_pos[k]) ? cle_loop_step_kernel<true> : cle_loop_step_kernel<false>;
 #endif
