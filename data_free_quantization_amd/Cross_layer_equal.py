@@ -13,6 +13,7 @@ import atexit
 from collections.abc import MutableMapping
 import ctypes as C
 import os
+import sys
 import time
 import warnings
 
@@ -128,6 +129,7 @@ class _DiffPlan:
 #: iteration cap of the device loop (the reference's loop has none; a run that
 #: reaches it warns)
 MAX_ITERS = int(os.environ.get("DFQ_CLE_MAX_ITERS", "100000"))
+_TIMING = bool(os.environ.get("DFQ_CLE_TIMING"))   # host-side split of create (stderr)
 
 
 def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8], Treshhold=2e-7, Count=20,
@@ -178,6 +180,7 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
     outlive the plan."""
     # module state straight from the parameter / buffer dicts (Module.__getattr__
     # per access was a good part of this host time)
+    tc = [time.perf_counter()] if _TIMING else None
     tl = tuple(Target_list)
     targets = [v._parameters["weight"] for v in graph.values() if type(v) in tl]
     n = len(relations)
@@ -207,6 +210,8 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
             rel.S = v
             rows[j][5] = v.data_ptr()
     rows = [tuple(r) for r in rows]
+    if tc:
+        tc.append(time.perf_counter())
     # the descriptor table as a numpy record array (layout of _lib.CleRel), one row per
     # relation from plain tuples instead of ctypes field by field
     tab = np.array(rows if rows else [(0,) * 13], dtype=_CLE_REL)
@@ -222,11 +227,17 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
     if ws_bytes < 0:
         raise RuntimeError("dfq_cle_plan_ws_bytes: invalid target sizes")
     ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=dev)
+    if tc:
+        tc.append(time.perf_counter())
     plan = C.c_void_p()
     _lib.check(L.dfq_cle_plan_create(descs, n, tp, tn, nt, float(s_min_max[0]), float(s_min_max[1]),
                                      int(bool(signed)), float(eps), _lib.REF_THREADS, ws.data_ptr(), ws.numel(),
                                      C.byref(plan)),
                "dfq_cle_plan_create", RuntimeError)
+    if tc:
+        tc.append(time.perf_counter())
+        print("DFQ_CLE_TIMING python create: relations %.1f us, tables + workspace %.1f us, plan_create %.1f us"
+              % tuple((b - a) * 1e6 for a, b in zip(tc, tc[1:])), file=sys.stderr)
     return plan, ws, dev
 
 
@@ -302,7 +313,11 @@ def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count,
     if launch:
         L = _lib.load()
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        t5 = time.perf_counter()
         rc = L.dfq_cle_plan_launch(plan, float(Treshhold), int(Count), MAX_ITERS, stream)
+        if _TIMING:
+            print("DFQ_CLE_TIMING python launch: stream %.1f us, plan_launch %.1f us"
+                  % ((t5 - t2) * 1e6, (time.perf_counter() - t5) * 1e6), file=sys.stderr)
         if rc == _lib.DFQ_OK:
             _PENDING = (plan, ws, {"create": (t2 - t0) * 1e3, "launch": (time.perf_counter() - t2) * 1e3})
             LAST_RUN.clear()

@@ -520,7 +520,8 @@ struct CleApplyLds {
 // {start, end} in s_memrealtime ticks (100 MHz) and the block's XCC / CU ids.
 __device__ uint64_t* g_cle_tl = nullptr;
 // ... and per block of the iteration's last launch (tiles / ranges / stop rule):
-// {start, end, role (1 tile, 2 range), 0}; slot kCleTl2Fin: the stop rule's {start, end}
+// {start, end, role (1 tile, 2 range), 0}; slot kCleTl2Fin: the stop rule's {start,
+// end, chunk sums staged, layer means done}
 __device__ uint64_t* g_cle_tl2 = nullptr;
 constexpr int kCleTl2Fin = 8192;
 #endif
@@ -1211,23 +1212,37 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
     // the state during this launch.
     CleState s0{};
     if (threadIdx.x == 0) s0 = *st;
+    // this thread's first layer's size and chunk count, loaded beside the chunk
+    // sums (was a dependent round trip after the staging)
+    int64_t ln0 = 1, lnt0 = 1;
+    if ((int)threadIdx.x < nl) {
+        ln0 = layers[threadIdx.x].n;
+        lnt0 = layers[threadIdx.x].nt;
+    }
     if (part_lds) {   // every chunk sum in one parallel pass of coherent loads
         for (int64_t i = threadIdx.x; i < (int64_t)nl * S; i += blockDim.x)
             part_lds[i] = kCoherent ? ld_coh(part + i) : part[i];
         __syncthreads();
         part = part_lds;
     }
+#ifdef DFQ_DIAGNOSTICS
+    if (kCoherent && g_cle_tl2 && threadIdx.x == 0) g_cle_tl2[4 * kCleTl2Fin + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
     double* m = nl <= 1024 ? sm : means;
     for (int l = threadIdx.x; l < nl; l += blockDim.x) {
         // serial: sum = 0 + (0 + slot); two_pass_reduction: its S-slot buffer
         // (at::get_num_threads()) summed as a contiguous reduction
         const float* pl = part + (int64_t)l * S;
         auto ld = [&](int64_t e) { return (part_lds || !kCoherent) ? pl[e] : ld_coh(pl + e); };
-        const float sum = layers[l].nt == 1 ? 0.f + (0.f + ld(0))
-                                            : 0.f + aten_inner_sum([&](int64_t e) { return ld(e); }, S);
-        m[l] = (double)(sum / (float)layers[l].n);
+        const bool first = l == (int)threadIdx.x;
+        const int64_t lnt = first ? lnt0 : layers[l].nt;
+        const float sum = lnt == 1 ? 0.f + (0.f + ld(0)) : 0.f + aten_inner_sum([&](int64_t e) { return ld(e); }, S);
+        m[l] = (double)(sum / (float)(first ? ln0 : layers[l].n));
     }
     __syncthreads();
+#ifdef DFQ_DIAGNOSTICS
+    if (kCoherent && g_cle_tl2 && threadIdx.x == 0) g_cle_tl2[4 * kCleTl2Fin + 3] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (threadIdx.x == 0) {
         double dt = 0.0;
         if constexpr (kLeafOnly) {
@@ -2296,7 +2311,9 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             }
             const uint64_t* f = &tl2[4 * kCleTl2Fin];
             if (f[0] && t0 != ~0ull)
-                fprintf(stderr, " [stop rule: %.2f - %.2f]", (double)(f[0] - t0) * 0.01, (double)(f[1] - t0) * 0.01);
+                fprintf(stderr, " [stop rule: %.2f - %.2f, sums staged %.2f, means %.2f]", (double)(f[0] - t0) * 0.01,
+                        (double)(f[1] - t0) * 0.01, f[2] ? (double)(f[2] - t0) * 0.01 : -1.0,
+                        f[3] ? (double)(f[3] - t0) * 0.01 : -1.0);
             fprintf(stderr, "\n");
         }
         DFQ_HIP_CHECK(hipStreamSynchronize(s));
