@@ -946,18 +946,14 @@ __global__ void cle_loop_snap_kernel(const CleLayer* __restrict__ layers, const 
 // Metric tiles taken by blocks blk, blk + nblk, ... (d: kCleTile + kCleTailWords
 // floats of LDS, b0: 512).
 struct CleNoUnitHook {
-    template <class Flush>
-    __device__ void operator()(const CleUnit&, const CleChunk&, int64_t, Flush flush) const { flush(); }
+    __device__ void operator()(const CleUnit&, const CleChunk&, int64_t) const {}
 };
 
-// hook(unit, chunk, nb1, flush) runs after each unit (LDS free again) and calls
-// flush() once the unit's hand-off has arrived: a full tile's snapshot stores
-// (snap := W) are issued there, so they no longer sit in front of the arrival's
-// vmcnt(0) drain, and its 32 W values per thread stay live only across the
-// arrival (not across the chunk combine or the stop rule).  NT: the snapshot
-// stores non-temporal (diagnostics A/B, DFQ_CLE_SNAP_NT); !DEFER: the snapshot
-// stores before the arrival (diagnostics A/B, DFQ_CLE_SNAP_EARLY)
-template <class Hook = CleNoUnitHook, bool NT = false, bool DEFER = true>
+// hook(unit, chunk, nb1) runs after each unit (LDS free again).  NT: the snapshot
+// stores non-temporal (diagnostics A/B, DFQ_CLE_SNAP_NT).  (The snapshot stores
+// issued after the unit's arrival instead -- out of the arrival's vmcnt(0) drain --
+// measured no faster and the tiles slower, 84 B of spills: profiles/r04/cle_ab_r04p.)
+template <class Hook = CleNoUnitHook, bool NT = false>
 __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
                                                const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units,
                                                int64_t nunits, float* __restrict__ b1buf, float* __restrict__ tailbuf,
@@ -974,14 +970,13 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
         const bool full = un.tile < nb1;
         const int64_t e0 = (int64_t)un.tile * kCleTile;
         const int64_t cnt = full ? kCleTile : len - e0;
-        float xs[2][16];   // a full tile's W values: snap := W after the hand-off (below)
         if (full) {
             // level 0 straight from the loads: thread t owns (block m, stream s) for
             // q = t and t + 256; its 16 elements 32 (16 m + j) + s sit at stride 32,
             // so each load instruction covers whole 128-B lines across the lanes,
             // and the 16-term sum runs in ATen's order in registers (32 loads in
             // flight per thread, no LDS staging of |W - W_prev|)
-            float ys[2][16];
+            float xs[2][16], ys[2][16];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int q = tid + h * kThreads;
@@ -995,18 +990,15 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int q = tid + h * kThreads;
+                const int64_t base = e0 + 32 * (16 * (q >> 5)) + (q & 31);
                 float a = 0.f;
 #pragma unroll
-                for (int j = 0; j < 16; ++j) a += fabsf(xs[h][j] - ys[h][j]);
-                b0[q] = a;   // b0[m * 32 + s]
-            }
-            if constexpr (!DEFER) {   // diagnostics A/B (DFQ_CLE_SNAP_EARLY): the snapshot before the arrival
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    float* ps = sn + e0 + 32 * (16 * ((tid + h * kThreads) >> 5)) + (tid & 31);
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) ps[32 * j] = xs[h][j];
+                for (int j = 0; j < 16; ++j) {
+                    a += fabsf(xs[h][j] - ys[h][j]);
+                    if constexpr (NT) __builtin_nontemporal_store(xs[h][j], &sn[base + 32 * j]);
+                    else sn[base + 32 * j] = xs[h][j];
                 }
+                b0[q] = a;   // b0[m * 32 + s]
             }
             __syncthreads();
             if (tid < 32) {   // level 1
@@ -1056,20 +1048,7 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
             }
         }
         __syncthreads();   // LDS reused by the next unit
-        hook(un, ch, nb1, [&]() {   // snap := W of a full tile (read again only after the launch boundary)
-            if (!DEFER || !full) return;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int q = tid + h * kThreads;
-                float* ps = sn + e0 + 32 * (16 * (q >> 5)) + (q & 31);
-                asm volatile("" : "+v"(ps));   // a fresh address: not the loads' 16 addresses kept live
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    if constexpr (NT) __builtin_nontemporal_store(xs[h][j], ps + 32 * j);
-                    else ps[32 * j] = xs[h][j];
-                }
-            }
-        });
+        hook(un, ch, nb1);
     }
 }
 
@@ -1205,28 +1184,28 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
                                                float* part_lds = nullptr, float* np_stack = nullptr,
                                                uint32_t* hflag = nullptr, uint64_t* sig = nullptr,
                                                uint64_t gen = 0, int flag_every = 0) {
-    // The stop rule's state, read up front in one batch of independent loads (they
-    // land while the chunk sums are staged): read field by field between the
-    // stores below, they were ~5 dependent round trips of a serial 7.6 us stop
-    // rule (DFQ_CLE_TL, the last launch's block timeline).  Nothing else writes
-    // the state during this launch.
-    CleState s0{};
-    if (threadIdx.x == 0) s0 = *st;
-    // this thread's first layer's size and chunk count, loaded beside the chunk
-    // sums (was a dependent round trip after the staging)
-    int64_t ln0 = 1, lnt0 = 1;
-    if ((int)threadIdx.x < nl) {
-        ln0 = layers[threadIdx.x].n;
-        lnt0 = layers[threadIdx.x].nt;
-    }
-    if (part_lds) {   // every chunk sum in one parallel pass of coherent loads
-        for (int64_t i = threadIdx.x; i < (int64_t)nl * S; i += blockDim.x)
-            part_lds[i] = kCoherent ? ld_coh(part + i) : part[i];
+    // The stop rule's inputs in one parallel pass of loads into LDS (part_lds): the
+    // chunk sums, the layers' {(float)n, serial} and the state's 10 words.  Read
+    // where they are used instead, they were dependent round trips of a serial
+    // stop rule (7.6 us, DFQ_CLE_TL, the last launch's block timeline); loaded
+    // into registers up front, they pushed the kernel past its 128 VGPRs.
+    // Nothing else writes the state during this launch.
+#ifdef DFQ_DIAGNOSTICS
+    uint64_t* tlm = (kCoherent && threadIdx.x == 0 && g_cle_tl2) ? g_cle_tl2 + 4 * kCleTl2Fin : nullptr;
+#endif
+    constexpr int kStateWords = (int)(sizeof(CleState) / 4);
+    static_assert(sizeof(CleState) % 4 == 0, "CleState: whole 4-B words");
+    const int64_t nps = (int64_t)nl * (S + 2);
+    if (part_lds) {
+        for (int64_t i = threadIdx.x; i < nps + kStateWords; i += blockDim.x) {
+            const float* src = i < nps ? part + i : reinterpret_cast<const float*>(st) + (i - nps);
+            part_lds[i] = kCoherent ? ld_coh(src) : *src;
+        }
         __syncthreads();
         part = part_lds;
     }
 #ifdef DFQ_DIAGNOSTICS
-    if (kCoherent && g_cle_tl2 && threadIdx.x == 0) g_cle_tl2[4 * kCleTl2Fin + 2] = __builtin_amdgcn_s_memrealtime();
+    if (tlm) tlm[2] = __builtin_amdgcn_s_memrealtime();
 #endif
     double* m = nl <= 1024 ? sm : means;
     for (int l = threadIdx.x; l < nl; l += blockDim.x) {
@@ -1234,16 +1213,19 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         // (at::get_num_threads()) summed as a contiguous reduction
         const float* pl = part + (int64_t)l * S;
         auto ld = [&](int64_t e) { return (part_lds || !kCoherent) ? pl[e] : ld_coh(pl + e); };
-        const bool first = l == (int)threadIdx.x;
-        const int64_t lnt = first ? lnt0 : layers[l].nt;
-        const float sum = lnt == 1 ? 0.f + (0.f + ld(0)) : 0.f + aten_inner_sum([&](int64_t e) { return ld(e); }, S);
-        m[l] = (double)(sum / (float)(first ? ln0 : layers[l].n));
+        const float* lm = part_lds ? part_lds + (int64_t)nl * S + 2 * l : nullptr;
+        const bool serial = lm ? lm[1] != 0.f : layers[l].nt == 1;
+        const float sum = serial ? 0.f + (0.f + ld(0)) : 0.f + aten_inner_sum([&](int64_t e) { return ld(e); }, S);
+        m[l] = (double)(sum / (lm ? lm[0] : (float)layers[l].n));
     }
     __syncthreads();
 #ifdef DFQ_DIAGNOSTICS
-    if (kCoherent && g_cle_tl2 && threadIdx.x == 0) g_cle_tl2[4 * kCleTl2Fin + 3] = __builtin_amdgcn_s_memrealtime();
+    if (tlm) tlm[3] = __builtin_amdgcn_s_memrealtime();
 #endif
     if (threadIdx.x == 0) {
+        CleState s0;
+        if (part_lds) __builtin_memcpy(&s0, part_lds + nps, sizeof(CleState));
+        else s0 = *st;
         double dt = 0.0;
         if constexpr (kLeafOnly) {
             dt = nl > 0 ? 0. + np_pairwise_leaf(m, nl) : 0.0;
@@ -1350,7 +1332,7 @@ union CleStepLds {
 
 // POS = false (no position-parallel 3x3 rescale tiles): capped at 128 VGPRs,
 // 4 waves per SIMD like the rescale body alone
-template <bool POS, bool NTS = false, bool DEFER = true>
+template <bool POS, bool NTS = false>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(POS ? 1 : 4)))
 cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ atasks, int64_t a0, int64_t a1,
                      int64_t nab, uint32_t* __restrict__ rng, int64_t M, int is_signed, float eps, double smin,
@@ -1413,7 +1395,8 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
             }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        const bool stage_part = (int64_t)F.nl * F.S + 2048 <= kCleTile;
+        // the chunk sums, layer sizes and state words (cle_final_body) after the means
+        const bool stage_part = (int64_t)F.nl * (F.S + 2) + (int64_t)(sizeof(CleState) / 4) + 2048 <= kCleTile;
         if (F.nl <= 128)   // numpy's pairwise sum over the layer means is one leaf
             cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
                                        stage_part ? lds + 2048 : nullptr, nullptr, F.hflag, F.sig, F.gen,
@@ -1435,10 +1418,8 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         return;
     }
     const uint32_t fin_members = (uint32_t)F.nbig;
-    auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1, auto flush) {
-        const bool last_tile = arrive(F.cnt + un.chunk, (uint32_t)(nb1 + 1));
-        flush();
-        if (!last_tile) return;   // not the chunk's last tile
+    auto hook = [&](const CleUnit& un, const CleChunk& ch, int64_t nb1) {
+        if (!arrive(F.cnt + un.chunk, (uint32_t)(nb1 + 1))) return;   // not the chunk's last tile
         {
             // the chunk's level-1 sums and tail words in one parallel pass of coherent
             // loads into LDS (free again: the unit is done), then one wave sums them
@@ -1460,7 +1441,7 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         }
         if (arrive(F.cnt + F.nchunks, fin_members)) finish();   // the iteration's last arrival
     };
-    cle_tiles_body<decltype(hook), NTS, DEFER>(layers, chunks, b1off, units + u0, u1 - u0, b1buf, tailbuf, blk - nab, ntb, lds,
+    cle_tiles_body<decltype(hook), NTS>(layers, chunks, b1off, units + u0, u1 - u0, b1buf, tailbuf, blk - nab, ntb, lds,
                    lds + kCleTile + kCleTailWords, hook);
     tl2_rec(1);
 }
@@ -2001,12 +1982,14 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_chunks = T.add<CleChunk>((int64_t)chunks.size());
     const int64_t o_units = T.add<CleUnit>((int64_t)units.size());
     const int64_t o_b1off = T.add<int64_t>((int64_t)b1off.size());
+    p->slots = std::max<int32_t>(ref_threads, 1);
+    // the chunk sums [layers][slots] (zeroed per run), then per layer {(float)n,
+    // nt == 1}: the stop rule stages both in one pass of loads
+    const int64_t o_part = T.add<float>((int64_t)(p->slots + 2) * n_targets);
     const int64_t host_bytes = T.total;   // the tables above are built on the host (and the group tables)
     const int64_t o_b1 = T.add<float>(32 * nb1_total);
     const int64_t o_tail = T.add<float>(kCleTailWords * (int64_t)chunks.size());
     const int64_t o_rng = T.add<uint32_t>(4 * M);
-    p->slots = std::max<int32_t>(ref_threads, 1);
-    const int64_t o_part = T.add<float>((int64_t)p->slots * n_targets);
     const int64_t o_means = T.add<double>(n_targets);
     const int64_t o_state = T.add<CleState>(1);
     const int64_t o_hist = T.add<double>(kCleHistCap);
@@ -2058,6 +2041,13 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     };
     put(o_rels, R); put(o_rt, rt); put(o_at, at); put(o_layers, layers); put(o_chunks, chunks); put(o_units, units);
     put(o_b1off, b1off);
+    {
+        float* lm = reinterpret_cast<float*>(hblob + o_part) + (int64_t)p->slots * n_targets;
+        for (int64_t l = 0; l < n_targets; ++l) {
+            lm[2 * l] = (float)layers[l].n;
+            lm[2 * l + 1] = layers[l].nt == 1 ? 1.f : 0.f;
+        }
+    }
     if (p->pooled) {   // async on the loop stream, which every launch of the plan uses
         if ((e = hipMemcpyAsync(base, hblob, host_bytes, hipMemcpyHostToDevice, ctx.st)) != hipSuccess) return fail(e);
         if ((e = hipEventRecord(ctx.pool_ev, ctx.st)) != hipSuccess) return fail(e);
@@ -2124,12 +2114,8 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         F.last = last ? 1 : 0;
 #ifdef DFQ_DIAGNOSTICS
         static const bool snap_nt = ab_env("DFQ_CLE_SNAP_NT") != nullptr;   // A/B: non-temporal snapshot stores
-        static const bool snap_early = ab_env("DFQ_CLE_SNAP_EARLY") != nullptr;   // A/B: snapshot before the arrival
-        auto kern = (!last && p->step_pos[k])
-                        ? (snap_nt ? cle_loop_step_kernel<true, true>
-                                   : snap_early ? cle_loop_step_kernel<true, false, false> : cle_loop_step_kernel<true>)
-                        : (snap_nt ? cle_loop_step_kernel<false, true>
-                                   : snap_early ? cle_loop_step_kernel<false, false, false> : cle_loop_step_kernel<false>);
+        auto kern = (!last && p->step_pos[k]) ? (snap_nt ? cle_loop_step_kernel<true, true> : cle_loop_step_kernel<true>)
+                                              : (snap_nt ? cle_loop_step_kernel<false, true> : cle_loop_step_kernel<false>);
 #else
         auto kern = (!last && p->step_pos[k]) ? cle_loop_step_kernel<true> : cle_loop_step_kernel<false>;
 #endif
