@@ -174,6 +174,28 @@ def _state(m, name):
     return getattr(m, name, None)
 
 
+def _tensor_info(t, memo):
+    """(data_ptr, shape, numel) of a weight, checked like _lib.require_device once
+    per tensor (every relation weight is also a target, and a relation's W2 is the
+    next one's W1): the per-tensor property calls were a good part of plan
+    creation's host time."""
+    k = id(t)
+    r = memo.get(k)
+    if r is None:
+        r = memo[k] = (_checked_ptr(t), t.shape, t.numel())
+    return r
+
+
+def _checked_ptr(t):
+    """data_ptr of a tensor the loop reads or writes, checked like _lib.require_device."""
+    if not (t.is_cuda and t.dtype is _F32 and t.is_contiguous()):
+        _lib.require_device(t)   # raises the reference-style error
+    return t.data_ptr()
+
+
+_F32 = torch.float32
+
+
 def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
     """dfq_cle_plan_create over the relations' tensors; returns (plan, workspace,
     device).  The workspace (W_prev snapshots, torch's caching allocator) must
@@ -183,6 +205,8 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
     tc = [time.perf_counter()] if _TIMING else None
     tl = tuple(Target_list)
     targets = [v._parameters["weight"] for v in graph.values() if type(v) in tl]
+    memo = {}
+    tinfo = [_tensor_info(t, memo) for t in targets]
     n = len(relations)
     rows = []
     fresh = []   # relations whose S the loop creates: views of one allocation, carved below
@@ -194,16 +218,16 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
             l1.bias = nn.Parameter(torch.zeros(p1["weight"].size(0), dtype=torch.float32, device=p1["weight"].device),
                                    requires_grad=False)
         bn = graph[bn_idx]
-        W1, W2, B1 = p1["weight"], l2._parameters["weight"], p1["bias"]
+        W1 = p1["weight"]
         bnw, bnb = _state(bn, "fake_weight"), _state(bn, "fake_bias")
-        _lib.require_device(W1, W2, B1, bnw, bnb)
+        w1p, s1, n1 = _tensor_info(W1, memo)
+        w2p, s2, n2 = _tensor_info(l2._parameters["weight"], memo)
         init = rel.S is None
         if init:
             fresh.append((len(rows), rel, W1))
-        s1, s2 = W1.shape, W2.shape
-        rows.append([W1.data_ptr(), W2.data_ptr(), B1.data_ptr(), 0 if bnw is None else bnw.data_ptr(),
-                     0 if bnb is None else bnb.data_ptr(), 0 if init else rel.S.data_ptr(), s1[0],
-                     W1.numel() // s1[0], s2[0], s2[1], W2.numel() // (s2[0] * s2[1]), 1 if init else 0, 0])
+        rows.append([w1p, w2p, _checked_ptr(p1["bias"]), 0 if bnw is None else _checked_ptr(bnw),
+                     0 if bnb is None else _checked_ptr(bnb), 0 if init else rel.S.data_ptr(), s1[0],
+                     n1 // s1[0], s2[0], s2[1], n2 // (s2[0] * s2[1]), 1 if init else 0, 0])
     if fresh:   # one allocation for every new Relation.S (a torch.empty per relation cost ~7 us each)
         flat = torch.empty(sum(w.size(0) for _, _, w in fresh), dtype=torch.float32, device=fresh[0][2].device)
         for (j, rel, w), v in zip(fresh, torch.split(flat, [w.size(0) for _, _, w in fresh])):
@@ -216,10 +240,9 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
     # relation from plain tuples instead of ctypes field by field
     tab = np.array(rows if rows else [(0,) * 13], dtype=_CLE_REL)
     descs = tab.ctypes.data_as(C.POINTER(_lib.CleRel))
-    _lib.require_device(*targets)
     nt = len(targets)
-    tp = (C.c_void_p * max(nt, 1))(*[t.data_ptr() for t in targets])
-    tn = (C.c_int64 * max(nt, 1))(*[t.numel() for t in targets])
+    tp = (C.c_void_p * max(nt, 1))(*[i[0] for i in tinfo])
+    tn = (C.c_int64 * max(nt, 1))(*[i[2] for i in tinfo])
     L = _lib.load()
     dev = targets[0].device if targets else torch.device("cuda", torch.cuda.current_device())
     # W_prev snapshots from torch's caching allocator (no hipMalloc / hipFree per call)
@@ -246,7 +269,7 @@ def _run_plan(plan, dev, Treshhold, Count):
     L = _lib.load()
     iters = C.c_int32(0)
     hist = _hist_buffer()
-    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    stream = _lib.raw_stream(dev)
     _lib.check(L.dfq_cle_plan_run(plan, float(Treshhold), int(Count), MAX_ITERS, C.byref(iters), hist, stream),
                "dfq_cle_plan_run")
     chains, steps, launches = C.c_int32(0), C.c_int32(0), C.c_int32(0)
@@ -312,7 +335,7 @@ def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count,
     t2 = time.perf_counter()
     if launch:
         L = _lib.load()
-        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        stream = _lib.raw_stream(dev)
         t5 = time.perf_counter()
         rc = L.dfq_cle_plan_launch(plan, float(Treshhold), int(Count), MAX_ITERS, stream)
         if _TIMING:

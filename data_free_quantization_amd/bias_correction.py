@@ -554,7 +554,7 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
             _TEMPLATES.move_to_end(sig)
             dev = where[1][0].device if where[1] else torch.device("cuda", torch.cuda.current_device())
             with torch.no_grad():
-                res = tpl.replay(where, dev, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+                res = tpl.replay(where, dev, _lib.raw_stream(dev))
             logger.info("Bias correction completed.")
             return res
     warned = []
