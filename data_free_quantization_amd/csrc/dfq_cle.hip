@@ -130,15 +130,16 @@ __device__ __forceinline__ void for_short_rows(int64_t a, int64_t b, int64_t len
 constexpr int64_t kCleChansPerTask = 1024;
 
 // min / max of n floats at p, one wave, 4 loads in flight per lane
-__device__ __forceinline__ void wave_range(const float* __restrict__ p, int64_t n, bool vec, int lane, float& vmin,
+__device__ __forceinline__ void wave_range(const float* __restrict__ p_, int64_t n, bool vec, int lane, float& vmin,
                                            float& vmax) {
+    const DFQ_GLOBAL float* __restrict__ p = (const DFQ_GLOBAL float*)p_;   // global: not flat
     vmin = INFINITY;
     vmax = -INFINITY;
     if (vec) {
-        const float4* p4 = reinterpret_cast<const float4*>(p);
+        const DFQ_GLOBAL f32x4* p4 = (const DFQ_GLOBAL f32x4*)p;
         const int64_t n4 = n >> 2;
         for (int64_t i = lane; i < n4; i += 4 * 64) {
-            float4 v[4];
+            f32x4 v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (i + 64 * u < n4) v[u] = p4[i + 64 * u];
@@ -170,14 +171,15 @@ __device__ __forceinline__ void wave_range(const float* __restrict__ p, int64_t 
 // factor (range-table reads) is evaluated after the first loads are issued, so
 // the data and the range words are one memory round trip, not two.
 template <class F>
-__device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, bool vec, int lane, F&& factor) {
+__device__ __forceinline__ void wave_scale(float* __restrict__ p_, int64_t n, bool vec, int lane, F&& factor) {
+    DFQ_GLOBAL float* __restrict__ p = (DFQ_GLOBAL float*)p_;   // global: not flat
     float f = 0.f;
     bool have = false;
     if (vec) {
-        float4* p4 = reinterpret_cast<float4*>(p);
+        DFQ_GLOBAL f32x4* p4 = (DFQ_GLOBAL f32x4*)p;
         const int64_t n4 = n >> 2;
         for (int64_t i = lane; i < n4; i += 4 * 64) {
-            float4 v[4];
+            f32x4 v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (i + 64 * u < n4) v[u] = p4[i + 64 * u];
@@ -214,17 +216,18 @@ __device__ __forceinline__ void wave_scale(float* __restrict__ p, int64_t n, boo
 
 // wave_scale that also returns the (min, max) of the products (every lane).
 template <class F>
-__device__ __forceinline__ void wave_scale_mm(float* __restrict__ p, int64_t n, bool vec, int lane, float& vmin,
+__device__ __forceinline__ void wave_scale_mm(float* __restrict__ p_, int64_t n, bool vec, int lane, float& vmin,
                                               float& vmax, F&& factor) {
+    DFQ_GLOBAL float* __restrict__ p = (DFQ_GLOBAL float*)p_;   // global: not flat
     vmin = INFINITY;
     vmax = -INFINITY;
     float f = 0.f;
     bool have = false;
     if (vec) {
-        float4* p4 = reinterpret_cast<float4*>(p);
+        DFQ_GLOBAL f32x4* p4 = (DFQ_GLOBAL f32x4*)p;
         const int64_t n4 = n >> 2;
         for (int64_t i = lane; i < n4; i += 4 * 64) {
-            float4 v[4];
+            f32x4 v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (i + 64 * u < n4) v[u] = p4[i + 64 * u];
@@ -270,8 +273,9 @@ __device__ __forceinline__ void wave_scale_mm(float* __restrict__ p, int64_t n, 
 // p[0..n) *= f() and the (min, max) of the products, one wave (scalar loads:
 // used for short depthwise rows); the factor is read after the first load
 template <class F>
-__device__ __forceinline__ void wave_scale_range(float* __restrict__ p, int64_t n, int lane, float& vmin, float& vmax,
+__device__ __forceinline__ void wave_scale_range(float* __restrict__ p_, int64_t n, int lane, float& vmin, float& vmax,
                                                  F&& factor) {
+    DFQ_GLOBAL float* __restrict__ p = (DFQ_GLOBAL float*)p_;   // global: not flat
     vmin = INFINITY;
     vmax = -INFINITY;
     float f = 0.f;
@@ -313,7 +317,7 @@ __device__ void tile_range_by_position(const CleRel& R, const CleTask& tk, uint3
     const int64_t rowlen = R.i2 * R.khw2;
     const int ncol = (int)(tk.c1 - tk.c0);
     const int npos = ncol * khw;
-    const float* base = R.w2 + tk.c0 * R.khw2;
+    const DFQ_GLOBAL float* base = (const DFQ_GLOBAL float*)(R.w2 + tk.c0 * R.khw2);
     float vmn[kTileMaxKhw], vmx[kTileMaxKhw];
 #pragma unroll
     for (int m = 0; m < kTileMaxKhw; ++m) {
@@ -321,7 +325,7 @@ __device__ void tile_range_by_position(const CleRel& R, const CleTask& tk, uint3
         vmx[m] = -INFINITY;
     }
     for (int64_t o = tk.a; o < tk.b; ++o) {
-        const float* rp = base + o * rowlen;
+        const DFQ_GLOBAL float* rp = base + o * rowlen;
         float v[kTileMaxKhw];
 #pragma unroll
         for (int m = 0; m < kTileMaxKhw; ++m)
@@ -374,7 +378,7 @@ __device__ __forceinline__ void cle_range_body(const CleRel* __restrict__ rels, 
                 float vmin = INFINITY, vmax = -INFINITY;
                 if (act)
                     for (int64_t i = sl; i < R.len1; i += G) {
-                        const float x = R.w1[c * R.len1 + i];
+                        const float x = ((DFQ_GLOBAL float*)R.w1)[c * R.len1 + i];
                         vmin = fminf(vmin, x);
                         vmax = fmaxf(vmax, x);
                     }
@@ -391,7 +395,7 @@ __device__ __forceinline__ void cle_range_body(const CleRel* __restrict__ rels, 
                 float vmin = INFINITY, vmax = -INFINITY;
                 if (act)
                     for (int64_t i = sl; i < seg; i += G) {
-                        const float x = R.w2[c * seg + i];
+                        const float x = ((DFQ_GLOBAL float*)R.w2)[c * seg + i];
                         vmin = fminf(vmin, x);
                         vmax = fmaxf(vmax, x);
                     }
@@ -434,7 +438,7 @@ __device__ __forceinline__ void cle_range_body(const CleRel* __restrict__ rels, 
                     float v[kColTileRows];
 #pragma unroll
                     for (int j = 0; j < kColTileRows; ++j)
-                        if (tk.a + j < tk.b) v[j] = R.w2[(tk.a + j) * rowlen + i];
+                        if (tk.a + j < tk.b) v[j] = ((DFQ_GLOBAL float*)R.w2)[(tk.a + j) * rowlen + i];
 #pragma unroll
                     for (int j = 0; j < kColTileRows; ++j)
                         if (tk.a + j < tk.b) {
@@ -456,7 +460,7 @@ __device__ __forceinline__ void cle_range_body(const CleRel* __restrict__ rels, 
                         vmax = -INFINITY;
                     }
                     g_prev = g;
-                    const float* p = R.w2 + o * rowlen + i * R.khw2;
+                    const DFQ_GLOBAL float* p = (const DFQ_GLOBAL float*)(R.w2 + o * rowlen + i * R.khw2);
                     for (int64_t k = 0; k < R.khw2; ++k) {
                         vmin = fminf(vmin, p[k]);
                         vmax = fmaxf(vmax, p[k]);
@@ -561,7 +565,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             for_short_rows(tk.a, tk.b, R.len1, [&](int64_t c, bool act, int sl, int G) {
                 float y0 = INFINITY, y1 = -INFINITY;
                 if (act && sl < R.len1) {   // G >= len1: one element per lane
-                    float* p = R.w1 + c * R.len1 + sl;
+                    DFQ_GLOBAL float* p = (DFQ_GLOBAL float*)(R.w1 + c * R.len1 + sl);
                     const float x = *p;   // in flight while the scale's range words load
                     const float y = x * cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).s;
                     *p = y;
@@ -582,7 +586,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             for_short_rows(tk.a, tk.b, seg, [&](int64_t c, bool act, int sl, int G) {
                 float z0 = INFINITY, z1 = -INFINITY;
                 if (act && sl < seg) {   // G >= seg: one element per lane
-                    float* p = R.w2 + c * seg + sl;
+                    DFQ_GLOBAL float* p = (DFQ_GLOBAL float*)(R.w2 + c * seg + sl);
                     const float x = *p;
                     const float inv = cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).inv;
                     const float sn = cle_rel_scale(rels, N, mins, maxs, c, is_signed, eps, smin, smax).s;
@@ -606,7 +610,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             for_short_rows(tk.a, tk.b, seg, [&](int64_t c, bool act, int sl, int G) {
                 float vmin = INFINITY, vmax = -INFINITY;
                 if (act && sl < seg) {   // G >= seg: one element per lane
-                    float* p = R.w2 + c * seg + sl;
+                    DFQ_GLOBAL float* p = (DFQ_GLOBAL float*)(R.w2 + c * seg + sl);
                     const float x = *p;
                     const float y = x * cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).inv;
                     *p = y;
@@ -645,7 +649,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             for (int64_t c = tk.a + wv; c < tk.b; c += kThreads / 64) {
                 const float inv = cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax).inv;
                 const float sn = cle_rel_scale(rels, N, mins, maxs, c, is_signed, eps, smin, smax).s;
-                float* p = R.w2 + c * seg;
+                DFQ_GLOBAL float* p = (DFQ_GLOBAL float*)(R.w2 + c * seg);
                 float z0 = INFINITY, z1 = -INFINITY;
                 for (int64_t i = lane; i < seg; i += 64) {
                     const float y = p[i] * inv;
@@ -686,7 +690,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             const int64_t rowlen = R.i2 * R.khw2;
             const int ncol = (int)(tk.c1 - tk.c0);
             const int npos = ncol * khw;
-            float* base = R.w2 + tk.c0 * R.khw2;
+            DFQ_GLOBAL float* base = (DFQ_GLOBAL float*)(R.w2 + tk.c0 * R.khw2);
             const bool fuse = R.fuse_next >= 0;
             if (t < ncol)
                 inv_s[t] = cle_rel_scale(rels, R, mins, maxs, (tk.a / R.o2g) * R.i2 + tk.c0 + t, is_signed, eps, smin, smax).inv;
@@ -708,7 +712,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
 #pragma unroll
             for (int r = 0; r < kPosTileMaxRows; ++r) {
                 if (tk.a + r >= tk.b) break;   // uniform
-                float* rp = base + (tk.a + r) * rowlen;
+                DFQ_GLOBAL float* rp = base + (tk.a + r) * rowlen;
                 float lo = INFINITY, hi = -INFINITY;
 #pragma unroll
                 for (int m = 0; m < kTileMaxKhw; ++m)
@@ -758,7 +762,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                 float v[kColTileRows];
 #pragma unroll
                 for (int j = 0; j < kColTileRows; ++j)
-                    if (act && j < nr) v[j] = R.w2[(tk.a + j) * rowlen + i];
+                    if (act && j < nr) v[j] = ((DFQ_GLOBAL float*)R.w2)[(tk.a + j) * rowlen + i];
                 const float inv =
                     act ? cle_rel_scale(rels, R, mins, maxs, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin, smax).inv : 0.f;
 #pragma unroll
@@ -767,7 +771,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                         float y = __builtin_nanf("");
                         if (act) {
                             y = v[j] * inv;
-                            R.w2[(tk.a + j) * rowlen + i] = y;
+                            ((DFQ_GLOBAL float*)R.w2)[(tk.a + j) * rowlen + i] = y;
                         }
                         rows[j * kThreads + threadIdx.x] = y;
                     }
@@ -814,7 +818,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                             inv = cle_rel_scale(rels, R, mins, maxs, g * R.i2 + i, is_signed, eps, smin, smax).inv;
                             g_prev = g;
                         }
-                        float* p = R.w2 + o * rowlen + i * R.khw2;
+                        DFQ_GLOBAL float* p = (DFQ_GLOBAL float*)(R.w2 + o * rowlen + i * R.khw2);
                         for (int64_t k = 0; k < R.khw2; ++k) {
                             const float y = p[k] * inv;
                             p[k] = y;
@@ -851,14 +855,14 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                     float v[kColTileRows];
 #pragma unroll
                     for (int j = 0; j < kColTileRows; ++j)
-                        if (tk.a + j < tk.b) v[j] = R.w2[(tk.a + j) * rowlen + i];
+                        if (tk.a + j < tk.b) v[j] = ((DFQ_GLOBAL float*)R.w2)[(tk.a + j) * rowlen + i];
                     const float inv = cle_rel_scale(rels, R, mins, maxs, (tk.a / R.o2g) * R.i2 + i, is_signed, eps, smin,
                                                 smax).inv;
-                    R.w2[tk.a * rowlen + i] = v[0] * inv;
+                    ((DFQ_GLOBAL float*)R.w2)[tk.a * rowlen + i] = v[0] * inv;
                     DFQ_CLE_TL_MARK(0)   // the column's loads and its scale have landed
 #pragma unroll
                     for (int j = 1; j < kColTileRows; ++j)
-                        if (tk.a + j < tk.b) R.w2[(tk.a + j) * rowlen + i] = v[j] * inv;
+                        if (tk.a + j < tk.b) ((DFQ_GLOBAL float*)R.w2)[(tk.a + j) * rowlen + i] = v[j] * inv;
                     DFQ_CLE_TL_MARK(1)
                     continue;
                 }
@@ -870,7 +874,7 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                         inv = cle_rel_scale(rels, R, mins, maxs, g * R.i2 + i, is_signed, eps, smin, smax).inv;
                         g_prev = g;
                     }
-                    float* p = R.w2 + o * rowlen + i * R.khw2;
+                    DFQ_GLOBAL float* p = (DFQ_GLOBAL float*)(R.w2 + o * rowlen + i * R.khw2);
                     for (int64_t k = 0; k < R.khw2; ++k) p[k] = p[k] * inv;
                 }
             }
@@ -963,8 +967,8 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
         const CleUnit un = units[u];
         const CleChunk ch = chunks[un.chunk];
         const CleLayer Ly = layers[ch.layer];
-        const float* __restrict__ w = Ly.w + ch.c0;
-        float* __restrict__ sn = Ly.snap + ch.c0;
+        const DFQ_GLOBAL float* __restrict__ w = (const DFQ_GLOBAL float*)(Ly.w + ch.c0);
+        DFQ_GLOBAL float* __restrict__ sn = (DFQ_GLOBAL float*)(Ly.snap + ch.c0);
         const int64_t len = ch.len, sz = len / 32, vs = len / 8;
         const int64_t nb1 = sz / 256;
         const bool full = un.tile < nb1;
@@ -1095,7 +1099,9 @@ __device__ __forceinline__ float cle_chunk_sum_with(const CleChunk& ch, LdB1&& b
 }
 
 __device__ __forceinline__ float cle_chunk_sum(const CleChunk& ch, const float* b1, const float* tb, int lane) {
-    return cle_chunk_sum_with(ch, [&](int64_t i) { return ld_coh(b1 + i); }, [&](int64_t i) { return ld_coh(tb + i); },
+    const DFQ_GLOBAL float* g1 = (const DFQ_GLOBAL float*)b1;
+    const DFQ_GLOBAL float* gt = (const DFQ_GLOBAL float*)tb;
+    return cle_chunk_sum_with(ch, [g1](int64_t i) { return ld_coh(g1 + i); }, [gt](int64_t i) { return ld_coh(gt + i); },
                               lane);
 }
 
@@ -1114,7 +1120,8 @@ __device__ __forceinline__ float cle_tiny_chunk_sum(const CleLayer* __restrict__
 
 // numpy pairwise float64 sum (identity 0 + pairwise_sum), as np.sum(diff_list).
 // numpy's pairwise leaf: n <= 128 values, 8 accumulators.
-__device__ __forceinline__ double np_pairwise_leaf(const double* x, int64_t n) {
+template <class P>   // P: a typed (LDS / global) pointer to the values
+__device__ __forceinline__ double np_pairwise_leaf(P x, int64_t n) {
     if (n < 8) {
         double res = 0.;
         for (int64_t i = 0; i < n; ++i) res += x[i];
@@ -1143,7 +1150,8 @@ struct NpFrame {
 };
 constexpr int kNpFrames = 48;
 constexpr int kNpStackFloats = kNpFrames * (int)(sizeof(NpFrame) + sizeof(double)) / 4;
-__device__ double np_pairwise(const double* a, int64_t n, float* stack) {
+template <class P>
+__device__ double np_pairwise(P a, int64_t n, float* stack) {
     if (n <= 128) return 0. + np_pairwise_leaf(a, n);
     NpFrame* fr = reinterpret_cast<NpFrame*>(stack);
     double* acc = reinterpret_cast<double*>(fr + kNpFrames);
@@ -1196,22 +1204,29 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
     constexpr int kStateWords = (int)(sizeof(CleState) / 4);
     static_assert(sizeof(CleState) % 4 == 0, "CleState: whole 4-B words");
     const int64_t nps = (int64_t)nl * (S + 2);
+    DFQ_LDS float* pls = (DFQ_LDS float*)part_lds;   // typed: LDS / global accesses, not flat
     if (part_lds) {
         for (int64_t i = threadIdx.x; i < nps + kStateWords; i += blockDim.x) {
-            const float* src = i < nps ? part + i : reinterpret_cast<const float*>(st) + (i - nps);
-            part_lds[i] = kCoherent ? ld_coh(src) : *src;
+            const DFQ_GLOBAL float* src = (const DFQ_GLOBAL float*)(i < nps ? part + i
+                                                                           : reinterpret_cast<const float*>(st) + (i - nps));
+            pls[i] = kCoherent ? ld_coh(src) : *src;
         }
         __syncthreads();
-        part = part_lds;
     }
 #ifdef DFQ_DIAGNOSTICS
     if (tlm) tlm[2] = __builtin_amdgcn_s_memrealtime();
 #endif
-    double* m = nl <= 1024 ? sm : means;
+    DFQ_LDS double* ms = (DFQ_LDS double*)sm;
+    DFQ_GLOBAL double* mg = (DFQ_GLOBAL double*)means;
+    const bool m_lds = nl <= 1024;
+    double* m = m_lds ? sm : means;
+    // (generic pointers here: the typed two-path form spilled 48-60 B in the loop
+    // kernel; wave 0 has no stores outstanding at this point, so the flat loads
+    // cost no extra wait)
     for (int l = threadIdx.x; l < nl; l += blockDim.x) {
         // serial: sum = 0 + (0 + slot); two_pass_reduction: its S-slot buffer
         // (at::get_num_threads()) summed as a contiguous reduction
-        const float* pl = part + (int64_t)l * S;
+        const float* pl = (part_lds ? part_lds : part) + (int64_t)l * S;
         auto ld = [&](int64_t e) { return (part_lds || !kCoherent) ? pl[e] : ld_coh(pl + e); };
         const float* lm = part_lds ? part_lds + (int64_t)nl * S + 2 * l : nullptr;
         const bool serial = lm ? lm[1] != 0.f : layers[l].nt == 1;
@@ -1224,13 +1239,16 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
 #endif
     if (threadIdx.x == 0) {
         CleState s0;
-        if (part_lds) __builtin_memcpy(&s0, part_lds + nps, sizeof(CleState));
-        else s0 = *st;
+        if (part_lds) {
+            __builtin_memcpy(&s0, part_lds + nps, sizeof(CleState));
+        } else {
+            s0 = *st;
+        }
         double dt = 0.0;
         if constexpr (kLeafOnly) {
-            dt = nl > 0 ? 0. + np_pairwise_leaf(m, nl) : 0.0;
+            dt = nl > 0 ? 0. + (m_lds ? np_pairwise_leaf(ms, nl) : np_pairwise_leaf(mg, nl)) : 0.0;
         } else {
-            dt = nl > 0 ? np_pairwise(m, nl, np_stack) : 0.0;
+            dt = nl > 0 ? (m_lds ? np_pairwise(ms, nl, np_stack) : np_pairwise(mg, nl, np_stack)) : 0.0;
         }
         const int it = s0.iters;
         hist[it] = dt;
@@ -1428,8 +1446,10 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
             const int64_t nw = 32 * nb1;
             const bool staged = nw + kCleTailWords <= kCleTile;
             if (staged) {
-                for (int64_t i = threadIdx.x; i < nw; i += kThreads) lds[i] = ld_coh(gb1 + i);
-                if (threadIdx.x < kCleTailWords) lds[nw + threadIdx.x] = ld_coh(gtb + threadIdx.x);
+                DFQ_LDS float* ll = (DFQ_LDS float*)lds;
+                const DFQ_GLOBAL float* g1 = (const DFQ_GLOBAL float*)gb1;
+                for (int64_t i = threadIdx.x; i < nw; i += kThreads) ll[i] = ld_coh(g1 + i);
+                if (threadIdx.x < kCleTailWords) ll[nw + threadIdx.x] = ld_coh((const DFQ_GLOBAL float*)gtb + threadIdx.x);
             }
             __syncthreads();
             if (threadIdx.x < 64) {

@@ -372,12 +372,23 @@ __device__ inline float wave_inner_sum(Get get, int64_t n, int lane) {
 // the words one block hands to another inside a launch (CLE: level-1 sums, chunk
 // tails, chunk sums; the BC chain: every vector a later phase reads) without an
 // L2 write-back.
+// Address-space qualified pointers: a pointer loaded from a descriptor is generic
+// (flat loads / stores: both wait counters, no SGPR-base addressing, a 64-bit
+// VGPR address per access); cast to the space it lives in where that is known.
+#define DFQ_GLOBAL __attribute__((address_space(1)))
+#define DFQ_LDS __attribute__((address_space(3)))
+typedef float f32x4 __attribute__((ext_vector_type(4)));   // float4 without the class (loads through DFQ_GLOBAL)
+
 __device__ __forceinline__ void st_coh(float* p, float v) {
     __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ float ld_coh(const float* p) {
     return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ float ld_coh(const DFQ_GLOBAL float* p) {
+    return __uint_as_float(__hip_atomic_load((const DFQ_GLOBAL uint32_t*)p, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT));
 }
 

@@ -167,7 +167,6 @@ __device__ __forceinline__ void glds4(const float* g, float* lds_base) {
 // Stores through address_space(1) pointers: the descriptor fields are generic
 // pointers, and a flat_store also counts on lgkmcnt, so every LDS wait would
 // drain the wave's outstanding stores.  global_store_* does not.
-#define DFQ_GLOBAL __attribute__((address_space(1)))
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <bool NT, typename V>
 __device__ __forceinline__ void st(V* p, const V& v) {
