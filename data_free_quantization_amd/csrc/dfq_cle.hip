@@ -1537,6 +1537,7 @@ struct CleDeviceCtx {
     uint32_t* h_flag = nullptr;    // pinned, written by the stop rule: (iterations << 1) | done
     uint32_t* d_flag = nullptr;    // its device address
     hipEvent_t iev[4] = {};        // behind each iteration in flight (the host's pacing)
+    hipEvent_t iev_fenced[4] = {}; // the same with a system-scope fence (diagnostics A/B, DFQ_CLE_EV_FENCE)
     // Table pool: one plan at a time keeps its tables here (device + pinned upload
     // mirror), so a plan costs no hipMalloc / hipFree (hipFree waits for the whole
     // device) and its upload is an async DMA on the loop stream.
@@ -1575,8 +1576,17 @@ static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
         e = hipHostMalloc(&ctx.h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx.d_flag), ctx.h_flag, 0);
     }
+    // The pacing events only tell this thread how far the stream got (the loop's
+    // outcome comes through the pinned host word, the results after a stream
+    // synchronize): no system-scope fence when they are recorded -- a fenced
+    // marker writes the L2 back and invalidates it between two iterations.
+    // (DFQ_CLE_EV_FENCE=1: fenced, diagnostics A/B.)
     for (int i = 0; i < 4 && e == hipSuccess; ++i)
-        if (!ctx.iev[i]) e = hipEventCreateWithFlags(&ctx.iev[i], hipEventDisableTiming);
+        if (!ctx.iev[i]) e = hipEventCreateWithFlags(&ctx.iev[i], hipEventDisableTiming | hipEventDisableSystemFence);
+#ifdef DFQ_DIAGNOSTICS
+    for (int i = 0; i < 4 && e == hipSuccess; ++i)
+        if (!ctx.iev_fenced[i]) e = hipEventCreateWithFlags(&ctx.iev_fenced[i], hipEventDisableTiming);
+#endif
     if (e == hipSuccess && !ctx.pool_ev) e = hipEventCreateWithFlags(&ctx.pool_ev, hipEventDisableTiming);
     if (e == hipSuccess && !ctx.in_ev) e = hipEventCreateWithFlags(&ctx.in_ev, hipEventDisableTiming);
     return e;
@@ -2254,6 +2264,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     int32_t burst = 1;
     if (const char* b = ab_env("DFQ_CLE_BURST")) burst = std::max(1, std::min(2, atoi(b)));   // <= 3 in flight: 4 events
     int32_t fill = 0;   // iterations still to enqueue in the current burst
+    hipEvent_t* iev = ab_env("DFQ_CLE_EV_FENCE") ? ctx.iev_fenced : ctx.iev;
     if (!init.done) {
         int64_t polls = 0;
         int32_t ran = 0;   // iterations known complete (the pacing events)
@@ -2263,13 +2274,13 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             if (p->flag_every) {
                 ran = (int32_t)(f >> 1);
             } else {
-                while (ran < launched && hipEventQuery(ctx.iev[ran & 3]) == hipSuccess) ++ran;
+                while (ran < launched && hipEventQuery(iev[ran & 3]) == hipSuccess) ++ran;
             }
             if (launched < max_iters && (fill > 0 || launched - ran <= kCleAhead)) {
                 if (fill == 0) fill = burst;
                 const int rc = cle_enqueue_iteration(p, s, launched);
                 if (rc != DFQ_OK) return rc;
-                if (!p->flag_every) DFQ_HIP_CHECK(hipEventRecord(ctx.iev[launched & 3], s));
+                if (!p->flag_every) DFQ_HIP_CHECK(hipEventRecord(iev[launched & 3], s));
                 ++launched;
                 --fill;
                 continue;
