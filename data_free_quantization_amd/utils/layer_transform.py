@@ -43,15 +43,18 @@ def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d], *, ranges: Optio
     ``quantize_targ_layer(weight_ranges=...)`` right after (main_dfq.py:211-214:
     the second fold, whose factors are exactly 1, then only reads the weights)."""
     pairs = []
-    for layer_idx in graph:
-        if bottoms[layer_idx] is None:
+    targ = tuple(targ_type)
+    for layer_idx, bn in graph.items():   # BN nodes first: most nodes are not (the same pairs, in graph order)
+        if type(bn) is not nn.BatchNorm2d:
             continue
-        for bot_idx in bottoms[layer_idx]:
-            bn, layer = graph[layer_idx], graph[bot_idx]
-            if type(bn) != nn.BatchNorm2d or type(layer) not in targ_type:
-                continue
-            pairs.append((bn, layer))
-            break
+        bots = bottoms[layer_idx]
+        if bots is None:
+            continue
+        for bot_idx in bots:
+            layer = graph[bot_idx]
+            if type(layer) in targ:
+                pairs.append((bn, layer))
+                break
     if not pairs:
         return model
     # a layer feeding two BNs is folded twice in sequence by the reference: one
@@ -94,7 +97,7 @@ def _fold_batch(pairs, ranges=None):
         need = [j for j, row in enumerate(st) if row[1] is None]
         for j, z in zip(need, _carve([st[j][0].shape[0] for j in need], False, dev)):
             layer = pairs[j][1]
-            b = nn.Parameter(z, requires_grad=False)
+            b = torch.Tensor._make_subclass(nn.Parameter, z, False)   # nn.Parameter(z, requires_grad=False)
             if "bias" in layer._parameters:   # registered as None: what Module.__setattr__ would do
                 layer._parameters["bias"] = b
             else:
