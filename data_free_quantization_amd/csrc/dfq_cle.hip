@@ -1350,8 +1350,9 @@ union CleStepLds {
 
 // POS = false (no position-parallel 3x3 rescale tiles): capped at 128 VGPRs,
 // 4 waves per SIMD like the rescale body alone
-template <bool POS, bool NTS = false>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(POS ? 1 : 4)))
+// WPE > 0: that many waves per SIMD (diagnostics A/B, DFQ_CLE_POS_WPE)
+template <bool POS, bool NTS = false, int WPE = 0>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : (POS ? 1 : 4))))
 cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ atasks, int64_t a0, int64_t a1,
                      int64_t nab, uint32_t* __restrict__ rng, int64_t M, int is_signed, float eps, double smin,
                      double smax, const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
@@ -2111,12 +2112,13 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
 // j: the iteration's index in the run (its parity is j & 1).
 static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     // grid caps: 2,048 / 4,096 blocks (caps of 128-1,024 measured 4-150 % slower on MobileNetV2)
-    // step / tile grid caps (A/B: DFQ_CLE_STEP_GRID / DFQ_CLE_TILE_GRID, diagnostics library)
-    static const int64_t kStepGrid = [] {
+    // step / tile grid caps (A/B: DFQ_CLE_STEP_GRID / DFQ_CLE_TILE_GRID, diagnostics library;
+    // read per call, not cached: cle_ab.py switches them between runs of one process)
+    const int64_t kStepGrid = [] {
         const char* e = ab_env("DFQ_CLE_STEP_GRID");
         return e && *e ? std::max<int64_t>(1, atoll(e)) : int64_t(2048);
     }();
-    static const int64_t kTileGrid = [] {
+    const int64_t kTileGrid = [] {
         const char* e = ab_env("DFQ_CLE_TILE_GRID");
         return e && *e ? std::max<int64_t>(1, atoll(e)) : int64_t(4096);
     }();
@@ -2143,9 +2145,13 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         if (nab + ntb + nrb == 0) continue;
         F.last = last ? 1 : 0;
 #ifdef DFQ_DIAGNOSTICS
-        static const bool snap_nt = ab_env("DFQ_CLE_SNAP_NT") != nullptr;   // A/B: non-temporal snapshot stores
-        auto kern = (!last && p->step_pos[k]) ? (snap_nt ? cle_loop_step_kernel<true, true> : cle_loop_step_kernel<true>)
-                                              : (snap_nt ? cle_loop_step_kernel<false, true> : cle_loop_step_kernel<false>);
+        // read per launch (not cached): cle_ab.py switches them between runs of one process
+        const bool snap_nt = ab_env("DFQ_CLE_SNAP_NT") != nullptr;   // A/B: non-temporal snapshot stores
+        const bool pos_wpe3 = ab_env("DFQ_CLE_POS_WPE") != nullptr;  // A/B: POS steps at 3 waves / SIMD
+        auto kern = (!last && p->step_pos[k])
+                        ? (snap_nt ? cle_loop_step_kernel<true, true>
+                                   : pos_wpe3 ? cle_loop_step_kernel<true, false, 3> : cle_loop_step_kernel<true>)
+                        : (snap_nt ? cle_loop_step_kernel<false, true> : cle_loop_step_kernel<false>);
 #else
         auto kern = (!last && p->step_pos[k]) ? cle_loop_step_kernel<true> : cle_loop_step_kernel<false>;
 #endif
