@@ -406,7 +406,7 @@ struct BnFoldChunk {
 // The fold factor of row o (bn_factor), without the divide and square root for
 // an identity BatchNorm (weight 1, var + eps == 1: the factor is exactly 1).
 __device__ __forceinline__ float fold_factor(const BnFoldJob& J, int64_t o) {
-    const float go = J.g[o], ve = J.v[o] + J.eps;
+    const float go = ((const DFQ_GLOBAL float*)J.g)[o], ve = ((const DFQ_GLOBAL float*)J.v)[o] + J.eps;
     return (go == 1.0f && ve == 1.0f) ? 1.0f : go / sqrtf(ve);
 }
 
@@ -457,10 +457,10 @@ bn_fold_weight_batch_kernel(const BnFoldJob* __restrict__ jobs, const BnFoldChun
             ident &= fold_factor(J, r) == 1.0f;
         ident = __syncthreads_and(ident);
         if (ident && (reinterpret_cast<uintptr_t>(J.w + ch.e0) & 15) == 0) {
-            const float4* w4 = reinterpret_cast<const float4*>(J.w + ch.e0);
+            const DFQ_GLOBAL f32x4* w4 = (const DFQ_GLOBAL f32x4*)(J.w + ch.e0);   // global, not flat
             const int64_t n4 = n >> 2;
             for (int64_t k = threadIdx.x; k < n4; k += 4 * (int64_t)blockDim.x) {
-                float4 v[4];
+                f32x4 v[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     if (k + u * (int64_t)blockDim.x < n4) v[u] = w4[k + u * blockDim.x];
@@ -473,12 +473,12 @@ bn_fold_weight_batch_kernel(const BnFoldJob* __restrict__ jobs, const BnFoldChun
             }
             done = 4 * n4;
         } else if ((reinterpret_cast<uintptr_t>(J.w + ch.e0) & 15) == 0) {   // 16-B groups
-            float4* w4 = reinterpret_cast<float4*>(J.w + ch.e0);
+            DFQ_GLOBAL f32x4* w4 = (DFQ_GLOBAL f32x4*)(J.w + ch.e0);
             const int64_t n4 = n >> 2;
             for (int64_t k = threadIdx.x; k < n4; k += blockDim.x) {
-                const float4 v = w4[k];
+                const f32x4 v = w4[k];
                 const int64_t i = ch.e0 + 4 * k;
-                float4 o;
+                f32x4 o;
                 int rem;
                 const float f = fold_factor(J, fold_row(J, r0, base, inv, i, &rem));
                 if (rem + 3 < (int)J.row_len) {   // the 4 elements share a row: one factor
@@ -500,11 +500,12 @@ bn_fold_weight_batch_kernel(const BnFoldJob* __restrict__ jobs, const BnFoldChun
             }
             done = 4 * n4;
         }
+        DFQ_GLOBAL float* wg = (DFQ_GLOBAL float*)J.w;
         for (int64_t k = done + threadIdx.x; k < n; k += blockDim.x) {
             const int64_t i = ch.e0 + k;
-            const float v = J.w[i];
+            const float v = wg[i];
             const float o = fold_one(J, r0, base, inv, i, v);
-            if (__float_as_uint(o) != __float_as_uint(v)) J.w[i] = o;
+            if (__float_as_uint(o) != __float_as_uint(v)) wg[i] = o;
             a = fminf(a, o);
             b = fmaxf(b, o);
         }
@@ -535,19 +536,21 @@ bn_fold_weight_batch_kernel(const BnFoldJob* __restrict__ jobs, const BnFoldChun
 __global__ void bn_fold_channel_batch_kernel(const BnFoldJob* __restrict__ jobs, int32_t njobs) {
     for (int32_t j = blockIdx.x; j < njobs; j += gridDim.x) {
         const BnFoldJob J = jobs[j];
+        typedef DFQ_GLOBAL float* G;   // global, not flat
+        const G g = (G)J.g, b = (G)J.b, m = (G)J.m, v = (G)J.v, bias = (G)J.bias, fw = (G)J.fake_w, fb = (G)J.fake_b;
         for (int64_t o = threadIdx.x; o < J.rows; o += blockDim.x) {
-            const float go = J.g[o], bo = J.b[o], mo = J.m[o], vo = J.v[o];
+            const float go = g[o], bo = b[o], mo = m[o], vo = v[o];
             const float f = bn_factor(go, vo, J.eps);
             const float shift = bo - (go * mo) / sqrtf(vo + J.eps);
             // a layer without a bias gets torch.zeros first (layer_transform.py:262-263)
-            const float b0 = (J.flags & DFQ_BN_FOLD_ZERO_BIAS) ? 0.0f : J.bias[o];
-            J.bias[o] = b0 * f + shift;
-            if (J.fake_w) J.fake_w[o] = fabsf(go);
-            if (J.fake_b) J.fake_b[o] = bo;
-            J.g[o] = 1.0f;
-            J.v[o] = 1.0f;
-            J.b[o] = 0.0f;
-            J.m[o] = 0.0f;
+            const float b0 = (J.flags & DFQ_BN_FOLD_ZERO_BIAS) ? 0.0f : bias[o];
+            bias[o] = b0 * f + shift;
+            if (J.fake_w) fw[o] = fabsf(go);
+            if (J.fake_b) fb[o] = bo;
+            g[o] = 1.0f;
+            v[o] = 1.0f;
+            b[o] = 0.0f;
+            m[o] = 0.0f;
         }
     }
 }
