@@ -702,13 +702,16 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
             // Every row's loads in flight together, then the rows' scaled stores:
             // one memory round trip per tile instead of one per row (~5 us a row
             // under the step's load, ResNet-50's 3x3 tiles; DFQ_CLE_TL)
+            // (row bases uniform, the lane's offset a 32-bit index: SGPR-base loads
+            // sharing one VGPR offset, not 36 64-bit VGPR addresses)
             float v[kPosTileMaxRows][kTileMaxKhw];
 #pragma unroll
-            for (int r = 0; r < kPosTileMaxRows; ++r)
+            for (int r = 0; r < kPosTileMaxRows; ++r) {
+                const DFQ_GLOBAL float* rb = base + (tk.a + r) * rowlen;
 #pragma unroll
                 for (int m = 0; m < kTileMaxKhw; ++m)
-                    if (tk.a + r < tk.b && m < khw && t + kThreads * m < npos)
-                        v[r][m] = base[(tk.a + r) * rowlen + t + kThreads * m];
+                    if (tk.a + r < tk.b && m < khw && t + kThreads * m < npos) v[r][m] = rb[t + kThreads * m];
+            }
 #pragma unroll
             for (int r = 0; r < kPosTileMaxRows; ++r) {
                 if (tk.a + r >= tk.b) break;   // uniform
