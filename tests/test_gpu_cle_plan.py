@@ -343,3 +343,42 @@ def test_async_caller_released_at_convergence(monkeypatch):
         assert torch.equal(ref[k].view(torch.int32), clones[k].view(torch.int32)), k
     cle.wait()
     assert cle.LAST_RUN["launched"]
+
+
+def _many_layer_graph(n_chains, seed=5):
+    """n_chains independent 3-layer 1x1 chains (8 channels, 64-weight layers):
+    3 * n_chains target layers, 2 * n_chains relations."""
+    from data_free_quantization_amd.utils.relation import Relation
+    rng = np.random.default_rng(seed)
+    g = OrderedDict()
+    g["Data"] = "Data"
+    rels = []
+    for c in range(n_chains):
+        g[f"x{c}a"] = _conv(8, 8, 1, rng=rng)
+        g[f"x{c}abn"] = _BN(8, rng)
+        g[f"x{c}b"] = _conv(8, 8, 1, rng=rng)
+        g[f"x{c}bbn"] = _BN(8, rng)
+        g[f"x{c}c"] = _conv(8, 8, 1, rng=rng)
+        rels += [Relation(f"x{c}a", f"x{c}b", f"x{c}abn"), Relation(f"x{c}b", f"x{c}c", f"x{c}bbn")]
+    return g, rels
+
+
+@pytest.mark.parametrize("n_chains", [47, 240])
+def test_device_cle_many_layers(n_chains, monkeypatch):
+    """Past numpy's one-leaf pairwise sum (> 128 layer means: the stop rule's frame
+    stack) and, at 720 layers, past the stop rule's LDS staging of the chunk sums,
+    layer sizes and state (the per-layer loads fallback): diffs, weights, biases and
+    scales bit-exact with the oracle replay."""
+    from data_free_quantization_amd import Cross_layer_equal as cle
+    monkeypatch.setenv("DFQ_CLE_MODE", "device")
+    g, rels = _many_layer_graph(n_chains)
+    W, B, BN, S, diffs = _replay(g, rels, (1e-8, 1e8), 1e-3, 20, False, 0.0)
+    cle.cross_layer_equalization(g, rels, [nn.Conv2d, nn.Linear], Treshhold=1e-3, Save_state=False)
+    torch.cuda.synchronize()
+    assert cle.LAST_RUN["chains"] == n_chains
+    assert cle.LAST_RUN["diffs"] == diffs
+    for k in W:
+        assert np.array_equal(g[k].weight.detach().cpu().numpy(), W[k]), k
+        assert np.array_equal(g[k].bias.detach().cpu().numpy(), B[k]), k
+    for i, r in enumerate(rels):
+        assert np.array_equal(r.S.cpu().numpy(), S[i]), i
