@@ -1353,9 +1353,10 @@ union CleStepLds {
 
 // POS = false (no position-parallel 3x3 rescale tiles): capped at 128 VGPRs,
 // 4 waves per SIMD like the rescale body alone
-// WPE > 0: that many waves per SIMD (diagnostics A/B, DFQ_CLE_POS_WPE)
-template <bool POS, bool NTS = false, int WPE = 0>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : (POS ? 1 : 4))))
+// (POS capped at 3 waves per SIMD -- 168 VGPRs, 124 B of spills -- measured slower:
+// profiles/r04/cle_ab_r04t.jsonl)
+template <bool POS, bool NTS = false>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(POS ? 1 : 4)))
 cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ atasks, int64_t a0, int64_t a1,
                      int64_t nab, uint32_t* __restrict__ rng, int64_t M, int is_signed, float eps, double smin,
                      double smax, const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
@@ -1541,7 +1542,6 @@ struct CleDeviceCtx {
     uint32_t* h_flag = nullptr;    // pinned, written by the stop rule: (iterations << 1) | done
     uint32_t* d_flag = nullptr;    // its device address
     hipEvent_t iev[4] = {};        // behind each iteration in flight (the host's pacing)
-    hipEvent_t iev_fenced[4] = {}; // the same with a system-scope fence (diagnostics A/B, DFQ_CLE_EV_FENCE)
     // Table pool: one plan at a time keeps its tables here (device + pinned upload
     // mirror), so a plan costs no hipMalloc / hipFree (hipFree waits for the whole
     // device) and its upload is an async DMA on the loop stream.
@@ -1582,15 +1582,10 @@ static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
     }
     // The pacing events only tell this thread how far the stream got (the loop's
     // outcome comes through the pinned host word, the results after a stream
-    // synchronize): no system-scope fence when they are recorded -- a fenced
-    // marker writes the L2 back and invalidates it between two iterations.
-    // (DFQ_CLE_EV_FENCE=1: fenced, diagnostics A/B.)
+    // synchronize): recorded without a system-scope fence.  (Fenced, they measured
+    // the same: profiles/r04/cle_ab_r04t.jsonl.)
     for (int i = 0; i < 4 && e == hipSuccess; ++i)
         if (!ctx.iev[i]) e = hipEventCreateWithFlags(&ctx.iev[i], hipEventDisableTiming | hipEventDisableSystemFence);
-#ifdef DFQ_DIAGNOSTICS
-    for (int i = 0; i < 4 && e == hipSuccess; ++i)
-        if (!ctx.iev_fenced[i]) e = hipEventCreateWithFlags(&ctx.iev_fenced[i], hipEventDisableTiming);
-#endif
     if (e == hipSuccess && !ctx.pool_ev) e = hipEventCreateWithFlags(&ctx.pool_ev, hipEventDisableTiming);
     if (e == hipSuccess && !ctx.in_ev) e = hipEventCreateWithFlags(&ctx.in_ev, hipEventDisableTiming);
     return e;
@@ -2150,11 +2145,8 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
 #ifdef DFQ_DIAGNOSTICS
         // read per launch (not cached): cle_ab.py switches them between runs of one process
         const bool snap_nt = ab_env("DFQ_CLE_SNAP_NT") != nullptr;   // A/B: non-temporal snapshot stores
-        const bool pos_wpe3 = ab_env("DFQ_CLE_POS_WPE") != nullptr;  // A/B: POS steps at 3 waves / SIMD
-        auto kern = (!last && p->step_pos[k])
-                        ? (snap_nt ? cle_loop_step_kernel<true, true>
-                                   : pos_wpe3 ? cle_loop_step_kernel<true, false, 3> : cle_loop_step_kernel<true>)
-                        : (snap_nt ? cle_loop_step_kernel<false, true> : cle_loop_step_kernel<false>);
+        auto kern = (!last && p->step_pos[k]) ? (snap_nt ? cle_loop_step_kernel<true, true> : cle_loop_step_kernel<true>)
+                                              : (snap_nt ? cle_loop_step_kernel<false, true> : cle_loop_step_kernel<false>);
 #else
         auto kern = (!last && p->step_pos[k]) ? cle_loop_step_kernel<true> : cle_loop_step_kernel<false>;
 #endif
@@ -2273,7 +2265,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     int32_t burst = 1;
     if (const char* b = ab_env("DFQ_CLE_BURST")) burst = std::max(1, std::min(2, atoi(b)));   // <= 3 in flight: 4 events
     int32_t fill = 0;   // iterations still to enqueue in the current burst
-    hipEvent_t* iev = ab_env("DFQ_CLE_EV_FENCE") ? ctx.iev_fenced : ctx.iev;
+    hipEvent_t* iev = ctx.iev;
     if (!init.done) {
         int64_t polls = 0;
         int32_t ran = 0;   // iterations known complete (the pacing events)

@@ -23,8 +23,7 @@ os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_HOST_RELEASE",
             "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY",
-            "DFQ_CLE_FLAG_EVERY", "CLE_AB_BLOCKING", "DFQ_CLE_SNAP_NT", "DFQ_CLE_BURST",
-            "DFQ_CLE_EV_FENCE", "DFQ_CLE_POS_WPE")
+            "DFQ_CLE_FLAG_EVERY", "CLE_AB_BLOCKING", "DFQ_CLE_SNAP_NT", "DFQ_CLE_BURST")
 CONFIGS = {
     "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
@@ -38,8 +37,6 @@ CONFIGS = {
     "flag_every": {"DFQ_CLE_FLAG_EVERY": "1"},      # the stop rule's host word every iteration (the host paces by it)
     "blocking": {"CLE_AB_BLOCKING": "1"},           # run_dfq's CLE blocking (no caller gate beside the loop)
     "snap_nt": {"DFQ_CLE_SNAP_NT": "1"},            # the metric tiles' snapshot stores non-temporal
-    "ev_fence": {"DFQ_CLE_EV_FENCE": "1"},          # the pacing events with a system-scope fence (before r04s)
-    "pos_wpe3": {"DFQ_CLE_POS_WPE": "3"},           # position-tile steps capped at 168 VGPRs (3 waves / SIMD)
     "burst2": {"DFQ_CLE_BURST": "2"},               # the host tops the queue up by two iterations at a time
 }
 
