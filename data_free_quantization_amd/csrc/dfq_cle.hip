@@ -1270,9 +1270,10 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         st->diff = diff;
         st->done = done;
         // the host's copy of the stop rule (pinned host memory; a system-scope
-        // vector store), written when the loop stops: the loop's host side polls it
-        // (cle_run_locked).  (Written every iteration instead, DFQ_CLE_FLAG_EVERY=1,
-        // it measured the same.)
+        // vector store), written every iteration: the loop's host side polls it for
+        // the stop and paces its enqueue by it (cle_run_locked).  flag_every = 0
+        // (diagnostics, DFQ_CLE_EVENT_PACING=1): written at the stop only, the host
+        // paced by an event behind each iteration instead.
         if (hflag && (done || flag_every))
             __hip_atomic_store(hflag, ((uint32_t)(it + 1) << 1) | (uint32_t)done, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1322,7 +1323,7 @@ struct CleFin {
     uint32_t* hflag;         // pinned host word: (iterations << 1) | done, or null
     uint64_t* sig;           // a launched run: the caller's gate word and the generation
     uint64_t gen;            // that releases it at convergence (else null)
-    int32_t flag_every;      // hflag written every iteration (diagnostics), else at the stop
+    int32_t flag_every;      // hflag written every iteration (else at the stop: event pacing, diagnostics)
 };
 
 // The launches of one iteration.  Launch k < steps runs the rescale tasks of
@@ -1492,7 +1493,7 @@ struct dfq_cle_plan {
     uint32_t* d_flag = nullptr;     // the stop rule's host word (the device context's, set by run)
     uint64_t* d_sig = nullptr;      // a launched run: the caller's gate word and its generation
     uint64_t gen = 0;
-    int32_t flag_every = 0;         // the stop rule's host word every iteration (diagnostics)
+    int32_t flag_every = 1;         // the stop rule's host word every iteration (0: event pacing, diagnostics)
     hipStream_t st = nullptr;       // the loop's stream (the device context's)
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
     std::vector<char> step_pos;          // per step: position-parallel W2 tiles (the POS rescale kernel)
@@ -2247,19 +2248,22 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
         DFQ_HIP_CHECK(hipStreamSynchronize(s));
     }
 #endif
-    // Iteration by iteration, kCleAhead of them queued behind the running one (an
-    // event behind each iteration paces this thread); the stop rule writes
-    // (iterations << 1) | done into pinned host memory when the loop stops
-    // (ctx.h_flag, a system-scope store), and this thread polls that word -- no
-    // copy or host round trip sits between two iterations on the loop stream, and
-    // at convergence at most kCleAhead iterations are left to run as no-ops.  (Round 3 enqueued batches of 4 iterations a batch ahead and read
+    // Iteration by iteration, kCleAhead of them queued behind the running one; the
+    // stop rule writes (iterations << 1) | done into pinned host memory every
+    // iteration (ctx.h_flag, a system-scope store), and this thread polls that word
+    // both for the stop and for its pacing -- no copy or host round trip sits
+    // between two iterations on the loop stream, and at convergence at most
+    // kCleAhead iterations are left to run as no-ops.  (An event recorded behind
+    // each iteration for the pacing instead, DFQ_CLE_EVENT_PACING=1: its marker
+    // packet added ~3.7 us before every iteration's first launch, MobileNetV2
+    // 3.51 vs 3.37 ms, profiles/r04/cle_trace_r04v_*, cle_ab_r04v.jsonl.)  (Round 3 enqueued batches of 4 iterations a batch ahead and read
     // the state back per batch; replaying a batch as a captured HIP graph
     // measured slower, profiles/r03/cle_ab_p.jsonl.)  A stream that drains
     // without the word saying done (a kernel error) ends the polling; the final
     // state read below decides.
     const double tc1 = now_us();
     int32_t launched = 0;
-    p->flag_every = ab_env("DFQ_CLE_FLAG_EVERY") != nullptr;
+    p->flag_every = ab_env("DFQ_CLE_EVENT_PACING") == nullptr;
     // diagnostics A/B: once the queue is down to kCleAhead iterations, top it up by
     // `burst` (the host's enqueue then meets fewer iteration boundaries)
     int32_t burst = 1;
@@ -2268,7 +2272,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     hipEvent_t* iev = ctx.iev;
     if (!init.done) {
         int64_t polls = 0;
-        int32_t ran = 0;   // iterations known complete (the pacing events)
+        int32_t ran = 0;   // iterations known complete (the host word; the events under DFQ_CLE_EVENT_PACING)
         for (;;) {
             const uint32_t f = __atomic_load_n(ctx.h_flag, __ATOMIC_ACQUIRE);
             if (f & 1u) break;
