@@ -2269,6 +2269,8 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     int32_t burst = 1;
     if (const char* b = ab_env("DFQ_CLE_BURST")) burst = std::max(1, std::min(2, atoi(b)));   // <= 3 in flight: 4 events
     int32_t fill = 0;   // iterations still to enqueue in the current burst
+    int32_t ahead = kCleAhead;   // diagnostics A/B: DFQ_CLE_AHEAD (1-3; events: 4 in flight at most)
+    if (const char* a = ab_env("DFQ_CLE_AHEAD")) ahead = std::max(1, std::min(p->flag_every ? 3 : 2, atoi(a)));
     hipEvent_t* iev = ctx.iev;
     if (!init.done) {
         int64_t polls = 0;
@@ -2281,7 +2283,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             } else {
                 while (ran < launched && hipEventQuery(iev[ran & 3]) == hipSuccess) ++ran;
             }
-            if (launched < max_iters && (fill > 0 || launched - ran <= kCleAhead)) {
+            if (launched < max_iters && (fill > 0 || launched - ran <= ahead)) {
                 if (fill == 0) fill = burst;
                 const int rc = cle_enqueue_iteration(p, s, launched);
                 if (rc != DFQ_OK) return rc;

@@ -23,7 +23,8 @@ os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_HOST_RELEASE",
             "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY",
-            "DFQ_CLE_EVENT_PACING", "CLE_AB_BLOCKING", "DFQ_CLE_SNAP_NT", "DFQ_CLE_BURST")
+            "DFQ_CLE_EVENT_PACING", "CLE_AB_BLOCKING", "DFQ_CLE_SNAP_NT", "DFQ_CLE_BURST",
+            "DFQ_CLE_AHEAD")
 CONFIGS = {
     "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
@@ -35,6 +36,8 @@ CONFIGS = {
     "ranges_early": {"DFQ_CLE_RANGES_EARLY": "1"},  # only the range tasks early
     "units_early": {"DFQ_CLE_TILES_EARLY": "1"},    # only the metric tiles early
     "event_pacing": {"DFQ_CLE_EVENT_PACING": "1"},  # the host paced by an event per iteration (before r04w)
+    "ahead2": {"DFQ_CLE_AHEAD": "2"},               # two iterations queued behind the running one
+    "ahead3": {"DFQ_CLE_AHEAD": "3"},
     "blocking": {"CLE_AB_BLOCKING": "1"},           # run_dfq's CLE blocking (no caller gate beside the loop)
     "snap_nt": {"DFQ_CLE_SNAP_NT": "1"},            # the metric tiles' snapshot stores non-temporal
     "burst2": {"DFQ_CLE_BURST": "2"},               # the host tops the queue up by two iterations at a time
