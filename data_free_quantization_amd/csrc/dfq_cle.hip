@@ -956,11 +956,11 @@ struct CleNoUnitHook {
     __device__ void operator()(const CleUnit&, const CleChunk&, int64_t) const {}
 };
 
-// hook(unit, chunk, nb1) runs after each unit (LDS free again).  NT: the snapshot
-// stores non-temporal (diagnostics A/B, DFQ_CLE_SNAP_NT).  (The snapshot stores
-// issued after the unit's arrival instead -- out of the arrival's vmcnt(0) drain --
-// measured no faster and the tiles slower, 84 B of spills: profiles/r04/cle_ab_r04p.)
-template <class Hook = CleNoUnitHook, bool NT = false>
+// hook(unit, chunk, nb1) runs after each unit (LDS free again).  (Tried on the
+// snapshot stores: issued after the unit's arrival -- out of the arrival's
+// vmcnt(0) drain -- no faster, tiles slower, 84 B of spills (cle_ab_r04p);
+// non-temporal, the same (cle_ab_r04z).)
+template <class Hook = CleNoUnitHook>
 __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
                                                const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units,
                                                int64_t nunits, float* __restrict__ b1buf, float* __restrict__ tailbuf,
@@ -1002,8 +1002,7 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     a += fabsf(xs[h][j] - ys[h][j]);
-                    if constexpr (NT) __builtin_nontemporal_store(xs[h][j], &sn[base + 32 * j]);
-                    else sn[base + 32 * j] = xs[h][j];
+                    sn[base + 32 * j] = xs[h][j];
                 }
                 b0[q] = a;   // b0[m * 32 + s]
             }
@@ -1027,8 +1026,7 @@ __device__ __forceinline__ void cle_tiles_body(const CleLayer* __restrict__ laye
                 for (int u = 0; u < 8; ++u)
                     if (e + u * kThreads < cnt) {
                         d[e + u * kThreads] = fabsf(x[u] - y[u]);
-                        if constexpr (NT) __builtin_nontemporal_store(x[u], &sn[e0 + e + u * kThreads]);
-                        else sn[e0 + e + u * kThreads] = x[u];
+                        sn[e0 + e + u * kThreads] = x[u];
                     }
             }
             __syncthreads();
@@ -1356,7 +1354,7 @@ union CleStepLds {
 // 4 waves per SIMD like the rescale body alone
 // (POS capped at 3 waves per SIMD -- 168 VGPRs, 124 B of spills -- measured slower:
 // profiles/r04/cle_ab_r04t.jsonl)
-template <bool POS, bool NTS = false>
+template <bool POS>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(POS ? 1 : 4)))
 cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ atasks, int64_t a0, int64_t a1,
                      int64_t nab, uint32_t* __restrict__ rng, int64_t M, int is_signed, float eps, double smin,
@@ -1467,7 +1465,7 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         }
         if (arrive(F.cnt + F.nchunks, fin_members)) finish();   // the iteration's last arrival
     };
-    cle_tiles_body<decltype(hook), NTS>(layers, chunks, b1off, units + u0, u1 - u0, b1buf, tailbuf, blk - nab, ntb, lds,
+    cle_tiles_body<decltype(hook)>(layers, chunks, b1off, units + u0, u1 - u0, b1buf, tailbuf, blk - nab, ntb, lds,
                    lds + kCleTile + kCleTailWords, hook);
     tl2_rec(1);
 }
@@ -2143,14 +2141,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         const int64_t nrb = std::min<int64_t>(r1 - r0, kStepGrid);
         if (nab + ntb + nrb == 0) continue;
         F.last = last ? 1 : 0;
-#ifdef DFQ_DIAGNOSTICS
-        // read per launch (not cached): cle_ab.py switches them between runs of one process
-        const bool snap_nt = ab_env("DFQ_CLE_SNAP_NT") != nullptr;   // A/B: non-temporal snapshot stores
-        auto kern = (!last && p->step_pos[k]) ? (snap_nt ? cle_loop_step_kernel<true, true> : cle_loop_step_kernel<true>)
-                                              : (snap_nt ? cle_loop_step_kernel<false, true> : cle_loop_step_kernel<false>);
-#else
         auto kern = (!last && p->step_pos[k]) ? cle_loop_step_kernel<true> : cle_loop_step_kernel<false>;
-#endif
         hipLaunchKernelGGL(kern, dim3((int)(nab + ntb + nrb)), dim3(kThreads), 0, s, p->d_rels, p->d_atasks, a0, a1, nab,
                            p->d_rng, p->M, p->is_signed, p->eps, p->smin, p->smax, p->d_layers, p->d_chunks,
                            p->d_b1off, p->d_units, u0, u1, ntb, p->d_b1, p->d_tail, p->d_rtasks, r0, r1, F, p->d_state,

@@ -23,7 +23,7 @@ os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_HOST_RELEASE",
             "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY",
-            "DFQ_CLE_EVENT_PACING", "CLE_AB_BLOCKING", "DFQ_CLE_SNAP_NT", "DFQ_CLE_BURST",
+            "DFQ_CLE_EVENT_PACING", "CLE_AB_BLOCKING", "DFQ_CLE_BURST",
             "DFQ_CLE_AHEAD")
 CONFIGS = {
     "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
@@ -39,7 +39,6 @@ CONFIGS = {
     "ahead2": {"DFQ_CLE_AHEAD": "2"},               # two iterations queued behind the running one
     "ahead3": {"DFQ_CLE_AHEAD": "3"},
     "blocking": {"CLE_AB_BLOCKING": "1"},           # run_dfq's CLE blocking (no caller gate beside the loop)
-    "snap_nt": {"DFQ_CLE_SNAP_NT": "1"},            # the metric tiles' snapshot stores non-temporal
     "burst2": {"DFQ_CLE_BURST": "2"},               # the host tops the queue up by two iterations at a time
 }
 
