@@ -2651,6 +2651,7 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
     } catch (...) {
     }
     if (!posted) body(a);   // no worker: run on this thread (blocking), which also releases
+    if (cle_timing()) fprintf(stderr, "DFQ_CLE_TIMING launch: total %.1f us\n", now_us() - tl0);
     return DFQ_OK;
 }
 
