@@ -108,7 +108,8 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    if path is None and os.environ.get("DFQ_LIB") == "diag":
+    by_env = path is None and os.environ.get("DFQ_LIB") == "diag"
+    if by_env:
         path = DIAG_LIB_PATH
     p = Path(path) if path else LIB_PATH
     if not p.exists():
@@ -180,8 +181,8 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
             fn.restype = res
     if L.dfq_abi_version() != 1:
         raise DFQLibraryError("libdfq_hip.so ABI version mismatch")
-    if path is None:
-        _LIB = L
+    if path is None or by_env:   # the process's library (the diagnostics one under DFQ_LIB=diag):
+        _LIB = L                 # cached -- loaded and typed per call it cost ~0.1 ms a call
     return L
 
 
