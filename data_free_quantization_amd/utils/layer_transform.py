@@ -13,6 +13,9 @@ Graph/bottoms follow SURVEY.md 8b.  Target tensors must be on a ROCm device.
 from __future__ import annotations
 
 import ctypes as C
+import os
+import sys
+import time
 from collections.abc import Mapping
 import types
 from typing import Dict, Optional
@@ -82,7 +85,11 @@ _BN_DESC = np.dtype([("ptr", "<u8", (8,)), ("eps", "<f4"), ("flags", "<i4"), ("r
 assert _BN_DESC.itemsize == C.sizeof(_lib.BnFoldDesc)
 
 
+_BN_TIMING = bool(os.environ.get("DFQ_BN_TIMING"))   # host-side split of the fold (stderr)
+
+
 def _fold_batch(pairs, ranges=None):
+    tb = [time.perf_counter()] if _BN_TIMING else None
     with torch.no_grad():
         # module state straight from the parameter / buffer dicts: Module.__getattr__
         # on every access was most of this function's host time
@@ -104,6 +111,8 @@ def _fold_batch(pairs, ranges=None):
                 layer.bias = b
             st[j] = (st[j][0], b) + st[j][2:]
         fresh = set(need)
+        if tb:
+            tb.append(time.perf_counter())
         n = len(pairs)
         fakes = _carve([row[2].numel() for row in st] * 2, False, dev)
         tab = np.zeros(n, dtype=_BN_DESC)
@@ -114,6 +123,8 @@ def _fold_batch(pairs, ranges=None):
             buf["fake_weight"], buf["fake_bias"] = fw, fb
             rows.append((w.data_ptr(), b.data_ptr(), g.data_ptr(), beta.data_ptr(), mean.data_ptr(), var.data_ptr(),
                          fw.data_ptr(), fb.data_ptr()))
+        if tb:
+            tb.append(time.perf_counter())
         tab["ptr"] = np.array(rows, dtype=np.uint64)
         tab["eps"] = [float(bn.eps) for bn, _ in pairs]
         if fresh:
@@ -132,11 +143,20 @@ def _fold_batch(pairs, ranges=None):
         if nb < 0:
             raise RuntimeError("dfq_bn_fold_ws_bytes: invalid layer shapes")
         ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=dev)   # stream-ordered (caching allocator)
+        if tb:
+            tb.append(time.perf_counter())
         rc = L.dfq_bn_fold_batch(descs, n, ws.data_ptr(), ws.numel(), _lib.stream_of(st[0][0]))
         _lib.check(rc, "dfq_bn_fold_batch")
+        if tb:
+            tb.append(time.perf_counter())
         for bn, _ in pairs:
             bn.__dict__["eps"] = 0   # plain attributes: what Module.__setattr__ ends in
             _identity_forward(bn)
+        if tb:
+            tb.append(time.perf_counter())
+            print("DFQ_BN_TIMING fold x%d: tensors + biases %.1f us, fakes + rows %.1f us, tables + workspace "
+                  "%.1f us, call %.1f us, identity BNs %.1f us" % ((len(pairs),) + tuple(
+                      (b - a) * 1e6 for a, b in zip(tb, tb[1:]))), file=sys.stderr)
 
 
 _TINY = float(torch.finfo(torch.float32).tiny)
