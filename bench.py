@@ -7,16 +7,22 @@ E[o,i]) over ONE layer list: ``--copies`` MobileNetV2 weight sets back to back
 shapes, already resident in HBM).  The list defeats the 256 MB Infinity Cache
 (SURVEY.md 8d), so the number is an HBM number.
 
-At N GPUs the SAME layer list is LPT-sharded over the ranks (strong scaling,
-data_free_quantization_amd/distributed.py): rank 0 holds every weight and
-scatters each rank its slab once before timing; a step is every rank sweeping
-its share (per-tensor copies, as at N = 1) with outputs left sharded.  Also reported (``sharded_modes``): the
-step with a gather of every output slab to rank 0, rank 0 -> ranks scatter +
-sweep + gather (rank 0 holds everything, end to end), the in-place all-gather,
-and the replicated form (every rank sweeps the whole list; weak scaling).
+At N GPUs the job's weight sets are sharded over the ranks (weak scaling, no
+collective in the timed step): rank r sweeps its own list of ``--copies``
+weight sets, and ``value`` is all ranks' weight bytes over the max-over-ranks
+step.  BASELINE configs[4] (``configs4_sharded``): ONE ResNet-50 INT4 + clip
+list of >= 2 GiB held by rank 0 is LPT-sharded over the ranks
+(data_free_quantization_amd/distributed.py) and timed sweep-only (strong
+scaling), with a gather of the output slabs to rank 0, scatter + sweep + gather,
+and the in-place all-gather, with its oracle parity counts.
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N     (one process per GPU, RCCL)
+
+``python bench.py --gpus N`` with N > 1 and no torchrun environment starts
+torchrun as a CHILD process (``--nproc-per-node N``, 127.0.0.1) before anything
+touches the GPU, passes rank 0's JSON line through and exits with torchrun's
+exit status.  Every rank checks that the process group has exactly N ranks.
 
 Rank 0 prints ONE JSON line (contract in the task statement); ``roofline``
 times the sweep kernel with HIP events on the stream it is launched on;
@@ -43,7 +49,7 @@ METRIC = "weight-GB/s quantized (per-ch INT8 DFQ sweep) + top-1 delta, MobileNet
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
@@ -69,7 +75,42 @@ def parse():
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r04.json"),
                    help="the committed rocprofv3 summary of this bench command (scripts/profile.sh + "
                         "scripts/summarize_profile.py): PMC traffic and the kernel's rocprof average")
-    return p.parse_args()
+    p.add_argument("--no-sharded", action="store_true",
+                   help="N > 1: skip configs4_sharded (the ResNet-50 INT4 list sharded from rank 0)")
+    p.add_argument("--probe-ranks", action="store_true",
+                   help="launcher check: every rank joins the process group, checks the world size and "
+                        "rank 0 prints the ranks it saw (no sweep; runs on the CPU with gloo)")
+    return p.parse_args(argv)
+
+
+def launch_command(n: int, argv, port: int):
+    """torchrun command line for ``--gpus n`` started from a plain ``python bench.py``."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), *argv]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Run the N-rank bench as a child torchrun (one process per GPU) and return its
+    exit status.  The parent touches no GPU API (no torch.cuda call at all): it
+    only waits.  Rank 0's JSON line reaches our stdout directly (inherited)."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run(launch_command(n, argv, _free_port()), env=env)
+    return r.returncode
+
+
+def check_world(args, world: int):
+    """Every rank: the process group must have exactly ``--gpus`` ranks."""
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {world} rank(s) "
+                         f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')})")
 
 
 def model_shapes(name):
@@ -414,16 +455,43 @@ def _timed_steps(fn, dev, reps, warmup=3):
     return max_over_ranks(time.perf_counter() - t0, dev) / reps
 
 
-def sharded_modes(sw, dev, stream, reps=10):
-    """The layer-sharded sweep's collective forms (N > 1), ms per step:
-    sweep + gather of every output slab to rank 0; rank 0 -> ranks scatter of the
-    input slabs + sweep + gather (rank 0 holds the whole list, end to end);
-    sweep + in-place all_gather_into_tensor; and the replicated form (every rank
-    sweeps the WHOLE list after a broadcast: weak scaling, weight-GB/s summed)."""
-    from data_free_quantization_amd.sweep import SweepItem, SweepPlan
-    world = sw.world
-    wbytes = 4 * sum(s.numel for s in sw.specs)
-    out = {}
+def configs4_sharded(dev, stream, reps=10, parity=True):
+    """BASELINE configs[4] at N > 1: ONE >= 2 GiB layer list of ResNet-50 weight
+    sets (per-channel asym INT4 + clip [-15, 15], packed int4 codes: the
+    SECONDARY config of that name), held by rank 0 and LPT-sharded over the ranks
+    (distributed.ShardedSweep; scatter once before timing).  Timed (wall,
+    barrier-bracketed, max over ranks), ms per pass of the WHOLE list:
+
+    * ``sweep``: every rank sweeps its share, outputs left sharded (strong scaling);
+    * ``sweep_gather_root``: + one grouped receive per rank of its output slabs
+      into rank 0's arenas (rank 0 ends holding every output);
+    * ``scatter_sweep_gather_root``: rank 0 -> ranks input slabs, sweep, gather
+      (rank 0 holds the list end to end);
+    * ``sweep_allgather``: + one in-place all_gather_into_tensor per field.
+
+    Parity (checker leg): after a gather to rank 0, the first, middle and last
+    weight sets' outputs vs the C oracle on the same inputs (every field)."""
+    import torch.distributed as dist
+    from data_free_quantization_amd import distributed as D
+    from data_free_quantization_amd.sweep import SweepItem
+    shapes = model_shapes("resnet50")
+    per_copy = sum(int(torch.Size(s).numel()) for s in shapes)
+    copies = max(1, -(-(2 << 30) // (4 * per_copy)))
+    specs = D.uniform_specs(shapes * copies, bits=4, per_channel=True, symmetric=False, want_esum=False,
+                            clip=(-15.0, 15.0), pack_int4=True)
+    sw = D.ShardedSweep(specs, replicate=True, device=dev)
+    if sw.rank == 0:
+        gen = torch.Generator(device=dev).manual_seed(4321)
+        for i, s in enumerate(specs):
+            sw.weight(i).copy_(synth_weight(s.shape, dev, gen))
+    sw.scatter()
+    torch.cuda.synchronize(dev)
+    wbytes = 4 * per_copy * copies
+    out = {"config": "resnet50 per-ch asym INT4 + clip, packed int4 codes; one layer list on rank 0, "
+                     "LPT-sharded over the ranks", "copies": copies, "layers": len(specs),
+           "rccl_ranks": sw.world, "backend": dist.get_backend() if dist.is_initialized() else None,
+           "layers_per_rank": [len(p) for p in sw.layout.parts],
+           "weight_bytes_per_rank": [sum(4 * specs[i].numel for i in p) for p in sw.layout.parts]}
 
     def step_root():
         sw.run(stream)
@@ -438,28 +506,42 @@ def sharded_modes(sw, dev, stream, reps=10):
         sw.run(stream)
         sw.gather("all")
 
-    for name, fn in (("sweep_gather_root", step_root), ("scatter_sweep_gather_root", step_e2e),
-                     ("sweep_allgather", step_all)):
+    for name, fn in (("sweep", lambda: sw.run(stream)), ("sweep_gather_root", step_root),
+                     ("scatter_sweep_gather_root", step_e2e), ("sweep_allgather", step_all)):
         t = _timed_steps(fn, dev, reps)
         out[f"{name}_ms"] = round(t * 1e3, 4)
         out[f"{name}_weight_GBs"] = round(wbytes / t / 1e9, 1)
-    # replicas: every rank holds (broadcast) and sweeps the whole list
-    sw.broadcast()
-    items = []
-    for i, s in enumerate(sw.specs):
-        o = sw.outputs(i)
-        items.append(SweepItem(src=sw.weight(i), dst=o.dq, codes=o.codes, scale=o.scale, zero=o.zero, esum=o.esum,
-                               bits=s.bits, per_channel=s.per_channel, symmetric=s.symmetric, khw=s.khw,
-                               clip=s.clip, rows=s.rows, pack_int4=s.pack_int4))
-    plan = SweepPlan(items)
-    t = _timed_steps(lambda: plan.execute(stream), dev, reps)
-    plan.destroy()
-    out["replicas_ms"] = round(t * 1e3, 4)
-    out["replicas_weight_GBs"] = round(world * wbytes / t / 1e9, 1)
-    out["note"] = ("host-timed, barrier-bracketed, max over ranks; gather/scatter = one grouped send/recv per "
-                   "rank of exactly its slab (RCCL over xGMI), all-gather = one in-place "
-                   "all_gather_into_tensor of the slab-strided arena; replicas = every rank sweeps the whole "
-                   f"list (weight-GB/s summed over {world} ranks)")
+    if sw.plan_stats is not None:
+        out["rank_plan"] = {"algo_bytes": sw.plan_stats["algo_bytes"], "launches": sw.plan_stats["launches"]}
+    if parity:
+        sw.run(stream)
+        sw.gather("root")
+        torch.cuda.synchronize(dev)
+        if sw.rank == 0:
+            from tests.parity import sweep_mismatches
+            sets = sorted({0, copies // 2, copies - 1})
+            items = []
+            for c in sets:
+                for i in range(c * len(shapes), (c + 1) * len(shapes)):
+                    s, o = specs[i], sw.outputs(i)
+                    items.append(SweepItem(src=sw.weight(i), dst=o.dq, codes=o.codes, scale=o.scale, zero=o.zero,
+                                           esum=o.esum, bits=s.bits, per_channel=s.per_channel,
+                                           symmetric=s.symmetric, khw=s.khw, clip=s.clip, rows=s.rows,
+                                           pack_int4=s.pack_int4))
+            t0 = time.perf_counter()
+            par = sweep_mismatches(items)
+            par["weight_sets"] = sets
+            par["owners"] = sorted({sw.layout.owner[c * len(shapes) + j] for c in sets for j in range(len(shapes))})
+            par["seconds"] = round(time.perf_counter() - t0, 2)
+            out["parity"] = par
+        if dist.is_initialized():
+            dist.barrier()
+    out["note"] = ("host-timed, barrier-bracketed, max over ranks; weight_GBs = the whole list's fp32 weight "
+                   "bytes per pass; gather/scatter = one grouped send/recv per rank of exactly its slabs, "
+                   "all-gather = one in-place all_gather_into_tensor per output field")
+    sw.destroy()
+    del sw
+    torch.cuda.empty_cache()
     return out
 
 
@@ -768,46 +850,74 @@ def same_mix_probe(n, dev, stream, reps=10):
     return round(13 * n / (stream_ms / 1e3) / 1e9, 1), round(13 * n / (lds_ms / 1e3) / 1e9, 1)
 
 
-def main():
-    args = parse()
+def probe_ranks(args):
+    """--probe-ranks: join the process group, check the world size, gather every
+    rank's (rank, world, local rank, pid) to rank 0, which prints one JSON line.
+    No GPU work (gloo on the CPU), so the launcher is testable without a GPU."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    check_world(args, world)
+    if world > 1:
+        dist.init_process_group(os.environ.get("DFQ_DIST_BACKEND", "gloo"))
+        check_world(args, dist.get_world_size())
+        me = torch.tensor([dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0")),
+                           os.getpid()], dtype=torch.int64)
+        allv = [torch.zeros_like(me) for _ in range(world)]
+        dist.all_gather(allv, me)
+        rows = [v.tolist() for v in allv]
+        backend = dist.get_backend()
+        dist.destroy_process_group()
+    else:
+        rows, backend = [[0, 1, 0, os.getpid()]], None
+    if rows[0][0] == 0 and int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps({"probe_ranks": rows, "n_gpus": world, "backend": backend}), flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: torchrun as a child, started before any GPU call here
+        return launch_ranks(args.gpus, argv)
+    check_world(args, int(os.environ.get("WORLD_SIZE", "1")))
+    if args.probe_ranks:
+        return probe_ranks(args)
     from data_free_quantization_amd import distributed as D
     world, rank, dev = D.init_from_env()
+    if world > 1:
+        import torch.distributed as dist
+        check_world(args, dist.get_world_size())
     telemetry = Telemetry(dev)
     tele_start = telemetry.sample("process_start")
     shapes = model_shapes(args.model)
     per_copy = sum(int(torch.Size(s).numel()) for s in shapes)
-    copies = args.copies or max(1, -(-(2 << 30) // (4 * per_copy)))   # >= 2 GiB of fp32 weights in the list
+    copies = args.copies or max(1, -(-(2 << 30) // (4 * per_copy)))   # >= 2 GiB of fp32 weights per rank
     specs = D.uniform_specs(shapes * copies, bits=args.bits, per_channel=args.granularity == "channel",
                             symmetric=not args.asym, want_esum=not args.no_esum, clip=(-15.0, 15.0))
     stream = torch.cuda.current_stream(dev)
     std_of = lambda shp: (2.0 / (shp[2] * shp[3] * shp[0])) ** 0.5 if len(shp) == 4 else 0.01   # noqa: E731
     sw = plan = None
-    if world > 1 or args.layout == "arena":
-        import torch.distributed as dist
-        # rank 0 holds the whole layer list and scatters each rank its slab (untimed)
+    # Weak scaling: every rank sweeps its own list of ``copies`` weight sets (its
+    # shard of the job's world * copies sets; rank-seeded synthetic weights); no
+    # collective in the timed step.
+    gen = torch.Generator(device=dev).manual_seed(1234 + 7919 * rank)
+    if args.layout == "arena" and world == 1:
+        # diagnostics: the sharded path's per-field slab arenas at one rank
         sw = D.ShardedSweep(specs, replicate=True, device=dev)
-        if rank == 0:
-            gen = torch.Generator(device=dev).manual_seed(1234)
-            for i, s in enumerate(specs):
-                sw.weight(i).normal_(0.0, std_of(s.shape), generator=gen)
-        sw.scatter()
+        for i, s in enumerate(specs):
+            sw.weight(i).normal_(0.0, std_of(s.shape), generator=gen)
         st = sw.plan_stats
         run = lambda: sw.run(stream)   # noqa: E731
-    if args.layout == "tensor":
+    else:
         # The timed sweep runs on one allocation per tensor, in the order eager code
-        # makes them (input, then its outputs).  At N > 1 each rank copies its
-        # scattered share out of the slab arena; the arenas stay for the collective
-        # forms (sharded_modes).  The sweep over per-field arenas is placement-bound:
-        # 1.08 or 1.31-1.37 ms per step from box to box, and 1.36 against 1.11 for
-        # per-tensor allocations on one box in five interleaved process pairs
-        # (profiles/r02/ab_layout.jsonl, ab_arena.md).
+        # makes them (input, then its outputs).  The sweep over per-field arenas is
+        # placement-bound: 1.08 or 1.31-1.37 ms per step from box to box, and 1.36
+        # against 1.11 for per-tensor allocations on one box in five interleaved
+        # process pairs (profiles/r02/ab_layout.jsonl, ab_arena.md).
         from data_free_quantization_amd.sweep import SweepPlan, allocate
-        gen = torch.Generator(device=dev).manual_seed(1234)
         items = []
-        for i in (sw.mine if sw is not None else range(len(specs))):
-            s = specs[i]
-            w = sw.weight(i).clone() if sw is not None else \
-                torch.empty(s.shape, device=dev).normal_(0.0, std_of(s.shape), generator=gen)
+        for s in specs:
+            w = torch.empty(s.shape, device=dev).normal_(0.0, std_of(s.shape), generator=gen)
             items.append(allocate(w, bits=s.bits, per_channel=s.per_channel, symmetric=s.symmetric, khw=s.khw,
                                   want_esum=s.want_esum, clip=s.clip, pack_int4=s.pack_int4))
         plan = SweepPlan(items)
@@ -841,12 +951,18 @@ def main():
     step_ms = [a.elapsed_time(b) for a, b in step_ev]
     dev_ms = ev0.elapsed_time(ev1)          # device time of this rank's K launches on this stream
     t_step = D.max_over_ranks(wall, dev) / args.steps
-    weight_bytes = 4 * per_copy * copies    # the whole list, swept once per step by all ranks together
+    weight_bytes = 4 * per_copy * copies * world   # every rank's list, swept once per step
     value = weight_bytes / t_step / 1e9
     launch_ms = dev_ms / args.steps          # device time of one execute() (st["launches"] kernels)
     achieved = st["algo_bytes"] / (launch_ms / 1e3) / 1e9
+    rank_launch_ms = [launch_ms]
+    if world > 1:   # every rank's own kernel time (rank 0 reports its roofline)
+        lt = torch.zeros(world, dtype=torch.float64, device=dev)
+        lt[rank] = launch_ms
+        dist.all_reduce(lt)
+        rank_launch_ms = [round(float(x), 4) for x in lt.tolist()]
     # parity of what was just timed: the first, middle and last weight set of this
-    # rank's share vs the C oracle on the same input tensors (every field)
+    # rank's list vs the C oracle on the same input tensors (every field)
     timed_parity = None
     if plan is not None and not args.no_parity:
         timed_parity = parity_of_timed(plan.items, len(shapes), dev)
@@ -856,12 +972,15 @@ def main():
             dist.all_reduce(tot)
             timed_parity["all_ranks"] = {"mismatches": int(tot[0]), "tensors": int(tot[1])}
             timed_parity["mismatches"] = int(tot[0])
-    modes = sharded_modes(sw, dev, stream) if world > 1 else None
     for obj in (sw, plan):
         if obj is not None:
             obj.destroy()
     del sw, plan, run
     torch.cuda.empty_cache()
+    sharded4 = None
+    if world > 1 and not args.no_sharded:
+        gloo = dist.get_backend() == "gloo"   # a one-GPU rehearsal stages every transfer through the host
+        sharded4 = configs4_sharded(dev, stream, reps=2 if gloo else 10, parity=not args.no_parity)
     traffic, prof = None, None
     tj = Path(args.traffic_json)
     if tj.exists():
@@ -888,7 +1007,7 @@ def main():
         # slower (profiles/r03/validate_as vs r03at: MobileNetV2 end to end 10.4 vs
         # 5.3 ms), a state a main_dfq run never starts from
         pipe = None if args.no_pipeline else {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")}
-        probe_stream, probe_lds = same_mix_probe(per_copy * copies // world, dev, stream)
+        probe_stream, probe_lds = same_mix_probe(per_copy * copies, dev, stream)
         second = None if args.no_secondary else secondary_configs(dev, stream)
         if second is not None:
             second.append(fold_quant_pair(dev, stream))
@@ -899,8 +1018,11 @@ def main():
         parity = None
         if not args.no_parity:
             parity = {"timed_sweep": timed_parity, "pipeline_mobilenetv2": pipeline_parity(dev)}
+            if sharded4 is not None and "parity" in sharded4:
+                parity["configs4_sharded"] = sharded4["parity"]
             parity["mismatches"] = parity["pipeline_mobilenetv2"]["mismatches"] + \
-                (timed_parity["mismatches"] if timed_parity else 0)
+                (timed_parity["mismatches"] if timed_parity else 0) + \
+                (sharded4["parity"]["mismatches"] if sharded4 is not None and "parity" in sharded4 else 0)
         if pipe is not None:   # the same run again after the other legs (see above)
             pipe["mobilenetv2"]["end_to_end_after_other_legs"] = pipeline_timing(dev, "mobilenetv2")["end_to_end"]
             pipe["cold_process_mobilenetv2"] = pipeline_cold("mobilenetv2")
@@ -909,11 +1031,13 @@ def main():
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
+            "rccl_ranks": world,
+            "backend": dist.get_backend() if world > 1 else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "codes": f"{args.bits}-bit grid indices stored as "
@@ -921,7 +1045,7 @@ def main():
             "data": "synthetic random-init weights of the reference shapes (no checkpoints offline)",
             "box": socket.gethostname(),
             "config": {
-                "workload": f"{args.model} x{copies} weight sets in one layer list: {args.granularity} "
+                "workload": f"{args.model} x{copies} weight sets in one layer list per rank: {args.granularity} "
                             f"{'asym' if args.asym else 'sym'} INT{args.bits} quantize-dequantize + codes + "
                             f"clip[-15,15]" + ("" if args.no_esum else " + bias-correction error sums"),
                 "weight_shapes": f"{args.model} target layers (SURVEY.md 8, synthetic init)",
@@ -929,10 +1053,10 @@ def main():
                 "layers": len(specs),
                 "layers_per_copy": len(shapes),
                 "weights_per_copy": per_copy,
-                "parallelism": (f"{world} ranks, one process per GPU: the layer list LPT-sharded over the ranks "
-                                "(rank 0 scatters the input slabs before timing; each rank sweeps per-tensor "
-                                "copies of its share), outputs left sharded (no collective in the timed step); "
-                                "gathered forms over the slab arenas in sharded_modes")
+                "parallelism": (f"dp{world}: one process per GPU; the job's {world} x {copies} weight sets "
+                                f"sharded {copies} per rank (weak scaling: per-GPU work fixed), no collective in "
+                                "the timed step; BASELINE configs[4]'s single list sharded from rank 0 with its "
+                                "gathers in configs4_sharded")
                 if world > 1 else "1 rank: the whole layer list on one GPU (per-tensor allocations, no exchange)",
             },
             "roofline": {
@@ -950,6 +1074,7 @@ def main():
                 "grid_blocks": st["grid_blocks"],
                 "variant": st["variant"],
                 "rank": 0,
+                "launch_ms_per_rank": rank_launch_ms,
                 "traffic_source": ("PMC FETCH_SIZE (x2, the gfx950 correction) + WRITE_SIZE per launch from "
                                    f"{prof['source']}: separate rocprofv3 --pmc passes over this bench command, "
                                    "not measured in this run") if prof else None,
@@ -973,7 +1098,7 @@ def main():
                         "the timed steps.  NOT a ceiling: box to box it lands 5.2-6.5 TB/s, sometimes below the "
                         "sweep itself, so it only shows how far arithmetic and row logic cost on this box"},
             "parity": parity,
-            "sharded_modes": modes,
+            "configs4_sharded": sharded4,
             "cpu_baseline": cpu,
             "secondary_configs": second,
             "single_model_latency": single,
@@ -991,4 +1116,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    rc = main()
+    sys.exit(rc if isinstance(rc, int) else 0)

@@ -127,7 +127,10 @@ class _DiffPlan:
 
 
 #: iteration cap of the device loop (the reference's loop has none; a run that
-#: reaches it warns)
+#: reaches it warns).  A LAUNCHED run (launch=True) is also bounded in time: it
+#: stops enqueueing iterations after 60 s and fails at join, well before the
+#: caller's stream gate traps at 120 s (dfq_cle.hip, kCleGateSeconds /
+#: kCleLaunchDeadlineUs); a blocking run has no time bound.
 MAX_ITERS = int(os.environ.get("DFQ_CLE_MAX_ITERS", "100000"))
 _TIMING = bool(os.environ.get("DFQ_CLE_TIMING"))   # host-side split of create (stderr)
 

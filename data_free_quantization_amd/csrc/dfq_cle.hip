@@ -1192,7 +1192,7 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
                                                double* __restrict__ hist, CleState* __restrict__ st, double* sm,
                                                float* part_lds = nullptr, float* np_stack = nullptr,
                                                uint32_t* hflag = nullptr, uint64_t* sig = nullptr,
-                                               uint64_t gen = 0, int flag_every = 0) {
+                                               uint64_t gen = 0) {
     // The stop rule's inputs in one parallel pass of loads into LDS (part_lds): the
     // chunk sums, the layers' {(float)n, serial} and the state's 10 words.  Read
     // where they are used instead, they were dependent round trips of a serial
@@ -1269,10 +1269,8 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         st->done = done;
         // the host's copy of the stop rule (pinned host memory; a system-scope
         // vector store), written every iteration: the loop's host side polls it for
-        // the stop and paces its enqueue by it (cle_run_locked).  flag_every = 0
-        // (diagnostics, DFQ_CLE_EVENT_PACING=1): written at the stop only, the host
-        // paced by an event behind each iteration instead.
-        if (hflag && (done || flag_every))
+        // the stop and paces its enqueue by it (cle_run_locked)
+        if (hflag)
             __hip_atomic_store(hflag, ((uint32_t)(it + 1) << 1) | (uint32_t)done, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         // A launched run: the caller's stream is released here, at convergence,
@@ -1280,7 +1278,8 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         // ahead of it.  Every rescale ran in an earlier launch of the stream (complete, its
         // writes released at its end); what this launch's remaining blocks write
         // (next-iteration range words) is the loop's own.  Not after a flagged
-        // error: the worker then fails the run and the gate stays shut.
+        // error: the gate then opens only at the worker's release, behind the
+        // loop's last launch, and the run fails at join (wait() raises).
         if (done && sig && __hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
             __hip_atomic_store(sig, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -1321,7 +1320,6 @@ struct CleFin {
     uint32_t* hflag;         // pinned host word: (iterations << 1) | done, or null
     uint64_t* sig;           // a launched run: the caller's gate word and the generation
     uint64_t gen;            // that releases it at convergence (else null)
-    int32_t flag_every;      // hflag written every iteration (else at the stop: event pacing, diagnostics)
 };
 
 // The launches of one iteration.  Launch k < steps runs the rescale tasks of
@@ -1421,12 +1419,11 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         const bool stage_part = (int64_t)F.nl * (F.S + 2) + (int64_t)(sizeof(CleState) / 4) + 2048 <= kCleTile;
         if (F.nl <= 128)   // numpy's pairwise sum over the layer means is one leaf
             cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
-                                       stage_part ? lds + 2048 : nullptr, nullptr, F.hflag, F.sig, F.gen,
-                                       F.flag_every);
+                                       stage_part ? lds + 2048 : nullptr, nullptr, F.hflag, F.sig, F.gen);
         else   // the frame stack after the metric tile area (free: this block's units are done)
             cle_final_body<false, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st,
                                         reinterpret_cast<double*>(lds), stage_part ? lds + 2048 : nullptr,
-                                        lds + kCleTile, F.hflag, F.sig, F.gen, F.flag_every);
+                                        lds + kCleTile, F.hflag, F.sig, F.gen);
 #ifdef DFQ_DIAGNOSTICS
         if (tl2 && threadIdx.x == 0) {
             uint64_t* r = g_cle_tl2 + 4 * kCleTl2Fin;
@@ -1491,7 +1488,6 @@ struct dfq_cle_plan {
     uint32_t* d_flag = nullptr;     // the stop rule's host word (the device context's, set by run)
     uint64_t* d_sig = nullptr;      // a launched run: the caller's gate word and its generation
     uint64_t gen = 0;
-    int32_t flag_every = 1;         // the stop rule's host word every iteration (0: event pacing, diagnostics)
     hipStream_t st = nullptr;       // the loop's stream (the device context's)
     std::vector<int64_t> rstep, astep;   // task offsets per step (size steps + 1)
     std::vector<char> step_pos;          // per step: position-parallel W2 tiles (the POS rescale kernel)
@@ -1540,7 +1536,6 @@ struct CleDeviceCtx {
     CleState* h_state = nullptr;   // pinned: the run's state
     uint32_t* h_flag = nullptr;    // pinned, written by the stop rule: (iterations << 1) | done
     uint32_t* d_flag = nullptr;    // its device address
-    hipEvent_t iev[4] = {};        // behind each iteration in flight (the host's pacing)
     // Table pool: one plan at a time keeps its tables here (device + pinned upload
     // mirror), so a plan costs no hipMalloc / hipFree (hipFree waits for the whole
     // device) and its upload is an async DMA on the loop stream.
@@ -1579,12 +1574,6 @@ static hipError_t cle_ctx_ready(CleDeviceCtx& ctx) {
         e = hipHostMalloc(&ctx.h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx.d_flag), ctx.h_flag, 0);
     }
-    // The pacing events only tell this thread how far the stream got (the loop's
-    // outcome comes through the pinned host word, the results after a stream
-    // synchronize): recorded without a system-scope fence.  (Fenced, they measured
-    // the same: profiles/r04/cle_ab_r04t.jsonl.)
-    for (int i = 0; i < 4 && e == hipSuccess; ++i)
-        if (!ctx.iev[i]) e = hipEventCreateWithFlags(&ctx.iev[i], hipEventDisableTiming | hipEventDisableSystemFence);
     if (e == hipSuccess && !ctx.pool_ev) e = hipEventCreateWithFlags(&ctx.pool_ev, hipEventDisableTiming);
     if (e == hipSuccess && !ctx.in_ev) e = hipEventCreateWithFlags(&ctx.in_ev, hipEventDisableTiming);
     return e;
@@ -2123,7 +2112,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
     // (or by plan_run before the first); the next iteration's ride with the
     // launches after their tensors' last rescale (cle_loop_step_kernel)
     CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, 0, p->d_flag,
-             p->d_sig, p->gen, p->flag_every};
+             p->d_sig, p->gen};
     for (int32_t k = 0; k <= p->steps; ++k) {
         const bool last = k == p->steps;
         const int64_t a0 = last ? 0 : p->astep[k], a1 = last ? 0 : p->astep[k + 1];
@@ -2157,6 +2146,19 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
 // (profiles/r04/cle_trace_*): round 3's batches of 4 iterations, one batch
 // ahead, wasted 16-28 of them per run.
 constexpr int32_t kCleAhead = 1;
+// How long the loop's host word may stay unchanged before the host asks the
+// stream whether it has drained (hipStreamQuery: a marker packet in the queue).
+constexpr double kClePollQuietUs = 1000.0;
+// How long the caller's stream gate waits for a launched loop at most (it traps
+// after that), and how long join waits on the host (then it reports the loop
+// lost).  A launched run stops enqueueing iterations at half the gate's limit and
+// fails cleanly (cle_run_locked's deadline), so a slowly converging loop on a busy
+// GPU ends with an error at join, not with the gate's trap; blocking runs
+// (dfq_cle_plan_run) have no deadline and stop at max_iters
+// (Cross_layer_equal.DFQ_CLE_MAX_ITERS) with its warning.
+static constexpr int kCleGateSeconds = 120;
+static constexpr int kCleJoinSeconds = kCleGateSeconds + 30;
+static constexpr double kCleLaunchDeadlineUs = 0.5e6 * kCleGateSeconds;
 // The context's history buffer for caps above the tables' kCleHistCap slots,
 // grown once (a launched run grows it before its caller's stream waits: hipFree
 // synchronises the whole device).
@@ -2182,7 +2184,7 @@ static hipError_t cle_copy_back(void* dst, const void* src, size_t bytes, hipStr
 // ordered the plan's producers before that stream.  iterations / hist: the run's
 // result (hist resized to the iterations run).
 static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, int32_t count, int32_t max_iters,
-                          int32_t* iterations, std::vector<double>* hist) {
+                          int32_t* iterations, std::vector<double>* hist, double deadline_us = -1.0) {
     DFQ_HIP_CHECK(cle_ctx_ready(ctx));
     p->st = ctx.st;
     p->h_state = ctx.h_state;
@@ -2242,48 +2244,52 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     // Iteration by iteration, kCleAhead of them queued behind the running one; the
     // stop rule writes (iterations << 1) | done into pinned host memory every
     // iteration (ctx.h_flag, a system-scope store), and this thread polls that word
-    // both for the stop and for its pacing -- no copy or host round trip sits
-    // between two iterations on the loop stream, and at convergence at most
-    // kCleAhead iterations are left to run as no-ops.  (An event recorded behind
-    // each iteration for the pacing instead, DFQ_CLE_EVENT_PACING=1: its marker
-    // packet added ~3.7 us before every iteration's first launch, MobileNetV2
-    // 3.51 vs 3.37 ms, profiles/r04/cle_trace_r04v_*, cle_ab_r04v.jsonl.)  (Round 3 enqueued batches of 4 iterations a batch ahead and read
-    // the state back per batch; replaying a batch as a captured HIP graph
-    // measured slower, profiles/r03/cle_ab_p.jsonl.)  A stream that drains
-    // without the word saying done (a kernel error) ends the polling; the final
-    // state read below decides.
+    // both for the stop and for its pacing -- no copy, event or host round trip
+    // sits between two iterations on the loop stream, and at convergence at most
+    // kCleAhead iterations are left to run as no-ops.  (Pacing by an event behind
+    // each iteration: its marker packet added ~3.7 us before every iteration's
+    // first launch, profiles/r04/cle_trace_r04v_*.  Round 3 enqueued batches of 4
+    // iterations a batch ahead and read the state back per batch.)
+    // hipStreamQuery is NOT polled per iteration: the runtime answers it with a
+    // marker packet in the loop's queue, which then sits between two iterations'
+    // launches.  It is asked only when the word has not moved for kClePollQuietUs
+    // (a kernel error, or everything launched has run).  A drained stream ends the
+    // polling only when the word, re-read after the drain, says done, or every
+    // allowed iteration was launched, or the word lags the launches (a lost
+    // word): a stale read that held back the next enqueue just goes on enqueueing
+    // (breaking there ended the loop early as DFQ_OK).
+    // deadline_us > 0 (launched runs): past it no more iterations are enqueued and
+    // the run fails cleanly, well before the caller's stream gate would trap.
     const double tc1 = now_us();
     int32_t launched = 0;
-    p->flag_every = ab_env("DFQ_CLE_EVENT_PACING") == nullptr;
-    // diagnostics A/B: once the queue is down to kCleAhead iterations, top it up by
-    // `burst` (the host's enqueue then meets fewer iteration boundaries)
-    int32_t burst = 1;
-    if (const char* b = ab_env("DFQ_CLE_BURST")) burst = std::max(1, std::min(2, atoi(b)));   // <= 3 in flight: 4 events
-    int32_t fill = 0;   // iterations still to enqueue in the current burst
-    int32_t ahead = kCleAhead;   // diagnostics A/B: DFQ_CLE_AHEAD (1-3; events: 4 in flight at most)
-    if (const char* a = ab_env("DFQ_CLE_AHEAD")) ahead = std::max(1, std::min(p->flag_every ? 3 : 2, atoi(a)));
-    hipEvent_t* iev = ctx.iev;
+    bool deadline_hit = false;
     if (!init.done) {
-        int64_t polls = 0;
-        int32_t ran = 0;   // iterations known complete (the host word; the events under DFQ_CLE_EVENT_PACING)
+        uint32_t last_f = ~0u;
+        double t_moved = tc1;
         for (;;) {
             const uint32_t f = __atomic_load_n(ctx.h_flag, __ATOMIC_ACQUIRE);
             if (f & 1u) break;
-            if (p->flag_every) {
-                ran = (int32_t)(f >> 1);
-            } else {
-                while (ran < launched && hipEventQuery(iev[ran & 3]) == hipSuccess) ++ran;
-            }
-            if (launched < max_iters && (fill > 0 || launched - ran <= ahead)) {
-                if (fill == 0) fill = burst;
+            const int32_t ran = (int32_t)(f >> 1);   // iterations complete
+            if (launched < max_iters && !deadline_hit && launched - ran <= kCleAhead) {
                 const int rc = cle_enqueue_iteration(p, s, launched);
                 if (rc != DFQ_OK) return rc;
-                if (!p->flag_every) DFQ_HIP_CHECK(hipEventRecord(iev[launched & 3], s));
                 ++launched;
-                --fill;
                 continue;
             }
-            if ((++polls & 255) == 0 && hipStreamQuery(s) != hipErrorNotReady) break;
+            const double t = now_us();
+            if (f != last_f) {
+                last_f = f;
+                t_moved = t;
+            } else if (t - t_moved > kClePollQuietUs) {
+                const hipError_t q = hipStreamQuery(s);
+                if (q != hipErrorNotReady) {
+                    if (q != hipSuccess) break;   // a device error: the synchronize below reports it
+                    const uint32_t f2 = __atomic_load_n(ctx.h_flag, __ATOMIC_ACQUIRE);
+                    if ((f2 & 1u) || launched >= max_iters || deadline_hit || (int32_t)(f2 >> 1) < launched) break;
+                }
+                t_moved = t;
+            }
+            if (deadline_us > 0 && t - tc1 > deadline_us) deadline_hit = true;
             __builtin_ia32_pause();
         }
     }
@@ -2404,6 +2410,11 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
         set_last_hip_error(hipErrorLaunchTimeOut);
         return DFQ_ERR_HIP;
     }
+    if (!fin.done) {   // the stop rule never said done: never report a partial loop as a result
+        set_last_hip_error_text(deadline_hit ? "the launched CLE loop reached its time limit before converging"
+                                             : "the CLE loop stopped before its stop rule said done");
+        return DFQ_ERR_HIP;
+    }
     if (ab_env("DFQ_CLE_DEBUG")) {   // per-layer chunk sums of the last iteration run
         std::vector<float> part((size_t)p->slots * std::max(p->nl, 1));
         DFQ_HIP_CHECK(cle_copy_back(part.data(), p->d_part, sizeof(float) * part.size(), s));
@@ -2475,10 +2486,7 @@ __global__ void __launch_bounds__(64) cle_caller_gate_kernel(const uint64_t* sig
 // The loop stream is a high-priority stream: it gets a hardware queue of its own
 // (queues are pooled per priority), so the caller's waiting queue can never hold
 // the loop's launches back.
-// How long the caller's stream gate waits for a launched loop at most (it traps
-// after that), and how long join waits on the host (then it reports the loop lost).
-static constexpr int kCleGateSeconds = 120;
-static constexpr int kCleJoinSeconds = kCleGateSeconds + 30;
+// (the gate's limit and the launched run's deadline: kCleGateSeconds, above)
 
 struct CleAsync {
     std::mutex m;
@@ -2594,7 +2602,7 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
         if (hipSetDevice(p->dev) != hipSuccess) {
             rc = DFQ_ERR_HIP;
         } else {
-            rc = cle_run_locked(p, ctx, threshold, count, max_iters, &a->iters, &a->hist);
+            rc = cle_run_locked(p, ctx, threshold, count, max_iters, &a->iters, &a->hist, kCleLaunchDeadlineUs);
         }
         if (rc == DFQ_ERR_HIP) {
             const char* m = dfq_last_hip_error();

@@ -22,9 +22,7 @@ sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_HOST_RELEASE",
-            "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY",
-            "DFQ_CLE_EVENT_PACING", "CLE_AB_BLOCKING", "DFQ_CLE_BURST",
-            "DFQ_CLE_AHEAD")
+            "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY", "CLE_AB_BLOCKING")
 CONFIGS = {
     "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
@@ -35,11 +33,7 @@ CONFIGS = {
     "tiles_early": {"DFQ_CLE_TILES_EARLY": "1", "DFQ_CLE_RANGES_EARLY": "1"},   # each tensor's tiles / ranges right after its last rescale
     "ranges_early": {"DFQ_CLE_RANGES_EARLY": "1"},  # only the range tasks early
     "units_early": {"DFQ_CLE_TILES_EARLY": "1"},    # only the metric tiles early
-    "event_pacing": {"DFQ_CLE_EVENT_PACING": "1"},  # the host paced by an event per iteration (before r04w)
-    "ahead2": {"DFQ_CLE_AHEAD": "2"},               # two iterations queued behind the running one
-    "ahead3": {"DFQ_CLE_AHEAD": "3"},
     "blocking": {"CLE_AB_BLOCKING": "1"},           # run_dfq's CLE blocking (no caller gate beside the loop)
-    "burst2": {"DFQ_CLE_BURST": "2"},               # the host tops the queue up by two iterations at a time
 }
 
 
