@@ -536,7 +536,9 @@ template <bool POS = true>
 __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, const CleTask* __restrict__ tasks,
                                                int64_t t0, int64_t t1, uint32_t* __restrict__ rng, int64_t M,
                                                int par, bool first_iter, int is_signed, float eps, double smin,
-                                               double smax, int64_t blk, int64_t nblk, CleApplyLds& A) {
+                                               double smax, int64_t blk, int64_t nblk, CleApplyLds& A,
+                                               float* __restrict__ vsave = nullptr, int32_t* __restrict__ vtag = nullptr,
+                                               int32_t iter = 0) {
     auto& red = A.red;
     float* rows = A.rows;
     float* inv_s = A.inv_s;
@@ -882,8 +884,19 @@ __device__ __forceinline__ void cle_apply_body(const CleRel* __restrict__ rels, 
                 }
             }
         } else {
+            // lagged schedule: the per-channel vectors before this iteration's
+            // multiply, and the iteration that saved them (per task), for the
+            // rollback of a speculative iteration (cle_loop_rollback_kernel)
+            if (vtag && threadIdx.x == 0) vtag[t] = iter;
             for (int64_t c = tk.a + threadIdx.x; c < tk.b; c += kThreads) {
                 const CleScale cs = cle_rel_scale(rels, R, mins, maxs, c, is_signed, eps, smin, smax);
+                if (vsave) {
+                    float* v = vsave + 2 * R.moff;   // [b1 | bnw | bnb | sacc] x c1
+                    if (R.b1) v[c] = R.b1[c];
+                    if (R.bnw) v[R.c1 + c] = R.bnw[c];
+                    if (R.bnb) v[2 * R.c1 + c] = R.bnb[c];
+                    if (R.sacc) v[3 * R.c1 + c] = R.sacc[c];
+                }
                 if (R.b1) R.b1[c] = R.b1[c] * cs.s;
                 if (R.bnw) R.bnw[c] = R.bnw[c] * cs.s;
                 if (R.bnb) R.bnb[c] = R.bnb[c] * cs.s;
@@ -1191,8 +1204,7 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
                                                const float* __restrict__ part, int32_t S, double* __restrict__ means,
                                                double* __restrict__ hist, CleState* __restrict__ st, double* sm,
                                                float* part_lds = nullptr, float* np_stack = nullptr,
-                                               uint32_t* hflag = nullptr, uint64_t* sig = nullptr,
-                                               uint64_t gen = 0) {
+                                               uint32_t* hflag = nullptr) {
     // The stop rule's inputs in one parallel pass of loads into LDS (part_lds): the
     // chunk sums, the layers' {(float)n, serial} and the state's 10 words.  Read
     // where they are used instead, they were dependent round trips of a serial
@@ -1273,15 +1285,9 @@ __device__ __forceinline__ void cle_final_body(const CleLayer* __restrict__ laye
         if (hflag)
             __hip_atomic_store(hflag, ((uint32_t)(it + 1) << 1) | (uint32_t)done, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
-        // A launched run: the caller's stream is released here, at convergence,
-        // instead of behind the host's check and the no-op iteration enqueued
-        // ahead of it.  Every rescale ran in an earlier launch of the stream (complete, its
-        // writes released at its end); what this launch's remaining blocks write
-        // (next-iteration range words) is the loop's own.  Not after a flagged
-        // error: the gate then opens only at the worker's release, behind the
-        // loop's last launch, and the run fails at join (wait() raises).
-        if (done && sig && __hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-            __hip_atomic_store(sig, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // (A launched run's caller gate opens behind the rollback launch that follows
+        // the loop -- cle_run_locked -- not here: the lagged schedule's next
+        // iteration may be running speculatively beside this stop rule.)
     }
 }
 
@@ -1316,32 +1322,32 @@ struct CleFin {
     double* hist;
     int64_t nchunks, nbig;   // all chunks / chunks with tiles (len >= 8)
     int32_t S, nl;
-    int32_t last;            // the iteration's last launch
+    int32_t last;            // the round-4 schedule's tiles-only launch (the stop rule's block without tiles)
     uint32_t* hflag;         // pinned host word: (iterations << 1) | done, or null
-    uint64_t* sig;           // a launched run: the caller's gate word and the generation
-    uint64_t gen;            // that releases it at convergence (else null)
+    int32_t stop_arrival;    // 1: the stop rule runs at the iteration's last tile arrival (round-4 schedule);
+                             // 0: as a block of its own (lagged schedule, stop_it)
 };
 
-// The launches of one iteration.  Launch k < steps runs the rescale tasks of
-// chain step k (blocks [0, nab)); every launch also runs the metric tiles
-// (blocks [nab, nab + ntb)) and the next iteration's range tasks (the rest) of
-// the tensors that are final once the steps before it have run -- a tensor no
-// later step touches is measured and ranged in the launch right after its last
-// rescale, where the step's latency-bound rescale tasks leave the chip idle,
-// instead of all of them after the last step.  The last launch (k = steps, no
-// rescale blocks) takes the last step's tensors and, through the arrival
-// counters, the chunk combine and the stop rule: every chunk of an iteration
-// arrives before its last launch ends, and some chunk always arrives in it (its
-// last step's tensors), so the stop rule runs there, after every rescale.
+// One launch of iteration group g.  The group's launches k < steps run the
+// rescale tasks of chain step k of iteration g (blocks [0, nab)); beside them run
+// metric tiles and next-iteration range tasks placed in this launch by the
+// planner (dfq_cle_plan_create): "own" ones of iteration g and "prev" ones of
+// iteration g - 1 (the lagged schedule: a tensor's tiles and ranges go anywhere
+// after its last rescale of iteration g-1 and before its first rescale of
+// iteration g).  Blocks: [0, nab) rescale, then nto own tiles, ntp prev tiles,
+// nro own ranges, nrp prev ranges.
 //
-// The stop rule (last arrival, last launch) advances st->iters and may set
-// st->done while range blocks of the same launch are still being dispatched, so
-// range blocks take the next iteration's parity from the launch argument
-// (iteration i of the run: parity (i + 1) & 1), never from st->iters; a range block
-// that starts after the stop rule said "done" skips its tasks (no later
-// iteration reads them).  Rescale and tile blocks read st->iters before the
-// stop rule can run (the rescale blocks of an earlier launch; the tile blocks
-// before their arrival).
+// Lagged schedule: iteration g's first steps run before iteration g-1's stop
+// rule (the last tile arrival) has decided -- speculatively.  When that stop rule
+// says done, iteration g is discarded: its rescale blocks skip from then on
+// (st->done) and cle_loop_rollback_kernel restores the weights from the snapshots
+// (= iteration g-1's weights: every tile of g-1 ran before any rescale of g
+// touched its tensor) and the per-channel vectors from the saves of iteration g.
+// Tiles of iteration i are placed after every tile of i-1 (the planner's band),
+// so they start only after stop(i-1): a tile never runs for a discarded
+// iteration, and its snapshot writes and arrivals are always real.  Every block
+// takes its iteration, parity and arrival round from the launch argument g,
+// never from st (the stop rule advances st mid-launch).
 static_assert(kCleTilesLds - kCleTile >= kNpStackFloats, "np_pairwise's frame stack after the tile area");
 union CleStepLds {
     CleApplyLds apply;
@@ -1357,21 +1363,23 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(P
 cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ atasks, int64_t a0, int64_t a1,
                      int64_t nab, uint32_t* __restrict__ rng, int64_t M, int is_signed, float eps, double smin,
                      double smax, const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
-                     const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t u0, int64_t u1,
-                     int64_t ntb, float* __restrict__ b1buf, float* __restrict__ tailbuf,
-                     const CleTask* __restrict__ rtasks, int64_t r0, int64_t r1, CleFin F,
-                     CleState* __restrict__ st, int32_t par_next) {
+                     const int64_t* __restrict__ b1off, const CleUnit* __restrict__ units, int64_t uo, int64_t nuo,
+                     int64_t nto, int64_t up, int64_t nup, int64_t ntp, float* __restrict__ b1buf,
+                     float* __restrict__ tailbuf, const CleTask* __restrict__ rtasks, int64_t ro, int64_t nro_t,
+                     int64_t nro, int64_t rp, int64_t nrp_t, int64_t nrp, CleFin F, CleState* __restrict__ st,
+                     int32_t g, float* __restrict__ vsave, int32_t* __restrict__ vtag, int32_t stop_it) {
     __shared__ CleStepLds L;
     __shared__ int flag;
     if (st->done) return;
-    const int64_t blk = blockIdx.x;
-    if (blk < nab) {   // this step's rescale tasks
-        cle_apply_body<POS>(rels, atasks, a0, a1, rng, M, st->iters & 1, st->iters == 0, is_signed, eps, smin, smax,
-                            blk, nab, L.apply);
+    int64_t blk = blockIdx.x;
+    if (blk < nab) {   // this step's rescale tasks (iteration g)
+        cle_apply_body<POS>(rels, atasks, a0, a1, rng, M, g & 1, g == 0, is_signed, eps, smin, smax, blk, nab, L.apply,
+                            vsave, vtag, g);
         return;
     }
+    blk -= nab;
 #ifdef DFQ_DIAGNOSTICS
-    const bool tl2 = F.last && g_cle_tl2 != nullptr && blk < kCleTl2Fin;
+    const bool tl2 = g_cle_tl2 != nullptr && blk < kCleTl2Fin;
     const uint64_t tl2_start = tl2 ? __builtin_amdgcn_s_memrealtime() : 0;
     auto tl2_rec = [&](int role) {
         if (tl2 && threadIdx.x == 0) {
@@ -1384,31 +1392,14 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
 #else
     auto tl2_rec = [](int) {};
 #endif
-    if (blk >= nab + ntb) {   // the next iteration's ranges of the tensors final by now
-        cle_range_body(rels, rtasks, r0, r1, rng, M, par_next, blk - nab - ntb, (int64_t)gridDim.x - nab - ntb,
-                       L.tiles);
-        tl2_rec(2);
-        return;
-    }
     float* lds = L.tiles;
-    const uint32_t round = (uint32_t)st->iters + 1u;
-    if (blk == nab && threadIdx.x == 0 && (int32_t)(round & 1u) != par_next)   // never expected
-        __hip_atomic_store(&st->error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // Arrival on counter c (handoff_arrive); returns whether this block arrived last.
-    auto arrive = [&](uint32_t* c, uint32_t members) -> bool {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) flag = handoff_arrive(c, round * members - 1u);
-        __syncthreads();
-        return flag != 0;
-    };
     // The last arrival of the iteration: tiny chunks' sums, then the per-layer
     // means, the history and the stop rule.
     auto finish = [&]() {
 #ifdef DFQ_DIAGNOSTICS
         const uint64_t tf0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (threadIdx.x == 0 && F.nchunks > F.nbig)   // tiny chunks exist (none in the zoo's models)
+        if (threadIdx.x == 0 && F.nchunks > F.nbig)   // tiny chunks exist (fallback schedule only)
             for (int64_t k = 0; k < F.nchunks; ++k) {
                 const CleChunk c2 = chunks[k];
                 if (c2.len < 8) st_coh(F.part + (int64_t)c2.layer * F.S + c2.t, 0.f + cle_tiny_chunk_sum(layers, c2));
@@ -1419,11 +1410,11 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         const bool stage_part = (int64_t)F.nl * (F.S + 2) + (int64_t)(sizeof(CleState) / 4) + 2048 <= kCleTile;
         if (F.nl <= 128)   // numpy's pairwise sum over the layer means is one leaf
             cle_final_body<true, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st, reinterpret_cast<double*>(lds),
-                                       stage_part ? lds + 2048 : nullptr, nullptr, F.hflag, F.sig, F.gen);
+                                       stage_part ? lds + 2048 : nullptr, nullptr, F.hflag);
         else   // the frame stack after the metric tile area (free: this block's units are done)
             cle_final_body<false, true>(layers, F.nl, F.part, F.S, F.means, F.hist, st,
                                         reinterpret_cast<double*>(lds), stage_part ? lds + 2048 : nullptr,
-                                        lds + kCleTile, F.hflag, F.sig, F.gen);
+                                        lds + kCleTile, F.hflag);
 #ifdef DFQ_DIAGNOSTICS
         if (tl2 && threadIdx.x == 0) {
             uint64_t* r = g_cle_tl2 + 4 * kCleTl2Fin;
@@ -1432,8 +1423,39 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         }
 #endif
     };
-    if (F.nbig == 0) {   // no chunk has tiles (tiny or no target layers): the last launch's one block finishes
-        if (blk == nab && F.last) finish();
+    if (stop_it >= 0) {   // lagged schedule: the stop rule of iteration stop_it, a block of its own
+        if (blk == 0) {
+            finish();
+            return;
+        }
+        blk -= 1;
+    }
+    const int64_t ntiles = nto + ntp;
+    if (blk >= ntiles) {   // next-iteration ranges of tensors final by now
+        blk -= ntiles;
+        const bool own = blk < nro;
+        const int64_t b = own ? blk : blk - nro;
+        // own: iteration g's tasks (ranges of g + 1); prev: iteration g - 1's (ranges of g)
+        cle_range_body(rels, rtasks, own ? ro : rp, (own ? ro : rp) + (own ? nro_t : nrp_t), rng, M,
+                       own ? (g + 1) & 1 : g & 1, b, own ? nro : nrp, L.tiles);
+        tl2_rec(2);
+        return;
+    }
+    const bool own = blk < nto;
+    const int32_t it = own ? g : g - 1;                    // the tiles' iteration
+    const int64_t tb = own ? blk : blk - nto;
+    const int64_t tnb = own ? nto : ntp;
+    const uint32_t round = (uint32_t)it + 1u;
+    // Arrival on counter c (handoff_arrive); returns whether this block arrived last.
+    auto arrive = [&](uint32_t* c, uint32_t members) -> bool {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) flag = handoff_arrive(c, round * members - 1u);
+        __syncthreads();
+        return flag != 0;
+    };
+    if (F.nbig == 0) {   // no chunk has tiles (tiny or no target layers): the fallback launch's one block finishes
+        if (own && tb == 0 && F.last) finish();
         return;
     }
     const uint32_t fin_members = (uint32_t)F.nbig;
@@ -1460,11 +1482,42 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
                 if (threadIdx.x == 0) st_coh(F.part + (int64_t)ch.layer * F.S + ch.t, 0.f + fa);
             }
         }
-        if (arrive(F.cnt + F.nchunks, fin_members)) finish();   // the iteration's last arrival
+        if (F.stop_arrival && arrive(F.cnt + F.nchunks, fin_members)) finish();   // the iteration's last arrival
     };
-    cle_tiles_body<decltype(hook)>(layers, chunks, b1off, units + u0, u1 - u0, b1buf, tailbuf, blk - nab, ntb, lds,
-                   lds + kCleTile + kCleTailWords, hook);
+    cle_tiles_body<decltype(hook)>(layers, chunks, b1off, units + (own ? uo : up), own ? nuo : nup, b1buf, tailbuf, tb,
+                                   tnb, lds, lds + kCleTile + kCleTailWords, hook);
     tl2_rec(1);
+}
+
+// After the loop: undo a speculative iteration (the lagged schedule's iteration
+// A = st->iters, started before stop(A - 1) said done).  Weights: every target
+// layer := its snapshot (iteration A - 1's weights; the tiles of A - 1 wrote it
+// before any rescale of A touched the tensor).  Vectors (B1, BN fake weight / bias,
+// S): restored from the saves of every per-channel task that ran in iteration A.
+// Correct whether or not iteration A started: without it the weights equal their
+// snapshots already and no save carries A.
+__global__ void __launch_bounds__(kThreads)
+cle_loop_rollback_kernel(const CleLayer* __restrict__ layers, int32_t nl, const CleRel* __restrict__ rels,
+                         const CleTask* __restrict__ atasks, int64_t n_at, const float* __restrict__ vsave,
+                         const int32_t* __restrict__ vtag, const CleState* __restrict__ st) {
+    const int32_t A = st->iters;
+    const int64_t gt = (int64_t)blockIdx.x * kThreads + threadIdx.x, gs = (int64_t)gridDim.x * kThreads;
+    for (int32_t l = 0; l < nl; ++l) {
+        const CleLayer Ly = layers[l];
+        for (int64_t i = gt; i < Ly.n; i += gs) Ly.w[i] = Ly.snap[i];
+    }
+    for (int64_t t = blockIdx.x; t < n_at; t += gridDim.x) {
+        const CleTask tk = atasks[t];
+        if (tk.kind != kApplyChannels || vtag[t] != A) continue;
+        const CleRel& R = rels[tk.rel];
+        const float* v = vsave + 2 * R.moff;
+        for (int64_t c = tk.a + threadIdx.x; c < tk.b; c += kThreads) {
+            if (R.b1) R.b1[c] = v[c];
+            if (R.bnw) R.bnw[c] = v[R.c1 + c];
+            if (R.bnb) R.bnb[c] = v[2 * R.c1 + c];
+            if (R.sacc) R.sacc[c] = v[3 * R.c1 + c];
+        }
+    }
 }
 
 }  // namespace dfq
@@ -1508,7 +1561,13 @@ struct dfq_cle_plan {
     uint32_t* d_cnt = nullptr;      // tiles_fin arrival counters [nchunks + 1]
     int64_t nbig = 0;               // chunks with tiles
     int64_t ri0 = 0, ri1 = 0;       // fused: each iteration's range tasks (the rest come from the rescales)
-    std::vector<int64_t> ulaunch, rlaunch;   // per launch k = 0..steps: units / range tasks [v[k], v[k + 1])
+    std::vector<int64_t> uoffs, roffs;   // per offset k < 2 nlaunch: units / range tasks [v[k], v[k + 1])
+    int32_t nlaunch = 0;                 // launches per iteration group (steps, + 1 for a tiles-only launch)
+    int32_t stop_off = -1;               // lagged: the stop rule's block offset (else the last tile arrival)
+    bool lagged = false;                 // some tiles run in the next group (speculative iterations)
+    float* d_vsave = nullptr;            // lagged: per-channel vectors before the iteration's multiply [2 M]
+    int32_t* d_vtag = nullptr;           // ... and the iteration that saved them, per rescale task
+    int64_t n_at = 0;                    // rescale tasks
     int dev = 0;
     struct CleAsync* async = nullptr;   // dfq_cle_plan_launch's worker and result
     bool abandoned = false;             // join gave up waiting for the launched loop
@@ -1890,82 +1949,187 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 for (int64_t g = 0; g <= nb1; ++g) units.push_back(CleUnit{ci, (int32_t)g});
         }
     }
-    // Each metric unit and each next-iteration range task runs in the launch right
-    // after the last step that rescales its tensor (cle_loop_step_kernel): launch
-    // k <= steps; resets of a relation's words after that relation's own step.
-    // The unfused schedule keeps them all in the last launch.
-    std::vector<int64_t> ulaunch(steps + 2, 0), rlaunch(steps + 2, 0);
-    // Every metric tile and next-iteration range task goes to the last launch (after
-    // the last step): placing each tensor's tiles and ranges in the launch right
-    // after its last rescale (diagnostics DFQ_CLE_TILES_EARLY=1) measured slower on
-    // every box -- MobileNetV2 CLE 3.89 vs 3.65 ms, ResNet-50 2.69 vs 2.62
-    // (profiles/r04/cle_ab_r04g.jsonl): beside the step's latency-bound rescale
-    // tasks they lengthen the chain's critical path.
-    const bool tiles_last = ab_env("DFQ_CLE_TILES_EARLY") == nullptr;
-    const bool ranges_last = ab_env("DFQ_CLE_RANGES_EARLY") == nullptr;   // the same A/B for the range tasks alone
-    {
-        std::vector<int32_t> last_step(n_targets, -1);
-        std::unordered_map<const float*, int32_t> layer_of;
-        for (int32_t l = 0; l < n_targets; ++l) layer_of[targets[l]] = l;
-        auto touch = [&](const float* w, int32_t k) {
-            auto it = layer_of.find(w);
-            if (it != layer_of.end()) last_step[it->second] = std::max(last_step[it->second], k);
-        };
-        for (int32_t r = 0; r < n_rel; ++r) {
-            touch(R[r].w1, step_of[r]);
-            touch(R[r].w2, step_of[r]);
+    // Placement of the metric tiles and the next iteration's range tasks.  An
+    // iteration group has nlaunch launches: the steps' rescale launches (and, in the
+    // round-4 schedule, one tiles-only launch after them).  Every tile unit and
+    // range task gets an OFFSET in [0, 2 nlaunch): offset k < nlaunch runs in
+    // launch k of its own iteration's group, offset nlaunch + k in launch k of the
+    // next group.  A tensor's tiles and ranges must run after its last rescale of
+    // iteration i and before its first rescale of iteration i + 1: offsets
+    // [last + 1, nlaunch + first - 1].  Resets of a relation's range words go after
+    // that relation's own step and before the next accumulation.
+    // Lagged schedule (nlaunch = steps: no tiles-only launch): the tiles of one
+    // iteration sit in a band of nlaunch - 1 offsets and the stop rule runs as a
+    // block of its own one offset after the band (it reads the chunk sums the
+    // tiles' last arrivals left, after a launch boundary): iteration i's stop rule
+    // runs beside the rescale tasks of iteration i + 1 instead of after a serial
+    // tile -> chunk-combine -> stop-rule chain in a launch of its own, and every
+    // tile of iteration i + 1 starts after it (cle_loop_step_kernel).
+    // MobileNetV2: 4 -> 3 launches per iteration.  Needs the fused range schedule
+    // and no tiny chunks (the stop rule takes their sums from the live weights);
+    // where no band fits (ResNet-50: a tensor rescaled at both steps) or without
+    // lag (DFQ_CLE_LAG=0, diagnostics): the round-4 schedule, everything in the
+    // tiles-only launch and the stop rule at the last tile arrival.
+    const bool tiny = std::any_of(chunks.begin(), chunks.end(), [](const CleChunk& c) { return c.len < 8; });
+    const bool have_tiles = std::any_of(chunks.begin(), chunks.end(), [](const CleChunk& c) { return c.len >= 8; });
+    bool lag_ok = fused && !tiny && have_tiles && steps > 0;
+    if (const char* e = ab_env("DFQ_CLE_LAG")) lag_ok = lag_ok && e[0] != '0';
+    int32_t band_force = -1;   // diagnostics A/B: the tiles' band start
+    if (const char* e = ab_env("DFQ_CLE_BAND")) band_force = atoi(e);
+    std::unordered_map<const float*, std::pair<int32_t, int32_t>> span;   // tensor -> (first, last) step
+    for (int32_t r = 0; r < n_rel; ++r)
+        for (const float* w : {(const float*)R[r].w1, (const float*)R[r].w2}) {
+            auto it = span.find(w);
+            if (it == span.end()) span[w] = {step_of[r], step_of[r]};
+            else it->second = {std::min(it->second.first, step_of[r]), std::max(it->second.second, step_of[r])};
         }
-        auto launch_of_w = [&](const float* w) -> int32_t {
-            if (!fused || ranges_last) return steps;
-            auto it = layer_of.find(w);
-            int32_t k = 0;
-            for (int32_t r = 0; r < n_rel; ++r)   // a tensor that is no target: after its relations' steps
-                if (R[r].w1 == w || R[r].w2 == w) k = std::max(k, step_of[r] + 1);
-            if (it != layer_of.end()) k = std::max(k, last_step[it->second] + 1);
-            return std::min(k, steps);
-        };
-        std::vector<std::vector<CleUnit>> ub(steps + 1);
-        for (const CleUnit& u : units) {
-            const int32_t l = chunks[u.chunk].layer;
-            ub[(fused && !tiles_last) ? std::min(last_step[l] + 1, steps) : steps].push_back(u);
+    // loads (bytes) per launch position of a group: the steps' rescale traffic
+    std::vector<double> base_load(steps + 1, 0.0);
+    for (int32_t k = 0; k < steps; ++k)
+        for (int64_t t = astep[k]; t < astep[k + 1]; ++t) {
+            const CleTask& tk = at[t];
+            const CleRel& q = R[tk.rel];
+            double n = 0;
+            if (tk.kind == kApplyW1) n = (double)(tk.b - tk.a) * q.len1;
+            else if (tk.kind == kApplyW2Tile) n = (double)(tk.b - tk.a) * (tk.c1 - tk.c0) * q.khw2;
+            else if (tk.kind != kApplyChannels) n = (double)(tk.b - tk.a) * q.o2g * q.khw2;
+            base_load[k] += 8.0 * n;
         }
-        // the stop rule runs at the iteration's last arrival, which must come in the
-        // last launch (after every rescale): if no unit landed there (the last
-        // step's tensors are all tiny), every unit goes there
-        if (ub[steps].empty())
-            for (int32_t k = 0; k < steps; ++k) {
-                ub[steps].insert(ub[steps].end(), ub[k].begin(), ub[k].end());
-                ub[k].clear();
+    auto range_bytes = [&](const CleTask& tk) -> double {
+        const CleRel& q = R[tk.rel];
+        switch (tk.kind) {
+            case kRangeW1: return 4.0 * (tk.b - tk.a) * q.len1;
+            case kRangeW2Contig: return 4.0 * (tk.b - tk.a) * q.o2g * q.khw2;
+            case kRangeW2Tile: return 4.0 * (tk.b - tk.a) * (tk.c1 - tk.c0) * q.khw2;
+            default: return 64.0;
+        }
+    };
+    std::vector<int32_t> layer_off(n_targets, 0);
+    int32_t stop_off = -1;   // lagged: the stop rule's own block at this offset (else: the last tile arrival)
+    std::vector<int32_t> rt_off;   // per task of [ri0, ri1)
+    int32_t nlaunch = steps + 1;
+    bool lagged = false;
+    // windows: [lo, hi] offsets for a tensor (untouched: anywhere)
+    auto window = [&](const float* w, int32_t nl_) -> std::pair<int32_t, int32_t> {
+        auto it = span.find(w);
+        if (it == span.end()) return {0, 2 * nl_ - 1};
+        return {it->second.second + 1, std::min(2 * nl_ - 1, nl_ + it->second.first - 1)};
+    };
+    auto place = [&](int32_t nl_) -> bool {
+        // range tasks: their own windows
+        std::vector<std::pair<int32_t, int32_t>> rwin;
+        for (int64_t t = ri0; t < ri1; ++t) {
+            const CleTask& tk = rt[t];
+            const CleRel& q = R[tk.rel];
+            std::pair<int32_t, int32_t> w;
+            if (tk.kind == kRangeW1) w = window(q.w1, nl_);
+            else if (tk.kind == kRangeW2Contig || tk.kind == kRangeW2Tile) w = window(q.w2, nl_);
+            else if (tk.kind == kRangeReset) {   // after the consumer step, before the next accumulation (>= nl_ + last + 1)
+                const auto it = span.find(q.w2);
+                w = {step_of[tk.rel] + 1, std::min(2 * nl_ - 1, nl_ + (it == span.end() ? 0 : it->second.second))};
+            } else {   // kRangeResetW1: after the consumer step, before the producer's step two groups on
+                w = {step_of[tk.rel] + 1, 2 * nl_ - 1};
             }
+            if (w.first > w.second) return false;
+            rwin.push_back(w);
+        }
+        // tiles: a band [B0, B0 + nl_ - 2] meeting every layer's window; the stop
+        // rule one offset after the band's last used offset
+        int32_t maxlo = 0, minhi = 2 * nl_ - 1;
+        std::vector<std::pair<int32_t, int32_t>> lwin(n_targets);
+        for (int32_t l = 0; l < n_targets; ++l) {
+            lwin[l] = window(targets[l], nl_);
+            if (lwin[l].first > lwin[l].second) return false;
+            maxlo = std::max(maxlo, lwin[l].first);
+            minhi = std::min(minhi, lwin[l].second);
+        }
+        const int32_t bw = nl_ - 1;   // band width
+        if (bw < 1) return false;
+        const int32_t b_lo = std::max(0, maxlo - bw + 1), b_hi = std::min(minhi, 2 * nl_ - 1 - bw);
+        if (b_lo > b_hi) return false;
+        std::vector<int32_t> lord(n_targets);
+        std::iota(lord.begin(), lord.end(), 0);
+        std::stable_sort(lord.begin(), lord.end(), [&](int32_t x, int32_t y) { return target_n[x] > target_n[y]; });
+        std::vector<int64_t> rord(rwin.size());
+        std::iota(rord.begin(), rord.end(), 0);
+        std::stable_sort(rord.begin(), rord.end(),
+                         [&](int64_t x, int64_t y) { return range_bytes(rt[ri0 + x]) > range_bytes(rt[ri0 + y]); });
+        double best = 1e300;
+        for (int32_t B0 = b_lo; B0 <= b_hi; ++B0) {
+            if (band_force >= 0 && B0 != band_force && band_force >= b_lo && band_force <= b_hi) continue;
+            std::vector<double> load(nl_, 0.0);
+            for (int32_t k = 0; k < steps && k < nl_; ++k) load[k] = base_load[k];
+            auto pick = [&](int32_t lo, int32_t hi, double bytes) {
+                int32_t bo = lo;
+                for (int32_t o = lo; o <= hi; ++o)
+                    if (load[o % nl_] < load[bo % nl_]) bo = o;
+                load[bo % nl_] += bytes;
+                return bo;
+            };
+            std::vector<int32_t> roff(rwin.size()), loff(n_targets);
+            for (int64_t x : rord) roff[x] = pick(rwin[x].first, rwin[x].second, range_bytes(rt[ri0 + x]));
+            int32_t maxoff = 0;
+            for (int32_t l : lord) {
+                loff[l] = pick(std::max(lwin[l].first, B0), std::min(lwin[l].second, B0 + bw - 1), 12.0 * target_n[l]);
+                maxoff = std::max(maxoff, loff[l]);
+            }
+            if (maxoff + 1 > 2 * nl_ - 1) continue;
+            double cost = *std::max_element(load.begin(), load.end());
+            if (cost < best) {
+                best = cost;
+                layer_off = loff;
+                rt_off = roff;
+                stop_off = maxoff + 1;
+            }
+        }
+        return best < 1e300;
+    };
+    if (lag_ok && place(steps) && stop_off >= steps) {
+        nlaunch = steps;
+        lagged = true;
+    } else {   // everything in the tiles-only launch after the steps (offset steps), the stop rule at the last arrival
+        nlaunch = steps + 1;
+        stop_off = -1;
+        layer_off.assign(n_targets, steps);
+        rt_off.assign((size_t)(ri1 - ri0), steps);
+    }
+    std::vector<int64_t> uoffs(2 * nlaunch + 1, 0), roffs(2 * nlaunch + 1, 0);
+    {
+        std::vector<std::vector<CleUnit>> ub(2 * nlaunch);
+        for (const CleUnit& u : units) ub[layer_off[chunks[u.chunk].layer]].push_back(u);
         units.clear();
-        for (int32_t k = 0; k <= steps; ++k) {
-            ulaunch[k] = (int64_t)units.size();
+        for (int32_t k = 0; k < 2 * nlaunch; ++k) {
+            uoffs[k] = (int64_t)units.size();
             units.insert(units.end(), ub[k].begin(), ub[k].end());
         }
-        ulaunch[steps + 1] = (int64_t)units.size();
-        if (fused) {   // (the unfused schedule's range tasks are per step: rstep)
-            std::vector<std::vector<CleTask>> rb(steps + 1);
-            for (int64_t t = ri0; t < ri1; ++t) {
-                const CleTask tk = rt[t];
-                const CleRel& q = R[tk.rel];
-                int32_t k;
-                if (tk.kind == kRangeW1) k = launch_of_w(q.w1);
-                else if (tk.kind == kRangeW2Contig || tk.kind == kRangeW2Tile) k = launch_of_w(q.w2);
-                else k = ranges_last ? steps : std::min(step_of[tk.rel] + 1, steps);   // resets: after the relation's own step
-                rb[k].push_back(tk);
-            }
+        uoffs[2 * nlaunch] = (int64_t)units.size();
+        if (fused) {   // (the unfused schedule's range tasks are per step: rstep; roffs stay empty)
+            std::vector<std::vector<CleTask>> rb(2 * nlaunch);
+            for (int64_t t = ri0; t < ri1; ++t) rb[rt_off[t - ri0]].push_back(rt[t]);
             rt.resize(ri0);
-            for (int32_t k = 0; k <= steps; ++k) {
-                rlaunch[k] = (int64_t)rt.size();
+            for (int32_t k = 0; k < 2 * nlaunch; ++k) {
+                roffs[k] = (int64_t)rt.size();
                 rt.insert(rt.end(), rb[k].begin(), rb[k].end());
             }
-            rlaunch[steps + 1] = (int64_t)rt.size();
+            roffs[2 * nlaunch] = (int64_t)rt.size();
             ri1 = (int64_t)rt.size();
         }
     }
+    if (cle_timing()) {   // the schedule: per offset, tile units and range tasks
+        fprintf(stderr, "DFQ_CLE_TIMING plan: steps %d nlaunch %d lagged %d stop %d; offsets (units/ranges):", steps,
+                nlaunch, (int)lagged, stop_off);
+        for (int32_t k = 0; k < 2 * nlaunch; ++k)
+            fprintf(stderr, " %d:%lld/%lld", k, (long long)(uoffs[k + 1] - uoffs[k]), (long long)(roffs[k + 1] - roffs[k]));
+        fprintf(stderr, "; rescale tasks per step:");
+        for (int32_t k = 0; k < steps; ++k) fprintf(stderr, " %lld", (long long)(astep[k + 1] - astep[k]));
+        fprintf(stderr, "\n");
+    }
     (void)hipGetDevice(&p->dev);
-    p->ulaunch = ulaunch;
-    p->rlaunch = rlaunch;
+    p->uoffs = uoffs;
+    p->roffs = roffs;
+    p->nlaunch = nlaunch;
+    p->lagged = lagged;
+    p->stop_off = stop_off;
     p->nunits = (int64_t)units.size();
     p->M = M;
     p->nl = n_targets;
@@ -2011,6 +2175,8 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const int64_t o_state = T.add<CleState>(1);
     const int64_t o_hist = T.add<double>(kCleHistCap);
     const int64_t o_cnt = T.add<uint32_t>((int64_t)chunks.size() + 1);
+    const int64_t o_vsave = T.add<float>(lagged ? 2 * M : 0);
+    const int64_t o_vtag = T.add<int32_t>(lagged ? (int64_t)at.size() : 0);
     const double tm0 = now_us();
     char* base = nullptr;
     char* hblob = nullptr;
@@ -2089,14 +2255,22 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->d_state = reinterpret_cast<CleState*>(base + o_state);
     p->d_hist = p->d_hist_tables = reinterpret_cast<double*>(base + o_hist);
     p->d_cnt = reinterpret_cast<uint32_t*>(base + o_cnt);
+    p->n_at = (int64_t)at.size();
+    if (lagged) {
+        p->d_vsave = reinterpret_cast<float*>(base + o_vsave);
+        p->d_vtag = reinterpret_cast<int32_t*>(base + o_vtag);
+    }
     for (const auto& c : chunks) p->nbig += c.len >= 8 ? 1 : 0;
     *out = p;
     return DFQ_OK;
 }
 
-// One CLE iteration's launches (steps, metric, stop rule) on stream s.
-// j: the iteration's index in the run (its parity is j & 1).
-static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
+// Iteration group g's launches on stream s: the rescale steps of iteration g
+// (g < max_iters), the tiles and ranges of iteration g placed in this group and
+// those of iteration g - 1 placed in the next group (cle_loop_step_kernel).
+// Groups 0 .. max_iters are enqueued (the last only finishes iteration
+// max_iters - 1).
+static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t g, int32_t max_iters) {
     // grid caps: 2,048 / 4,096 blocks (caps of 128-1,024 measured 4-150 % slower on MobileNetV2)
     // step / tile grid caps (A/B: DFQ_CLE_STEP_GRID / DFQ_CLE_TILE_GRID, diagnostics library;
     // read per call, not cached: cle_ab.py switches them between runs of one process)
@@ -2108,33 +2282,40 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t j) {
         const char* e = ab_env("DFQ_CLE_TILE_GRID");
         return e && *e ? std::max<int64_t>(1, atoll(e)) : int64_t(4096);
     }();
-    // fused schedule: this iteration's ranges were taken during the previous one
-    // (or by plan_run before the first); the next iteration's ride with the
-    // launches after their tensors' last rescale (cle_loop_step_kernel)
     CleFin F{p->d_cnt, p->d_part, p->d_means, p->d_hist, p->nchunks, p->nbig, p->slots, p->nl, 0, p->d_flag,
-             p->d_sig, p->gen};
-    for (int32_t k = 0; k <= p->steps; ++k) {
-        const bool last = k == p->steps;
-        const int64_t a0 = last ? 0 : p->astep[k], a1 = last ? 0 : p->astep[k + 1];
-        if (!last && !p->fused && p->rstep[k + 1] > p->rstep[k]) {   // unfused: this step's ranges first
+             p->stop_off < 0 ? 1 : 0};
+    const int32_t NL = p->nlaunch;
+    const bool run_g = g < max_iters, prev = g >= 1;
+    for (int32_t k = 0; k < NL; ++k) {
+        const bool step = k < p->steps;
+        const int64_t a0 = step ? p->astep[k] : 0, a1 = step ? p->astep[k + 1] : 0;
+        if (step && run_g && !p->fused && p->rstep[k + 1] > p->rstep[k]) {   // unfused: this step's ranges first
             hipLaunchKernelGGL(cle_loop_range_kernel, dim3((int)std::min<int64_t>(p->rstep[k + 1] - p->rstep[k], kStepGrid)),
                                dim3(kThreads), 0, s, p->d_rels, p->d_rtasks, p->rstep[k], p->rstep[k + 1], p->d_rng,
                                p->M, p->d_state, 0);
             DFQ_LAUNCH_CHECK();
         }
-        const int64_t u0 = p->ulaunch[k], u1 = p->ulaunch[k + 1];
-        const int64_t r0 = p->fused ? p->rlaunch[k] : 0, r1 = p->fused ? p->rlaunch[k + 1] : 0;
-        const int64_t nab = std::min<int64_t>(a1 - a0, kStepGrid);
-        int64_t ntb = std::min<int64_t>(u1 - u0, kTileGrid);
-        if (last) ntb = std::max<int64_t>(ntb, 1);   // the stop rule's block when no chunk has tiles
-        const int64_t nrb = std::min<int64_t>(r1 - r0, kStepGrid);
-        if (nab + ntb + nrb == 0) continue;
-        F.last = last ? 1 : 0;
-        auto kern = (!last && p->step_pos[k]) ? cle_loop_step_kernel<true> : cle_loop_step_kernel<false>;
-        hipLaunchKernelGGL(kern, dim3((int)(nab + ntb + nrb)), dim3(kThreads), 0, s, p->d_rels, p->d_atasks, a0, a1, nab,
-                           p->d_rng, p->M, p->is_signed, p->eps, p->smin, p->smax, p->d_layers, p->d_chunks,
-                           p->d_b1off, p->d_units, u0, u1, ntb, p->d_b1, p->d_tail, p->d_rtasks, r0, r1, F, p->d_state,
-                           (j + 1) & 1);
+        const int64_t nab = run_g ? std::min<int64_t>(a1 - a0, kStepGrid) : 0;
+        const int64_t uo = p->uoffs[k], nuo = run_g ? p->uoffs[k + 1] - uo : 0;
+        const int64_t up = p->uoffs[NL + k], nup = prev ? p->uoffs[NL + k + 1] - up : 0;
+        const int64_t ro = p->roffs[k], nro_t = (g + 1 < max_iters) ? p->roffs[k + 1] - ro : 0;
+        const int64_t rp = p->roffs[NL + k], nrp_t = (prev && run_g) ? p->roffs[NL + k + 1] - rp : 0;
+        int64_t nto = std::min<int64_t>(nuo, kTileGrid);
+        const int64_t ntp = std::min<int64_t>(nup, kTileGrid);
+        F.last = (k == p->steps) ? 1 : 0;
+        if (F.last && run_g && p->nbig == 0) nto = std::max<int64_t>(nto, 1);   // the stop rule's block without tiles
+        const int64_t nro = std::min<int64_t>(nro_t, kStepGrid), nrp = std::min<int64_t>(nrp_t, kStepGrid);
+        // lagged schedule: the stop rule's block (iteration g's, or g - 1's placed in this group)
+        int32_t stop_it = -1;
+        if (p->stop_off == k && run_g) stop_it = g;
+        else if (p->stop_off == NL + k && prev) stop_it = g - 1;
+        const int64_t nblk = nab + (stop_it >= 0 ? 1 : 0) + nto + ntp + nro + nrp;
+        if (nblk == 0) continue;
+        auto kern = (step && p->step_pos[k]) ? cle_loop_step_kernel<true> : cle_loop_step_kernel<false>;
+        hipLaunchKernelGGL(kern, dim3((int)nblk), dim3(kThreads), 0, s, p->d_rels, p->d_atasks, a0, a1, nab, p->d_rng,
+                           p->M, p->is_signed, p->eps, p->smin, p->smax, p->d_layers, p->d_chunks, p->d_b1off,
+                           p->d_units, uo, nuo, nto, up, nup, ntp, p->d_b1, p->d_tail, p->d_rtasks, ro, nro_t, nro, rp,
+                           nrp_t, nrp, F, p->d_state, g, p->d_vsave, p->d_vtag, stop_it);
         DFQ_LAUNCH_CHECK();
     }
     return DFQ_OK;
@@ -2214,6 +2395,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     }
     DFQ_HIP_CHECK(hipMemsetAsync(p->d_part, 0, sizeof(float) * p->slots * std::max(p->nl, 1), s));
     DFQ_HIP_CHECK(hipMemsetAsync(p->d_cnt, 0, sizeof(uint32_t) * (p->nchunks + 1), s));
+    if (p->d_vtag && p->n_at > 0) DFQ_HIP_CHECK(hipMemsetAsync(p->d_vtag, 0xFF, sizeof(int32_t) * p->n_at, s));
     if (p->nchunks > 0) {
         hipLaunchKernelGGL(cle_loop_snap_kernel, dim3((int)std::min<int64_t>(std::max<int64_t>(p->nunits, 1), 4096)),
                            dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_units, p->nunits);
@@ -2263,6 +2445,13 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     const double tc1 = now_us();
     int32_t launched = 0;
     bool deadline_hit = false;
+#ifdef DFQ_DIAGNOSTICS
+    const char* pd = ab_env("DFQ_CLE_TEST_POLL_DELAY_US");
+    const int poll_delay_us = pd ? atoi(pd) : 0;
+    const double quiet_us = pd ? 0.0 : kClePollQuietUs;   // the query on every poll, as round 4 did
+#else
+    const double quiet_us = kClePollQuietUs;
+#endif
     if (!init.done) {
         uint32_t last_f = ~0u;
         double t_moved = tc1;
@@ -2270,22 +2459,27 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             const uint32_t f = __atomic_load_n(ctx.h_flag, __ATOMIC_ACQUIRE);
             if (f & 1u) break;
             const int32_t ran = (int32_t)(f >> 1);   // iterations complete
-            if (launched < max_iters && !deadline_hit && launched - ran <= kCleAhead) {
-                const int rc = cle_enqueue_iteration(p, s, launched);
+            if (launched <= max_iters && !deadline_hit && launched - ran <= kCleAhead) {
+                const int rc = cle_enqueue_iteration(p, s, launched, max_iters);
                 if (rc != DFQ_OK) return rc;
                 ++launched;
                 continue;
             }
+#ifdef DFQ_DIAGNOSTICS
+            // test switch: the polling thread descheduled between its load of the word
+            // and the stream query below (the stale-word race of ADVICE r04)
+            if (poll_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(poll_delay_us));
+#endif
             const double t = now_us();
             if (f != last_f) {
                 last_f = f;
                 t_moved = t;
-            } else if (t - t_moved > kClePollQuietUs) {
+            } else if (t - t_moved >= quiet_us) {
                 const hipError_t q = hipStreamQuery(s);
                 if (q != hipErrorNotReady) {
                     if (q != hipSuccess) break;   // a device error: the synchronize below reports it
                     const uint32_t f2 = __atomic_load_n(ctx.h_flag, __ATOMIC_ACQUIRE);
-                    if ((f2 & 1u) || launched >= max_iters || deadline_hit || (int32_t)(f2 >> 1) < launched) break;
+                    if ((f2 & 1u) || launched > max_iters || deadline_hit || (int32_t)(f2 >> 1) + 1 < launched) break;
                 }
                 t_moved = t;
             }
@@ -2293,6 +2487,12 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             __builtin_ia32_pause();
         }
     }
+    if (!init.done && p->lagged) {   // undo a speculative iteration, then release a launched run's caller
+        hipLaunchKernelGGL(cle_loop_rollback_kernel, dim3(1024), dim3(kThreads), 0, s, p->d_layers, p->nl, p->d_rels,
+                           p->d_atasks, p->n_at, p->d_vsave, p->d_vtag, p->d_state);
+        DFQ_LAUNCH_CHECK();
+    }
+    if (p->d_sig) DFQ_HIP_CHECK(hipStreamWriteValue64(s, p->d_sig, p->gen, 0));
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
     if (cle_timing())
         fprintf(stderr, "DFQ_CLE_TIMING run: loop %.1f us (%d iterations launched)\n", now_us() - tc1, launched);
@@ -2639,9 +2839,9 @@ extern "C" int dfq_cle_plan_launch(dfq_cle_plan* p, double threshold, int32_t co
     }
     p->async = a;
     ctx.pending = p;
-    p->d_sig = static_cast<uint64_t*>(ctx.sig);   // the stop rule opens the gate at convergence
+    p->d_sig = static_cast<uint64_t*>(ctx.sig);   // released behind the loop's rollback (cle_run_locked)
+    if (ab_env("DFQ_CLE_HOST_RELEASE")) p->d_sig = nullptr;   // diagnostics: only the worker's release, after the run
     p->gen = gen;
-    if (ab_env("DFQ_CLE_HOST_RELEASE")) p->d_sig = nullptr;   // diagnostics: the worker's release only
     bool posted = false;
     try {
         if (!ctx.worker) {
@@ -2693,8 +2893,8 @@ extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t
     if (chains) *chains = p->chains;
     if (steps) *steps = p->steps;
     // per iteration: the rescale launches (+ per-step range launches when the
-    // schedule is not fused), then tiles + next ranges + chunk combine + stop rule
-    if (launches) *launches = (p->fused ? p->steps : 2 * p->steps) + 1;
+    // schedule is not fused), + a tiles-only launch unless the schedule is lagged
+    if (launches) *launches = p->fused ? p->nlaunch : 2 * p->steps + 1;
     return DFQ_OK;
 }
 

@@ -21,18 +21,16 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
-SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_HOST_RELEASE",
-            "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY", "CLE_AB_BLOCKING")
+SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "CLE_AB_BLOCKING")
 CONFIGS = {
-    "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
+    "tiles_fin": {},                                # the product (lagged schedule where the plan allows it)
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
     "tile_grid_1024": {"DFQ_CLE_TILE_GRID": "1024"},
     "step_grid_1024": {"DFQ_CLE_STEP_GRID": "1024"},
     "step_grid_4096": {"DFQ_CLE_STEP_GRID": "4096"},
-    "host_release": {"DFQ_CLE_HOST_RELEASE": "1"},  # launched runs: the worker's release only
-    "tiles_early": {"DFQ_CLE_TILES_EARLY": "1", "DFQ_CLE_RANGES_EARLY": "1"},   # each tensor's tiles / ranges right after its last rescale
-    "ranges_early": {"DFQ_CLE_RANGES_EARLY": "1"},  # only the range tasks early
-    "units_early": {"DFQ_CLE_TILES_EARLY": "1"},    # only the metric tiles early
+    "no_lag": {"DFQ_CLE_LAG": "0"},                 # round 4's schedule: tiles / ranges / stop rule in a launch of their own
+    "band1": {"DFQ_CLE_BAND": "1"},                 # the tiles' band start (lagged schedule)
+    "band2": {"DFQ_CLE_BAND": "2"},
     "blocking": {"CLE_AB_BLOCKING": "1"},           # run_dfq's CLE blocking (no caller gate beside the loop)
 }
 

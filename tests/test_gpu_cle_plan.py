@@ -305,7 +305,7 @@ def test_async_join_watchdog_keeps_callers_stream_held(monkeypatch):
     monkeypatch.setenv("DFQ_CLE_MODE", "device")
     monkeypatch.setenv("DFQ_CLE_TEST_RELEASE_DELAY_MS", "2500")
     monkeypatch.setenv("DFQ_CLE_TEST_JOIN_LIMIT_MS", "200")
-    monkeypatch.setenv("DFQ_CLE_HOST_RELEASE", "1")   # a loop that has not converged: no release from the stop rule
+    monkeypatch.setenv("DFQ_CLE_HOST_RELEASE", "1")   # only the worker's (delayed) release opens the gate
     g, rels = _graph(3)
     torch.cuda.synchronize()
     marker = torch.zeros(1, device=DEV)

@@ -42,12 +42,18 @@ import json, os, sys
 sys.path.insert(0, os.environ["DFQ_ROOT"])
 from tests.parity import pipeline_mismatches
 from data_free_quantization_amd import Cross_layer_equal as cle
-SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_TILES_EARLY", "DFQ_CLE_RANGES_EARLY")
+SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_TEST_POLL_DELAY_US")
 CONFIGS = {
-    "tiles_fin": {},                                # the product: tiles / ranges / stop rule in the last launch
+    "product": {},                                  # the product: lagged schedule where the plan allows it
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches (graphs the fused schedule rejects)
     "tile_grid_64": {"DFQ_CLE_TILE_GRID": "64"},    # few tile blocks: each walks many metric units
-    "tiles_early": {"DFQ_CLE_TILES_EARLY": "1", "DFQ_CLE_RANGES_EARLY": "1"},   # tiles / ranges after each tensor's last rescale
+    "no_lag": {"DFQ_CLE_LAG": "0"},                 # tiles / ranges / stop rule in a launch of their own (round 4)
+    "band1": {"DFQ_CLE_BAND": "1"},                 # lagged, the tiles' band forced
+    "band2": {"DFQ_CLE_BAND": "2"},
+    # the host thread "descheduled" 300 us after every load of the stop rule's word,
+    # then querying the stream: the queued iterations drain meanwhile (ADVICE r04's
+    # stale-word race ended the loop early here)
+    "poll_delay": {"DFQ_CLE_TEST_POLL_DELAY_US": "300"},
 }
 out = []
 for tag, env in CONFIGS.items():
@@ -63,8 +69,8 @@ print("RESULT " + json.dumps(out))
 
 
 def test_cle_schedules_equal_reference_with_oversized_range_grid():
-    """Every CLE schedule (the product's step launches, the early tile placement,
-    the per-step range launches, a small tile grid), with a range grid far above
+    """Every CLE schedule (the product's lagged launches, round 4's tiles-only
+    launch, forced tile bands, the per-step range launches, a small tile grid), with a range grid far above
     residency (every range task its own block), equals the reference fixture on
     MobileNetV2, ResNet-50 and DeepLab."""
     env = dict(os.environ, DFQ_ROOT=ROOT, DFQ_LIB="diag", DFQ_CLE_STEP_GRID="1000000", DFQ_CLE_MODE="device",
@@ -76,5 +82,9 @@ def test_cle_schedules_equal_reference_with_oversized_range_grid():
     assert all(x["mismatches"] == 0 for x in res), res
     for name in ("mobilenetv2", "resnet50", "deeplab"):   # the A/B really switched paths
         la = {x["config"]: x["launches"] for x in res if x["model"] == name}
-        assert la["unfused_steps"] > la["tiles_fin"] > 1, (name, la)
-        assert la["tile_grid_64"] == la["tiles_early"] == la["tiles_fin"], (name, la)
+        assert la["unfused_steps"] > la["product"] > 1, (name, la)
+        assert la["tile_grid_64"] == la["product"] == la["band1"] == la["poll_delay"], (name, la)
+        assert la["no_lag"] >= la["product"], (name, la)
+    # MobileNetV2 takes the lagged schedule: one launch fewer per iteration
+    la = {x["config"]: x["launches"] for x in res if x["model"] == "mobilenetv2"}
+    assert la["no_lag"] == la["product"] + 1, la
