@@ -150,6 +150,7 @@ def cross_layer_equalization(graph, relations, Target_list, s_min_max=[1e-8, 1e8
     default): True returns as soon as the loop is under way; only the device's
     current stream is ordered behind it, and its errors surface at ``wait()``."""
     print("Cross layer equalization")
+    _lib.weights_changed()
     if Save_state:
         warnings.warn("Save_state plots (ourplots.save_layer) are visualization, not part of the weight path; "
                       "skipped")

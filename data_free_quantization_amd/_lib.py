@@ -25,6 +25,7 @@ DFQ_ERR_NOMEM, DFQ_ERR_SHAPE, DFQ_ERR_WORKSPACE = -4, -5, -6
 EXPORTS = [
     "dfq_abi_version", "dfq_preload", "dfq_error_string", "dfq_last_hip_error",
     "dfq_quantize_ws_bytes", "dfq_quantize_tensor", "dfq_chunk_range", "dfq_range", "dfq_fake_quant_given",
+    "dfq_act_observe",
     "dfq_sweep_plan_create", "dfq_sweep_plan_ws_bytes", "dfq_sweep_plan_create_ws", "dfq_sweep_plan_execute",
     "dfq_sweep_plan_stats", "dfq_sweep_plan_destroy",
     "dfq_bn_fold", "dfq_bn_fold_ws_bytes", "dfq_bn_fold_batch", "dfq_clamp", "dfq_clamp_batch",
@@ -127,6 +128,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_quantize_tensor": ([C.POINTER(TensorDesc), P, SZ, P], C.c_int),
         "dfq_chunk_range": ([P, I64, I64, P, P, P], C.c_int),
         "dfq_range": ([P, I64, P, P], C.c_int),
+        "dfq_act_observe": ([P, I64, I64, P, P, P, I32, I32, F64, P, P], C.c_int),
         "dfq_fake_quant_given": ([P, P, I64, I32, I32, I32, P, P, P, F64, F64, P], C.c_int),
         "dfq_sweep_plan_create": ([C.POINTER(TensorDesc), I32, C.POINTER(P)], C.c_int),
         "dfq_sweep_plan_ws_bytes": ([C.POINTER(TensorDesc), I32], C.c_int64),
@@ -244,6 +246,18 @@ def require_device(*tensors: Optional[torch.Tensor]):
 
 def ptr(t: Optional[torch.Tensor]):
     return None if t is None else C.c_void_p(t.data_ptr())
+
+
+#: Generation of the model weights as the DFQ transforms see them: every transform
+#: that rewrites weights or biases in place through the library (which bypasses
+#: torch's version counters) advances it, so caches of derived weights
+#: (utils.quantize's per-layer fake-quant cache) know they are stale.
+WEIGHT_GENERATION = 0
+
+
+def weights_changed() -> None:
+    global WEIGHT_GENERATION
+    WEIGHT_GENERATION += 1
 
 
 #: intra-op thread count of the reference run the BC reductions reproduce

@@ -38,6 +38,7 @@ def bias_absorption(graph, relations, bottoms, N=3, visualize=False):
     """Every absorbing relation in ONE dfq_bias_absorb_batch call (two launches;
     the same per-element fp32 order as one call per relation)."""
     print("Start bias absorption")
+    _lib.weights_changed()
     if visualize:
         warnings.warn("bias-absorption histograms are visualization, not part of the weight path; skipped")
     with torch.no_grad():

@@ -541,6 +541,7 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
     assert isinstance(bottoms, dict), "Expected 'bottoms' to be a dictionary."
     assert isinstance(targ_type, (type, tuple)), "Expected 'targ_type' to be a type or tuple of types."
     logger.info("Starting bias correction...")
+    _lib.weights_changed()
     # A graph of a structure walked before replays the compiled walk: the walk's
     # control flow and every op's fields depend on the structure only (keys, node
     # types, bottoms, shapes), never on a tensor value; the addresses are bound

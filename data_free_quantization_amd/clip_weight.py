@@ -18,6 +18,7 @@ def clip_weight(graph, range_clip=None, targ_type=[nn.Conv2d, nn.Linear]):
     assert isinstance(range_clip, (list, tuple)) and len(range_clip) == 2, \
         "range_clip should be a list or tuple of two elements"
     lo, hi = float(range_clip[0]), float(range_clip[1])
+    _lib.weights_changed()
     ws = []
     for idx, layer in graph.items():
         if isinstance(layer, tuple(targ_type)):

@@ -1714,6 +1714,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         M += 2 * d.c1;
         R[r] = c;
     }
+    const double tp1 = now_us();
     // chains: connected components over the tensors a relation touches
     std::vector<int32_t> parent(n_rel);
     std::iota(parent.begin(), parent.end(), 0);
@@ -1796,6 +1797,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             steps = std::max(steps, step_of[r] + 1);
         }
     }
+    const double tp2 = now_us();
     // tasks: per-step range + rescale launches, or (fused) one range launch for
     // every relation's W2 (and untouched W1) followed by the rescale launches
     std::vector<CleTask> rt, at;
@@ -1908,6 +1910,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         if (!fused) rstep.push_back((int64_t)rt.size());
         astep.push_back((int64_t)at.size());
     }
+    const double tp3 = now_us();
     // metric chunks: torch.mean = sum / n; the sum is two_pass_reduction over
     // min(threads, ceil(n / 32768)) equal chunks when n >= 32768 (serial below)
     dfq_cle_plan* p = new (std::nothrow) dfq_cle_plan();
@@ -1949,6 +1952,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 for (int64_t g = 0; g <= nb1; ++g) units.push_back(CleUnit{ci, (int32_t)g});
         }
     }
+    const double tp4 = now_us();
     // Placement of the metric tiles and the next iteration's range tasks.  An
     // iteration group has nlaunch launches: the steps' rescale launches (and, in the
     // round-4 schedule, one tiles-only launch after them).  Every tile unit and
@@ -1976,69 +1980,93 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     if (const char* e = ab_env("DFQ_CLE_LAG")) lag_ok = lag_ok && e[0] != '0';
     int32_t band_force = -1;   // diagnostics A/B: the tiles' band start
     if (const char* e = ab_env("DFQ_CLE_BAND")) band_force = atoi(e);
-    std::unordered_map<const float*, std::pair<int32_t, int32_t>> span;   // tensor -> (first, last) step
-    for (int32_t r = 0; r < n_rel; ++r)
-        for (const float* w : {(const float*)R[r].w1, (const float*)R[r].w2}) {
-            auto it = span.find(w);
-            if (it == span.end()) span[w] = {step_of[r], step_of[r]};
-            else it->second = {std::min(it->second.first, step_of[r]), std::max(it->second.second, step_of[r])};
-        }
-    // loads (bytes) per launch position of a group: the steps' rescale traffic
-    std::vector<double> base_load(steps + 1, 0.0);
-    for (int32_t k = 0; k < steps; ++k)
-        for (int64_t t = astep[k]; t < astep[k + 1]; ++t) {
-            const CleTask& tk = at[t];
-            const CleRel& q = R[tk.rel];
-            double n = 0;
-            if (tk.kind == kApplyW1) n = (double)(tk.b - tk.a) * q.len1;
-            else if (tk.kind == kApplyW2Tile) n = (double)(tk.b - tk.a) * (tk.c1 - tk.c0) * q.khw2;
-            else if (tk.kind != kApplyChannels) n = (double)(tk.b - tk.a) * q.o2g * q.khw2;
-            base_load[k] += 8.0 * n;
-        }
-    auto range_bytes = [&](const CleTask& tk) -> double {
-        const CleRel& q = R[tk.rel];
-        switch (tk.kind) {
-            case kRangeW1: return 4.0 * (tk.b - tk.a) * q.len1;
-            case kRangeW2Contig: return 4.0 * (tk.b - tk.a) * q.o2g * q.khw2;
-            case kRangeW2Tile: return 4.0 * (tk.b - tk.a) * (tk.c1 - tk.c0) * q.khw2;
-            default: return 64.0;
-        }
+    // (first, last) step of every tensor the relations rescale: a linear table (a few
+    // hundred tensors at most), looked up once per relation and target layer
+    std::vector<const float*> sp_w;
+    std::vector<std::pair<int32_t, int32_t>> sp_v;
+    auto sp_find = [&](const float* w) -> int32_t {
+        for (size_t i = 0; i < sp_w.size(); ++i)
+            if (sp_w[i] == w) return (int32_t)i;
+        return -1;
     };
+    std::vector<int32_t> rel_t1(n_rel), rel_t2(n_rel);
+    for (int32_t r = 0; r < n_rel; ++r)
+        for (int side = 0; side < 2; ++side) {
+            const float* w = side ? R[r].w2 : R[r].w1;
+            int32_t i = sp_find(w);
+            if (i < 0) {
+                i = (int32_t)sp_w.size();
+                sp_w.push_back(w);
+                sp_v.push_back({step_of[r], step_of[r]});
+            } else {
+                sp_v[i] = {std::min(sp_v[i].first, step_of[r]), std::max(sp_v[i].second, step_of[r])};
+            }
+            (side ? rel_t2 : rel_t1)[r] = i;
+        }
+    std::vector<int32_t> lay_t(n_targets);
+    for (int32_t l = 0; l < n_targets; ++l) lay_t[l] = lag_ok ? sp_find(targets[l]) : -1;
     std::vector<int32_t> layer_off(n_targets, 0);
     int32_t stop_off = -1;   // lagged: the stop rule's own block at this offset (else: the last tile arrival)
     std::vector<int32_t> rt_off;   // per task of [ri0, ri1)
     int32_t nlaunch = steps + 1;
     bool lagged = false;
-    // windows: [lo, hi] offsets for a tensor (untouched: anywhere)
-    auto window = [&](const float* w, int32_t nl_) -> std::pair<int32_t, int32_t> {
-        auto it = span.find(w);
-        if (it == span.end()) return {0, 2 * nl_ - 1};
-        return {it->second.second + 1, std::min(2 * nl_ - 1, nl_ + it->second.first - 1)};
-    };
+    // placement (lagged schedule only): loads in bytes per launch position of a
+    // group -- the steps' rescale traffic, then greedy by size: each range task and
+    // each layer's tiles to the least-loaded admissible offset
     auto place = [&](int32_t nl_) -> bool {
-        // range tasks: their own windows
-        std::vector<std::pair<int32_t, int32_t>> rwin;
-        for (int64_t t = ri0; t < ri1; ++t) {
-            const CleTask& tk = rt[t];
+        auto window = [&](int32_t ti) -> std::pair<int32_t, int32_t> {   // [lo, hi] offsets (untouched: anywhere)
+            if (ti < 0) return {0, 2 * nl_ - 1};
+            return {sp_v[ti].second + 1, std::min(2 * nl_ - 1, nl_ + sp_v[ti].first - 1)};
+        };
+        std::vector<double> base_load(nl_, 0.0);
+        for (int32_t k = 0; k < steps && k < nl_; ++k)
+            for (int64_t t = astep[k]; t < astep[k + 1]; ++t) {
+                const CleTask& tk = at[t];
+                const CleRel& q = R[tk.rel];
+                double n = 0;
+                if (tk.kind == kApplyW1) n = (double)(tk.b - tk.a) * q.len1;
+                else if (tk.kind == kApplyW2Tile) n = (double)(tk.b - tk.a) * (tk.c1 - tk.c0) * q.khw2;
+                else if (tk.kind != kApplyChannels) n = (double)(tk.b - tk.a) * q.o2g * q.khw2;
+                base_load[k] += 8.0 * n;
+            }
+        // range tasks: their own windows and bytes
+        const int64_t nr = ri1 - ri0;
+        std::vector<std::pair<int32_t, int32_t>> rwin((size_t)nr);
+        std::vector<double> rbytes((size_t)nr);
+        for (int64_t x = 0; x < nr; ++x) {
+            const CleTask& tk = rt[ri0 + x];
             const CleRel& q = R[tk.rel];
             std::pair<int32_t, int32_t> w;
-            if (tk.kind == kRangeW1) w = window(q.w1, nl_);
-            else if (tk.kind == kRangeW2Contig || tk.kind == kRangeW2Tile) w = window(q.w2, nl_);
-            else if (tk.kind == kRangeReset) {   // after the consumer step, before the next accumulation (>= nl_ + last + 1)
-                const auto it = span.find(q.w2);
-                w = {step_of[tk.rel] + 1, std::min(2 * nl_ - 1, nl_ + (it == span.end() ? 0 : it->second.second))};
-            } else {   // kRangeResetW1: after the consumer step, before the producer's step two groups on
-                w = {step_of[tk.rel] + 1, 2 * nl_ - 1};
+            switch (tk.kind) {
+                case kRangeW1:
+                    w = window(rel_t1[tk.rel]);
+                    rbytes[x] = 4.0 * (tk.b - tk.a) * q.len1;
+                    break;
+                case kRangeW2Contig:
+                    w = window(rel_t2[tk.rel]);
+                    rbytes[x] = 4.0 * (tk.b - tk.a) * q.o2g * q.khw2;
+                    break;
+                case kRangeW2Tile:
+                    w = window(rel_t2[tk.rel]);
+                    rbytes[x] = 4.0 * (tk.b - tk.a) * (tk.c1 - tk.c0) * q.khw2;
+                    break;
+                case kRangeReset:   // after the consumer step, before the next accumulation (>= nl_ + last + 1)
+                    w = {step_of[tk.rel] + 1, std::min(2 * nl_ - 1, nl_ + sp_v[rel_t2[tk.rel]].second)};
+                    rbytes[x] = 64.0;
+                    break;
+                default:            // kRangeResetW1: after the consumer step, before the producer's step two groups on
+                    w = {step_of[tk.rel] + 1, 2 * nl_ - 1};
+                    rbytes[x] = 64.0;
             }
             if (w.first > w.second) return false;
-            rwin.push_back(w);
+            rwin[x] = w;
         }
         // tiles: a band [B0, B0 + nl_ - 2] meeting every layer's window; the stop
         // rule one offset after the band's last used offset
         int32_t maxlo = 0, minhi = 2 * nl_ - 1;
         std::vector<std::pair<int32_t, int32_t>> lwin(n_targets);
         for (int32_t l = 0; l < n_targets; ++l) {
-            lwin[l] = window(targets[l], nl_);
+            lwin[l] = window(lay_t[l]);
             if (lwin[l].first > lwin[l].second) return false;
             maxlo = std::max(maxlo, lwin[l].first);
             minhi = std::min(minhi, lwin[l].second);
@@ -2049,16 +2077,17 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         if (b_lo > b_hi) return false;
         std::vector<int32_t> lord(n_targets);
         std::iota(lord.begin(), lord.end(), 0);
-        std::stable_sort(lord.begin(), lord.end(), [&](int32_t x, int32_t y) { return target_n[x] > target_n[y]; });
-        std::vector<int64_t> rord(rwin.size());
+        std::sort(lord.begin(), lord.end(),
+                  [&](int32_t x, int32_t y) { return target_n[x] != target_n[y] ? target_n[x] > target_n[y] : x < y; });
+        std::vector<int64_t> rord((size_t)nr);
         std::iota(rord.begin(), rord.end(), 0);
-        std::stable_sort(rord.begin(), rord.end(),
-                         [&](int64_t x, int64_t y) { return range_bytes(rt[ri0 + x]) > range_bytes(rt[ri0 + y]); });
+        std::sort(rord.begin(), rord.end(),
+                  [&](int64_t x, int64_t y) { return rbytes[x] != rbytes[y] ? rbytes[x] > rbytes[y] : x < y; });
         double best = 1e300;
+        std::vector<int32_t> roff((size_t)nr), loff(n_targets);
         for (int32_t B0 = b_lo; B0 <= b_hi; ++B0) {
             if (band_force >= 0 && B0 != band_force && band_force >= b_lo && band_force <= b_hi) continue;
-            std::vector<double> load(nl_, 0.0);
-            for (int32_t k = 0; k < steps && k < nl_; ++k) load[k] = base_load[k];
+            std::vector<double> load = base_load;
             auto pick = [&](int32_t lo, int32_t hi, double bytes) {
                 int32_t bo = lo;
                 for (int32_t o = lo; o <= hi; ++o)
@@ -2066,8 +2095,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 load[bo % nl_] += bytes;
                 return bo;
             };
-            std::vector<int32_t> roff(rwin.size()), loff(n_targets);
-            for (int64_t x : rord) roff[x] = pick(rwin[x].first, rwin[x].second, range_bytes(rt[ri0 + x]));
+            for (int64_t x : rord) roff[x] = pick(rwin[x].first, rwin[x].second, rbytes[x]);
             int32_t maxoff = 0;
             for (int32_t l : lord) {
                 loff[l] = pick(std::max(lwin[l].first, B0), std::min(lwin[l].second, B0 + bw - 1), 12.0 * target_n[l]);
@@ -2238,8 +2266,9 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         return fail(e);
     }
     if (cle_timing())
-        fprintf(stderr, "DFQ_CLE_TIMING create: plan %.1f us, tables %lld B %.1f us, copy %lld B %.1f us\n",
-                tm0 - tc0, (long long)T.total, tm1 - tm0, (long long)host_bytes, now_us() - tm1);
+        fprintf(stderr, "DFQ_CLE_TIMING create: plan %.1f us (relations %.1f, chains %.1f, tasks %.1f, chunks %.1f, "
+                "placement %.1f), tables %lld B %.1f us, copy %lld B %.1f us\n", tm0 - tc0, tp1 - tc0, tp2 - tp1,
+                tp3 - tp2, tp4 - tp3, tm0 - tp4, (long long)T.total, tm1 - tm0, (long long)host_bytes, now_us() - tm1);
     p->d_rels = reinterpret_cast<CleRel*>(base + o_rels);
     p->d_rtasks = reinterpret_cast<CleTask*>(base + o_rt);
     p->d_atasks = reinterpret_cast<CleTask*>(base + o_at);

@@ -8,23 +8,6 @@ namespace dfq {
 constexpr int kThreads = 256;
 constexpr int kColTileRows = 16;   // W2 rows per column tile (range and rescale tiles)
 
-// Wave min / max by DPP (VALU lane permutes: quad swaps, half-row and row
-// mirrors) inside each 16-lane row, then the four rows' results by readlane:
-// the same values as the shuffle forms (min / max are exact; only the combine
-// order differs) at a fraction of their cost -- each __shfl_xor step is an LDS
-// permute round trip, and the rescale tiles reduce every row of their tile.
-__device__ __forceinline__ float dpp_f(float v, int ctrl) {
-    const int x = __float_as_int(v);
-    switch (ctrl) {   // the control must be a compile-time constant
-        case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));
-        case 0x4E: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false));
-        case 0x141: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x141, 0xF, 0xF, false));
-        default: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x140, 0xF, 0xF, false));
-    }
-}
-__device__ __forceinline__ float rl_f(float v, int lane) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
 __device__ __forceinline__ void cle_wave_minmax(float& lo, float& hi) {
     lo = fminf(lo, dpp_f(lo, 0xB1));
     hi = fmaxf(hi, dpp_f(hi, 0xB1));

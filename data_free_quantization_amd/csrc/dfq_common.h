@@ -24,6 +24,50 @@ __device__ __forceinline__ float dec_ord(uint32_t e) {
     return __uint_as_float(u);
 }
 
+// Wave min / max by DPP (VALU lane permutes: quad swaps, half-row and row
+// mirrors) inside each 16-lane row, then the four rows' results by readlane:
+// the same values as the shuffle forms (min / max are exact; only the combine
+// order differs) at a fraction of their cost -- each __shfl_xor step is an LDS
+// permute round trip, and the rescale tiles reduce every row of their tile.
+__device__ __forceinline__ float dpp_f(float v, int ctrl) {
+    const int x = __float_as_int(v);
+    switch (ctrl) {   // the control must be a compile-time constant
+        case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));
+        case 0x4E: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false));
+        case 0x141: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x141, 0xF, 0xF, false));
+        default: return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x140, 0xF, 0xF, false));
+    }
+}
+__device__ __forceinline__ float rl_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+// (min, max) over aligned groups of G lanes (G a power of two <= 64, wave-uniform):
+// DPP quad swaps and half-row / row mirrors inside 16-lane rows (VALU, no LDS
+// round trip), then LDS-permute shuffles only for the 32- and 64-lane groups.
+// Every lane ends with its group's result.
+__device__ __forceinline__ void group_minmax(float& lo, float& hi, int G) {
+    if (G >= 2) {
+        lo = fminf(lo, dpp_f(lo, 0xB1));
+        hi = fmaxf(hi, dpp_f(hi, 0xB1));
+    }
+    if (G >= 4) {
+        lo = fminf(lo, dpp_f(lo, 0x4E));
+        hi = fmaxf(hi, dpp_f(hi, 0x4E));
+    }
+    if (G >= 8) {
+        lo = fminf(lo, dpp_f(lo, 0x141));
+        hi = fmaxf(hi, dpp_f(hi, 0x141));
+    }
+    if (G >= 16) {
+        lo = fminf(lo, dpp_f(lo, 0x140));
+        hi = fmaxf(hi, dpp_f(hi, 0x140));
+    }
+    for (int off = 16; off < G; off <<= 1) {
+        lo = fminf(lo, __shfl_xor(lo, off, kWave));
+        hi = fmaxf(hi, __shfl_xor(hi, off, kWave));
+    }
+}
+
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = fminf(v, __shfl_xor(v, off, kWave));

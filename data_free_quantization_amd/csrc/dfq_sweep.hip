@@ -270,60 +270,78 @@ __device__ __forceinline__ void quant_vec4(const DevTensor& T, int n, int64_t ba
     const float inv_len = T.inv_len;
     const float coff = sym ? 128.f : 0.f;
     const uint32_t cflip = sym ? 0x80808080u : 0u;
-#pragma unroll 2
-    for (int j = lane; j < nj; j += kWave) {
-        const float4 xv = reinterpret_cast<const float4*>(data)[j];
-        float s = pc.s, mn = pc.mn;
-        if (whole) {   // one row per float4 (4 | len, 4 | goff)
-            int r = (int)(((float)(4 * j + eoff) + 0.5f) * inv_len);
-            r = min(r, 63);
-            s = ls[r];
-            mn = lmn[r];
-        }
-        const float negmn = whole ? -mn : pc.negmn;
-        const float rs = __builtin_amdgcn_rcpf(s);
-        float t[4] = {(xv.x + negmn) * rs, (xv.y + negmn) * rs, (xv.z + negmn) * rs, (xv.w + negmn) * rs};
-        bool need[4];
+    // kB float4s per lane at a time: their LDS loads (the values, then each one's
+    // row parameters) are all issued before the first is used -- one LDS round
+    // trip per kB float4s instead of two dependent ones per float4 (a task has at
+    // most 8 float4s per lane; ~2 waves per SIMD hide little latency on their own)
+    constexpr int kB = 4;
+    for (int j0 = lane; j0 < nj; j0 += kB * kWave) {
+        float4 xb[kB];
+        float sb[kB], mb[kB];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            t[k] = __builtin_amdgcn_fmed3f(t[k], qmin, qmax);
-            const float d = __builtin_amdgcn_fractf(t[k]) - 0.5f;
-            need[k] = !(fabsf(d) > fabsf(t[k]) * 0x1p-20f);
+        for (int u = 0; u < kB; ++u) {
+            const int j = j0 + u * kWave;
+            if (j < nj) {
+                xb[u] = reinterpret_cast<const float4*>(data)[j];
+                if (whole) {   // one row per float4 (4 | len, 4 | goff)
+                    int r = (int)(((float)(4 * j + eoff) + 0.5f) * inv_len);
+                    r = min(r, 63);
+                    sb[u] = ls[r];
+                    mb[u] = lmn[r];
+                }
+            }
         }
-        if (__builtin_amdgcn_ballot_w64(need[0] | need[1] | need[2] | need[3])) {   // wave-uniform, rare
-            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (need[k]) t[k] = __builtin_amdgcn_fmed3f((xs[k] + negmn) / s, qmin, qmax);
-        }
-        float q[4], y[4];
+        for (int u = 0; u < kB; ++u) {
+            const int j = j0 + u * kWave;
+            if (j >= nj) break;
+            const float4 xv = xb[u];
+            const float s = whole ? sb[u] : pc.s, mn = whole ? mb[u] : pc.mn;
+            const float negmn = whole ? -mn : pc.negmn;
+            const float rs = __builtin_amdgcn_rcpf(s);
+            float t[4] = {(xv.x + negmn) * rs, (xv.y + negmn) * rs, (xv.z + negmn) * rs, (xv.w + negmn) * rs};
+            bool need[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            q[k] = rintf(t[k]);
-            y[k] = q[k] * s;
-            y[k] = y[k] + mn;
-            if constexpr (CLIP) y[k] = __builtin_amdgcn_fmed3f(y[k], clo, chi);
-        }
-        st<NT>(reinterpret_cast<float4*>(dq) + j, make_float4(y[0], y[1], y[2], y[3]));
-        if constexpr (CB == 1) {
-            uint32_t c = __builtin_amdgcn_cvt_pk_u8_f32(q[0] + coff, 0, 0u);
-            c = __builtin_amdgcn_cvt_pk_u8_f32(q[1] + coff, 1, c);
-            c = __builtin_amdgcn_cvt_pk_u8_f32(q[2] + coff, 2, c);
-            c = __builtin_amdgcn_cvt_pk_u8_f32(q[3] + coff, 3, c);
-            st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, c ^ cflip);
-        } else if constexpr (CB == 3) {   // DFQ_PACK_INT4: 4 codes -> 2 bytes (base % 4 == 0)
-            const uint32_t c = ((uint32_t)(int)q[0] & 0xFu) | (((uint32_t)(int)q[1] & 0xFu) << 4) |
-                               (((uint32_t)(int)q[2] & 0xFu) << 8) | (((uint32_t)(int)q[3] & 0xFu) << 12);
-            st<NT>(reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(T.codes) + base / 2) + j, (uint16_t)c);
-        } else if constexpr (CB == 2) {
-            const uint64_t c = ((uint64_t)(uint16_t)(int)q[0]) | ((uint64_t)(uint16_t)(int)q[1] << 16) |
-                               ((uint64_t)(uint16_t)(int)q[2] << 32) | ((uint64_t)(uint16_t)(int)q[3] << 48);
-            st<NT>(reinterpret_cast<uint64_t*>(static_cast<uint16_t*>(T.codes) + base) + j, c);
-        }
-        if constexpr (EM != 0) {
-            const float4 ev = make_float4(y[0] - xv.x, y[1] - xv.y, y[2] - xv.z, y[3] - xv.w);
-            if constexpr (EM == 1) st<NT>(reinterpret_cast<float4*>(T.esum + base) + j, ev);
-            else reinterpret_cast<float4*>(data)[j] = ev;
+            for (int k = 0; k < 4; ++k) {
+                t[k] = __builtin_amdgcn_fmed3f(t[k], qmin, qmax);
+                const float d = __builtin_amdgcn_fractf(t[k]) - 0.5f;
+                need[k] = !(fabsf(d) > fabsf(t[k]) * 0x1p-20f);
+            }
+            if (__builtin_amdgcn_ballot_w64(need[0] | need[1] | need[2] | need[3])) {   // wave-uniform, rare
+                const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (need[k]) t[k] = __builtin_amdgcn_fmed3f((xs[k] + negmn) / s, qmin, qmax);
+            }
+            float q[4], y[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                q[k] = rintf(t[k]);
+                y[k] = q[k] * s;
+                y[k] = y[k] + mn;
+                if constexpr (CLIP) y[k] = __builtin_amdgcn_fmed3f(y[k], clo, chi);
+            }
+            st<NT>(reinterpret_cast<float4*>(dq) + j, make_float4(y[0], y[1], y[2], y[3]));
+            if constexpr (CB == 1) {
+                uint32_t c = __builtin_amdgcn_cvt_pk_u8_f32(q[0] + coff, 0, 0u);
+                c = __builtin_amdgcn_cvt_pk_u8_f32(q[1] + coff, 1, c);
+                c = __builtin_amdgcn_cvt_pk_u8_f32(q[2] + coff, 2, c);
+                c = __builtin_amdgcn_cvt_pk_u8_f32(q[3] + coff, 3, c);
+                st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, c ^ cflip);
+            } else if constexpr (CB == 3) {   // DFQ_PACK_INT4: 4 codes -> 2 bytes (base % 4 == 0)
+                const uint32_t c = ((uint32_t)(int)q[0] & 0xFu) | (((uint32_t)(int)q[1] & 0xFu) << 4) |
+                                   (((uint32_t)(int)q[2] & 0xFu) << 8) | (((uint32_t)(int)q[3] & 0xFu) << 12);
+                st<NT>(reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(T.codes) + base / 2) + j, (uint16_t)c);
+            } else if constexpr (CB == 2) {
+                const uint64_t c = ((uint64_t)(uint16_t)(int)q[0]) | ((uint64_t)(uint16_t)(int)q[1] << 16) |
+                                   ((uint64_t)(uint16_t)(int)q[2] << 32) | ((uint64_t)(uint16_t)(int)q[3] << 48);
+                st<NT>(reinterpret_cast<uint64_t*>(static_cast<uint16_t*>(T.codes) + base) + j, c);
+            }
+            if constexpr (EM != 0) {
+                const float4 ev = make_float4(y[0] - xv.x, y[1] - xv.y, y[2] - xv.z, y[3] - xv.w);
+                if constexpr (EM == 1) st<NT>(reinterpret_cast<float4*>(T.esum + base) + j, ev);
+                else reinterpret_cast<float4*>(data)[j] = ev;
+            }
         }
     }
 }
@@ -361,7 +379,7 @@ template <int MAXROWS, bool VEC, bool NT = false, int ESPEC = 2, bool SCREEN = t
 __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& task, float* data, float* ls,
                                              float* lmn, const uint32_t* __restrict__ slot_min,
                                              const uint32_t* __restrict__ slot_max, int lane, float bmn = 0.f,
-                                             float bmx = 0.f, int goff = -1) {
+                                             float bmx = 0.f, int goff = -1, uint64_t* tlm = nullptr) {
     const int n = task.n;
     const bool sym = is_sym(T.mode);
     const int len = (int)T.row_len;
@@ -388,11 +406,21 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
             if (r < nrows) {
                 const float* row = data + r * len;
                 if (VEC) {
+                    // 4 LDS loads in flight per lane, then their min / max (a lane walks
+                    // up to 16 float4s of its row; one round trip per 4 instead of per 1)
                     const int q4 = len >> 2;
-                    for (int i = sl; i < q4; i += G) {
-                        const float4 v = reinterpret_cast<const float4*>(row)[i];
-                        vmin = fminf(vmin, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
-                        vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+                    const float4* row4 = reinterpret_cast<const float4*>(row);
+                    for (int i = sl; i < q4; i += 4 * G) {
+                        float4 v[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (i + u * G < q4) v[u] = row4[i + u * G];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (i + u * G < q4) {
+                                vmin = fminf(vmin, fminf(fminf(v[u].x, v[u].y), fminf(v[u].z, v[u].w)));
+                                vmax = fmaxf(vmax, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
+                            }
                     }
                 } else {
                     for (int i = sl; i < len; i += G) {
@@ -402,10 +430,8 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
                     }
                 }
             }
-            for (int off = G >> 1; off >= 1; off >>= 1) {
-                vmin = fminf(vmin, __shfl_xor(vmin, off, kWave));
-                vmax = fmaxf(vmax, __shfl_xor(vmax, off, kWave));
-            }
+            group_minmax(vmin, vmax, G);   // DPP inside 16-lane rows (no LDS round trips)
+            if (tlm && r0 == 0) tlm[2] = wall_clock64();   // diagnostics: the first rows' ranges reduced
             if (sl == 0 && r < nrows) {
                 const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
                 ls[r] = p.s;
@@ -414,6 +440,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
                 if (T.scale) st<false>(T.scale + row_g, p.s);
                 if (T.zero) st<false>(T.zero + row_g, p.mn);
             }
+            if (tlm && r0 == 0) tlm[3] = wall_clock64();   // diagnostics: their parameters built
         }
         wave_lds_sync();
     } else {
@@ -433,6 +460,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         }
     }
 
+    if (tlm) tlm[0] = wall_clock64();   // diagnostics timeline (variant 13): parameters done
     // 3. quantize / dequantize / clip from LDS; write dq + codes; eps for bias correction.
     //    eps overwrites the x it came from (same lane, same slot), so no hazard.
     const bool clip = (T.flags & DFQ_CLIP) != 0;
@@ -578,6 +606,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         }
     }
 
+    if (tlm) tlm[1] = wall_clock64();   // quantize loop issued
     // 4. KHW error sums: E[p] = sum_k eps[p*khw + k] in ATen's order
     if (want_e && khw > 1) {
         wave_lds_sync();
@@ -746,12 +775,14 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                 }
                 block_lds_sync();   // the slots are rewritten by the next task
             }
+            uint64_t marks[4] = {0, 0, 0, 0};
+            uint64_t* tlm = TL ? marks : nullptr;
             if (T.vec4)
                 compute_task<MAXROWS, true, NT, ESPEC, SCREEN, FAST>(T, task, wl, ls, lmn, slot_min, slot_max, lane,
-                                                                     bmn, bmx, goff);
+                                                                     bmn, bmx, goff, tlm);
             else
                 compute_task<MAXROWS, false, NT, ESPEC, SCREEN, FAST>(T, task, wl, ls, lmn, slot_min, slot_max, lane,
-                                                                      bmn, bmx, goff);
+                                                                      bmn, bmx, goff, tlm);
             if constexpr (TL) {
                 if (lane == 0 && t < g_timeline_cap) {
                     uint32_t hw;
@@ -759,11 +790,15 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                     uint32_t xcc;
                     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
                     const uint64_t tl2 = wall_clock64();
-                    uint64_t* r = g_timeline + 4 * t;
+                    uint64_t* r = g_timeline + 8 * t;   // {start, landed, params, quantized, done, hw ids}
                     r[0] = tl0;
                     r[1] = tl1;
-                    r[2] = tl2;
-                    r[3] = ((uint64_t)xcc << 32) | hw;
+                    r[2] = marks[0];
+                    r[3] = marks[1];
+                    r[4] = tl2;
+                    r[5] = ((uint64_t)xcc << 32) | hw;
+                    r[6] = marks[2];
+                    r[7] = marks[3];
                 }
             }
             task = next;

@@ -668,6 +668,93 @@ __global__ void chunk_mean_kernel(const float* __restrict__ mins, const float* _
     }
 }
 
+// ---------------------------------------------------------------------------
+// QuantMeasure.forward's statistics (utils/quantize.py:94-126) in two launches
+// instead of ~8 torch ops: the rows' (min, max) of x.view(rows, -1) by a 2-D grid
+// (each block a slice of one row, ordered-uint atomics into a per-observer word
+// pair), then one wave takes the rows' means in ATen's order and applies the
+// observer's updates.  The word pairs are re-armed by that wave (self-cleaning:
+// the host arms them once when it allocates them).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads)
+observe_rows_kernel(const float* __restrict__ x, int64_t rows, int64_t row_len, int64_t slices,
+                    uint32_t* __restrict__ words) {
+    __shared__ float smn[kThreads / kWave], smx[kThreads / kWave];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+    const int64_t per = ceil_div(row_len, slices);
+    for (int64_t b = blockIdx.x; b < rows * slices; b += gridDim.x) {
+        const int64_t r = b / slices, k = b % slices;
+        const int64_t e0 = k * per, e1 = min(row_len, e0 + per);
+        const float* row = x + r * row_len;
+        float a = INFINITY, c = -INFINITY;
+        const bool v4 = (row_len % 4 == 0) && (per % 4 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0);
+        if (v4) {
+            const float4* q = reinterpret_cast<const float4*>(row + e0);
+            for (int64_t i = threadIdx.x; i < (e1 - e0) / 4; i += kThreads) {
+                const float4 v = q[i];
+                a = fminf(a, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+                c = fmaxf(c, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+            }
+        } else {
+            for (int64_t i = e0 + threadIdx.x; i < e1; i += kThreads) {
+                const float v = row[i];
+                a = fminf(a, v);
+                c = fmaxf(c, v);
+            }
+        }
+        a = wave_min(a);
+        c = wave_max(c);
+        if (lane == 0) {
+            smn[w] = a;
+            smx[w] = c;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int q = 1; q < kThreads / kWave; ++q) {
+                a = fminf(a, smn[q]);
+                c = fmaxf(c, smx[q]);
+            }
+            atomicMax(&words[2 * r], ~enc_ord(a));
+            atomicMax(&words[2 * r + 1], enc_ord(c));
+        }
+        __syncthreads();
+    }
+}
+
+// One wave.  mn / mx = the means of the rows' mins / maxs (fp32, ATen's sum order,
+// as flat.min(-1)[0].mean()).  update_stat: running_max = mx if mx > running_max
+// (Python max on tensors), running_min likewise; training: running_* =
+// running_* * (1 - m) + (mn|mx) * m, each op rounded to fp32 as the in-place torch
+// ops do.  out2 = the range the fake quant uses: (mn, mx) in training, the running
+// values otherwise.
+__global__ void observe_finish_kernel(uint32_t* __restrict__ words, int64_t rows, float* __restrict__ running_min,
+                                      float* __restrict__ running_max, int32_t update_stat, int32_t training,
+                                      float one_minus_m, float m, float* __restrict__ out2) {
+    const int lane = threadIdx.x;
+    const float smn = wave_inner_sum([&](int64_t i) { return dec_ord(~words[2 * i]); }, rows, lane);
+    const float smx = wave_inner_sum([&](int64_t i) { return dec_ord(words[2 * i + 1]); }, rows, lane);
+    __syncthreads();   // every lane has read the words
+    for (int64_t i = lane; i < 2 * rows; i += kWave) words[i] = 0u;   // re-armed for the next call
+    if (lane == 0) {
+        const float mn = smn / (float)rows, mx = smx / (float)rows;
+        float rmn = *running_min, rmx = *running_max;
+        if (update_stat) {
+            rmx = (mx > rmx) ? mx : rmx;
+            rmn = (mn < rmn) ? mn : rmn;
+        }
+        if (training) {
+            const float t0 = rmn * one_minus_m, t1 = mn * m;
+            rmn = t0 + t1;
+            const float t2 = rmx * one_minus_m, t3 = mx * m;
+            rmx = t2 + t3;
+        }
+        *running_min = rmn;
+        *running_max = rmx;
+        out2[0] = training ? mn : rmn;
+        out2[1] = training ? mx : rmx;
+    }
+}
+
 }  // namespace dfq
 
 using namespace dfq;
@@ -1325,6 +1412,24 @@ extern "C" int dfq_chunk_range(const float* x, int64_t rows, int64_t row_len, fl
                        rowbuf + rows);
     DFQ_LAUNCH_CHECK();
     hipLaunchKernelGGL(chunk_mean_kernel, dim3(1), dim3(kWave), 0, s, rowbuf, rowbuf + rows, rows, out2);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+extern "C" int dfq_act_observe(const float* x, int64_t rows, int64_t row_len, uint32_t* words, float* running_min,
+                               float* running_max, int32_t update_stat, int32_t training, double momentum,
+                               float* out2, void* stream) {
+    if (!x || !words || !running_min || !running_max || !out2 || rows < 1) return DFQ_ERR_INVALID;
+    if (row_len < 1) return DFQ_ERR_SHAPE;   // torch: min over an empty dim raises
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // slices of >= 16K elements per block, >= 1024 blocks when the tensor allows
+    const int64_t slices = std::max<int64_t>(1, std::min<int64_t>(ceil_div(row_len, (int64_t)16384),
+                                                                  ceil_div((int64_t)1024, rows)));
+    const int grid = (int)std::min<int64_t>(rows * slices, 8192);
+    hipLaunchKernelGGL(observe_rows_kernel, dim3(grid), dim3(kThreads), 0, s, x, rows, row_len, slices, words);
+    DFQ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(observe_finish_kernel, dim3(1), dim3(kWave), 0, s, words, rows, running_min, running_max,
+                       update_stat, training, (float)(1.0 - momentum), (float)momentum, out2);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }

@@ -90,53 +90,83 @@ _BN_TIMING = bool(os.environ.get("DFQ_BN_TIMING"))   # host-side split of the fo
 
 def _fold_batch(pairs, ranges=None):
     tb = [time.perf_counter()] if _BN_TIMING else None
+    _lib.weights_changed()
     with torch.no_grad():
         # module state straight from the parameter / buffer dicts: Module.__getattr__
         # on every access was most of this function's host time
-        st = []
-        for bn, layer in pairs:
-            lp, bp, bb = layer._parameters, bn._parameters, bn._buffers
-            st.append((lp["weight"], lp.get("bias"), bp["weight"], bp["bias"], bb["running_mean"], bb["running_var"]))
-        _lib.require_device(*[t for row in st for t in row if t is not None])
-        dev = st[0][0].device
+        lps = [layer._parameters for _, layer in pairs]
+        bps = [bn._parameters for bn, _ in pairs]
+        bbs = [bn._buffers for bn, _ in pairs]
+        W = [lp["weight"] for lp in lps]
+        Bi = [lp.get("bias") for lp in lps]
+        G = [bp["weight"] for bp in bps]
+        Be = [bp["bias"] for bp in bps]
+        Mu = [bb["running_mean"] for bb in bbs]
+        Va = [bb["running_var"] for bb in bbs]
+        if tb:
+            tb.append(time.perf_counter())
+        _lib.require_device(*W, *G, *Be, *Mu, *Va, *[b for b in Bi if b is not None])
+        if tb:
+            tb.append(time.perf_counter())
+        dev = W[0].device
+        n = len(pairs)
+        rows_n = np.array([w.shape[0] for w in W], dtype=np.int64)
+        chans = np.array([g.numel() for g in G], dtype=np.int64)
+        tab = np.zeros(n, dtype=_BN_DESC)
+        ptr = tab["ptr"]
         # :262-263 give a bias-less layer torch.zeros; here the fold reads such a
-        # bias as 0 (DFQ_BN_FOLD_ZERO_BIAS) and writes every element of it
-        need = [j for j, row in enumerate(st) if row[1] is None]
-        for j, z in zip(need, _carve([st[j][0].shape[0] for j in need], False, dev)):
+        # bias as 0 (DFQ_BN_FOLD_ZERO_BIAS) and writes every element of it.  The new
+        # biases and the fake weight / bias buffers are views of ONE allocation
+        # whose addresses come from the offsets (no data_ptr call per view).
+        need = [j for j, b in enumerate(Bi) if b is None]
+        nb_f = int(rows_n[need].sum()) if need else 0
+        nch = int(chans.sum())
+        flat = torch.empty(max(nb_f + 2 * nch, 1), dtype=torch.float32, device=dev)
+        base = np.uint64(flat.data_ptr())
+        if tb:
+            tb.append(time.perf_counter())
+        views = torch.split(flat[:nb_f + 2 * nch], [int(rows_n[j]) for j in need] + chans.tolist() * 2)
+        if tb:
+            tb.append(time.perf_counter())
+        for j, z in zip(need, views[:len(need)]):
             layer = pairs[j][1]
             b = torch.Tensor._make_subclass(nn.Parameter, z, False)   # nn.Parameter(z, requires_grad=False)
             if "bias" in layer._parameters:   # registered as None: what Module.__setattr__ would do
                 layer._parameters["bias"] = b
             else:
                 layer.bias = b
-            st[j] = (st[j][0], b) + st[j][2:]
-        fresh = set(need)
         if tb:
             tb.append(time.perf_counter())
-        n = len(pairs)
-        fakes = _carve([row[2].numel() for row in st] * 2, False, dev)
-        tab = np.zeros(n, dtype=_BN_DESC)
-        rows = []
-        for j, ((bn, _), (w, b, g, beta, mean, var)) in enumerate(zip(pairs, st)):
-            fw, fb = fakes[j], fakes[n + j]
+        if need:
+            boff = np.zeros(n, dtype=np.uint64)
+            boff[need] = np.concatenate([[0], np.cumsum(rows_n[need])[:-1]]).astype(np.uint64)
+        coff = np.concatenate([[0], np.cumsum(chans)[:-1]]).astype(np.uint64) + np.uint64(nb_f)
+        fw_v, fb_v = views[len(need):len(need) + n], views[len(need) + n:]
+        for (bn, _), fw, fb in zip(pairs, fw_v, fb_v):
             buf = bn._buffers   # register_buffer("fake_weight" / "fake_bias") without the per-call checks
             buf["fake_weight"], buf["fake_bias"] = fw, fb
-            rows.append((w.data_ptr(), b.data_ptr(), g.data_ptr(), beta.data_ptr(), mean.data_ptr(), var.data_ptr(),
-                         fw.data_ptr(), fb.data_ptr()))
+        ptr[:, 0] = [t.data_ptr() for t in W]
+        ptr[:, 1] = [0 if t is None else t.data_ptr() for t in Bi]
+        if need:
+            ptr[need, 1] = base + np.uint64(4) * boff[need]
+        ptr[:, 2] = [t.data_ptr() for t in G]
+        ptr[:, 3] = [t.data_ptr() for t in Be]
+        ptr[:, 4] = [t.data_ptr() for t in Mu]
+        ptr[:, 5] = [t.data_ptr() for t in Va]
+        ptr[:, 6] = base + np.uint64(4) * coff
+        ptr[:, 7] = base + np.uint64(4) * (coff + np.uint64(nch))
         if tb:
             tb.append(time.perf_counter())
-        tab["ptr"] = np.array(rows, dtype=np.uint64)
-        tab["eps"] = [float(bn.eps) for bn, _ in pairs]
-        if fresh:
-            tab["flags"][list(fresh)] = _lib.DFQ_BN_FOLD_ZERO_BIAS
+        tab["eps"] = [bn.eps for bn, _ in pairs]
+        if need:
+            tab["flags"][need] = _lib.DFQ_BN_FOLD_ZERO_BIAS
         if ranges is not None:   # 8 bytes per fold, in one allocation (zeroed by the call)
             rbuf = torch.empty(2 * n, dtype=torch.int32, device=dev)
             tab["range_enc"] = rbuf.data_ptr() + 8 * np.arange(n, dtype=np.uint64)
             for j, (_, layer) in enumerate(pairs):
                 ranges[layer] = rbuf[2 * j:2 * j + 2]
-        shapes = [row[0].shape for row in st]
-        tab["rows"] = [sh[0] for sh in shapes]
-        tab["row_len"] = [row[0].numel() // sh[0] for row, sh in zip(st, shapes)]
+        tab["rows"] = rows_n
+        tab["row_len"] = [w.numel() for w in W] // rows_n
         descs = tab.ctypes.data_as(C.POINTER(_lib.BnFoldDesc))
         L = _lib.load()
         nb = int(L.dfq_bn_fold_ws_bytes(descs, n))
@@ -145,7 +175,7 @@ def _fold_batch(pairs, ranges=None):
         ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=dev)   # stream-ordered (caching allocator)
         if tb:
             tb.append(time.perf_counter())
-        rc = L.dfq_bn_fold_batch(descs, n, ws.data_ptr(), ws.numel(), _lib.stream_of(st[0][0]))
+        rc = L.dfq_bn_fold_batch(descs, n, ws.data_ptr(), ws.numel(), _lib.stream_of(W[0]))
         _lib.check(rc, "dfq_bn_fold_batch")
         if tb:
             tb.append(time.perf_counter())
@@ -154,7 +184,8 @@ def _fold_batch(pairs, ranges=None):
             _identity_forward(bn)
         if tb:
             tb.append(time.perf_counter())
-            print("DFQ_BN_TIMING fold x%d: tensors + biases %.1f us, fakes + rows %.1f us, tables + workspace "
+            print("DFQ_BN_TIMING fold x%d: module dicts %.1f us, device checks %.1f us, shapes + allocation %.1f us, "
+                  "split %.1f us, bias Parameters %.1f us, fakes + rows %.1f us, tables + workspace "
                   "%.1f us, call %.1f us, identity BNs %.1f us" % ((len(pairs),) + tuple(
                       (b - a) * 1e6 for a, b in zip(tb, tb[1:]))), file=sys.stderr)
 
@@ -202,8 +233,8 @@ def quantize_targ_layer(graph, bit_weight=8, bits_bias=16, targ_type=None, *, gr
     every rank holding the model): each rank sweeps its LPT share of the tensors
     into its slab of an output arena, one in-place all-gather (RCCL) gives every
     rank every result, and each rank writes them back into its parameters
-    (distributed.ShardedSweep).  Results are identical to the unsharded call.
-    """
+    (distributed.ShardedSweep).  Results are identical to the unsharded call."""
+    _lib.weights_changed()
     if shard and torch.distributed.is_initialized():
         return _quantize_targ_layer_sharded(graph, bit_weight, bits_bias, targ_type, granularity=granularity,
                                             symmetric=symmetric, clip=clip, state=state, group=group)

@@ -247,6 +247,9 @@ class QuantMeasure(nn.Module):
         self.update_stat = update_stat
 
     def forward(self, input):
+        if _no_autograd(input) and (self.update_stat or self.training) and input.is_cuda \
+                and input.dtype is torch.float32 and input.numel() > 0 and input.dim() > 0:
+            return self._forward_fused(input)
         flat = input.detach().view(input.size(0), -1)
         if self.update_stat:
             # Python max(a, b) / min(a, b) on tensors: b if b > a (b < a) else a --
@@ -269,8 +272,39 @@ class QuantMeasure(nn.Module):
             return fake_quant_given(input, self.num_bits, min_dev=mn, max_dev=mx)
         return quantize(input, self.num_bits, min_value=float(mn), max_value=float(mx), num_chunks=16)
 
+    def _forward_fused(self, input):
+        """Inference with live statistics: the observer update in ONE dfq_act_observe
+        call (rows' min / max, their ATen-order means, the update_stat select and
+        the training momentum, two launches) and the fake quant in one more --
+        instead of eight torch ops and their allocations per call.  The running
+        buffers are updated in place (the reference rebinds them to new tensors
+        of the same values)."""
+        x = input.detach()
+        if not x.is_contiguous():
+            x = x.contiguous()
+        rows = x.size(0)
+        d = self.__dict__
+        words = d.get("_obs_words")
+        if words is None or words.numel() != 2 * rows or words.device != x.device:
+            words = d["_obs_words"] = torch.zeros(2 * rows, dtype=torch.int32, device=x.device)   # armed once
+            d["_obs_out"] = torch.empty(2, dtype=torch.float32, device=x.device)
+        out2 = d["_obs_out"]
+        rmin, rmax = self._buffers["running_min"], self._buffers["running_max"]
+        _lib.require_device(rmin, rmax)
+        _lib.check(_lib.load().dfq_act_observe(_lib.ptr(x), rows, x.numel() // rows, _lib.ptr(words), _lib.ptr(rmin),
+                                               _lib.ptr(rmax), int(bool(self.update_stat)), int(bool(self.training)),
+                                               float(self.momentum), _lib.ptr(out2), _lib.stream_of(x)),
+                   "dfq_act_observe", RuntimeError)
+        return fake_quant_given(input, self.num_bits, min_dev=out2[0], max_dev=out2[1])
+
     def set_update_stat(self, update_stat):
         self.update_stat = update_stat
+
+
+def invalidate_weight_cache() -> None:
+    """Drop every Quant* layer's cached weight / bias fake-quant (after rewriting
+    weights through ``.data`` outside the DFQ transforms)."""
+    _lib.weights_changed()
 
 
 class _QuantWeightMixin:
@@ -280,11 +314,24 @@ class _QuantWeightMixin:
     def _qparams(self, weight, bias):
         if _no_autograd(weight, bias):
             # inference: float(weight.min()) / float(weight.max()) and the bias's own
-            # 0-d fp32 range stay on the device (dfq_range), one async launch each
+            # 0-d fp32 range stay on the device (dfq_range), one async launch each.
+            # The result depends only on the weight and bias bytes and the bit
+            # widths, so it is kept while none of them changed: the key holds both
+            # tensors' identity, address and torch version counter, and the DFQ
+            # transforms' generation (_lib.WEIGHT_GENERATION: they write through
+            # the library, past the version counters).  Code that rewrites weights
+            # through ``.data`` (a fresh version counter) must call
+            # ``invalidate_weight_cache()``.
+            key = (id(weight), weight.data_ptr(), weight._version, self.num_bits, _lib.WEIGHT_GENERATION,
+                   None if bias is None else (id(bias), bias.data_ptr(), bias._version), self.num_bits_bias)
+            hit = self.__dict__.get("_qw_cache")
+            if hit is not None and hit[0] == key:
+                return hit[1], hit[2]
             qweight = fake_quant_given(weight, self.num_bits, range_enc=device_range(weight))
             qbias = None
             if bias is not None:
                 qbias = fake_quant_given(bias, self.num_bits_bias, range_enc=device_range(bias), scale_f32=True)
+            self.__dict__["_qw_cache"] = (key, qweight, qbias)
             return qweight, qbias
         qweight = quantize(weight, num_bits=self.num_bits, min_value=float(weight.min()),
                            max_value=float(weight.max()))

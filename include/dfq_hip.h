@@ -125,6 +125,18 @@ int dfq_quantize_tensor(const dfq_tensor_desc* desc, void* ws, size_t ws_bytes, 
  * out2 = {mean_r min(x[r]), mean_r max(x[r])} in fp32, the mean in ATen's sum
  * order.  rowbuf: 2*rows device floats of scratch.  Async on `stream`. */
 int dfq_chunk_range(const float* x, int64_t rows, int64_t row_len, float* rowbuf, float* out2, void* stream);
+/* QuantMeasure.forward's statistics (utils/quantize.py:94-126), async, two
+ * launches: mn / mx = the means over rows of x.view(rows, -1)'s row mins / maxs
+ * (fp32, ATen's sum order); update_stat: running_max = mx if mx > running_max
+ * (running_min likewise); training: running_* = running_* * (1 - momentum) +
+ * (mn|mx) * momentum (fp32 ops, in that order, after the update).  out2 (2 device
+ * floats) = the range the fake quant then uses: (mn, mx) in training, the running
+ * values otherwise.  words: 2*rows device uint32 of per-observer scratch, zeroed
+ * ONCE by the caller; every call leaves them zeroed again.  Replaces the
+ * QuantMeasure statistics of the reference (no C counterpart there). */
+int dfq_act_observe(const float* x, int64_t rows, int64_t row_len, uint32_t* words, float* running_min,
+                    float* running_max, int32_t update_stat, int32_t training, double momentum, float* out2,
+                    void* stream);
 /* Whole-tensor (min, max) on the device, async: range_enc (2 device uint32) =
  * {~enc(min), enc(max)} in the library's order-preserving encoding (the input of
  * dfq_fake_quant_given); it is zeroed on `stream` first. */

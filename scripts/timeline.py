@@ -27,7 +27,7 @@ stream = torch.cuda.current_stream(dev)
 items, _, _, _ = bench.build_batch(model, dev, copies=copies, seed=5)
 plan = SweepPlan(items)
 n = plan.stats["n_tasks_main"]
-buf = torch.zeros(4 * n, dtype=torch.int64, device=dev)
+buf = torch.zeros(8 * n, dtype=torch.int64, device=dev)
 L = _lib.load()
 us = bench.time_plan(plan, stream, dev, 100, 10) * 1e3
 _lib.check(L.dfq_debug_timeline(buf.data_ptr(), n), "timeline")
@@ -35,19 +35,26 @@ for _ in range(3):
     plan.execute(stream)
 torch.cuda.synchronize(dev)
 _lib.check(L.dfq_debug_timeline(None, 0), "timeline off")
-r = buf.view(n, 4).cpu().numpy().astype(np.int64)
+r = buf.view(n, 8).cpu().numpy().astype(np.int64)
 t0 = r[:, 0].min()
-start, landed, done = [(r[:, k] - t0) / 100.0 for k in range(3)]   # us
+start, landed, params, quant, done = [(r[:, k] - t0) / 100.0 for k in range(5)]   # us
+has_sub = r[:, 6] > 0   # whole-row tasks: first rows' ranges reduced, their parameters built
+ranged, built = [(r[:, k] - t0) / 100.0 for k in (6, 7)]
 q = lambda a: [round(float(np.percentile(a, p)), 2) for p in (0, 10, 50, 90, 99, 100)]
 out = {"model": model, "copies": copies, "tasks": n, "grid": plan.stats["grid_blocks"], "event_us": round(us, 2),
        "span_us": round(float(done.max()), 2),
        "start_pct": q(start), "landed_pct": q(landed), "done_pct": q(done),
-       "load_lat_pct": q(landed - start), "compute_pct": q(done - landed)}
+       "load_lat_pct": q(landed - start), "compute_pct": q(done - landed),
+       "row_params_pct": q(params - landed), "quant_loop_pct": q(quant - params), "esum_tail_pct": q(done - quant),
+       "whole_row_tasks": int(has_sub.sum()),
+       "row_reduce_pct": q((ranged - landed)[has_sub]) if has_sub.any() else None,
+       "make_qparams_pct": q((built - ranged)[has_sub]) if has_sub.any() else None,
+       "params_sync_pct": q((params - built)[has_sub]) if has_sub.any() else None}
 # how many waves were live over time (1 us bins)
 bins = np.arange(0, done.max() + 1.0, 1.0)
 live = [int(((start <= b) & (done > b)).sum()) for b in bins]
 out["live_tasks_per_us"] = live
-xcc = (r[:, 3] >> 32)
+xcc = (r[:, 5] >> 32)
 out["tasks_per_xcc"] = np.bincount(xcc, minlength=8).tolist()
 print(json.dumps(out))
 plan.destroy()
