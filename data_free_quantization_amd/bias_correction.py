@@ -418,7 +418,11 @@ def _structure(graph, bottoms, targ_type, bn_type, signed, bits_weight, error_su
             k = kinds[(t, targ_type, bn_type)] = (1 if issubclass(t, bn_type) else
                                                   2 if issubclass(t, targ_type) and t is not str else 0)
         if k == 1:
-            fw, fb = _buf(v, "fake_weight"), _buf(v, "fake_bias")
+            bufs = getattr(v, "_buffers", {})
+            fw, fb = bufs.get("fake_weight"), bufs.get("fake_bias")
+            if fw is None or fb is None:   # a BN merge_batchnorm never folded: the walk must not use it
+                shp += (i, -7)             # (the live walk raises, as the reference does, if it does)
+                continue
             ptrs[i] = (fw.data_ptr(), fb.data_ptr())
             tensors += (fw, fb)
             shp += (i, -1, *fw.shape, -2, *fb.shape)
@@ -616,6 +620,8 @@ def bias_correction(graph, bottoms, targ_type, bits_weight=8, bn_type=torch.nn.B
                     if no_bn:   # find_prev_bn printed a warning: not a walk to replay silently
                         sig = None
                     pre = None if error_sums is None else error_sums.get(keys[idx_layer])
+                    if pre is None:   # E computed inside the walk (a fake quant outside the chain): not replayable
+                        sig = None
                     E, o, i2 = _error_sums(_param(node, "weight"), bits_weight, signed, pre)
                     if stream is None:
                         stream = _lib.stream_of(E[0])

@@ -17,6 +17,8 @@
 #include <cstring>
 #include <condition_variable>
 #include <functional>
+#include <list>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -1676,44 +1678,31 @@ extern "C" int64_t dfq_cle_plan_ws_bytes(const int64_t* target_n, int32_t n_targ
     return b;
 }
 
-extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
-                                   const int64_t* target_n, int32_t n_targets, double s_min, double s_max,
-                                   int32_t is_signed, float eps, int32_t ref_threads, void* ws, int64_t ws_bytes,
-                                   dfq_cle_plan** out) {
-    if (!out || n_rel < 0 || n_targets < 0 || (n_rel > 0 && !rels) || (n_targets > 0 && (!targets || !target_n)))
-        return DFQ_ERR_INVALID;
-    const double tc0 = now_us();
-    const int64_t need_ws = dfq_cle_plan_ws_bytes(target_n, n_targets);
-    if (need_ws < 0) return DFQ_ERR_INVALID;
-    if (ws && (ws_bytes < need_ws || reinterpret_cast<uintptr_t>(ws) % 256 != 0)) return DFQ_ERR_INVALID;
-    *out = nullptr;
-    // relations: shapes as dfq_cle_relation
-    std::vector<CleRel> R(n_rel);
+// Everything dfq_cle_plan_create derives from the relations' and targets' shapes
+// and tensor identities -- chains, steps, tasks, metric chunks and units, the
+// placement -- but no address: a plan of the same structure reuses it and binds
+// its own tensors (cle_structure_key / the cache in dfq_cle_plan_create).
+struct CleStructure {
+    std::vector<CleRel> R;   // fused / depthwise / self-range flags set (addresses: the first plan's)
     int64_t M = 0;
-    for (int32_t r = 0; r < n_rel; ++r) {
-        const dfq_cle_rel& d = rels[r];
-        if (!d.w1 || !d.w2 || !d.b1 || d.c1 <= 0 || d.len1 <= 0 || d.o2 <= 0 || d.i2 <= 0 || d.khw2 <= 0)
-            return DFQ_ERR_INVALID;
-        int64_t groups = 1;
-        if (d.c1 != d.i2) {
-            groups = d.c1 / d.i2;
-            if (groups <= 0 || groups * d.i2 != d.c1) return DFQ_ERR_SHAPE;
-        }
-        if (d.o2 % groups != 0) return DFQ_ERR_SHAPE;
-        CleRel c{};
-        c.w1 = d.w1; c.w2 = d.w2; c.b1 = d.b1; c.bnw = d.bn_w; c.bnb = d.bn_b; c.sacc = d.s_acc;
-        c.c1 = d.c1; c.len1 = d.len1; c.o2 = d.o2; c.i2 = d.i2; c.khw2 = d.khw2; c.o2g = d.o2 / groups;
-        c.moff = M;
-        c.sacc_init = d.s_acc_init;
-        c.vec1 = (d.len1 % 4 == 0 && reinterpret_cast<uintptr_t>(d.w1) % 16 == 0) ? 1 : 0;
-        c.vec2 = (d.i2 == 1 && (c.o2g * d.khw2) % 4 == 0 && reinterpret_cast<uintptr_t>(d.w2) % 16 == 0) ? 1 : 0;
-        c.fuse_next = -1;
-        c.dw_prev = -1;
-        c.w1_self = 0;
-        c.w2_self = 0;
-        M += 2 * d.c1;
-        R[r] = c;
-    }
+    int32_t chains = 0, steps = 0;
+    bool fused = false;
+    std::vector<CleTask> rt, at;
+    std::vector<int64_t> rstep, astep;
+    int64_t ri0 = 0, ri1 = 0;
+    std::vector<CleLayer> layers;   // n, nt (w / snap bound per plan)
+    std::vector<CleChunk> chunks;
+    std::vector<CleUnit> units;
+    std::vector<int64_t> b1off;
+    int64_t nb1_total = 0;
+    std::vector<int64_t> uoffs, roffs;
+    int32_t nlaunch = 0, stop_off = -1;
+    bool lagged = false;
+    double t_chains = 0, t_tasks = 0, t_chunks = 0, t_place = 0;
+};
+
+static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, float* const* targets,
+                               const int64_t* target_n, int32_t n_targets, int32_t ref_threads, CleStructure& S) {
     const double tp1 = now_us();
     // chains: connected components over the tensors a relation touches
     std::vector<int32_t> parent(n_rel);
@@ -1913,26 +1902,15 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     const double tp3 = now_us();
     // metric chunks: torch.mean = sum / n; the sum is two_pass_reduction over
     // min(threads, ceil(n / 32768)) equal chunks when n >= 32768 (serial below)
-    dfq_cle_plan* p = new (std::nothrow) dfq_cle_plan();
-    if (!p) return DFQ_ERR_NOMEM;
     std::vector<CleLayer> layers(n_targets);
     std::vector<CleChunk> chunks;
     std::vector<CleUnit> units;
     std::vector<int64_t> b1off;
     int64_t nb1_total = 0;
-    char* snap_base = static_cast<char*>(ws);
-    if (!snap_base && need_ws > 0) {   // no caller workspace: the plan owns its snapshots
-        hipError_t e = hipMalloc(&p->d_snap_owned, need_ws);
-        if (e != hipSuccess) { set_last_hip_error(e); cle_plan_free(p); return DFQ_ERR_HIP; }
-        snap_base = static_cast<char*>(p->d_snap_owned);
-    }
-    int64_t snap_off = 0;
     for (int32_t l = 0; l < n_targets; ++l) {
         const int64_t n = target_n[l];
-        if (!targets[l] || n <= 0) { cle_plan_free(p); return DFQ_ERR_INVALID; }
-        float* snap = reinterpret_cast<float*>(snap_base + snap_off);
-        snap_off += snap_bytes(n);
-        layers[l] = CleLayer{targets[l], snap, n, 1};
+        if (!targets[l] || n <= 0) return DFQ_ERR_INVALID;
+        layers[l] = CleLayer{nullptr, nullptr, n, 1};   // the tensor and its snapshot: bound per plan
         int64_t nt = 1;
         if (n >= 32768 && ref_threads > 1) nt = std::min<int64_t>(ref_threads, ceil_div(n, (int64_t)32768));
         layers[l].nt = nt;
@@ -1942,7 +1920,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             if (b >= n) break;
             const int64_t len = std::min<int64_t>(n, b + chunk) - b;
             const int64_t sz = len / 32;
-            if (aten_ceil_log2(sz) / 4 > 4) { cle_plan_free(p); return DFQ_ERR_UNSUPPORTED; }   // > 16M / chunk
+            if (aten_ceil_log2(sz) / 4 > 4) return DFQ_ERR_UNSUPPORTED;   // > 16M / chunk
             const int32_t ci = (int32_t)chunks.size();
             chunks.push_back(CleChunk{l, (int32_t)t, b, len});
             const int64_t nb1 = sz / 256;
@@ -2143,18 +2121,196 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             ri1 = (int64_t)rt.size();
         }
     }
-    if (cle_timing()) {   // the schedule: per offset, tile units and range tasks
+    S.R = std::move(R);
+    S.M = M;
+    S.chains = chains;
+    S.steps = steps;
+    S.fused = fused;
+    S.rt = std::move(rt);
+    S.at = std::move(at);
+    S.rstep = std::move(rstep);
+    S.astep = std::move(astep);
+    S.ri0 = ri0;
+    S.ri1 = ri1;
+    S.layers = std::move(layers);
+    S.chunks = std::move(chunks);
+    S.units = std::move(units);
+    S.b1off = std::move(b1off);
+    S.nb1_total = nb1_total;
+    S.uoffs = std::move(uoffs);
+    S.roffs = std::move(roffs);
+    S.nlaunch = nlaunch;
+    S.stop_off = stop_off;
+    S.lagged = lagged;
+    const double tp5 = now_us();
+    S.t_chains = tp2 - tp1;
+    S.t_tasks = tp3 - tp2;
+    S.t_chunks = tp4 - tp3;
+    S.t_place = tp5 - tp4;
+    return DFQ_OK;
+}
+
+// The structure key: shapes, flags and the identity pattern of every tensor
+// address (which relation / target slots share a tensor), the metric's thread
+// count and the diagnostics library's schedule switches.  Two calls with equal
+// keys get equal structures.
+static std::vector<int64_t> cle_structure_key(const std::vector<CleRel>& R, int64_t M, float* const* targets,
+                                              const int64_t* target_n, int32_t n_targets, int32_t ref_threads) {
+    std::vector<std::pair<uintptr_t, int32_t>> ps;
+    ps.reserve(5 * R.size() + n_targets);
+    for (const CleRel& c : R)
+        for (const void* q : {(const void*)c.w1, (const void*)c.w2, (const void*)c.b1, (const void*)c.bnw,
+                              (const void*)c.bnb})
+            ps.push_back({reinterpret_cast<uintptr_t>(q), (int32_t)ps.size()});
+    for (int32_t l = 0; l < n_targets; ++l) ps.push_back({reinterpret_cast<uintptr_t>(targets[l]), (int32_t)ps.size()});
+    std::vector<int32_t> id(ps.size());
+    std::vector<std::pair<uintptr_t, int32_t>> srt = ps;
+    std::sort(srt.begin(), srt.end());
+    for (size_t i = 0; i < srt.size();) {   // every slot -> the first slot holding the same address
+        size_t j = i;
+        while (j < srt.size() && srt[j].first == srt[i].first) ++j;
+        for (size_t k = i; k < j; ++k) id[srt[k].second] = srt[i].first ? srt[i].second : -1;
+        i = j;
+    }
+    std::vector<int64_t> key;
+    key.reserve(16 * R.size() + 2 * n_targets + 16);
+    key.push_back((int64_t)R.size());
+    key.push_back(M);
+    key.push_back(n_targets);
+    key.push_back(ref_threads);
+    for (const char* sw : {"DFQ_CLE_FUSED", "DFQ_CLE_LAG", "DFQ_CLE_BAND"}) {   // diagnostics library only
+        const char* v = ab_env(sw);
+        int64_t h = v ? 1 : 0;
+        for (int k = 0; v && v[k] && k < 8; ++k) h = h * 131 + (unsigned char)v[k];
+        key.push_back(h);
+    }
+    size_t q = 0;
+    for (const CleRel& c : R) {
+        key.insert(key.end(), {c.c1, c.len1, c.o2, c.i2, c.khw2, (int64_t)c.sacc_init, (int64_t)c.vec1, (int64_t)c.vec2,
+                               (int64_t)(c.sacc != nullptr)});
+        for (int k = 0; k < 5; ++k) key.push_back(id[q++]);
+    }
+    for (int32_t l = 0; l < n_targets; ++l) {
+        key.push_back(target_n[l]);
+        key.push_back(id[q++]);
+    }
+    return key;
+}
+
+static std::mutex g_struct_mu;
+static std::list<std::pair<std::vector<int64_t>, std::shared_ptr<const CleStructure>>> g_struct_cache;
+constexpr size_t kStructCacheCap = 8;
+
+extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
+                                   const int64_t* target_n, int32_t n_targets, double s_min, double s_max,
+                                   int32_t is_signed, float eps, int32_t ref_threads, void* ws, int64_t ws_bytes,
+                                   dfq_cle_plan** out) {
+    if (!out || n_rel < 0 || n_targets < 0 || (n_rel > 0 && !rels) || (n_targets > 0 && (!targets || !target_n)))
+        return DFQ_ERR_INVALID;
+    const double tc0 = now_us();
+    const int64_t need_ws = dfq_cle_plan_ws_bytes(target_n, n_targets);
+    if (need_ws < 0) return DFQ_ERR_INVALID;
+    if (ws && (ws_bytes < need_ws || reinterpret_cast<uintptr_t>(ws) % 256 != 0)) return DFQ_ERR_INVALID;
+    *out = nullptr;
+    // relations: shapes as dfq_cle_relation
+    std::vector<CleRel> R(n_rel);
+    int64_t M = 0;
+    for (int32_t r = 0; r < n_rel; ++r) {
+        const dfq_cle_rel& d = rels[r];
+        if (!d.w1 || !d.w2 || !d.b1 || d.c1 <= 0 || d.len1 <= 0 || d.o2 <= 0 || d.i2 <= 0 || d.khw2 <= 0)
+            return DFQ_ERR_INVALID;
+        int64_t groups = 1;
+        if (d.c1 != d.i2) {
+            groups = d.c1 / d.i2;
+            if (groups <= 0 || groups * d.i2 != d.c1) return DFQ_ERR_SHAPE;
+        }
+        if (d.o2 % groups != 0) return DFQ_ERR_SHAPE;
+        CleRel c{};
+        c.w1 = d.w1; c.w2 = d.w2; c.b1 = d.b1; c.bnw = d.bn_w; c.bnb = d.bn_b; c.sacc = d.s_acc;
+        c.c1 = d.c1; c.len1 = d.len1; c.o2 = d.o2; c.i2 = d.i2; c.khw2 = d.khw2; c.o2g = d.o2 / groups;
+        c.moff = M;
+        c.sacc_init = d.s_acc_init;
+        c.vec1 = (d.len1 % 4 == 0 && reinterpret_cast<uintptr_t>(d.w1) % 16 == 0) ? 1 : 0;
+        c.vec2 = (d.i2 == 1 && (c.o2g * d.khw2) % 4 == 0 && reinterpret_cast<uintptr_t>(d.w2) % 16 == 0) ? 1 : 0;
+        c.fuse_next = -1;
+        c.dw_prev = -1;
+        c.w1_self = 0;
+        c.w2_self = 0;
+        M += 2 * d.c1;
+        R[r] = c;
+    }
+    const double tp1 = now_us();
+    // the structure (chains, tasks, chunks, placement) from the cache when a plan of
+    // the same shapes and tensor-sharing pattern was built before
+    std::shared_ptr<const CleStructure> S;
+    bool cached = false;
+    const std::vector<int64_t> key = cle_structure_key(R, M, targets, target_n, n_targets, ref_threads);
+    {
+        std::lock_guard<std::mutex> lock(g_struct_mu);
+        for (auto it = g_struct_cache.begin(); it != g_struct_cache.end(); ++it)
+            if (it->first == key) {
+                S = it->second;
+                g_struct_cache.splice(g_struct_cache.begin(), g_struct_cache, it);   // most recent first
+                cached = true;
+                break;
+            }
+    }
+    if (!S) {
+        auto built = std::make_shared<CleStructure>();
+        const int rc = cle_build_structure(R, M, n_rel, targets, target_n, n_targets, ref_threads, *built);
+        if (rc != DFQ_OK) return rc;
+        S = built;
+        std::lock_guard<std::mutex> lock(g_struct_mu);
+        g_struct_cache.emplace_front(key, S);
+        if (g_struct_cache.size() > kStructCacheCap) g_struct_cache.pop_back();
+    }
+    const double tp5 = now_us();
+    // this plan's addresses into its copy of the relations and layers
+    std::vector<CleRel> Rb = S->R;
+    for (int32_t r = 0; r < n_rel; ++r) {
+        Rb[r].w1 = R[r].w1; Rb[r].w2 = R[r].w2; Rb[r].b1 = R[r].b1;
+        Rb[r].bnw = R[r].bnw; Rb[r].bnb = R[r].bnb; Rb[r].sacc = R[r].sacc;
+    }
+    dfq_cle_plan* p = new (std::nothrow) dfq_cle_plan();
+    if (!p) return DFQ_ERR_NOMEM;
+    std::vector<CleLayer> layers = S->layers;
+    {
+        char* snap_base = static_cast<char*>(ws);
+        if (!snap_base && need_ws > 0) {   // no caller workspace: the plan owns its snapshots
+            hipError_t e = hipMalloc(&p->d_snap_owned, need_ws);
+            if (e != hipSuccess) { set_last_hip_error(e); cle_plan_free(p); return DFQ_ERR_HIP; }
+            snap_base = static_cast<char*>(p->d_snap_owned);
+        }
+        int64_t snap_off = 0;
+        for (int32_t l = 0; l < n_targets; ++l) {
+            layers[l].w = targets[l];
+            layers[l].snap = reinterpret_cast<float*>(snap_base + snap_off);
+            snap_off += snap_bytes(target_n[l]);
+        }
+    }
+    const std::vector<CleTask>& rt = S->rt;
+    const std::vector<CleTask>& at = S->at;
+    const std::vector<CleChunk>& chunks = S->chunks;
+    const std::vector<CleUnit>& units = S->units;
+    const std::vector<int64_t>& b1off = S->b1off;
+    const std::vector<int64_t>& rstep = S->rstep;
+    const std::vector<int64_t>& astep = S->astep;
+    const int64_t nb1_total = S->nb1_total, ri0 = S->ri0, ri1 = S->ri1;
+    const int32_t steps = S->steps, chains = S->chains, nlaunch = S->nlaunch, stop_off = S->stop_off;
+    const bool fused = S->fused, lagged = S->lagged;
+    if (cle_timing() && !cached) {   // the schedule: per offset, tile units and range tasks
         fprintf(stderr, "DFQ_CLE_TIMING plan: steps %d nlaunch %d lagged %d stop %d; offsets (units/ranges):", steps,
                 nlaunch, (int)lagged, stop_off);
         for (int32_t k = 0; k < 2 * nlaunch; ++k)
-            fprintf(stderr, " %d:%lld/%lld", k, (long long)(uoffs[k + 1] - uoffs[k]), (long long)(roffs[k + 1] - roffs[k]));
+            fprintf(stderr, " %d:%lld/%lld", k, (long long)(S->uoffs[k + 1] - S->uoffs[k]),
+                    (long long)(S->roffs[k + 1] - S->roffs[k]));
         fprintf(stderr, "; rescale tasks per step:");
         for (int32_t k = 0; k < steps; ++k) fprintf(stderr, " %lld", (long long)(astep[k + 1] - astep[k]));
         fprintf(stderr, "\n");
     }
     (void)hipGetDevice(&p->dev);
-    p->uoffs = uoffs;
-    p->roffs = roffs;
+    p->uoffs = S->uoffs;
+    p->roffs = S->roffs;
     p->nlaunch = nlaunch;
     p->lagged = lagged;
     p->stop_off = stop_off;
@@ -2170,7 +2326,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     p->step_pos.assign(std::max<int32_t>(steps, 1), 0);
     for (int32_t k = 0; k < steps; ++k)
         for (int64_t t = astep[k]; t < astep[k + 1]; ++t)
-            if (at[t].kind == kApplyW2Tile && R[at[t].rel].khw2 > 1) p->step_pos[k] = 1;
+            if (at[t].kind == kApplyW2Tile && Rb[at[t].rel].khw2 > 1) p->step_pos[k] = 1;
     p->ri0 = ri0;
     p->ri1 = ri1;
 #ifdef DFQ_DIAGNOSTICS
@@ -2250,7 +2406,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
     auto put = [&](int64_t off, const auto& v) {
         if (!v.empty()) std::memcpy(hblob + off, v.data(), sizeof(v[0]) * v.size());
     };
-    put(o_rels, R); put(o_rt, rt); put(o_at, at); put(o_layers, layers); put(o_chunks, chunks); put(o_units, units);
+    put(o_rels, Rb); put(o_rt, rt); put(o_at, at); put(o_layers, layers); put(o_chunks, chunks); put(o_units, units);
     put(o_b1off, b1off);
     {
         float* lm = reinterpret_cast<float*>(hblob + o_part) + (int64_t)p->slots * n_targets;
@@ -2266,9 +2422,10 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         return fail(e);
     }
     if (cle_timing())
-        fprintf(stderr, "DFQ_CLE_TIMING create: plan %.1f us (relations %.1f, chains %.1f, tasks %.1f, chunks %.1f, "
-                "placement %.1f), tables %lld B %.1f us, copy %lld B %.1f us\n", tm0 - tc0, tp1 - tc0, tp2 - tp1,
-                tp3 - tp2, tp4 - tp3, tm0 - tp4, (long long)T.total, tm1 - tm0, (long long)host_bytes, now_us() - tm1);
+        fprintf(stderr, "DFQ_CLE_TIMING create: plan %.1f us (relations %.1f, structure %s %.1f: chains %.1f, tasks %.1f, "
+                "chunks %.1f, placement %.1f), tables %lld B %.1f us, copy %lld B %.1f us\n", tm0 - tc0, tp1 - tc0,
+                cached ? "cached" : "built", tp5 - tp1, S->t_chains, S->t_tasks, S->t_chunks, S->t_place,
+                (long long)T.total, tm1 - tm0, (long long)host_bytes, now_us() - tm1);
     p->d_rels = reinterpret_cast<CleRel*>(base + o_rels);
     p->d_rtasks = reinterpret_cast<CleTask*>(base + o_rt);
     p->d_atasks = reinterpret_cast<CleTask*>(base + o_at);

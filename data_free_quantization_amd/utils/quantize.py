@@ -247,8 +247,8 @@ class QuantMeasure(nn.Module):
         self.update_stat = update_stat
 
     def forward(self, input):
-        if _no_autograd(input) and (self.update_stat or self.training) and input.is_cuda \
-                and input.dtype is torch.float32 and input.numel() > 0 and input.dim() > 0:
+        if (self.update_stat or self.training) and input.is_cuda and input.dtype is torch.float32 \
+                and input.numel() > 0 and input.dim() > 0:
             return self._forward_fused(input)
         flat = input.detach().view(input.size(0), -1)
         if self.update_stat:
@@ -273,12 +273,13 @@ class QuantMeasure(nn.Module):
         return quantize(input, self.num_bits, min_value=float(mn), max_value=float(mx), num_chunks=16)
 
     def _forward_fused(self, input):
-        """Inference with live statistics: the observer update in ONE dfq_act_observe
-        call (rows' min / max, their ATen-order means, the update_stat select and
-        the training momentum, two launches) and the fake quant in one more --
-        instead of eight torch ops and their allocations per call.  The running
-        buffers are updated in place (the reference rebinds them to new tensors
-        of the same values)."""
+        """Live statistics: the observer update in ONE dfq_act_observe call (rows'
+        min / max, their means in ATen's CPU sum order -- the order of every other
+        reduction this library reproduces, and of the reference's CPU fixtures --
+        the update_stat select and the training momentum, two launches) and, at
+        inference, the fake quant in one more: instead of eight torch ops and
+        their allocations per call.  The running buffers are updated in place (the
+        reference rebinds them to new tensors of the same values)."""
         x = input.detach()
         if not x.is_contiguous():
             x = x.contiguous()
@@ -295,7 +296,10 @@ class QuantMeasure(nn.Module):
                                                _lib.ptr(rmax), int(bool(self.update_stat)), int(bool(self.training)),
                                                float(self.momentum), _lib.ptr(out2), _lib.stream_of(x)),
                    "dfq_act_observe", RuntimeError)
-        return fake_quant_given(input, self.num_bits, min_dev=out2[0], max_dev=out2[1])
+        if _no_autograd(input):
+            return fake_quant_given(input, self.num_bits, min_dev=out2[0], max_dev=out2[1])
+        mn, mx = out2.tolist()   # the STE path: the reference's float(mn) / float(mx)
+        return quantize(input, self.num_bits, min_value=mn, max_value=mx, num_chunks=16)
 
     def set_update_stat(self, update_stat):
         self.update_stat = update_stat
