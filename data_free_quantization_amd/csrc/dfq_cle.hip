@@ -1957,6 +1957,12 @@ static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, 
     bool lag_ok = fused && !tiny && have_tiles && steps > 0;
     if (const char* e = ab_env("DFQ_CLE_LAG")) lag_ok = lag_ok && e[0] != '0';
     int32_t band_force = -1;   // diagnostics A/B: the tiles' band start
+    // diagnostics A/B: the lagged schedule's stop rule at the last tile arrival
+    // (band of nlaunch offsets) instead of as a block of its own after the band
+    const bool stop_arrival = [] {
+        const char* e = ab_env("DFQ_CLE_STOP");
+        return e && e[0] == 'a';
+    }();
     if (const char* e = ab_env("DFQ_CLE_BAND")) band_force = atoi(e);
     // (first, last) step of every tensor the relations rescale: a linear table (a few
     // hundred tensors at most), looked up once per relation and target layer
@@ -1991,6 +1997,7 @@ static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, 
     // placement (lagged schedule only): loads in bytes per launch position of a
     // group -- the steps' rescale traffic, then greedy by size: each range task and
     // each layer's tiles to the least-loaded admissible offset
+    int32_t lag_max = -1;   // the placement's largest tile offset
     auto place = [&](int32_t nl_) -> bool {
         auto window = [&](int32_t ti) -> std::pair<int32_t, int32_t> {   // [lo, hi] offsets (untouched: anywhere)
             if (ti < 0) return {0, 2 * nl_ - 1};
@@ -2049,7 +2056,7 @@ static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, 
             maxlo = std::max(maxlo, lwin[l].first);
             minhi = std::min(minhi, lwin[l].second);
         }
-        const int32_t bw = nl_ - 1;   // band width
+        const int32_t bw = stop_arrival ? nl_ : nl_ - 1;   // band width
         if (bw < 1) return false;
         const int32_t b_lo = std::max(0, maxlo - bw + 1), b_hi = std::min(minhi, 2 * nl_ - 1 - bw);
         if (b_lo > b_hi) return false;
@@ -2079,18 +2086,19 @@ static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, 
                 loff[l] = pick(std::max(lwin[l].first, B0), std::min(lwin[l].second, B0 + bw - 1), 12.0 * target_n[l]);
                 maxoff = std::max(maxoff, loff[l]);
             }
-            if (maxoff + 1 > 2 * nl_ - 1) continue;
+            if (!stop_arrival && maxoff + 1 > 2 * nl_ - 1) continue;
             double cost = *std::max_element(load.begin(), load.end());
             if (cost < best) {
                 best = cost;
                 layer_off = loff;
                 rt_off = roff;
-                stop_off = maxoff + 1;
+                stop_off = stop_arrival ? -1 : maxoff + 1;
+                lag_max = maxoff;
             }
         }
         return best < 1e300;
     };
-    if (lag_ok && place(steps) && stop_off >= steps) {
+    if (lag_ok && place(steps) && (stop_arrival ? lag_max >= steps : stop_off >= steps)) {
         nlaunch = steps;
         lagged = true;
     } else {   // everything in the tiles-only launch after the steps (offset steps), the stop rule at the last arrival
@@ -2178,7 +2186,7 @@ static std::vector<int64_t> cle_structure_key(const std::vector<CleRel>& R, int6
     key.push_back(M);
     key.push_back(n_targets);
     key.push_back(ref_threads);
-    for (const char* sw : {"DFQ_CLE_FUSED", "DFQ_CLE_LAG", "DFQ_CLE_BAND"}) {   // diagnostics library only
+    for (const char* sw : {"DFQ_CLE_FUSED", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_STOP"}) {   // diagnostics library only
         const char* v = ab_env(sw);
         int64_t h = v ? 1 : 0;
         for (int k = 0; v && v[k] && k < 8; ++k) h = h * 131 + (unsigned char)v[k];

@@ -270,78 +270,60 @@ __device__ __forceinline__ void quant_vec4(const DevTensor& T, int n, int64_t ba
     const float inv_len = T.inv_len;
     const float coff = sym ? 128.f : 0.f;
     const uint32_t cflip = sym ? 0x80808080u : 0u;
-    // kB float4s per lane at a time: their LDS loads (the values, then each one's
-    // row parameters) are all issued before the first is used -- one LDS round
-    // trip per kB float4s instead of two dependent ones per float4 (a task has at
-    // most 8 float4s per lane; ~2 waves per SIMD hide little latency on their own)
-    constexpr int kB = 4;
-    for (int j0 = lane; j0 < nj; j0 += kB * kWave) {
-        float4 xb[kB];
-        float sb[kB], mb[kB];
-#pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            const int j = j0 + u * kWave;
-            if (j < nj) {
-                xb[u] = reinterpret_cast<const float4*>(data)[j];
-                if (whole) {   // one row per float4 (4 | len, 4 | goff)
-                    int r = (int)(((float)(4 * j + eoff) + 0.5f) * inv_len);
-                    r = min(r, 63);
-                    sb[u] = ls[r];
-                    mb[u] = lmn[r];
-                }
-            }
+#pragma unroll 2
+    for (int j = lane; j < nj; j += kWave) {
+        const float4 xv = reinterpret_cast<const float4*>(data)[j];
+        float s = pc.s, mn = pc.mn;
+        if (whole) {   // one row per float4 (4 | len, 4 | goff)
+            int r = (int)(((float)(4 * j + eoff) + 0.5f) * inv_len);
+            r = min(r, 63);
+            s = ls[r];
+            mn = lmn[r];
         }
+        const float negmn = whole ? -mn : pc.negmn;
+        const float rs = __builtin_amdgcn_rcpf(s);
+        float t[4] = {(xv.x + negmn) * rs, (xv.y + negmn) * rs, (xv.z + negmn) * rs, (xv.w + negmn) * rs};
+        bool need[4];
 #pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            const int j = j0 + u * kWave;
-            if (j >= nj) break;
-            const float4 xv = xb[u];
-            const float s = whole ? sb[u] : pc.s, mn = whole ? mb[u] : pc.mn;
-            const float negmn = whole ? -mn : pc.negmn;
-            const float rs = __builtin_amdgcn_rcpf(s);
-            float t[4] = {(xv.x + negmn) * rs, (xv.y + negmn) * rs, (xv.z + negmn) * rs, (xv.w + negmn) * rs};
-            bool need[4];
+        for (int k = 0; k < 4; ++k) {
+            t[k] = __builtin_amdgcn_fmed3f(t[k], qmin, qmax);
+            const float d = __builtin_amdgcn_fractf(t[k]) - 0.5f;
+            need[k] = !(fabsf(d) > fabsf(t[k]) * 0x1p-20f);
+        }
+        if (__builtin_amdgcn_ballot_w64(need[0] | need[1] | need[2] | need[3])) {   // wave-uniform, rare
+            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                t[k] = __builtin_amdgcn_fmed3f(t[k], qmin, qmax);
-                const float d = __builtin_amdgcn_fractf(t[k]) - 0.5f;
-                need[k] = !(fabsf(d) > fabsf(t[k]) * 0x1p-20f);
-            }
-            if (__builtin_amdgcn_ballot_w64(need[0] | need[1] | need[2] | need[3])) {   // wave-uniform, rare
-                const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+            for (int k = 0; k < 4; ++k)
+                if (need[k]) t[k] = __builtin_amdgcn_fmed3f((xs[k] + negmn) / s, qmin, qmax);
+        }
+        float q[4], y[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (need[k]) t[k] = __builtin_amdgcn_fmed3f((xs[k] + negmn) / s, qmin, qmax);
-            }
-            float q[4], y[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                q[k] = rintf(t[k]);
-                y[k] = q[k] * s;
-                y[k] = y[k] + mn;
-                if constexpr (CLIP) y[k] = __builtin_amdgcn_fmed3f(y[k], clo, chi);
-            }
-            st<NT>(reinterpret_cast<float4*>(dq) + j, make_float4(y[0], y[1], y[2], y[3]));
-            if constexpr (CB == 1) {
-                uint32_t c = __builtin_amdgcn_cvt_pk_u8_f32(q[0] + coff, 0, 0u);
-                c = __builtin_amdgcn_cvt_pk_u8_f32(q[1] + coff, 1, c);
-                c = __builtin_amdgcn_cvt_pk_u8_f32(q[2] + coff, 2, c);
-                c = __builtin_amdgcn_cvt_pk_u8_f32(q[3] + coff, 3, c);
-                st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, c ^ cflip);
-            } else if constexpr (CB == 3) {   // DFQ_PACK_INT4: 4 codes -> 2 bytes (base % 4 == 0)
-                const uint32_t c = ((uint32_t)(int)q[0] & 0xFu) | (((uint32_t)(int)q[1] & 0xFu) << 4) |
-                                   (((uint32_t)(int)q[2] & 0xFu) << 8) | (((uint32_t)(int)q[3] & 0xFu) << 12);
-                st<NT>(reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(T.codes) + base / 2) + j, (uint16_t)c);
-            } else if constexpr (CB == 2) {
-                const uint64_t c = ((uint64_t)(uint16_t)(int)q[0]) | ((uint64_t)(uint16_t)(int)q[1] << 16) |
-                                   ((uint64_t)(uint16_t)(int)q[2] << 32) | ((uint64_t)(uint16_t)(int)q[3] << 48);
-                st<NT>(reinterpret_cast<uint64_t*>(static_cast<uint16_t*>(T.codes) + base) + j, c);
-            }
-            if constexpr (EM != 0) {
-                const float4 ev = make_float4(y[0] - xv.x, y[1] - xv.y, y[2] - xv.z, y[3] - xv.w);
-                if constexpr (EM == 1) st<NT>(reinterpret_cast<float4*>(T.esum + base) + j, ev);
-                else reinterpret_cast<float4*>(data)[j] = ev;
-            }
+        for (int k = 0; k < 4; ++k) {
+            q[k] = rintf(t[k]);
+            y[k] = q[k] * s;
+            y[k] = y[k] + mn;
+            if constexpr (CLIP) y[k] = __builtin_amdgcn_fmed3f(y[k], clo, chi);
+        }
+        st<NT>(reinterpret_cast<float4*>(dq) + j, make_float4(y[0], y[1], y[2], y[3]));
+        if constexpr (CB == 1) {
+            uint32_t c = __builtin_amdgcn_cvt_pk_u8_f32(q[0] + coff, 0, 0u);
+            c = __builtin_amdgcn_cvt_pk_u8_f32(q[1] + coff, 1, c);
+            c = __builtin_amdgcn_cvt_pk_u8_f32(q[2] + coff, 2, c);
+            c = __builtin_amdgcn_cvt_pk_u8_f32(q[3] + coff, 3, c);
+            st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, c ^ cflip);
+        } else if constexpr (CB == 3) {   // DFQ_PACK_INT4: 4 codes -> 2 bytes (base % 4 == 0)
+            const uint32_t c = ((uint32_t)(int)q[0] & 0xFu) | (((uint32_t)(int)q[1] & 0xFu) << 4) |
+                               (((uint32_t)(int)q[2] & 0xFu) << 8) | (((uint32_t)(int)q[3] & 0xFu) << 12);
+            st<NT>(reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(T.codes) + base / 2) + j, (uint16_t)c);
+        } else if constexpr (CB == 2) {
+            const uint64_t c = ((uint64_t)(uint16_t)(int)q[0]) | ((uint64_t)(uint16_t)(int)q[1] << 16) |
+                               ((uint64_t)(uint16_t)(int)q[2] << 32) | ((uint64_t)(uint16_t)(int)q[3] << 48);
+            st<NT>(reinterpret_cast<uint64_t*>(static_cast<uint16_t*>(T.codes) + base) + j, c);
+        }
+        if constexpr (EM != 0) {
+            const float4 ev = make_float4(y[0] - xv.x, y[1] - xv.y, y[2] - xv.z, y[3] - xv.w);
+            if constexpr (EM == 1) st<NT>(reinterpret_cast<float4*>(T.esum + base) + j, ev);
+            else reinterpret_cast<float4*>(data)[j] = ev;
         }
     }
 }

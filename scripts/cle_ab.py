@@ -21,7 +21,8 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
-SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "CLE_AB_BLOCKING")
+SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_STOP",
+            "CLE_AB_BLOCKING")
 CONFIGS = {
     "tiles_fin": {},                                # the product (lagged schedule where the plan allows it)
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches
@@ -29,6 +30,7 @@ CONFIGS = {
     "step_grid_1024": {"DFQ_CLE_STEP_GRID": "1024"},
     "step_grid_4096": {"DFQ_CLE_STEP_GRID": "4096"},
     "no_lag": {"DFQ_CLE_LAG": "0"},                 # round 4's schedule: tiles / ranges / stop rule in a launch of their own
+    "stop_arrival": {"DFQ_CLE_STOP": "arrival"},    # lagged, the stop rule at the last tile arrival (band of 3)
     "band1": {"DFQ_CLE_BAND": "1"},                 # the tiles' band start (lagged schedule)
     "band2": {"DFQ_CLE_BAND": "2"},
     "blocking": {"CLE_AB_BLOCKING": "1"},           # run_dfq's CLE blocking (no caller gate beside the loop)

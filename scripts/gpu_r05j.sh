@@ -14,7 +14,7 @@ tail -3 "$out/pytest.log"
 DFQ_CLE_TIMING=1 timeout -k 10 200 python -u scripts/cle_ab.py --reps 2 --configs tiles_fin > "$out/plan.log" 2>&1 \
     || { echo "plan print failed rc=$?"; tail -30 "$out/plan.log"; exit 1; }
 grep "TIMING create\|python create" "$out/plan.log" | tail -6
-timeout -k 10 300 python -u scripts/cle_ab.py --reps 7 --configs tiles_fin,no_lag > "$out/cle_ab.jsonl" 2>&1 \
+timeout -k 10 300 python -u scripts/cle_ab.py --reps 7 --configs tiles_fin,no_lag,stop_arrival > "$out/cle_ab.jsonl" 2>&1 \
     || { echo "cle_ab failed rc=$?"; tail -30 "$out/cle_ab.jsonl"; exit 1; }
 cat "$out/cle_ab.jsonl"
 timeout -k 10 200 python -u scripts/forward_latency.py 32 > "$out/forward.log" 2>&1 \

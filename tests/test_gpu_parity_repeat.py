@@ -42,7 +42,8 @@ import json, os, sys
 sys.path.insert(0, os.environ["DFQ_ROOT"])
 from tests.parity import pipeline_mismatches
 from data_free_quantization_amd import Cross_layer_equal as cle
-SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_TEST_POLL_DELAY_US")
+SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_STOP",
+            "DFQ_CLE_TEST_POLL_DELAY_US")
 CONFIGS = {
     "product": {},                                  # the product: lagged schedule where the plan allows it
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches (graphs the fused schedule rejects)
@@ -50,6 +51,7 @@ CONFIGS = {
     "no_lag": {"DFQ_CLE_LAG": "0"},                 # tiles / ranges / stop rule in a launch of their own (round 4)
     "band1": {"DFQ_CLE_BAND": "1"},                 # lagged, the tiles' band forced
     "band2": {"DFQ_CLE_BAND": "2"},
+    "stop_arrival": {"DFQ_CLE_STOP": "arrival"},    # lagged, the stop rule at the last tile arrival
     # the host thread "descheduled" 300 us after every load of the stop rule's word,
     # then querying the stream: the queued iterations drain meanwhile (ADVICE r04's
     # stale-word race ended the loop early here)
