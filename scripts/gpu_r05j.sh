@@ -6,8 +6,8 @@ tag=${1:-r05j}
 out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_forward.py tests/test_gpu_act_range.py tests/test_gpu_act_fast.py \
-    "tests/test_gpu_pipeline.py::test_compiled_bc_walk_edge_cases" tests/test_gpu_cle_plan.py tests/test_gpu_parity_repeat.py \
+timeout -k 10 900 python -u -m pytest "tests/test_gpu_pipeline.py::test_compiled_bc_walk_edge_cases" tests/test_gpu_forward.py tests/test_gpu_act_range.py tests/test_gpu_act_fast.py \
+    tests/test_gpu_cle_plan.py tests/test_gpu_parity_repeat.py \
     -m gpu -x -q --timeout 400 --timeout-method thread > "$out/pytest.log" 2>&1 \
     || { echo "pytest failed rc=$?"; tail -60 "$out/pytest.log"; exit 1; }
 tail -3 "$out/pytest.log"
