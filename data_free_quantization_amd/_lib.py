@@ -37,7 +37,7 @@ EXPORTS = [
     "dfq_act_moments", "dfq_act_minmax", "dfq_act_affine",
 ]
 #: entry points only the diagnostics library exports (include/dfq_diag.h)
-DIAG_EXPORTS = ["dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline"]
+DIAG_EXPORTS = ["dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline", "dfq_debug_ablate"]
 DIAG_LIB_PATH = PKG / "libdfq_diag.so"
 
 
@@ -170,6 +170,7 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
     diag = {
         "dfq_probe_stream": ([P, P, P, P, I64, I32, P], C.c_int),
         "dfq_debug_timeline": ([P, I64], C.c_int),
+        "dfq_debug_ablate": ([C.c_uint32], C.c_int),
         "dfq_probe_lds": ([P, P, P, P, I64, I32, I32, P], C.c_int),
     }
     for name, (args, res) in sig.items():

@@ -45,6 +45,21 @@ __device__ __forceinline__ float rl_f(float v, int lane) {
 // DPP quad swaps and half-row / row mirrors inside 16-lane rows (VALU, no LDS
 // round trip), then LDS-permute shuffles only for the 32- and 64-lane groups.
 // Every lane ends with its group's result.
+// 3-input min / max as single v_min3_f32 / v_max3_f32 without the operand
+// canonicalisation the compiler adds to fminf / fmaxf of loaded values (one v_max
+// x, x per operand).  Quiet NaNs are ignored as by fminf / fmaxf; only a signalling
+// NaN operand (which no fp32 weight produced by torch holds) could differ.
+__device__ __forceinline__ float min3_nc(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float max3_nc(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __device__ __forceinline__ void group_minmax(float& lo, float& hi, int G) {
     if (G >= 2) {
         lo = fminf(lo, dpp_f(lo, 0xB1));

@@ -97,7 +97,7 @@ struct alignas(16) DevTensor {
     float inv_len;     // 1/row_len, for the element -> row map inside a task
     int32_t vec4;      // 16-B loads / stores legal
     int32_t code_bytes;
-    int32_t pad;
+    uint32_t len_magic;  // ceil(2^32 / row_len): element -> row as one v_mul_hi_u32 (row_len >= 2)
     const uint32_t* range_enc;   // DFQ_DEVICE_RANGE
 };
 
@@ -127,12 +127,13 @@ struct alignas(16) DevTask {
 static_assert(sizeof(DevTask) == 32, "one 32-B scalar load per task record");
 __device__ __forceinline__ int64_t task_elem_start(const DevTask& k, const DevTensor& T) { return k.src - T.src; }
 
-// Per-wave LDS image: [NB buffers of CHUNK floats][MAXROWS scales][MAXROWS mins],
+// Per-wave LDS image: [NB buffers of CHUNK floats][MAXROWS scales][MAXROWS mins]
+// [MAXROWS reciprocal scales],
 // carved out of ONE __shared__ array (a second __shared__ object next to an
 // LDS-DMA target can make hipcc drain vmcnt before every ds_read).
 template <int CHUNK, int MAXROWS, int NB>
 struct LdsLayout {
-    static constexpr int kPerWave = NB * CHUNK + 2 * MAXROWS;
+    static constexpr int kPerWave = NB * CHUNK + 3 * MAXROWS;
     static constexpr int kTotal = kWavesPerBlock * kPerWave;
 };
 
@@ -251,101 +252,146 @@ __device__ __forceinline__ void issue_task_load(const DevTask& task, float* data
 
 // The VEC quantize loop with the task's output set fixed at compile time (clip,
 // code format, error-sum form): straight-line per-float4 bodies without the
-// generic loop's per-iteration flag branches, clamps as v_med3 (no operand
-// canonicalisation: fminf / fmaxf on values the compiler cannot prove canonical
-// cost a v_max x, x each), byte codes by v_cvt_pk_u8_f32 (q is integral and in
-// [qmin, qmax]: exact; symmetric codes offset by 128 and flipped back by one
-// xor), stores addressed from the task's uniform base pointers.  Bit-identical
-// with the generic loop (same per-element operation sequence: the med3 clamp
-// equals fminf(fmaxf(.)) for qmin <= qmax and non-NaN inputs).
+// generic loop's per-iteration flag branches.  Bit-identical with the generic loop
+// (same IEEE operation sequence per element); what differs is how each step is
+// issued on a wave64 SIMD, where every VALU op costs 4 cycles and this loop is the
+// single-model sweep's VALU budget:
+//  * fp32 pairs as packed ops (v_pk_add_f32 / v_pk_mul_f32: two lanes' worth per op);
+//  * the element -> row map as one v_mul_hi_u32 by ceil(2^32 / row_len) (exact for
+//    e < 2^16, row_len < 2^13), the row's 1/s read from LDS next to s and mn (no
+//    per-float4 v_rcp);
+//  * rint(t) as (t + 1.5*2^23) - 1.5*2^23 (t is clamped to [qmin, qmax], |t| < 2^22:
+//    round-to-nearest-even at the integer ulp, the same value as rintf); the sum's
+//    low mantissa bits are q's two's complement, so the codes are byte / half
+//    selects (v_perm_b32) of it;
+//  * the reciprocal screen as |t - rint(t)| >= 0.5 - qabs 2^-20 (qabs = the larger of
+//    |qmin|, |qmax| >= |t|): a superset of the elements within |t| 2^-20 of a
+//    rounding boundary, which are the only ones whose reciprocal quotient can round
+//    differently from the IEEE divide; those take the divide.
+//  * clamps as v_med3 (no operand canonicalisation: fminf / fmaxf on values the
+//    compiler cannot prove canonical cost a v_max x, x each).
 // CB: 0 no codes, 1 int8 / uint8, 2 int16, 3 packed int4.  EM: 0 no error sums,
 // 1 E stored (KH*KW = 1), 2 eps back to LDS (KH*KW > 1).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool CLIP, int CB, int EM, bool NT>
 __device__ __forceinline__ void quant_vec4(const DevTensor& T, int n, int64_t base, float* data, const float* ls,
-                                           const float* lmn, const QParams& pc, bool whole, int eoff, int lane,
-                                           float qmin, float qmax, bool sym) {
+                                           const float* lmn, const float* lrs, const QParams& pc, bool whole,
+                                           int eoff, int lane, float qmin, float qmax, bool sym) {
+    constexpr float kMagic = 12582912.0f;   // 1.5 * 2^23
     const int nj = n >> 2;
     float* dq = T.dst + base;
     const float clo = T.clip_lo, chi = T.clip_hi;
-    const float inv_len = T.inv_len;
-    const float coff = sym ? 128.f : 0.f;
-    const uint32_t cflip = sym ? 0x80808080u : 0u;
-#pragma unroll 2
-    for (int j = lane; j < nj; j += kWave) {
-        const float4 xv = reinterpret_cast<const float4*>(data)[j];
-        float s = pc.s, mn = pc.mn;
-        if (whole) {   // one row per float4 (4 | len, 4 | goff)
-            int r = (int)(((float)(4 * j + eoff) + 0.5f) * inv_len);
-            r = min(r, 63);
-            s = ls[r];
-            mn = lmn[r];
-        }
-        const float negmn = whole ? -mn : pc.negmn;
-        const float rs = __builtin_amdgcn_rcpf(s);
-        float t[4] = {(xv.x + negmn) * rs, (xv.y + negmn) * rs, (xv.z + negmn) * rs, (xv.w + negmn) * rs};
-        bool need[4];
+    // whole-row tasks: the element's row; pieces: their one parameter set, in slot 0
+    const uint32_t magic = whole ? T.len_magic : 0u;
+    const float thr = 0.5f - fmaxf(-qmin, qmax) * 0x1p-20f;
+    const f32x2 mg = {kMagic, kMagic};
+    struct Q4 {   // one float4's state between the screen and the stores
+        float4 x;
+        float s, mn;
+        float t[4];
+        f32x2 ta, tb, qa, qb, da, db;
+    };
+    auto prep = [&](int j, uint32_t e, Q4& q) {
+        q.x = reinterpret_cast<const float4*>(data)[j];
+        const uint32_t r = __umulhi(e, magic);   // one row per float4 (4 | len, 4 | goff)
+        q.s = ls[r];
+        q.mn = lmn[r];
+        const float rs = lrs[r];
+        const f32x2 nm = {-q.mn, -q.mn};   // x + (-mn) (symmetric: x + -0.0, which is x)
+        const f32x2 rs2 = {rs, rs};
+        const f32x2 a = (f32x2{q.x.x, q.x.y} + nm) * rs2, b = (f32x2{q.x.z, q.x.w} + nm) * rs2;
+        q.t[0] = __builtin_amdgcn_fmed3f(a.x, qmin, qmax);
+        q.t[1] = __builtin_amdgcn_fmed3f(a.y, qmin, qmax);
+        q.t[2] = __builtin_amdgcn_fmed3f(b.x, qmin, qmax);
+        q.t[3] = __builtin_amdgcn_fmed3f(b.y, qmin, qmax);
+        q.ta = f32x2{q.t[0], q.t[1]} + mg;
+        q.tb = f32x2{q.t[2], q.t[3]} + mg;
+        q.qa = q.ta - mg;
+        q.qb = q.tb - mg;
+        // opaque to the optimiser: merged with the rare path's values as they are,
+        // not recomputed from t after the branch
+        asm("" : "+v"(q.ta), "+v"(q.tb), "+v"(q.qa), "+v"(q.qb));
+        q.da = f32x2{q.t[0], q.t[1]} - q.qa;
+        q.db = f32x2{q.t[2], q.t[3]} - q.qb;
+    };
+    auto dmax = [&](const Q4& q) { return fmaxf(fmaxf(fabsf(q.da.x), fabsf(q.da.y)), fmaxf(fabsf(q.db.x), fabsf(q.db.y))); };
+    auto fix = [&](Q4& q) {   // the IEEE divide for the screened elements
+        const float negmn = -q.mn;
+        if (fabsf(q.da.x) >= thr) q.t[0] = __builtin_amdgcn_fmed3f((q.x.x + negmn) / q.s, qmin, qmax);
+        if (fabsf(q.da.y) >= thr) q.t[1] = __builtin_amdgcn_fmed3f((q.x.y + negmn) / q.s, qmin, qmax);
+        if (fabsf(q.db.x) >= thr) q.t[2] = __builtin_amdgcn_fmed3f((q.x.z + negmn) / q.s, qmin, qmax);
+        if (fabsf(q.db.y) >= thr) q.t[3] = __builtin_amdgcn_fmed3f((q.x.w + negmn) / q.s, qmin, qmax);
+        q.ta = f32x2{q.t[0], q.t[1]} + mg;
+        q.tb = f32x2{q.t[2], q.t[3]} + mg;
+        q.qa = q.ta - mg;
+        q.qb = q.tb - mg;
+    };
+    auto out = [&](int j, const Q4& q) {
+        const f32x2 s2 = {q.s, q.s}, mn2 = {q.mn, q.mn};
+        const f32x2 ya = q.qa * s2 + mn2, yb = q.qb * s2 + mn2;   // q * s, then + mn: two roundings (no contraction)
+        float y[4] = {ya.x, ya.y, yb.x, yb.y};
+        if constexpr (CLIP) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            t[k] = __builtin_amdgcn_fmed3f(t[k], qmin, qmax);
-            const float d = __builtin_amdgcn_fractf(t[k]) - 0.5f;
-            need[k] = !(fabsf(d) > fabsf(t[k]) * 0x1p-20f);
-        }
-        if (__builtin_amdgcn_ballot_w64(need[0] | need[1] | need[2] | need[3])) {   // wave-uniform, rare
-            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (need[k]) t[k] = __builtin_amdgcn_fmed3f((xs[k] + negmn) / s, qmin, qmax);
-        }
-        float q[4], y[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            q[k] = rintf(t[k]);
-            y[k] = q[k] * s;
-            y[k] = y[k] + mn;
-            if constexpr (CLIP) y[k] = __builtin_amdgcn_fmed3f(y[k], clo, chi);
+            for (int k = 0; k < 4; ++k) y[k] = __builtin_amdgcn_fmed3f(y[k], clo, chi);
         }
         st<NT>(reinterpret_cast<float4*>(dq) + j, make_float4(y[0], y[1], y[2], y[3]));
-        if constexpr (CB == 1) {
-            uint32_t c = __builtin_amdgcn_cvt_pk_u8_f32(q[0] + coff, 0, 0u);
-            c = __builtin_amdgcn_cvt_pk_u8_f32(q[1] + coff, 1, c);
-            c = __builtin_amdgcn_cvt_pk_u8_f32(q[2] + coff, 2, c);
-            c = __builtin_amdgcn_cvt_pk_u8_f32(q[3] + coff, 3, c);
-            st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, c ^ cflip);
+        const uint32_t u0 = __float_as_uint(q.ta.x), u1 = __float_as_uint(q.ta.y);
+        const uint32_t u2 = __float_as_uint(q.tb.x), u3 = __float_as_uint(q.tb.y);
+        if constexpr (CB == 1) {   // bytes 0 of u0..u3
+            const uint32_t c = __builtin_amdgcn_perm(u1, u0, 0x0c0c0400u) | __builtin_amdgcn_perm(u3, u2, 0x04000c0cu);
+            st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, c);
         } else if constexpr (CB == 3) {   // DFQ_PACK_INT4: 4 codes -> 2 bytes (base % 4 == 0)
-            const uint32_t c = ((uint32_t)(int)q[0] & 0xFu) | (((uint32_t)(int)q[1] & 0xFu) << 4) |
-                               (((uint32_t)(int)q[2] & 0xFu) << 8) | (((uint32_t)(int)q[3] & 0xFu) << 12);
+            const uint32_t c = (u0 & 0xFu) | ((u1 & 0xFu) << 4) | ((u2 & 0xFu) << 8) | ((u3 & 0xFu) << 12);
             st<NT>(reinterpret_cast<uint16_t*>(static_cast<uint8_t*>(T.codes) + base / 2) + j, (uint16_t)c);
-        } else if constexpr (CB == 2) {
-            const uint64_t c = ((uint64_t)(uint16_t)(int)q[0]) | ((uint64_t)(uint16_t)(int)q[1] << 16) |
-                               ((uint64_t)(uint16_t)(int)q[2] << 32) | ((uint64_t)(uint16_t)(int)q[3] << 48);
+        } else if constexpr (CB == 2) {   // halves 0 of u0..u3
+            const uint64_t c = (uint64_t)__builtin_amdgcn_perm(u1, u0, 0x05040100u) |
+                               ((uint64_t)__builtin_amdgcn_perm(u3, u2, 0x05040100u) << 32);
             st<NT>(reinterpret_cast<uint64_t*>(static_cast<uint16_t*>(T.codes) + base) + j, c);
         }
         if constexpr (EM != 0) {
-            const float4 ev = make_float4(y[0] - xv.x, y[1] - xv.y, y[2] - xv.z, y[3] - xv.w);
+            const f32x2 ea = f32x2{y[0], y[1]} - f32x2{q.x.x, q.x.y}, eb = f32x2{y[2], y[3]} - f32x2{q.x.z, q.x.w};
+            const float4 ev = make_float4(ea.x, ea.y, eb.x, eb.y);
             if constexpr (EM == 1) st<NT>(reinterpret_cast<float4*>(T.esum + base) + j, ev);
             else reinterpret_cast<float4*>(data)[j] = ev;
         }
+    };
+    // two independent float4s per lane and step (one dependent chain per float4 is
+    // too little work between LDS round trips at 2-3 waves per SIMD); the second
+    // one past the task's end recomputes the first and stores nothing
+    uint32_t e = (uint32_t)(4 * lane + eoff);
+    for (int j = lane; j < nj; j += 2 * kWave, e += 8 * kWave) {
+        const int j1 = j + kWave;
+        const bool has1 = j1 < nj;
+        Q4 qa, qb;
+        prep(j, e, qa);
+        prep(has1 ? j1 : j, has1 ? e + 4 * kWave : e, qb);
+        if (__builtin_amdgcn_ballot_w64(fmaxf(dmax(qa), dmax(qb)) >= thr)) {   // wave-uniform, rare
+            fix(qa);
+            fix(qb);
+        }
+        out(j, qa);
+        if (has1) out(j1, qb);
     }
 }
 
 template <bool CLIP, int CB, bool NT>
 __device__ __forceinline__ void quant_vec4_e(int em, const DevTensor& T, int n, int64_t base, float* data,
-                                             const float* ls, const float* lmn, const QParams& pc, bool whole,
-                                             int eoff, int lane, float qmin, float qmax, bool sym) {
-    if (em == 0) quant_vec4<CLIP, CB, 0, NT>(T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
-    else if (em == 1) quant_vec4<CLIP, CB, 1, NT>(T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
-    else quant_vec4<CLIP, CB, 2, NT>(T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
+                                             const float* ls, const float* lmn, const float* lrs, const QParams& pc,
+                                             bool whole, int eoff, int lane, float qmin, float qmax, bool sym) {
+    if (em == 0) quant_vec4<CLIP, CB, 0, NT>(T, n, base, data, ls, lmn, lrs, pc, whole, eoff, lane, qmin, qmax, sym);
+    else if (em == 1) quant_vec4<CLIP, CB, 1, NT>(T, n, base, data, ls, lmn, lrs, pc, whole, eoff, lane, qmin, qmax, sym);
+    else quant_vec4<CLIP, CB, 2, NT>(T, n, base, data, ls, lmn, lrs, pc, whole, eoff, lane, qmin, qmax, sym);
 }
 
 template <bool CLIP, bool NT>
 __device__ __forceinline__ void quant_vec4_c(int cb, int em, const DevTensor& T, int n, int64_t base, float* data,
-                                             const float* ls, const float* lmn, const QParams& pc, bool whole,
-                                             int eoff, int lane, float qmin, float qmax, bool sym) {
+                                             const float* ls, const float* lmn, const float* lrs, const QParams& pc,
+                                             bool whole, int eoff, int lane, float qmin, float qmax, bool sym) {
     switch (cb) {
-        case 0: quant_vec4_e<CLIP, 0, NT>(em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym); break;
-        case 1: quant_vec4_e<CLIP, 1, NT>(em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym); break;
-        case 2: quant_vec4_e<CLIP, 2, NT>(em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym); break;
-        default: quant_vec4_e<CLIP, 3, NT>(em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
+        case 0: quant_vec4_e<CLIP, 0, NT>(em, T, n, base, data, ls, lmn, lrs, pc, whole, eoff, lane, qmin, qmax, sym); break;
+        case 1: quant_vec4_e<CLIP, 1, NT>(em, T, n, base, data, ls, lmn, lrs, pc, whole, eoff, lane, qmin, qmax, sym); break;
+        case 2: quant_vec4_e<CLIP, 2, NT>(em, T, n, base, data, ls, lmn, lrs, pc, whole, eoff, lane, qmin, qmax, sym); break;
+        default: quant_vec4_e<CLIP, 3, NT>(em, T, n, base, data, ls, lmn, lrs, pc, whole, eoff, lane, qmin, qmax, sym);
     }
 }
 
@@ -361,7 +407,8 @@ template <int MAXROWS, bool VEC, bool NT = false, int ESPEC = 2, bool SCREEN = t
 __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& task, float* data, float* ls,
                                              float* lmn, const uint32_t* __restrict__ slot_min,
                                              const uint32_t* __restrict__ slot_max, int lane, float bmn = 0.f,
-                                             float bmx = 0.f, int goff = -1, uint64_t* tlm = nullptr) {
+                                             float bmx = 0.f, int goff = -1, uint64_t* tlm = nullptr,
+                                             uint32_t abl = 0) {
     const int n = task.n;
     const bool sym = is_sym(T.mode);
     const int len = (int)T.row_len;
@@ -385,7 +432,10 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
         for (int r0 = 0; r0 < nrows; r0 += p2) {
             const int r = r0 + sub;
             float vmin = INFINITY, vmax = -INFINITY;
-            if (r < nrows) {
+            if (abl & 1) {   // diagnostics ablation: no row reduce
+                vmin = -1.f;
+                vmax = 1.f;
+            } else if (r < nrows) {
                 const float* row = data + r * len;
                 if (VEC) {
                     // 4 LDS loads in flight per lane, then their min / max (a lane walks
@@ -393,16 +443,16 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
                     const int q4 = len >> 2;
                     const float4* row4 = reinterpret_cast<const float4*>(row);
                     for (int i = sl; i < q4; i += 4 * G) {
+                        // past the row's end a lane re-reads the row's last float4 (min / max
+                        // are idempotent): no per-load exec masks
                         float4 v[4];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u)
-                            if (i + u * G < q4) v[u] = row4[i + u * G];
+                        for (int u = 0; u < 4; ++u) v[u] = row4[min(i + u * G, q4 - 1)];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u)
-                            if (i + u * G < q4) {
-                                vmin = fminf(vmin, fminf(fminf(v[u].x, v[u].y), fminf(v[u].z, v[u].w)));
-                                vmax = fmaxf(vmax, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
-                            }
+                        for (int u = 0; u < 4; ++u) {
+                            vmin = min3_nc(min3_nc(vmin, v[u].x, v[u].y), v[u].z, v[u].w);
+                            vmax = max3_nc(max3_nc(vmax, v[u].x, v[u].y), v[u].z, v[u].w);
+                        }
                     }
                 } else {
                     for (int i = sl; i < len; i += G) {
@@ -418,6 +468,7 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
                 const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
                 ls[r] = p.s;
                 lmn[r] = p.mn;
+                lmn[MAXROWS + r] = __builtin_amdgcn_rcpf(p.s);   // the quantize loop's 1/s
                 const int64_t row_g = task.row0 + r;
                 if (T.scale) st<false>(T.scale + row_g, p.s);
                 if (T.zero) st<false>(T.zero + row_g, p.mn);
@@ -440,6 +491,12 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
             if (T.scale) st<false>(T.scale + row_g, pc.s);
             if (T.zero) st<false>(T.zero + row_g, pc.mn);
         }
+        if (VEC && lane == 0) {   // the fixed-form quantize loop reads parameters from slot 0
+            ls[0] = pc.s;
+            lmn[0] = pc.mn;
+            lmn[MAXROWS] = __builtin_amdgcn_rcpf(pc.s);
+        }
+        if (VEC) wave_lds_sync();
     }
 
     if (tlm) tlm[0] = wall_clock64();   // diagnostics timeline (variant 13): parameters done
@@ -538,14 +595,39 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
             }
         }
     };
-    if constexpr (VEC) {
+    if (abl & 6) {   // diagnostics ablation: 2 = stores without the arithmetic, 4 = no quantize loop
+        if ((abl & 64) && VEC) {   // 64 (with 4): the arithmetic without the stores
+            const int nj = n >> 2;
+            float acc = 0.f;
+            for (int j = lane; j < nj; j += kWave) {
+                const float4 xv = reinterpret_cast<const float4*>(data)[j];
+                float q0, q1, q2, q3;
+                const float4 y = four(xv, params_for(4 * j), q0, q1, q2, q3);
+                acc += (y.x + y.y) + (y.z + y.w) + (q0 + q1) + (q2 + q3);
+            }
+            if (acc == 1234.5678f) st<false>(T.dst + base, acc);   // keeps the work
+        } else if (!(abl & 4) && VEC) {
+            const int nj = n >> 2;
+            for (int j = lane; j < nj; j += kWave) {
+                const float4 xv = reinterpret_cast<const float4*>(data)[j];
+                st<NT>(reinterpret_cast<float4*>(T.dst + base) + j, xv);
+                if (T.codes) st<NT>(reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(T.codes) + base) + j, __float_as_uint(xv.x));
+            }
+        } else if (!(abl & 4)) {
+            for (int e = lane; e < n; e += kWave) {
+                st<false>(T.dst + base + e, data[e]);
+                if (T.codes) st<false>(static_cast<uint8_t*>(T.codes) + base + e, (uint8_t)__float_as_uint(data[e]));
+            }
+        }
+    } else if constexpr (VEC) {
         bool done = false;
         if constexpr (SCREEN && FAST && MAXROWS == 64) {
+            const float* lrs = lmn + MAXROWS;
             if (T.dst && (!clip || T.clip_lo <= T.clip_hi)) {   // one compile-time body per (clip, codes, E form)
                 const int cb = !T.codes ? 0 : (T.code_bytes == 1 ? 1 : (T.code_bytes == 0 ? 3 : 2));
                 const int em = !want_e ? 0 : (khw == 1 ? 1 : 2);
-                if (clip) quant_vec4_c<true, NT>(cb, em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
-                else quant_vec4_c<false, NT>(cb, em, T, n, base, data, ls, lmn, pc, whole, eoff, lane, qmin, qmax, sym);
+                if (clip) quant_vec4_c<true, NT>(cb, em, T, n, base, data, ls, lmn, lrs, pc, whole, eoff, lane, qmin, qmax, sym);
+                else quant_vec4_c<false, NT>(cb, em, T, n, base, data, ls, lmn, lrs, pc, whole, eoff, lane, qmin, qmax, sym);
                 done = true;
             }
         }
@@ -631,6 +713,11 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
 // in s_memrealtime ticks (100 MHz) plus the executing wave's hardware ids.
 __device__ uint64_t* g_timeline = nullptr;
 __device__ int64_t g_timeline_cap = 0;
+// Diagnostics ablations (variant 13 only; dfq_debug_ablate): 1 no row reduce, 2 stores
+// without the quantize arithmetic, 4 no quantize loop, 8 no input loads, 16 return at
+// once (the launch alone), 32 task / tensor records and loads only (no compute),
+// 64|4 the quantize arithmetic without its stores.
+__device__ uint32_t g_ablate = 0;
 
 template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false, int ESPEC = 2, bool TL = false, bool SCREEN = true,
           bool FAST = true>
@@ -647,19 +734,33 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
     float* lmn = ls + MAXROWS;
     const int64_t wave0 = (int64_t)blockIdx.x * kWavesPerBlock + w;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    if constexpr (TL) {
+        if (g_ablate & 16) return;   // diagnostics ablation: the launch alone
+    }
     if constexpr (!PREFETCH) {
         DevTask task;
         if (wave0 < ntasks) task = tasks[wave0];
         for (int64_t t = wave0; t < ntasks; t += nwaves) {
             uint64_t tl0 = 0, tl1 = 0;
-            if constexpr (TL) tl0 = wall_clock64();
-            issue_task_load<NT>(task, wl, lane);   // needs only the task record
+            uint32_t abl = 0;
+            if constexpr (TL) {
+                tl0 = wall_clock64();
+                abl = g_ablate;
+            }
+            if (!(abl & 8)) issue_task_load<NT>(task, wl, lane);   // needs only the task record
             const DevTensor T = tensors[task.tensor];
             DevTask next = task;   // next record's scalar load overlaps this task
             if (t + nwaves < ntasks) next = tasks[t + nwaves];
             vm_wait_all();
             if constexpr (TL) tl1 = wall_clock64();
             wave_lds_sync();
+            if constexpr (TL) {
+                if (abl & 32) {   // diagnostics ablation: task and tensor records (and loads) only
+                    if (lane == 0 && T.row_len == -7) g_timeline[0] = 0;   // keeps T's load
+                    task = next;
+                    continue;
+                }
+            }
             float bmn = 0.f, bmx = 0.f;
             int goff = -1;
             if (task.nrows <= kGroupTag) {
@@ -714,6 +815,7 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                                                    T.given_max);
                     ls[lane] = p.s;
                     lmn[lane] = p.mn;
+                    lmn[MAXROWS + lane] = __builtin_amdgcn_rcpf(p.s);
                     if (rr * len >= g0) {   // the row starts in this piece: its parameters are stored once
                         const int64_t row_g = task.row0 + rr;
                         if (T.scale) st<false>(T.scale + row_g, p.s);
@@ -761,10 +863,10 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
             uint64_t* tlm = TL ? marks : nullptr;
             if (T.vec4)
                 compute_task<MAXROWS, true, NT, ESPEC, SCREEN, FAST>(T, task, wl, ls, lmn, slot_min, slot_max, lane,
-                                                                     bmn, bmx, goff, tlm);
+                                                                     bmn, bmx, goff, tlm, abl);
             else
                 compute_task<MAXROWS, false, NT, ESPEC, SCREEN, FAST>(T, task, wl, ls, lmn, slot_min, slot_max, lane,
-                                                                      bmn, bmx, goff, tlm);
+                                                                      bmn, bmx, goff, tlm, abl);
             if constexpr (TL) {
                 if (lane == 0 && t < g_timeline_cap) {
                     uint32_t hw;
@@ -772,13 +874,13 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                     uint32_t xcc;
                     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
                     const uint64_t tl2 = wall_clock64();
-                    uint64_t* r = g_timeline + 8 * t;   // {start, landed, params, quantized, done, hw ids}
+                    uint64_t* r = g_timeline + 8 * t;   // {start, landed, params, quantized, done, tensor | xcc | hw ids, ...}
                     r[0] = tl0;
                     r[1] = tl1;
                     r[2] = marks[0];
                     r[3] = marks[1];
                     r[4] = tl2;
-                    r[5] = ((uint64_t)xcc << 32) | hw;
+                    r[5] = ((uint64_t)task.tensor << 40) | ((uint64_t)(xcc & 0xFF) << 32) | hw;
                     r[6] = marks[2];
                     r[7] = marks[3];
                 }
@@ -851,6 +953,9 @@ static DevTensor to_dev(const dfq_tensor_desc& d) {
     t.given_min = d.given_min; t.given_max = d.given_max;
     t.range_enc = (d.flags & DFQ_DEVICE_RANGE) ? d.range_enc : nullptr;
     t.inv_len = d.row_len > 0 ? 1.0f / (float)d.row_len : 0.f;
+    t.len_magic = (d.row_len >= 2 && d.row_len < (int64_t(1) << 31))
+                      ? (uint32_t)(((uint64_t(1) << 32) + (uint64_t)d.row_len - 1) / (uint64_t)d.row_len)
+                      : 0u;
     t.code_bytes = (d.flags & DFQ_PACK_INT4) ? 0 : (d.bits <= 8 ? 1 : 2);   // 0: packed nibbles
     const int64_t n = d.rows * d.row_len;
     const bool channel = d.mode >= DFQ_CHANNEL_ASYM;
@@ -935,8 +1040,17 @@ static void shuffle_quads(Built& B) {
     }
 }
 
+// DFQ_SWEEP_TASK_CAP=<elements> (diagnostics): whole-row tasks of short rows hold at
+// most this many elements (rows longer than the cap keep one row per task).
+static int64_t task_cap(int chunk) {
+    const char* e = ab_env("DFQ_SWEEP_TASK_CAP");
+    const int64_t c = (e && *e) ? atoll(e) : chunk;
+    return std::max<int64_t>(1, std::min<int64_t>(c, chunk));
+}
+
 static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Variant& V) {
     const int64_t rspan = reduce_span();
+    const int64_t tcap = task_cap(V.chunk);
     const bool use_blockrow = blockrow_enabled();
     const int kChunk = V.chunk, kMaxRows = V.max_rows;
     for (int32_t ti = 0; ti < n; ++ti) {
@@ -1040,7 +1154,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
             // the scalar path: at most one row per lane keeps such a task's latency
             // near a vector task's (single-model sweeps are latency-bound)
             const int64_t row_cap = d.row_len < 32 ? kWave : kMaxRows;
-            int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(row_cap, kChunk / d.row_len));
+            int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(row_cap, tcap / d.row_len));
             if (packed && (d.row_len & 1) && rpt > 1) rpt &= ~int64_t(1);   // even task starts
             for (int64_t r = 0; r < d.rows; r += rpt) {
                 const int64_t nr = std::min<int64_t>(rpt, d.rows - r);
@@ -1103,7 +1217,7 @@ static int variant_from_env() {
 
 
 static int lds_bytes(const Variant& V) {
-    return 4 * kWavesPerBlock * ((V.prefetch ? 2 : 1) * V.chunk + 2 * V.max_rows);
+    return 4 * kWavesPerBlock * ((V.prefetch ? 2 : 1) * V.chunk + 3 * V.max_rows);
 }
 
 using MainKernel = void (*)(const DevTensor*, const DevTask*, int64_t, const uint32_t*, const uint32_t*);
@@ -1381,6 +1495,12 @@ extern "C" int dfq_debug_timeline(void* buf, int64_t cap) {
     uint64_t* p = static_cast<uint64_t*>(buf);
     DFQ_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), &p, sizeof(p)));
     DFQ_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_timeline_cap), &cap, sizeof(cap)));
+    return DFQ_OK;
+}
+
+// Diagnostics: variant 13's ablation bits (g_ablate); results are wrong while set.
+extern "C" int dfq_debug_ablate(uint32_t flags) {
+    DFQ_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_ablate), &flags, sizeof(flags)));
     return DFQ_OK;
 }
 #endif  // DFQ_DIAGNOSTICS

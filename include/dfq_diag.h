@@ -32,6 +32,11 @@ int dfq_probe_stream(const float* x, float* y, void* codes, float* esum, int64_t
  * main-list task {start, data landed, done (s_memrealtime, 100 MHz), xcc<<32|hw_id};
  * buf NULL / cap 0 disables. */
 int dfq_debug_timeline(void* buf, int64_t cap);
+// Sweep variant 13 ablations (1 no row reduce, 2 stores without the quantize
+// arithmetic, 4 no quantize loop, 8 no input loads, 16 the launch alone, 32 task and
+// tensor records without compute): attribution runs only, the outputs are wrong
+// while any bit is set.
+int dfq_debug_ablate(uint32_t flags);
 /* The sweep's memory pattern without arithmetic: 2048-element wave tasks through
  * LDS-DMA, non-temporal dq / codes / E stores (copy_only: dq only).  n % 2048 == 0. */
 int dfq_probe_lds(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t copy_only,

@@ -1,7 +1,8 @@
 """Single-model sweep latency per kernel variant: one weight set,
 per-channel sym INT8 + codes + clip + BC sums, device us per execute from HIP
 graph replays (a Python execute() alone costs more than one small sweep).
-usage: python scripts/single_ab.py [variants...]   (env DFQ_SWEEP_BLOCKS_PER_CU applies)"""
+usage: python scripts/single_ab.py [variants...]   (env DFQ_SWEEP_BLOCKS_PER_CU applies;
+DFQ_SINGLE_ESUM=0: no E, the W8 rows)"""
 import os
 os.environ.setdefault("DFQ_LIB", "diag")   # A/B variants, switches and probes: libdfq_diag.so
 import json
@@ -19,8 +20,9 @@ variants = [int(v) for v in sys.argv[1:]] or [6]
 dev = torch.device("cuda:0")
 stream = torch.cuda.current_stream(dev)
 for model in ("mobilenetv2", "resnet50", "deeplab"):
-    items, _, _, _ = bench.build_batch(model, dev, copies=1, seed=5)
-    row = {"model": model, "bpc": os.environ.get("DFQ_SWEEP_BLOCKS_PER_CU", "64")}
+    esum = os.environ.get("DFQ_SINGLE_ESUM", "1") != "0"   # 0: BASELINE.md's W8 rows (no E)
+    items, _, _, _ = bench.build_batch(model, dev, copies=1, seed=5, esum=esum)
+    row = {"model": model, "esum": esum, "bpc": os.environ.get("DFQ_SWEEP_BLOCKS_PER_CU", "64")}
     for v in variants:
         os.environ["DFQ_SWEEP_VARIANT"] = str(v)
         plan = SweepPlan(items)

@@ -1,0 +1,28 @@
+"""Single-model sweep executes for a PMC pass (one MobileNetV2 weight set,
+per-channel W8 + codes + clip, no E): run under
+`rocprofv3 --pmc ... --kernel-include-regex sweep_main -- python3 scripts/single_pmc.py [lib.so] [model]`.
+An optional library path selects an A/B build (scripts/ab_variant_libs.py)."""
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+from data_free_quantization_amd import _lib  # noqa: E402
+
+if len(sys.argv) > 1 and sys.argv[1] not in ("", "-"):
+    _lib.LIB_PATH = Path(sys.argv[1])
+model = sys.argv[2] if len(sys.argv) > 2 else "mobilenetv2"
+import bench  # noqa: E402
+from data_free_quantization_amd.sweep import SweepPlan  # noqa: E402
+
+dev = torch.device("cuda:0")
+items, _, _, _ = bench.build_batch(model, dev, copies=1, seed=5)
+plan = SweepPlan(items)
+s = torch.cuda.current_stream(dev)
+for _ in range(20):
+    plan.execute(s)
+torch.cuda.synchronize()
+plan.destroy()
+print("ok", model, _lib.LIB_PATH)

@@ -54,7 +54,21 @@ out = {"model": model, "copies": copies, "tasks": n, "grid": plan.stats["grid_bl
 bins = np.arange(0, done.max() + 1.0, 1.0)
 live = [int(((start <= b) & (done > b)).sum()) for b in bins]
 out["live_tasks_per_us"] = live
-xcc = (r[:, 5] >> 32)
+xcc = (r[:, 5] >> 32) & 0xFF
 out["tasks_per_xcc"] = np.bincount(xcc, minlength=8).tolist()
+# per task kind (float4 rows / scalar rows, row length): where the compute goes
+tix = r[:, 5] >> 40
+kinds = {}
+for ti in np.unique(tix):
+    w = items[int(ti)].src
+    rl = int(w[0].numel()) if w.dim() > 1 else int(w.numel())
+    key = f"{'vec' if rl % 4 == 0 else 'scalar'}_len{rl if rl <= 64 else ('<=576' if rl <= 576 else '>576')}"
+    kinds.setdefault(key, []).append(ti)
+for key, tis in sorted(kinds.items()):
+    m = np.isin(tix, tis)
+    out["kind_" + key] = {"tasks": int(m.sum()), "compute_p50": round(float(np.median((done - landed)[m])), 2),
+                          "row_params_p50": round(float(np.median((params - landed)[m])), 2),
+                          "quant_p50": round(float(np.median((quant - params)[m])), 2),
+                          "done_p90": round(float(np.percentile(done[m], 90)), 2)}
 print(json.dumps(out))
 plan.destroy()
