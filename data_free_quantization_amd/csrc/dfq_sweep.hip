@@ -1040,17 +1040,8 @@ static void shuffle_quads(Built& B) {
     }
 }
 
-// DFQ_SWEEP_TASK_CAP=<elements> (diagnostics): whole-row tasks of short rows hold at
-// most this many elements (rows longer than the cap keep one row per task).
-static int64_t task_cap(int chunk) {
-    const char* e = ab_env("DFQ_SWEEP_TASK_CAP");
-    const int64_t c = (e && *e) ? atoll(e) : chunk;
-    return std::max<int64_t>(1, std::min<int64_t>(c, chunk));
-}
-
 static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Variant& V) {
     const int64_t rspan = reduce_span();
-    const int64_t tcap = task_cap(V.chunk);
     const bool use_blockrow = blockrow_enabled();
     const int kChunk = V.chunk, kMaxRows = V.max_rows;
     for (int32_t ti = 0; ti < n; ++ti) {
@@ -1154,7 +1145,7 @@ static int build(const dfq_tensor_desc* descs, int32_t n, Built& B, const Varian
             // the scalar path: at most one row per lane keeps such a task's latency
             // near a vector task's (single-model sweeps are latency-bound)
             const int64_t row_cap = d.row_len < 32 ? kWave : kMaxRows;
-            int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(row_cap, tcap / d.row_len));
+            int64_t rpt = std::max<int64_t>(1, std::min<int64_t>(row_cap, kChunk / d.row_len));
             if (packed && (d.row_len & 1) && rpt > 1) rpt &= ~int64_t(1);   // even task starts
             for (int64_t r = 0; r < d.rows; r += rpt) {
                 const int64_t nr = std::min<int64_t>(rpt, d.rows - r);

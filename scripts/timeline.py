@@ -24,7 +24,8 @@ model = sys.argv[1] if len(sys.argv) > 1 else "mobilenetv2"
 copies = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 dev = torch.device("cuda:0")
 stream = torch.cuda.current_stream(dev)
-items, _, _, _ = bench.build_batch(model, dev, copies=copies, seed=5)
+esum = os.environ.get("DFQ_SINGLE_ESUM", "1") != "0"   # 0: BASELINE.md's W8 rows (no E)
+items, _, _, _ = bench.build_batch(model, dev, copies=copies, seed=5, esum=esum)
 plan = SweepPlan(items)
 n = plan.stats["n_tasks_main"]
 buf = torch.zeros(8 * n, dtype=torch.int64, device=dev)
@@ -70,5 +71,14 @@ for key, tis in sorted(kinds.items()):
                           "row_params_p50": round(float(np.median((params - landed)[m])), 2),
                           "quant_p50": round(float(np.median((quant - params)[m])), 2),
                           "done_p90": round(float(np.percentile(done[m], 90)), 2)}
+# the last tasks to finish: what they are and where their time went
+kind_of = {}
+for key, tis in kinds.items():
+    for ti in tis:
+        kind_of[int(ti)] = key
+last = np.argsort(done)[-12:][::-1]
+out["last_tasks"] = [{"kind": kind_of[int(tix[i])], "tensor": int(tix[i]), "start": round(float(start[i]), 2),
+                      "landed": round(float(landed[i]), 2), "params": round(float(params[i]), 2),
+                      "quant": round(float(quant[i]), 2), "done": round(float(done[i]), 2)} for i in last]
 print(json.dumps(out))
 plan.destroy()
