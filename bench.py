@@ -1007,11 +1007,15 @@ def main(argv=None):
         # slower (profiles/r03/validate_as vs r03at: MobileNetV2 end to end 10.4 vs
         # 5.3 ms), a state a main_dfq run never starts from
         pipe = None if args.no_pipeline else {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")}
-        probe_stream, probe_lds = same_mix_probe(per_copy * copies, dev, stream)
         second = None if args.no_secondary else secondary_configs(dev, stream)
         if second is not None:
             second.append(fold_quant_pair(dev, stream))
         single = None if args.no_secondary else single_model_latency(dev, stream)
+        # the same-mix probe last: a ResNet-50 x22 list allocated into the blocks its
+        # ~7 GB of probe buffers left ran 0.699 of peak against 0.770 before it in the
+        # same process (scripts/r50_state.py; DESIGN.md 3.1 "ResNet-50 in the bench")
+        probe_stream, probe_lds = same_mix_probe(per_copy * copies, dev, stream)
+        torch.cuda.empty_cache()
         cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
         if cpu is not None:
             cpu["transforms"] = cpu_baseline_transforms(dev, args.cpu_seconds)
