@@ -2853,12 +2853,17 @@ namespace dfq {
 // launch, sleeping between polls.  A CP wait packet (hipStreamWaitValue64) in
 // the caller's queue measured 1.8x slower loops (MobileNetV2 CLE 2.73 -> 4.97 ms:
 // the polling packet holds up the dispatch of the loop's queue), a running
-// one-wave kernel costs nothing.  Bounded and fail-closed: past `limit` ticks of
-// the 100 MHz clock (kCleGateSeconds: never reached by a loop that is running --
-// a MobileNetV2 loop takes milliseconds) it traps instead of returning.  The
-// queue faults and the process aborts, so nothing the caller queued behind the
-// loop (absorption, the second fold, quantize, bias correction) ever runs on
-// weights the loop may still be rescaling; a lost release cannot hang the queue.
+// one-wave kernel costs nothing.  Bounded: past `limit` ticks of the 100 MHz
+// clock (kCleGateSeconds: never reached by a loop that is running -- a
+// MobileNetV2 loop takes milliseconds) it traps instead of returning, so a lost
+// release cannot hang the queue and nothing queued behind the gate runs on weights
+// a still-running loop is rescaling.  A loop that FAILS (a HIP error, the launch
+// deadline) is not held back this way: the worker releases the gate behind
+// whatever the loop enqueued, the caller's queued stages (absorption, the second
+// fold, quantize, bias correction) run on the failed loop's weights, and the
+// failure is raised at the join (Cross_layer_equal.wait(), which run_dfq,
+// main_dfq and every read of the loop's results call), so those results are
+// never returned as a success.
 __global__ void __launch_bounds__(64) cle_caller_gate_kernel(const uint64_t* sig, uint64_t gen, uint64_t limit) {
     if (threadIdx.x != 0) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
