@@ -70,14 +70,6 @@ def merge_batchnorm(model, graph, bottoms, targ_type=[QConv2d], *, ranges: Optio
     return model
 
 
-def _carve(total_sizes, fill_zero, device):
-    """Views of ONE allocation, one per size (a model's worth of small vectors in a
-    single allocator call and one split instead of one each)."""
-    flat = (torch.zeros if fill_zero else torch.empty)(max(sum(total_sizes), 1), dtype=torch.float32,
-                                                       device=device)
-    return list(torch.split(flat[:sum(total_sizes)], list(total_sizes))) if total_sizes else []
-
-
 # dfq_bn_fold_desc as a numpy record (same layout as _lib.BnFoldDesc): the table
 # of a model's folds is filled column-wise instead of field by field
 _BN_DESC = np.dtype([("ptr", "<u8", (8,)), ("eps", "<f4"), ("flags", "<i4"), ("rows", "<i8"),
