@@ -232,20 +232,11 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
         rows.append([w1p, w2p, _checked_ptr(p1["bias"]), 0 if bnw is None else _checked_ptr(bnw),
                      0 if bnb is None else _checked_ptr(bnb), 0 if init else rel.S.data_ptr(), s1[0],
                      n1 // s1[0], s2[0], s2[1], n2 // (s2[0] * s2[1]), 1 if init else 0, 0])
-    if fresh:   # one allocation for every new Relation.S (a torch.empty per relation cost ~7 us each),
-        # one [k, c] block per channel count unbound into rows (Tensor.unbind: ~1.5 us a view,
-        # torch.split ~2.5); addresses from the offsets
-        by_width = {}
-        for f in fresh:
-            by_width.setdefault(rows[f[0]][6], []).append(f)   # rows[j][6]: W1's output channels
-        flat = torch.empty(sum(c * len(fs) for c, fs in by_width.items()), dtype=torch.float32,
-                           device=fresh[0][2].device)
-        base, off = flat.data_ptr(), 0
-        for c, fs in by_width.items():
-            for i, ((j, rel, _), v) in enumerate(zip(fs, flat[off:off + c * len(fs)].view(-1, c).unbind(0))):
-                rel.S = v
-                rows[j][5] = base + 4 * (off + i * c)
-            off += c * len(fs)
+    if fresh:   # one allocation for every new Relation.S (a torch.empty per relation cost ~7 us each)
+        flat = torch.empty(sum(w.size(0) for _, _, w in fresh), dtype=torch.float32, device=fresh[0][2].device)
+        for (j, rel, w), v in zip(fresh, torch.split(flat, [w.size(0) for _, _, w in fresh])):
+            rel.S = v
+            rows[j][5] = v.data_ptr()
     rows = [tuple(r) for r in rows]
     if tc:
         tc.append(time.perf_counter())

@@ -109,58 +109,44 @@ def _fold_batch(pairs, ranges=None):
         # :262-263 give a bias-less layer torch.zeros; here the fold reads such a
         # bias as 0 (DFQ_BN_FOLD_ZERO_BIAS) and writes every element of it.  The new
         # biases and the fake weight / bias buffers are views of ONE allocation
-        # whose addresses come from the offsets (no data_ptr call per view): per
-        # channel count C one [k, C] block -- that width's new biases, then its fake
-        # weights, then its fake biases -- unbound into its rows (Tensor.unbind makes
-        # a view in ~1.5 us where torch.split took ~2.5: 159 views on MobileNetV2).
-        need_l = [b is None for b in Bi]
-        chans_l = chans.tolist()
-        if any(need_l) and any(nd and r != c for nd, r, c in zip(need_l, rows_n.tolist(), chans_l)):
-            raise RuntimeError("merge_batchnorm: a layer's output channels differ from its BatchNorm's")
-        by_width = {}
-        for j, c in enumerate(chans_l):
-            by_width.setdefault(c, []).append(j)
-        groups, total = [], 0
-        for cw, js in by_width.items():   # plain Python: numpy per group cost more than it saved
-            jb = [j for j in js if need_l[j]]
-            groups.append((cw, js, jb, total))
-            total += (len(jb) + 2 * len(js)) * cw
-        flat = torch.empty(max(total, 1), dtype=torch.float32, device=dev)
-        base = flat.data_ptr()
+        # whose addresses come from the offsets (no data_ptr call per view).
+        need = [j for j, b in enumerate(Bi) if b is None]
+        nb_f = int(rows_n[need].sum()) if need else 0
+        nch = int(chans.sum())
+        flat = torch.empty(max(nb_f + 2 * nch, 1), dtype=torch.float32, device=dev)
+        base = np.uint64(flat.data_ptr())
         if tb:
             tb.append(time.perf_counter())
-        views = [flat[off:off + (len(jb) + 2 * len(js)) * cw].view(-1, cw).unbind(0) for cw, js, jb, off in groups]
+        views = torch.split(flat[:nb_f + 2 * nch], [int(rows_n[j]) for j in need] + chans.tolist() * 2)
         if tb:
             tb.append(time.perf_counter())
-        p1 = [0 if t is None else t.data_ptr() for t in Bi]
-        p6, p7 = [0] * n, [0] * n
-        for (cw, js, jb, off), rows in zip(groups, views):
-            for i, (j, z) in enumerate(zip(jb, rows)):
-                layer = pairs[j][1]
-                b = torch.Tensor._make_subclass(nn.Parameter, z, False)   # nn.Parameter(z, requires_grad=False)
-                if "bias" in layer._parameters:   # registered as None: what Module.__setattr__ would do
-                    layer._parameters["bias"] = b
-                else:
-                    layer.bias = b
-                p1[j] = base + 4 * (off + i * cw)
+        for j, z in zip(need, views[:len(need)]):
+            layer = pairs[j][1]
+            b = torch.Tensor._make_subclass(nn.Parameter, z, False)   # nn.Parameter(z, requires_grad=False)
+            if "bias" in layer._parameters:   # registered as None: what Module.__setattr__ would do
+                layer._parameters["bias"] = b
+            else:
+                layer.bias = b
         if tb:
             tb.append(time.perf_counter())
-        for (cw, js, jb, off), rows in zip(groups, views):
-            nb, m = len(jb), len(js)
-            for i, j in enumerate(js):
-                buf = pairs[j][0]._buffers   # register_buffer("fake_weight" / "fake_bias") without the per-call checks
-                buf["fake_weight"], buf["fake_bias"] = rows[nb + i], rows[nb + m + i]
-                p6[j] = base + 4 * (off + (nb + i) * cw)
-                p7[j] = base + 4 * (off + (nb + m + i) * cw)
+        if need:
+            boff = np.zeros(n, dtype=np.uint64)
+            boff[need] = np.concatenate([[0], np.cumsum(rows_n[need])[:-1]]).astype(np.uint64)
+        coff = np.concatenate([[0], np.cumsum(chans)[:-1]]).astype(np.uint64) + np.uint64(nb_f)
+        fw_v, fb_v = views[len(need):len(need) + n], views[len(need) + n:]
+        for (bn, _), fw, fb in zip(pairs, fw_v, fb_v):
+            buf = bn._buffers   # register_buffer("fake_weight" / "fake_bias") without the per-call checks
+            buf["fake_weight"], buf["fake_bias"] = fw, fb
         ptr[:, 0] = [t.data_ptr() for t in W]
-        ptr[:, 1] = p1
+        ptr[:, 1] = [0 if t is None else t.data_ptr() for t in Bi]
+        if need:
+            ptr[need, 1] = base + np.uint64(4) * boff[need]
         ptr[:, 2] = [t.data_ptr() for t in G]
         ptr[:, 3] = [t.data_ptr() for t in Be]
         ptr[:, 4] = [t.data_ptr() for t in Mu]
         ptr[:, 5] = [t.data_ptr() for t in Va]
-        ptr[:, 6] = p6
-        ptr[:, 7] = p7
-        need = [j for j, nd in enumerate(need_l) if nd]
+        ptr[:, 6] = base + np.uint64(4) * coff
+        ptr[:, 7] = base + np.uint64(4) * (coff + np.uint64(nch))
         if tb:
             tb.append(time.perf_counter())
         tab["eps"] = [bn.eps for bn, _ in pairs]
