@@ -661,3 +661,44 @@ def test_screened_quantize_at_rounding_boundaries(bits, mode):
     assert np.array_equal(it.scale.cpu().numpy(), o["scale"])
     assert np.array_equal(it.esum.cpu().numpy(), o["esum"])
     plan.destroy()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("row_len", [64, 9])
+@pytest.mark.parametrize("bits,clip", [(8, None), (8, (-0.75, 0.75)), (4, None)])
+def test_signed_zeros_and_tiny_values_bitwise(mode, row_len, bits, clip):
+    """The sweep's fixed-form loop rounds with (t + 1.5*2^23) - 1.5*2^23, which gives
+    +0 where rintf gives -0 (t in (-0.5, -0]); the dequantized value is q*s + mn,
+    so the sign only survives when mn is -0.  Rows with -0.0 / +0.0 entries, a -0.0
+    row minimum, all-zero rows of either sign and denormal-to-tiny magnitudes,
+    on the vector (64) and scalar (9) paths: dq compared BIT FOR BIT with the
+    oracle (signed zeros not folded), codes, scale and zero exactly."""
+    from data_free_quantization_amd.sweep import allocate, SweepPlan
+    rng = np.random.default_rng(bits * 100 + mode * 10 + row_len)
+    rows = 48
+    x = rng.standard_normal((rows, row_len)).astype(np.float32) * np.float32(0.5)
+    x[0] = 0.0
+    x[1] = -0.0
+    x[2, :] = np.abs(x[2]); x[2, 0] = -0.0            # row minimum -0.0 (asym mn = -0)
+    x[3, :] = np.abs(x[3]); x[3, 0] = 0.0             # row minimum +0.0
+    x[4] = np.float32(1e-40) * rng.choice([-1, 1], row_len)   # denormals
+    x[5] = np.float32(1e-30) * rng.standard_normal(row_len).astype(np.float32)
+    x[6, ::2] = -0.0
+    x[7, ::3] = 0.0
+    x[8] = -np.abs(x[8]); x[8, -1] = -0.0             # row maximum -0.0
+    t = torch.from_numpy(x).to(DEV)
+    per_channel, sym = mode >= 2, mode in (1, 3)
+    it = allocate(t, bits=bits, per_channel=per_channel, symmetric=sym, khw=1, want_esum=True, clip=clip,
+                  pack_int4=False)
+    plan = SweepPlan([it])
+    plan.execute()
+    torch.cuda.synchronize()
+    o = O.quantize(x, bits, mode, rows=rows, khw=1, flags=O.F_CLIP if clip else 0, clip=clip or (0.0, 0.0),
+                   want_esum=True)
+    got = it.dst.cpu().numpy()
+    assert np.array_equal(got.view(np.int32), o["dq"].view(np.int32)), "dq differs bitwise (signed zero or value)"
+    assert np.array_equal(it.codes.cpu().numpy().view(o["codes"].dtype), o["codes"])
+    assert np.array_equal(it.scale.cpu().numpy().view(np.int32), o["scale"].view(np.int32))
+    assert np.array_equal(it.zero.cpu().numpy().view(np.int32), o["zero"].view(np.int32))
+    assert np.array_equal(it.esum.cpu().numpy().view(np.int32), o["esum"].view(np.int32))
+    plan.destroy()
