@@ -193,8 +193,10 @@ _PRELOADED = False
 
 
 def preload() -> C.CDLL:
-    """Load the library and every kernel's code object on the current device
-    (dfq_preload) so the first DFQ stage does not pay for it.  Needs a GPU."""
+    """Load the library, every kernel's code object on the current device and the
+    buffers a first run would allocate (dfq_preload: CLE pools, history, signal
+    word and worker, pinned staging slots) so the first DFQ stage does not pay for
+    them.  Needs a GPU."""
     global _PRELOADED
     L = load()
     if not _PRELOADED:

@@ -3113,6 +3113,13 @@ extern "C" int dfq_cle_plan_destroy(dfq_cle_plan* p) {
 
 
 namespace dfq {
+// What a first CLE run on a device would otherwise allocate inside the caller's
+// timed region (a cold main_dfq run: plan create 314 against 55 us warm, launch 160
+// against 20): the table pools at a size that holds the zoo models' tables, the
+// iteration history for the default DFQ_CLE_MAX_ITERS, the signal word of launched
+// runs and their worker thread.
+constexpr size_t kClePreloadPool = size_t(4) << 20, kClePreloadHostPool = size_t(2) << 20;
+constexpr int32_t kClePreloadHistIters = 100000;   // Cross_layer_equal.MAX_ITERS' default
 hipError_t preload_cle() {   // see dfq_preload
     int dev = 0;
     hipError_t e0 = hipGetDevice(&dev);
@@ -3121,6 +3128,30 @@ hipError_t preload_cle() {   // see dfq_preload
         CleDeviceCtx& ctx = cle_device_ctx(dev);
         std::lock_guard<std::mutex> lock(ctx.mu);
         if ((e0 = cle_ctx_ready(ctx)) != hipSuccess) return e0;
+        if (!ctx.pool_busy && ctx.pool_cap < kClePreloadPool) {
+            (void)hipFree(ctx.d_pool);
+            ctx.d_pool = nullptr;
+            ctx.pool_cap = 0;
+            if ((e0 = hipMalloc(&ctx.d_pool, kClePreloadPool)) != hipSuccess) return e0;
+            ctx.pool_cap = kClePreloadPool;
+        }
+        if (!ctx.pool_busy && ctx.hpool_cap < kClePreloadHostPool) {
+            (void)hipHostFree(ctx.h_pool);
+            ctx.h_pool = nullptr;
+            ctx.hpool_cap = 0;
+            if ((e0 = hipHostMalloc(&ctx.h_pool, kClePreloadHostPool, hipHostMallocDefault)) != hipSuccess) return e0;
+            ctx.hpool_cap = kClePreloadHostPool;
+        }
+        if ((e0 = cle_hist_ready(ctx, kClePreloadHistIters)) != hipSuccess) return e0;
+        (void)cle_signal_ready(ctx);   // unsupported: launched runs fall back to blocking ones
+        if (!ctx.worker) {
+            try {
+                CleWorker* w = new CleWorker();
+                std::thread(cle_worker_loop, w).detach();
+                ctx.worker = w;
+            } catch (...) {   // created at the first launch instead
+            }
+        }
     }
     hipFuncAttributes a;
     hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(cle_loop_step_kernel<true>));

