@@ -1,4 +1,7 @@
+#!/bin/bash
 set -o pipefail
+# Same box, same command: the headline bench plain, under rocprofv3 --kernel-trace
+# --stats, and plain again (is a profiled launch slower than an unprofiled one?).
 mkdir -p gpurun_out/r05ak
 export TMPDIR=/tmp
 A="--steps 20 --warmup 3 --cpu-seconds 0 --no-pipeline --no-secondary --no-parity"
