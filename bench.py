@@ -7,14 +7,15 @@ E[o,i]) over ONE layer list: ``--copies`` MobileNetV2 weight sets back to back
 shapes, already resident in HBM).  The list defeats the 256 MB Infinity Cache
 (SURVEY.md 8d), so the number is an HBM number.
 
-At N GPUs the job's weight sets are sharded over the ranks (weak scaling, no
-collective in the timed step): rank r sweeps its own list of ``--copies``
-weight sets, and ``value`` is all ranks' weight bytes over the max-over-ranks
-step.  BASELINE configs[4] (``configs4_sharded``): ONE ResNet-50 INT4 + clip
-list of >= 2 GiB held by rank 0 is LPT-sharded over the ranks
-(data_free_quantization_amd/distributed.py) and timed sweep-only (strong
-scaling), with a gather of the output slabs to rank 0, scatter + sweep + gather,
-and the in-place all-gather, with its oracle parity counts.
+At N GPUs the SAME list is LPT-sharded over the ranks by algorithmic bytes
+(distributed.ShardLayout): each rank materialises only its own
+layers and the timed step is its sweep with the outputs left sharded (strong
+scaling); ``value`` is the whole list's weight bytes over the max-over-ranks
+step.  Beside it: ``sharded_gathers`` (the same list in the sharded sweep's slab
+arenas: sweep, sweep + gather to rank 0, sweep + in-place all-gather),
+``weak_scaling`` (every rank its own whole list) and BASELINE configs[4]
+(``configs4_sharded``: ONE ResNet-50 INT4 + clip list of >= 2 GiB held by rank 0,
+scattered, swept and gathered, with its oracle parity counts).
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N     (one process per GPU, RCCL)
@@ -455,6 +456,117 @@ def _timed_steps(fn, dev, reps, warmup=3):
     return max_over_ranks(time.perf_counter() - t0, dev) / reps
 
 
+def _std_of(shp):
+    """Synthetic init scale: conv ~ N(0, sqrt(2/(k*k*O))), linear ~ N(0, 0.01)."""
+    return (2.0 / (shp[2] * shp[3] * shp[0])) ** 0.5 if len(shp) == 4 else 0.01
+
+
+def make_list(specs, mine, dev, seed):
+    """Per-tensor allocations (input, then its outputs, in the order eager code
+    makes them) of the layers ``mine`` of the list ``specs``.  Every layer's
+    synthetic weight is drawn from ONE generator in list order -- a layer this rank
+    does not hold is drawn into a scratch buffer and dropped -- so layer i holds the
+    same values whatever the world size and no broadcast is needed.  (The sweep
+    over per-field arenas is placement-bound: 1.08 or 1.31-1.37 ms per step box to
+    box, 1.36 against 1.11 for per-tensor allocations on one box in five
+    interleaved process pairs; profiles/r02/ab_layout.jsonl, ab_arena.md.)"""
+    from data_free_quantization_amd.sweep import allocate
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    keep = set(mine)
+    scratch = None
+    if len(keep) < len(specs):
+        scratch = torch.empty(max(s.numel for i, s in enumerate(specs) if i not in keep), device=dev)
+    items = []
+    for i, s in enumerate(specs):
+        if i in keep:
+            w = torch.empty(s.shape, device=dev).normal_(0.0, _std_of(s.shape), generator=gen)
+            items.append(allocate(w, bits=s.bits, per_channel=s.per_channel, symmetric=s.symmetric, khw=s.khw,
+                                  want_esum=s.want_esum, clip=s.clip, pack_int4=s.pack_int4))
+        else:
+            scratch[:s.numel].view(s.shape).normal_(0.0, _std_of(s.shape), generator=gen)
+    del scratch
+    return items
+
+
+def _plan_of(items):
+    from data_free_quantization_amd.sweep import SweepPlan
+    return SweepPlan(items)
+
+
+def sharded_gathers(specs, dev, stream, reps=10):
+    """Beside the headline (the one list LPT-sharded, outputs left sharded): the same
+    list in the sharded sweep's per-field slab arenas (distributed.ShardedSweep,
+    the layout its collectives move), timed per pass of the whole list (wall,
+    barrier-bracketed, max over ranks): ``sweep_ms`` (outputs sharded),
+    ``sweep_gather_root_ms`` (+ one grouped receive per rank of its output slabs
+    into rank 0's arenas) and ``sweep_allgather_ms`` (+ one in-place
+    all_gather_into_tensor per output field: every rank ends holding every output).
+    Each rank fills only its own layers' inputs (same generator order as the
+    headline)."""
+    import torch.distributed as dist
+    from data_free_quantization_amd import distributed as D
+    sw = D.ShardedSweep(specs, replicate=True, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(1234)
+    mine = set(sw.mine)
+    for i, s in enumerate(specs):   # the headline's values (one generator in list order)
+        if i in mine:
+            sw.weight(i).normal_(0.0, _std_of(s.shape), generator=gen)
+        else:
+            torch.empty(s.shape, device=dev).normal_(0.0, _std_of(s.shape), generator=gen)
+    torch.cuda.synchronize(dev)
+    wbytes = 4 * sum(s.numel for s in specs)
+    out = {"rccl_ranks": sw.world, "backend": dist.get_backend() if dist.is_initialized() else None,
+           "layers_per_rank": [len(p) for p in sw.layout.parts],
+           "output_bytes_per_rank": [sum(sw.layout.used[f][r] for f in sw.layout.fields if f != "w")
+                                     for r in range(sw.world)]}
+
+    def step_root():
+        sw.run(stream)
+        sw.gather("root")
+
+    def step_all():
+        sw.run(stream)
+        sw.gather("all")
+
+    for name, fn in (("sweep", lambda: sw.run(stream)), ("sweep_gather_root", step_root),
+                     ("sweep_allgather", step_all)):
+        t = _timed_steps(fn, dev, reps)
+        out[f"{name}_ms"] = round(t * 1e3, 4)
+        out[f"{name}_weight_GBs"] = round(wbytes / t / 1e9, 1)
+    out["note"] = ("the headline's list in per-field slab arenas; host-timed, barrier-bracketed, max over ranks; "
+                   "weight_GBs = the whole list's fp32 weight bytes per pass")
+    sw.destroy()
+    del sw
+    torch.cuda.empty_cache()
+    return out
+
+
+def weak_scaling(specs, weights, dev, stream, rank, world, steps, warmup):
+    """Secondary: every rank sweeps its OWN whole list (rank-seeded synthetic
+    weights, per-tensor allocations), no collective; weight-GB/s = all ranks'
+    weight bytes over the max-over-ranks step (the round-5 headline)."""
+    import torch.distributed as dist
+    from data_free_quantization_amd import distributed as D
+    items = make_list(specs, range(len(specs)), dev, 1234 + 7919 * rank)
+    plan = _plan_of(items)
+    for _ in range(max(warmup, 1)):
+        plan.execute(stream)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        plan.execute(stream)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t = D.max_over_ranks(time.perf_counter() - t0, dev) / steps
+    plan.destroy()
+    del plan, items
+    torch.cuda.empty_cache()
+    return {"ms_per_step": round(t * 1e3, 4), "value": round(4 * weights * world / t / 1e9, 2),
+            "unit": "GB/s", "lists": world,
+            "note": "every rank its own whole list, no collective; value = all ranks' weight bytes / max step"}
+
+
 def configs4_sharded(dev, stream, reps=10, parity=True):
     """BASELINE configs[4] at N > 1: ONE >= 2 GiB layer list of ResNet-50 weight
     sets (per-channel asym INT4 + clip [-15, 15], packed int4 codes: the
@@ -717,16 +829,16 @@ def cpu_baseline_transforms(dev, seconds):
                       f"BC: _quantize_error + spatial sum over every target weight, best of 3"}
 
 
-def parity_of_timed(items, layers_per_copy, dev):
+def parity_of_timed(items, mine, layers_per_copy, copies, dev):
     """Checker leg (test infrastructure, like cpu_baseline): the timed plan's
-    outputs on the first, middle and last weight set of this rank's list vs the C
-    oracle (oracle/dfq_oracle.c) run on the same input tensors -- dq, codes, scale,
-    zero and the bias-correction sums E, element by element (tests/parity.py)."""
+    outputs on this rank's layers (``items`` are the list's layers ``mine``) of the
+    list's first, middle and last weight sets vs the C oracle
+    (oracle/dfq_oracle.c) run on the same input tensors -- dq, codes, scale, zero
+    and the bias-correction sums E, element by element (tests/parity.py)."""
     from tests.parity import sweep_mismatches
     torch.cuda.synchronize(dev)
-    copies = len(items) // layers_per_copy
     sets = sorted({0, copies // 2, copies - 1}) if copies else []
-    sample = [it for c in sets for it in items[c * layers_per_copy:(c + 1) * layers_per_copy]]
+    sample = [it for it, i in zip(items, mine) if i // layers_per_copy in sets]
     t0 = time.perf_counter()
     out = sweep_mismatches(sample)
     out["weight_sets"] = sets
@@ -895,32 +1007,29 @@ def main(argv=None):
     specs = D.uniform_specs(shapes * copies, bits=args.bits, per_channel=args.granularity == "channel",
                             symmetric=not args.asym, want_esum=not args.no_esum, clip=(-15.0, 15.0))
     stream = torch.cuda.current_stream(dev)
-    std_of = lambda shp: (2.0 / (shp[2] * shp[3] * shp[0])) ** 0.5 if len(shp) == 4 else 0.01   # noqa: E731
     sw = plan = None
-    # Weak scaling: every rank sweeps its own list of ``copies`` weight sets (its
-    # shard of the job's world * copies sets; rank-seeded synthetic weights); no
-    # collective in the timed step.
-    gen = torch.Generator(device=dev).manual_seed(1234 + 7919 * rank)
+    # The headline: ONE layer list of ``copies`` weight sets (the N = 1 workload),
+    # LPT-sharded over the ranks (distributed.ShardLayout, the partition the
+    # sharded sweep and its gathers use).  Each rank materialises only its own
+    # layers -- every layer's synthetic weight comes from one generator in list
+    # order, so a layer holds the same values at every N and no broadcast is
+    # needed -- and the timed step is its sweep with the outputs
+    # left sharded (strong scaling).  The gathers are timed beside it
+    # (sharded_gathers); N independent lists are the secondary weak_scaling key.
+    layout = D.ShardLayout(specs, world)
+    mine = layout.parts[rank]
     if args.layout == "arena" and world == 1:
         # diagnostics: the sharded path's per-field slab arenas at one rank
+        gen = torch.Generator(device=dev).manual_seed(1234)
         sw = D.ShardedSweep(specs, replicate=True, device=dev)
         for i, s in enumerate(specs):
-            sw.weight(i).normal_(0.0, std_of(s.shape), generator=gen)
+            sw.weight(i).normal_(0.0, _std_of(s.shape), generator=gen)
         st = sw.plan_stats
         run = lambda: sw.run(stream)   # noqa: E731
+        items = None
     else:
-        # The timed sweep runs on one allocation per tensor, in the order eager code
-        # makes them (input, then its outputs).  The sweep over per-field arenas is
-        # placement-bound: 1.08 or 1.31-1.37 ms per step from box to box, and 1.36
-        # against 1.11 for per-tensor allocations on one box in five interleaved
-        # process pairs (profiles/r02/ab_layout.jsonl, ab_arena.md).
-        from data_free_quantization_amd.sweep import SweepPlan, allocate
-        items = []
-        for s in specs:
-            w = torch.empty(s.shape, device=dev).normal_(0.0, std_of(s.shape), generator=gen)
-            items.append(allocate(w, bits=s.bits, per_channel=s.per_channel, symmetric=s.symmetric, khw=s.khw,
-                                  want_esum=s.want_esum, clip=s.clip, pack_int4=s.pack_int4))
-        plan = SweepPlan(items)
+        items = make_list(specs, mine, dev, 1234)
+        plan = _plan_of(items)
         st = plan.stats
         run = lambda: plan.execute(stream)   # noqa: E731
     tele = [telemetry.sample("before_prewarm")]
@@ -951,32 +1060,43 @@ def main(argv=None):
     step_ms = [a.elapsed_time(b) for a, b in step_ev]
     dev_ms = ev0.elapsed_time(ev1)          # device time of this rank's K launches on this stream
     t_step = D.max_over_ranks(wall, dev) / args.steps
-    weight_bytes = 4 * per_copy * copies * world   # every rank's list, swept once per step
+    weight_bytes = 4 * per_copy * copies     # the one layer list, swept once per step (sharded at N > 1)
     value = weight_bytes / t_step / 1e9
     launch_ms = dev_ms / args.steps          # device time of one execute() (st["launches"] kernels)
     achieved = st["algo_bytes"] / (launch_ms / 1e3) / 1e9
-    rank_launch_ms = [launch_ms]
-    if world > 1:   # every rank's own kernel time (rank 0 reports its roofline)
-        lt = torch.zeros(world, dtype=torch.float64, device=dev)
-        lt[rank] = launch_ms
+    rank_launch_ms, rank_algo = [launch_ms], [st["algo_bytes"]]
+    if world > 1:   # every rank's own kernel time and bytes (rank 0 reports its roofline)
+        lt = torch.zeros(2, world, dtype=torch.float64, device=dev)
+        lt[0, rank], lt[1, rank] = launch_ms, float(st["algo_bytes"])
         dist.all_reduce(lt)
-        rank_launch_ms = [round(float(x), 4) for x in lt.tolist()]
-    # parity of what was just timed: the first, middle and last weight set of this
-    # rank's list vs the C oracle on the same input tensors (every field)
+        rank_launch_ms = [round(float(x), 4) for x in lt[0].tolist()]
+        rank_algo = [int(x) for x in lt[1].tolist()]
+    # parity of what was just timed: this rank's layers of the list's first, middle
+    # and last weight sets vs the C oracle on the same input tensors (every field)
     timed_parity = None
-    if plan is not None and not args.no_parity:
-        timed_parity = parity_of_timed(plan.items, len(shapes), dev)
-        if world > 1:   # every rank checked its own share: the job's total
-            tot = torch.tensor([timed_parity["mismatches"], timed_parity["tensors"]], dtype=torch.int64,
-                               device=dev)
+    if items is not None and not args.no_parity:
+        timed_parity = parity_of_timed(items, mine, len(shapes), copies, dev)
+        if world > 1:   # every rank checked its own share: the job's total, and who held them
+            tot = torch.zeros(2 + world, dtype=torch.int64, device=dev)
+            tot[0], tot[1] = timed_parity["mismatches"], timed_parity["tensors"]
+            tot[2 + rank] = 1 if timed_parity["tensors"] else 0
             dist.all_reduce(tot)
             timed_parity["all_ranks"] = {"mismatches": int(tot[0]), "tensors": int(tot[1])}
             timed_parity["mismatches"] = int(tot[0])
+            timed_parity["tensors"] = int(tot[1])
+            timed_parity["owners"] = [r for r in range(world) if int(tot[2 + r])]
+        else:
+            timed_parity["owners"] = [0]
     for obj in (sw, plan):
         if obj is not None:
             obj.destroy()
-    del sw, plan, run
+    del sw, plan, run, items
     torch.cuda.empty_cache()
+    gathers = weak = None
+    if world > 1:
+        gloo = dist.get_backend() == "gloo"   # a one-GPU rehearsal stages every transfer through the host
+        gathers = sharded_gathers(specs, dev, stream, reps=2 if gloo else 10)
+        weak = weak_scaling(specs, per_copy * copies, dev, stream, rank, world, args.steps, args.warmup)
     sharded4 = None
     if world > 1 and not args.no_sharded:
         gloo = dist.get_backend() == "gloo"   # a one-GPU rehearsal stages every transfer through the host
@@ -1041,7 +1161,7 @@ def main(argv=None):
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "codes": f"{args.bits}-bit grid indices stored as "
@@ -1049,7 +1169,7 @@ def main(argv=None):
             "data": "synthetic random-init weights of the reference shapes (no checkpoints offline)",
             "box": socket.gethostname(),
             "config": {
-                "workload": f"{args.model} x{copies} weight sets in one layer list per rank: {args.granularity} "
+                "workload": f"{args.model} x{copies} weight sets in one layer list: {args.granularity} "
                             f"{'asym' if args.asym else 'sym'} INT{args.bits} quantize-dequantize + codes + "
                             f"clip[-15,15]" + ("" if args.no_esum else " + bias-correction error sums"),
                 "weight_shapes": f"{args.model} target layers (SURVEY.md 8, synthetic init)",
@@ -1057,11 +1177,14 @@ def main(argv=None):
                 "layers": len(specs),
                 "layers_per_copy": len(shapes),
                 "weights_per_copy": per_copy,
-                "parallelism": (f"dp{world}: one process per GPU; the job's {world} x {copies} weight sets "
-                                f"sharded {copies} per rank (weak scaling: per-GPU work fixed), no collective in "
-                                "the timed step; BASELINE configs[4]'s single list sharded from rank 0 with its "
-                                "gathers in configs4_sharded")
+                "parallelism": (f"layer-sharded x{world}: one process per GPU; the one list's {len(specs)} layers "
+                                "LPT-sharded over the ranks by algorithmic bytes, each rank materialises and sweeps "
+                                "its share (per-tensor allocations), outputs left sharded in the timed step "
+                                "(strong scaling); the gathers to rank 0 / to every rank in sharded_gathers, "
+                                "N independent lists in weak_scaling")
                 if world > 1 else "1 rank: the whole layer list on one GPU (per-tensor allocations, no exchange)",
+                "layers_per_rank": [len(p) for p in layout.parts],
+                "algo_bytes_per_rank": rank_algo,
             },
             "roofline": {
                 "bound": "hbm",
@@ -1102,6 +1225,8 @@ def main(argv=None):
                         "the timed steps.  NOT a ceiling: box to box it lands 5.2-6.5 TB/s, sometimes below the "
                         "sweep itself, so it only shows how far arithmetic and row logic cost on this box"},
             "parity": parity,
+            "sharded_gathers": gathers,
+            "weak_scaling": weak,
             "configs4_sharded": sharded4,
             "cpu_baseline": cpu,
             "secondary_configs": second,

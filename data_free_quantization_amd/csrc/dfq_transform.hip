@@ -562,6 +562,13 @@ __global__ void bn_fold_channel_batch_kernel(const BnFoldJob* __restrict__ jobs,
 // observer's running_min / running_max), read as the exact doubles float()
 // would produce, so no host round trip is needed.
 // ---------------------------------------------------------------------------
+// A NaN element stays NaN (torch's clamp_ propagates it; qdq's fminf / fmaxf
+// clamp would map it to qmin).
+__device__ __forceinline__ float qdq_nan(float x, const QParams& p, float& q) {
+    const float y = qdq(x, p, q);
+    return x != x ? x : y;
+}
+
 __global__ void __launch_bounds__(kThreads)
 fq_given_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, int bits, int sym, int flags,
                 const float* __restrict__ min_dev, const float* __restrict__ max_dev,
@@ -580,14 +587,15 @@ fq_given_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, i
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
             const float4 v = reinterpret_cast<const float4*>(x)[i];
             float4 o;
-            o.x = qdq(v.x, p, q);
-            o.y = qdq(v.y, p, q);
-            o.z = qdq(v.z, p, q);
-            o.w = qdq(v.w, p, q);
+            o.x = qdq_nan(v.x, p, q);
+            o.y = qdq_nan(v.y, p, q);
+            o.z = qdq_nan(v.z, p, q);
+            o.w = qdq_nan(v.w, p, q);
             reinterpret_cast<float4*>(y)[i] = o;
         }
     } else {
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = qdq(x[i], p, q);
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+            y[i] = qdq_nan(x[i], p, q);
     }
 }
 
@@ -676,10 +684,16 @@ __global__ void chunk_mean_kernel(const float* __restrict__ mins, const float* _
 // observer's updates.  The word pairs are re-armed by that wave (self-cleaning:
 // the host arms them once when it allocates them).
 // ---------------------------------------------------------------------------
+//
+// NaN: torch's min / max propagate it, so a slice holding one stores the words of
+// -NaN (min) and +NaN (max) -- the largest values of both ordered encodings, so
+// the atomics keep them -- and the rows' means, the momentum update and the
+// fake-quant range come out NaN as in the reference.
 __global__ void __launch_bounds__(kThreads)
 observe_rows_kernel(const float* __restrict__ x, int64_t rows, int64_t row_len, int64_t slices,
                     uint32_t* __restrict__ words) {
     __shared__ float smn[kThreads / kWave], smx[kThreads / kWave];
+    __shared__ int snan[kThreads / kWave];
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
     const int64_t per = ceil_div(row_len, slices);
     for (int64_t b = blockIdx.x; b < rows * slices; b += gridDim.x) {
@@ -687,6 +701,7 @@ observe_rows_kernel(const float* __restrict__ x, int64_t rows, int64_t row_len, 
         const int64_t e0 = k * per, e1 = min(row_len, e0 + per);
         const float* row = x + r * row_len;
         float a = INFINITY, c = -INFINITY;
+        bool nan = false;
         const bool v4 = (row_len % 4 == 0) && (per % 4 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0);
         if (v4) {
             const float4* q = reinterpret_cast<const float4*>(row + e0);
@@ -694,25 +709,35 @@ observe_rows_kernel(const float* __restrict__ x, int64_t rows, int64_t row_len, 
                 const float4 v = q[i];
                 a = fminf(a, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
                 c = fmaxf(c, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+                nan |= (v.x != v.x) | (v.y != v.y) | (v.z != v.z) | (v.w != v.w);
             }
         } else {
             for (int64_t i = e0 + threadIdx.x; i < e1; i += kThreads) {
                 const float v = row[i];
                 a = fminf(a, v);
                 c = fmaxf(c, v);
+                nan |= (v != v);
             }
         }
         a = wave_min(a);
         c = wave_max(c);
+        const bool wnan = __ballot(nan) != 0;
         if (lane == 0) {
             smn[w] = a;
             smx[w] = c;
+            snan[w] = wnan ? 1 : 0;
         }
         __syncthreads();
         if (threadIdx.x == 0) {
+            int anynan = snan[0];
             for (int q = 1; q < kThreads / kWave; ++q) {
                 a = fminf(a, smn[q]);
                 c = fmaxf(c, smx[q]);
+                anynan |= snan[q];
+            }
+            if (anynan) {
+                a = __uint_as_float(0xFFC00000u);   // -NaN: enc_ord's smallest, so ~enc wins atomicMax
+                c = __uint_as_float(0x7FC00000u);   // +NaN: enc_ord's largest
             }
             atomicMax(&words[2 * r], ~enc_ord(a));
             atomicMax(&words[2 * r + 1], enc_ord(c));

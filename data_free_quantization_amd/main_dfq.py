@@ -222,7 +222,11 @@ def main(argv=None):
         if args.quantize:
             replace_op()
         start = time.time()
-        accuracy = inference_all(model, args.task, args)
+        # the weights are final from here: the Quant* layers keep their weight /
+        # bias fake-quant between batches (utils.quantize.frozen_weights)
+        from .utils.quantize import frozen_weights
+        with frozen_weights():
+            accuracy = inference_all(model, args.task, args)
         print(f"Inference time is {time.time() - start} seconds")
         if args.quantize:
             restore_op()

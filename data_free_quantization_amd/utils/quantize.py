@@ -9,6 +9,7 @@ Tensors must live on a ROCm device; there is no CPU fallback.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import struct
 from dataclasses import dataclass
@@ -284,17 +285,22 @@ class QuantMeasure(nn.Module):
         if not x.is_contiguous():
             x = x.contiguous()
         rows = x.size(0)
-        d = self.__dict__
-        words = d.get("_obs_words")
-        if words is None or words.numel() != 2 * rows or words.device != x.device:
-            words = d["_obs_words"] = torch.zeros(2 * rows, dtype=torch.int32, device=x.device)   # armed once
-            d["_obs_out"] = torch.empty(2, dtype=torch.float32, device=x.device)
-        out2 = d["_obs_out"]
+        # the call's scratch: the self-re-arming row words (zeroed once, reset by
+        # the kernel) and the 2-float range the fake quant reads asynchronously --
+        # one pair per (device, stream), so calls on two streams never share them
+        stream = _lib.stream_of(x)
+        bufs = self.__dict__.setdefault("_obs_bufs", {})
+        key = (x.device, stream.value)
+        words, out2 = bufs.get(key, (None, None))
+        if words is None or words.numel() != 2 * rows:
+            words = torch.zeros(2 * rows, dtype=torch.int32, device=x.device)   # armed once
+            out2 = torch.empty(2, dtype=torch.float32, device=x.device)
+            bufs[key] = (words, out2)
         rmin, rmax = self._buffers["running_min"], self._buffers["running_max"]
         _lib.require_device(rmin, rmax)
         _lib.check(_lib.load().dfq_act_observe(_lib.ptr(x), rows, x.numel() // rows, _lib.ptr(words), _lib.ptr(rmin),
                                                _lib.ptr(rmax), int(bool(self.update_stat)), int(bool(self.training)),
-                                               float(self.momentum), _lib.ptr(out2), _lib.stream_of(x)),
+                                               float(self.momentum), _lib.ptr(out2), stream),
                    "dfq_act_observe", RuntimeError)
         if _no_autograd(input):
             return fake_quant_given(input, self.num_bits, min_dev=out2[0], max_dev=out2[1])
@@ -306,9 +312,33 @@ class QuantMeasure(nn.Module):
 
 
 def invalidate_weight_cache() -> None:
-    """Drop every Quant* layer's cached weight / bias fake-quant (after rewriting
-    weights through ``.data`` outside the DFQ transforms)."""
+    """Drop every Quant* layer's cached weight / bias fake-quant (inside a
+    ``frozen_weights()`` scope, after rewriting weights through ``.data``)."""
     _lib.weights_changed()
+
+
+_FROZEN = 0   # depth of open frozen_weights() scopes
+
+
+@contextlib.contextmanager
+def frozen_weights():
+    """Inference over fixed weights: inside this scope the Quant* layers keep their
+    weight / bias fake-quant between forwards instead of re-quantizing on every call
+    as the reference does (/root/reference/utils/quantize.py:225-238).  The caller
+    promises that weights change only through the library's transforms or torch's
+    own in-place ops (both seen by the cache key); a write through ``.data`` inside
+    the scope needs ``invalidate_weight_cache()``.  Outside any scope -- the default
+    -- every forward re-quantizes, so the reference's ``weight.data.copy_`` idiom
+    (utils/layer_transform.py:300,303, clip_weight.py:29, bias_absorption.py:78-80)
+    is always seen.  main_dfq's evaluation runs inside one."""
+    global _FROZEN
+    _lib.weights_changed()   # nothing cached before the scope is trusted in it
+    _FROZEN += 1
+    try:
+        yield
+    finally:
+        _FROZEN -= 1
+        _lib.weights_changed()
 
 
 class _QuantWeightMixin:
@@ -319,23 +349,26 @@ class _QuantWeightMixin:
         if _no_autograd(weight, bias):
             # inference: float(weight.min()) / float(weight.max()) and the bias's own
             # 0-d fp32 range stay on the device (dfq_range), one async launch each.
-            # The result depends only on the weight and bias bytes and the bit
-            # widths, so it is kept while none of them changed: the key holds both
-            # tensors' identity, address and torch version counter, and the DFQ
-            # transforms' generation (_lib.WEIGHT_GENERATION: they write through
-            # the library, past the version counters).  Code that rewrites weights
-            # through ``.data`` (a fresh version counter) must call
-            # ``invalidate_weight_cache()``.
-            key = (id(weight), weight.data_ptr(), weight._version, self.num_bits, _lib.WEIGHT_GENERATION,
-                   None if bias is None else (id(bias), bias.data_ptr(), bias._version), self.num_bits_bias)
-            hit = self.__dict__.get("_qw_cache")
-            if hit is not None and hit[0] == key:
-                return hit[1], hit[2]
+            # Inside frozen_weights() the result is kept while the key holds: the
+            # module's OWN parameters (a temporary -- QConv2d's scaled weight -- is
+            # never cached: its id and address are reused), their torch version
+            # counters, and the DFQ transforms' generation (_lib.WEIGHT_GENERATION:
+            # they write through the library, past the version counters).
+            cacheable = _FROZEN > 0 and weight is self.weight and bias is self.bias
+            if cacheable:
+                key = (weight.data_ptr(), weight._version, self.num_bits, _lib.WEIGHT_GENERATION,
+                       None if bias is None else (bias.data_ptr(), bias._version), self.num_bits_bias)
+                hit = self.__dict__.get("_qw_cache")
+                if hit is not None and hit[0] == key:
+                    return hit[1], hit[2]
             qweight = fake_quant_given(weight, self.num_bits, range_enc=device_range(weight))
             qbias = None
             if bias is not None:
                 qbias = fake_quant_given(bias, self.num_bits_bias, range_enc=device_range(bias), scale_f32=True)
-            self.__dict__["_qw_cache"] = (key, qweight, qbias)
+            if cacheable:
+                self.__dict__["_qw_cache"] = (key, qweight, qbias)
+            else:
+                self.__dict__.pop("_qw_cache", None)
             return qweight, qbias
         qweight = quantize(weight, num_bits=self.num_bits, min_value=float(weight.min()),
                            max_value=float(weight.max()))
@@ -431,6 +464,7 @@ class QConv2d(QuantConv2d):
                 self.bias.data.copy_(b)
         self.scale_prev = None
         self.scale = None
+        invalidate_weight_cache()   # written through .data
 
     def forward(self, input):
         input = self.quant(input)
@@ -467,6 +501,7 @@ class QLinear(QuantLinear):
                 self.bias.data.copy_(b)
         self.scale_prev = None
         self.scale = None
+        invalidate_weight_cache()   # written through .data
 
     def forward(self, input):
         input = self.quant(input)

@@ -12,7 +12,7 @@ import torch.nn as nn
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from data_free_quantization_amd import zoo  # noqa: E402
 from data_free_quantization_amd.utils import layer_transform as L  # noqa: E402
-from data_free_quantization_amd.utils.quantize import QuantConv2d, QuantLinear, set_layer_bits  # noqa: E402
+from data_free_quantization_amd.utils.quantize import QuantConv2d, QuantLinear, frozen_weights, set_layer_bits  # noqa: E402,E501
 from data_free_quantization_amd.utils.tracer import TorchTransformer  # noqa: E402
 
 batch = int(sys.argv[1]) if len(sys.argv) > 1 else 32
@@ -49,10 +49,13 @@ finally:
 model.eval()
 L.replace_op()
 try:
-    q_ms = timed(lambda: model(x))
+    q_ms = timed(lambda: model(x))          # the default: weights re-quantized every forward
+    with frozen_weights():                  # main_dfq's evaluation scope: weight fake quant kept
+        qf_ms = timed(lambda: model(x))
 finally:
     L.restore_op()
 print(json.dumps({"batch": batch, "fp32_ms": round(fp32_ms, 3), "quant_ms": round(q_ms, 3),
+                  "quant_frozen_weights_ms": round(qf_ms, 3),
                   "quant_training_mode_observers_ms": round(train_obs_ms, 3)}))
 
 # breakdown: observers frozen (no update_stat), then without the op interception

@@ -43,6 +43,10 @@ if not os.environ.get("DFQ_MKL_DEFAULT"):
 REF = Path(os.environ.get("DFQ_REFERENCE", "/root/reference"))
 HERE = Path(__file__).resolve().parent
 ROOT = HERE.parent.parent
+# where the fixtures are written (DFQ_GOLDEN_OUT: a scratch directory, for the
+# regeneration check in tests/test_golden_regen.py); the committed ones are read
+# from HERE
+OUT = Path(os.environ.get("DFQ_GOLDEN_OUT", str(HERE)))
 sys.dont_write_bytecode = True
 os.environ.setdefault("MPLBACKEND", "Agg")
 sys.path.insert(0, str(ROOT))
@@ -165,7 +169,7 @@ def quant_cases():
     add("clip", x, 8, "tensor_asym", clip=(-0.1, 0.1), khw=9, esum=True)
     add("clip_ch", x, 4, "channel_sym", clip=(-0.25, 0.3), khw=9, esum=True)
     arrays["meta"] = np.array(json.dumps(meta))
-    np.savez_compressed(HERE / "quant_cases.npz", **arrays)
+    np.savez_compressed(OUT / "quant_cases.npz", **arrays)
     print("quant cases:", len(meta))
 
 
@@ -204,7 +208,7 @@ def chunk_cases():
                     arrays[f"dqh{idx}"] = np.array(h(dq))
                     meta.append(entry)
     arrays["meta"] = np.array(json.dumps(meta))
-    np.savez_compressed(HERE / "chunk_cases.npz", **arrays)
+    np.savez_compressed(OUT / "chunk_cases.npz", **arrays)
     print("chunk cases:", len(meta), "errors:", sum(m["error"] is not None for m in meta))
 
 
@@ -342,7 +346,7 @@ def transform_cases():
     A["bc_Ed"], A["bc_dw_bias_out"] = t2n(Ed), t2n(layer.bias)
 
     A["meta"] = np.array(json.dumps(meta))
-    np.savez_compressed(HERE / "transform_cases.npz", **A)
+    np.savez_compressed(OUT / "transform_cases.npz", **A)
     print("transform cases:", len(meta))
 
 
@@ -429,11 +433,11 @@ def pipeline(name: str, seed: int = 0, per_channel: bool = False, threads: int =
             hs = []
             for k in tkeys:
                 W = graph[k].weight.detach().clone()
-                out = torch.empty_like(W)
+                qw = torch.empty_like(W)   # (not `out`: that is the fixture path, saved below)
                 for o in range(W.shape[0]):
                     sl = W[o].clone()
-                    out[o] = ref_quantize(sl, 8, float(sl.min()), float(sl.max()), symmetric=sym)
-                hs.append(h(t2n(out)))
+                    qw[o] = ref_quantize(sl, 8, float(sl.min()), float(sl.max()), symmetric=sym)
+                hs.append(h(t2n(qw)))
             P[f"{mode}8_wh"] = np.stack([np.frombuffer(bytes.fromhex(x), dtype=np.uint8) for x in hs])
     if bits_weight != 8:   # main_dfq.py:209 (a host config step; no tensor changes on plain modules)
         from utils.quantize import set_layer_bits as ref_slb
@@ -456,9 +460,9 @@ def pipeline(name: str, seed: int = 0, per_channel: bool = False, threads: int =
     P["stats"] = np.array(json.dumps(stats))
     P["bits"] = np.array([bits_weight, 8, bits_bias], dtype=np.int64)   # weight, activation, bias
     if out is None:
-        out = HERE / (f"pipeline_{name}.npz" if threads == 8 else f"pipeline_{name}_t{threads}.npz")
+        out = OUT / (f"pipeline_{name}.npz" if threads == 8 else f"pipeline_{name}_t{threads}.npz")
         if bits_weight != 8:
-            out = HERE / f"pipeline_{name}_w{bits_weight}.npz"
+            out = OUT / f"pipeline_{name}_w{bits_weight}.npz"
     np.savez_compressed(out, **P)
     torch.set_num_threads(8)
     print(name, "relations", len(res), "cle iters", len(spy.diffs), "bc", str(P["bc_error"]), stats)
@@ -520,7 +524,7 @@ def act_ranges(name: str, seed: int = 0):
     run("bn1")
     ref_merge_bn(model, graph, bottoms, TARG)
     run("bn2")
-    np.savez_compressed(HERE / f"act_ranges_{name}.npz", **A)
+    np.savez_compressed(OUT / f"act_ranges_{name}.npz", **A)
     print(name, "act ranges:", len(tkeys), "layer quantizers,", len(ops.quants), "op quantizers",
           str(A["bn1_error"]), str(A["bn2_error"]))
 
@@ -676,7 +680,7 @@ def forward_logits(name: str, seed: int = 0, bits_weight: int = 8):
         A[f"ops_layer_max{tag}"] = np.array([float(q.running_max) for q in lq], dtype=np.float32)
         A[f"ops_op_min{tag}"] = np.array([float(q.running_min) for q in oq], dtype=np.float32)
         A[f"ops_op_max{tag}"] = np.array([float(q.running_max) for q in oq], dtype=np.float32)
-    np.savez_compressed(HERE / (f"forward_{name}.npz" if bits_weight == 8 else f"forward_{name}_w{bits_weight}a8.npz"),
+    np.savez_compressed(OUT / (f"forward_{name}.npz" if bits_weight == 8 else f"forward_{name}_w{bits_weight}a8.npz"),
                         **A)
     d = lambda a, b: float(np.abs(A[a].astype(np.float64) - A[b]).max())   # noqa: E731
     print(name, "forward fixture:", len(names), "op nodes,", f"{time.time() - t0:.1f} s;",
@@ -704,7 +708,7 @@ def state_dict_keys():
     out = {"mobilenetv2": RefMBv2(), "deeplab": RefDeepLab(sync_bn=False),
            "resnet50_backbone": RefResNet(Bottleneck, [3, 4, 6, 3], 16, nn.BatchNorm2d, pretrained=False)}
     res = {k: [[n, list(t.shape)] for n, t in m.state_dict().items()] for k, m in out.items()}
-    (HERE / "state_dict_keys.json").write_text(json.dumps(res))
+    (OUT / "state_dict_keys.json").write_text(json.dumps(res))
     print("state_dict keys:", {k: len(v) for k, v in res.items()})
 
 
@@ -735,7 +739,7 @@ def seg_transforms():
         out[f"out_label{i}"] = sample["label"].numpy()
         meta.append({"w": w, "h": h, "crop": crop})
     out["meta"] = np.array(json.dumps({"cases": meta, "mean": mean, "std": std}))
-    np.savez_compressed(HERE / "seg_transforms.npz", **out)
+    np.savez_compressed(OUT / "seg_transforms.npz", **out)
     print("seg_transforms:", len(cases), "cases")
 
 
@@ -757,6 +761,8 @@ if __name__ == "__main__":
     for m in ("mobilenetv2", "resnet50", "deeplab", "resnet18"):
         if m in which:
             pipeline(m, per_channel=(m == "mobilenetv2"))
+        if f"{m}_ch" in which:   # + the per-channel reference hashes (tests/test_golden_regen.py: a fast
+            pipeline(m, per_channel=True)   # model through the per-channel block)
         for t in (1, 16):
             if f"{m}_t{t}" in which:
                 pipeline(m, threads=t)

@@ -87,9 +87,11 @@ def test_single_gpu_no_spawn():
 @pytest.mark.gpu
 def test_bench_two_ranks_one_gpu():
     """The real bench at --gpus 2 as the driver may call it (no torchrun env), both
-    ranks on the one GPU with gloo between them: the line must say n_gpus 2, two
-    ranks, and 0 parity mismatches (timed sweep of both ranks and configs[4]'s
-    sharded list)."""
+    ranks on the one GPU with gloo between them.  The headline must be the ONE
+    N = 1 list (MobileNetV2 x155, 8,215 layers) LPT-sharded over the two ranks
+    (strong scaling, outputs left sharded), every rank's share checked against the
+    oracle with 0 mismatches and both ranks holding checked layers; the gathers,
+    weak scaling and configs[4]'s sharded list beside it."""
     r = subprocess.run([sys.executable, "-u", str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
                         "--no-secondary", "--no-pipeline", "--prewarm-ms", "50"],
                        capture_output=True, text=True, timeout=600, env=_env(OMP_NUM_THREADS="4"), cwd=str(ROOT))
@@ -99,10 +101,23 @@ def test_bench_two_ranks_one_gpu():
     assert len(lines) == 1
     res = lines[0]
     print(json.dumps({k: res[k] for k in ("value", "ms_per_step", "n_gpus", "rccl_ranks", "backend", "scaling")}))
+    print(json.dumps(res["sharded_gathers"]), json.dumps(res["weak_scaling"]))
     print(json.dumps(res["configs4_sharded"]))
-    assert res["n_gpus"] == 2 and res["rccl_ranks"] == 2 and res["scaling"] == "weak"
-    assert res["parity"]["timed_sweep"]["all_ranks"]["tensors"] > 0
-    assert res["parity"]["mismatches"] == 0
+    assert res["n_gpus"] == 2 and res["rccl_ranks"] == 2 and res["scaling"] == "strong"
+    cfg = res["config"]
+    assert cfg["layers"] == 8215 and cfg["copies"] == 155
+    assert sum(cfg["layers_per_rank"]) == 8215 and all(n > 0 for n in cfg["layers_per_rank"])
+    assert len(cfg["algo_bytes_per_rank"]) == 2
+    # value = the whole list's weight bytes (not N lists) over the max-over-ranks step
+    assert abs(res["value"] - 4 * cfg["weights_per_copy"] * 155 / (res["ms_per_step"] / 1e3) / 1e9) \
+        <= 0.01 * res["value"]
+    tp = res["parity"]["timed_sweep"]
+    assert tp["all_ranks"]["tensors"] == 3 * 53 and tp["owners"] == [0, 1]
+    assert res["parity"]["mismatches"] == 0 and tp["mismatches"] == 0
+    g = res["sharded_gathers"]
+    assert g["layers_per_rank"] == cfg["layers_per_rank"]
+    assert all(g[k] > 0 for k in ("sweep_ms", "sweep_gather_root_ms", "sweep_allgather_ms"))
+    assert res["weak_scaling"]["lists"] == 2
     c4 = res["configs4_sharded"]
     assert c4["rccl_ranks"] == 2 and all(n > 0 for n in c4["layers_per_rank"])
     assert c4["parity"]["mismatches"] == 0 and c4["parity"]["owners"] == [0, 1]

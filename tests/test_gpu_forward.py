@@ -105,15 +105,14 @@ def test_quantized_forward_matches_reference(name, tmp_path, monkeypatch):
         L.module_tensor_op = None
 
 
-def test_weight_fake_quant_cache_follows_weight_changes():
-    """QuantConv2d / QuantLinear keep their weight and bias fake-quant while the
-    tensors are unchanged; a torch in-place write (version
-    counter), a DFQ transform writing through the library (clip_weight:
-    _lib.WEIGHT_GENERATION) and invalidate_weight_cache() each make the next
-    forward re-quantize.  Each forward is compared with a layer that never cached."""
-    import torch.nn as nn
-    from data_free_quantization_amd.clip_weight import clip_weight
-    from data_free_quantization_amd.utils.quantize import QuantConv2d, QuantLinear, invalidate_weight_cache
+def test_weight_fake_quant_default_sees_data_writes():
+    """Outside frozen_weights() -- the default -- QuantConv2d / QuantLinear
+    re-quantize on every forward like the reference (utils/quantize.py:225-238), so
+    writes through ``.data`` (the reference's own idiom: layer_transform.py:300,303,
+    clip_weight.py:29, bias_absorption.py:78-80) are seen with no call to
+    invalidate_weight_cache().  Each forward is compared with
+    a layer that never cached."""
+    from data_free_quantization_amd.utils.quantize import QuantConv2d, QuantLinear
     torch.manual_seed(3)
     dev = torch.device("cuda:0")
     conv = QuantConv2d(8, 16, 3, padding=1, num_bits=4).to(dev).eval()
@@ -137,19 +136,95 @@ def test_weight_fake_quant_cache_follows_weight_changes():
         return all(torch.equal(p, q) for p, q in zip(a, b))
 
     y0 = run()
-    assert conv.__dict__.get("_qw_cache") is not None
-    assert same(run(), y0)                          # cached: identical
-    with torch.no_grad():
-        conv.weight.mul_(1.5)                       # torch in-place write: version counter
+    assert conv.__dict__.get("_qw_cache") is None          # nothing cached by default
+    conv.weight.data.copy_(conv.weight.data * 0.5)        # layer_transform.py:300's form
     y1 = run()
     assert not same(y1, y0) and same(y1, fresh())
-    clip_weight({"c": conv, "l": lin}, range_clip=[-0.05, 0.05], targ_type=[nn.Conv2d, nn.Linear])
-    y2 = run()                                      # written through the library
+    conv.bias.data.add_(0.25)                              # bias_absorption.py:78-80's form
+    lin.weight.data.clamp_(-0.05, 0.05)                    # clip_weight.py:29's form
+    y2 = run()
     assert not same(y2, y1) and same(y2, fresh())
-    conv.weight.data.mul_(0.5)                      # through .data: the caller invalidates
-    invalidate_weight_cache()
-    y3 = run()
-    assert not same(y3, y2) and same(y3, fresh())
+
+
+def test_weight_fake_quant_cache_in_frozen_scope():
+    """Inside frozen_weights() the layers keep their weight / bias fake-quant while
+    the tensors are unchanged; a torch in-place write (version counter), a DFQ
+    transform writing through the library (clip_weight: _lib.WEIGHT_GENERATION)
+    and invalidate_weight_cache() each make the next forward re-quantize.  A
+    QConv2d with a scale (a temporary weight each forward) is never cached and
+    follows in-place changes of its weight and scale; merge_scale_to_weight
+    invalidates."""
+    import torch.nn as nn
+    from data_free_quantization_amd.clip_weight import clip_weight
+    from data_free_quantization_amd.utils.quantize import (QConv2d, QuantConv2d, QuantLinear, frozen_weights,
+                                                           invalidate_weight_cache)
+    torch.manual_seed(3)
+    dev = torch.device("cuda:0")
+    conv = QuantConv2d(8, 16, 3, padding=1, num_bits=4).to(dev).eval()
+    lin = QuantLinear(16, 10, num_bits=4).to(dev).eval()
+    qc = QConv2d(8, 16, 3, padding=1, num_bits=4).to(dev).eval()
+    x = torch.randn(2, 8, 6, 6, device=dev)
+    for m in (conv, lin, qc):
+        m.quant.running_min.fill_(-3.0)
+        m.quant.running_max.fill_(3.0)
+
+    def run():
+        with torch.no_grad():
+            y = conv(x)
+            return y, lin(y.mean((2, 3)))
+
+    def fresh():
+        for m in (conv, lin):
+            m.__dict__.pop("_qw_cache", None)
+        return run()
+
+    def same(a, b):
+        return all(torch.equal(p, q) for p, q in zip(a, b))
+
+    def qc_ref():
+        with torch.no_grad():
+            w, b = qc._scaled()
+            ref = QuantConv2d(8, 16, 3, padding=1, num_bits=4).to(dev).eval()
+            ref.weight.data.copy_(w)
+            ref.bias.data.copy_(b)
+            ref.quant.running_min.fill_(-3.0)
+            ref.quant.running_max.fill_(3.0)
+            return ref(x)
+
+    with frozen_weights():
+        y0 = run()
+        assert conv.__dict__.get("_qw_cache") is not None
+        assert same(run(), y0)                          # cached: identical
+        with torch.no_grad():
+            conv.weight.mul_(1.5)                       # torch in-place write: version counter
+        y1 = run()
+        assert not same(y1, y0) and same(y1, fresh())
+        clip_weight({"c": conv, "l": lin}, range_clip=[-0.05, 0.05], targ_type=[nn.Conv2d, nn.Linear])
+        y2 = run()                                      # written through the library
+        assert not same(y2, y1) and same(y2, fresh())
+        conv.weight.data.mul_(0.5)                      # through .data inside the scope: the caller invalidates
+        invalidate_weight_cache()
+        y3 = run()
+        assert not same(y3, y2) and same(y3, fresh())
+        # QConv2d with a scale: the scaled weight is a temporary, never cached
+        qc.set_scale(torch.rand(16, device=dev) + 0.5)
+        with torch.no_grad():
+            z0 = qc(x)
+            assert qc.__dict__.get("_qw_cache") is None and torch.equal(z0, qc_ref())
+            qc.scale.mul_(2.0)                          # in-place scale change
+            z1 = qc(x)
+            assert not torch.equal(z1, z0) and torch.equal(z1, qc_ref())
+            qc.weight.mul_(0.5)                         # in-place weight change
+            z2 = qc(x)
+            assert torch.equal(z2, qc_ref())
+            qc.merge_scale_to_weight()                  # .data writes + invalidate; own weight from here
+            z3 = qc(x)
+            assert torch.equal(z3, qc_ref())
+            assert torch.equal(qc(x), z3) and qc.__dict__.get("_qw_cache") is not None
+    # leaving the scope: back to re-quantizing every forward
+    conv.weight.data.mul_(2.0)
+    y4 = run()
+    assert not same(y4, y3) and same(y4, fresh())
 
 
 @pytest.mark.parametrize("shape", [(32, 16, 7, 7), (8, 3, 224, 224), (5, 1001), (32, 96, 14, 14), (1, 17)])
@@ -189,4 +264,75 @@ def test_fused_observer_matches_torch_cpu(shape, mode):
         assert q.running_max.cpu().view(torch.int32).item() == rmax.view(torch.int32).item(), (call, q.running_max, rmax)
         ref = quantize(x.to(dev), 8, min_value=float(lo), max_value=float(hi))
         assert torch.equal(y, ref), call
-        assert int(q.__dict__["_obs_words"].abs().sum()) == 0   # re-armed
+        assert all(int(w.abs().sum()) == 0 for w, _ in q.__dict__["_obs_bufs"].values())   # re-armed
+
+
+def test_fused_observer_scratch_per_stream():
+    """Two observer calls enqueued on two streams do not share the scratch the fake
+    quant reads asynchronously: each (device, stream) has its own, and
+    both outputs equal a one-stream run of the same inputs."""
+    from data_free_quantization_amd.utils.quantize import QuantMeasure
+    dev = torch.device("cuda:0")
+    torch.manual_seed(11)
+    xa, xb = torch.randn(8, 64, device=dev), 3.0 * torch.randn(8, 64, device=dev)
+
+    def observer():
+        q = QuantMeasure(update_stat=True).to(dev)
+        q.eval()
+        return q
+
+    qa, qb = observer(), observer()
+    with torch.no_grad():
+        ref_a, ref_b = qa(xa), qb(xb)
+    torch.cuda.synchronize()
+    q = observer()
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    with torch.no_grad():
+        with torch.cuda.stream(s1):
+            ya = q(xa)
+        q2 = observer()
+        q2.__dict__["_obs_bufs"] = q.__dict__["_obs_bufs"]   # one observer's scratch dict, two streams
+        with torch.cuda.stream(s2):
+            yb = q2(xb)
+    torch.cuda.synchronize()
+    assert len(q.__dict__["_obs_bufs"]) == 2
+    assert torch.equal(ya, ref_a) and torch.equal(yb, ref_b)
+
+
+@pytest.mark.parametrize("mode", ["update_stat", "training"])
+def test_fused_observer_propagates_nan(mode):
+    """An activation batch holding a NaN: torch's flat.min / max(-1) propagate it
+    (utils/quantize.py:103-111), so the reference's running range and fake-quant
+    range are NaN where the row has one.  The fused observer gives the
+    same running values (NaN-aware, bitwise otherwise) and NaN outputs where the
+    reference's quantize() gives them."""
+    from data_free_quantization_amd.utils.quantize import QuantMeasure
+    dev = torch.device("cuda:0")
+    torch.manual_seed(5)
+    x = torch.randn(4, 3, 8, 8)
+    x[2, 1, 3, 4] = float("nan")
+    q = QuantMeasure(update_stat=(mode == "update_stat")).to(dev)
+    q.train(mode == "training")
+    q.running_min.fill_(-0.25)
+    q.running_max.fill_(0.5)
+    ref = QuantMeasure(update_stat=(mode == "update_stat"))   # the same module on the CPU: torch ops
+    ref.train(mode == "training")
+    ref.running_min.fill_(-0.25)
+    ref.running_max.fill_(0.5)
+    flat = x.view(4, -1)
+    mn, mx = flat.min(-1)[0].mean(), flat.max(-1)[0].mean()
+    assert torch.isnan(mn) and torch.isnan(mx)
+    with torch.no_grad():
+        y = q(x.to(dev)).cpu()
+    if mode == "training":
+        rmin, rmax = (torch.tensor([-0.25]) * 0.9).add(mn * 0.1), (torch.tensor([0.5]) * 0.9).add(mx * 0.1)
+    else:
+        rmin, rmax = torch.tensor([-0.25]), torch.tensor([0.5])   # Python min/max keep the old value
+    for ours, want in ((q.running_min.cpu(), rmin), (q.running_max.cpu(), rmax)):
+        assert bool(torch.isnan(ours)) == bool(torch.isnan(want))
+        if not torch.isnan(want):
+            assert ours.view(torch.int32).item() == want.view(torch.int32).item()
+    if mode == "training":   # range NaN: every output NaN, as quantize() with a NaN scale
+        assert torch.isnan(y).all()
+    else:                    # range finite: only the NaN input stays NaN
+        assert int(torch.isnan(y).sum()) == 1
