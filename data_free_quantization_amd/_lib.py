@@ -172,6 +172,8 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_debug_timeline": ([P, I64], C.c_int),
         "dfq_debug_ablate": ([C.c_uint32], C.c_int),
         "dfq_probe_lds": ([P, P, P, P, I64, I32, I32, P], C.c_int),
+        "dfq_diag_cle_check_structure": ([C.POINTER(CleRel), I32, C.POINTER(P), C.POINTER(I64), I32, I32,
+                                          C.POINTER(I64), C.c_char_p, I32], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -2205,24 +2205,11 @@ static std::vector<int64_t> cle_structure_key(const std::vector<CleRel>& R, int6
     return key;
 }
 
-static std::mutex g_struct_mu;
-static std::list<std::pair<std::vector<int64_t>, std::shared_ptr<const CleStructure>>> g_struct_cache;
-constexpr size_t kStructCacheCap = 8;
-
-extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
-                                   const int64_t* target_n, int32_t n_targets, double s_min, double s_max,
-                                   int32_t is_signed, float eps, int32_t ref_threads, void* ws, int64_t ws_bytes,
-                                   dfq_cle_plan** out) {
-    if (!out || n_rel < 0 || n_targets < 0 || (n_rel > 0 && !rels) || (n_targets > 0 && (!targets || !target_n)))
-        return DFQ_ERR_INVALID;
-    const double tc0 = now_us();
-    const int64_t need_ws = dfq_cle_plan_ws_bytes(target_n, n_targets);
-    if (need_ws < 0) return DFQ_ERR_INVALID;
-    if (ws && (ws_bytes < need_ws || reinterpret_cast<uintptr_t>(ws) % 256 != 0)) return DFQ_ERR_INVALID;
-    *out = nullptr;
-    // relations: shapes as dfq_cle_relation
-    std::vector<CleRel> R(n_rel);
-    int64_t M = 0;
+// The relations' descriptors as the device's records: shapes checked as
+// dfq_cle_relation; each relation's [W1 | W2] range words at moff (M in all).
+static int cle_rels_from_desc(const dfq_cle_rel* rels, int32_t n_rel, std::vector<CleRel>& R, int64_t& M) {
+    R.assign(n_rel, CleRel{});
+    M = 0;
     for (int32_t r = 0; r < n_rel; ++r) {
         const dfq_cle_rel& d = rels[r];
         if (!d.w1 || !d.w2 || !d.b1 || d.c1 <= 0 || d.len1 <= 0 || d.o2 <= 0 || d.i2 <= 0 || d.khw2 <= 0)
@@ -2247,6 +2234,27 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         M += 2 * d.c1;
         R[r] = c;
     }
+    return DFQ_OK;
+}
+
+static std::mutex g_struct_mu;
+static std::list<std::pair<std::vector<int64_t>, std::shared_ptr<const CleStructure>>> g_struct_cache;
+constexpr size_t kStructCacheCap = 8;
+
+extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
+                                   const int64_t* target_n, int32_t n_targets, double s_min, double s_max,
+                                   int32_t is_signed, float eps, int32_t ref_threads, void* ws, int64_t ws_bytes,
+                                   dfq_cle_plan** out) {
+    if (!out || n_rel < 0 || n_targets < 0 || (n_rel > 0 && !rels) || (n_targets > 0 && (!targets || !target_n)))
+        return DFQ_ERR_INVALID;
+    const double tc0 = now_us();
+    const int64_t need_ws = dfq_cle_plan_ws_bytes(target_n, n_targets);
+    if (need_ws < 0) return DFQ_ERR_INVALID;
+    if (ws && (ws_bytes < need_ws || reinterpret_cast<uintptr_t>(ws) % 256 != 0)) return DFQ_ERR_INVALID;
+    *out = nullptr;
+    std::vector<CleRel> R;
+    int64_t M = 0;
+    if (const int rc = cle_rels_from_desc(rels, n_rel, R, M); rc != DFQ_OK) return rc;
     const double tp1 = now_us();
     // the structure (chains, tasks, chunks, placement) from the cache when a plan of
     // the same shapes and tensor-sharing pattern was built before
@@ -3159,3 +3167,206 @@ hipError_t preload_cle() {   // see dfq_preload
     return e;
 }
 }  // namespace dfq
+
+#ifdef DFQ_DIAGNOSTICS
+#include "dfq_diag.h"   // default visibility for the entry point below
+// ---- diagnostics: the plan structure's index invariants, on the host -----------
+// Builds the structure dfq_cle_plan_create would (chains, tasks, metric chunks and
+// units, the lagged placement) -- host code only, no device memory, so it runs on
+// a machine without a GPU and with stand-in addresses -- and checks every index
+// the step, range, tile, stop-rule and rollback blocks derive from it:
+//  * task tables: step offsets monotone and inside the tables; every task's
+//    relation, rows / channels / columns inside that relation's shapes;
+//  * range words and rollback saves: moff + 2 c1 <= M (both parities' words) and
+//    2 moff + 4 c1 <= 2 M (vsave: b1 | bn_w | bn_b | S per channel);
+//  * metric chunks and units: layer, element span, level-1 slots inside the tables;
+//  * placement: per launch offset the unit / range slices partition the tables;
+//    a tensor's tiles and ranges sit after its last rescale of iteration i and
+//    before its first rescale of iteration i + 1 (its window), range resets after
+//    their relation's step; lagged plans: the stop rule one offset after every tile
+//    of its iteration and before the next iteration's first tile.
+// The round-5 fault of a development tree was in this code's
+// domain; tests/test_cle_structure.py runs it on every zoo model and schedule
+// switch and on fuzzed relation graphs.
+// info[0..7] = steps, nlaunch, lagged, stop_off, rescale tasks, range tasks, units,
+// chunks.  Returns DFQ_OK, or DFQ_ERR_INVALID with the first violation in msg.
+extern "C" int dfq_diag_cle_check_structure(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
+                                            const int64_t* target_n, int32_t n_targets, int32_t ref_threads,
+                                            int64_t* info, char* msg, int32_t msg_cap) {
+    auto fail = [&](const char* fmt, long long a, long long b, long long c) {
+        if (msg && msg_cap > 0) snprintf(msg, (size_t)msg_cap, fmt, a, b, c);
+        return DFQ_ERR_INVALID;
+    };
+    if (n_rel < 0 || n_targets < 0 || (n_rel > 0 && !rels) || (n_targets > 0 && (!targets || !target_n)))
+        return fail("bad arguments %lld %lld %lld", n_rel, n_targets, 0);
+    std::vector<CleRel> R0;
+    int64_t M = 0;
+    if (const int rc = cle_rels_from_desc(rels, n_rel, R0, M); rc != DFQ_OK) return rc;
+    CleStructure S;
+    if (const int rc = cle_build_structure(R0, M, n_rel, targets, target_n, n_targets, ref_threads, S); rc != DFQ_OK)
+        return rc;
+    const std::vector<CleRel>& R = S.R;
+    const int32_t steps = S.steps, NL = S.nlaunch;
+    if (info) {
+        const int64_t v[8] = {steps, NL, S.lagged ? 1 : 0, S.stop_off, (int64_t)S.at.size(), (int64_t)S.rt.size(),
+                              (int64_t)S.units.size(), (int64_t)S.chunks.size()};
+        std::memcpy(info, v, sizeof(v));
+    }
+    // relations: range words and rollback saves inside their tables, links valid
+    for (int32_t r = 0; r < n_rel; ++r) {
+        const CleRel& c = R[r];
+        if (c.moff < 0 || c.moff + 2 * c.c1 > S.M) return fail("rel %lld: range words [%lld, +2 c1) past M %lld", r, c.moff, S.M);
+        if (2 * c.moff + 4 * c.c1 > 2 * S.M) return fail("rel %lld: rollback saves past 2 M (moff %lld, c1 %lld)", r, c.moff, c.c1);
+        if (c.fuse_next >= n_rel || c.dw_prev >= n_rel || c.fuse_next < -1 || c.dw_prev < -1)
+            return fail("rel %lld: link out of range (fuse_next %lld, dw_prev %lld)", r, c.fuse_next, c.dw_prev);
+        if (c.fuse_next >= 0 && R[c.fuse_next].moff + R[c.fuse_next].c1 > S.M)
+            return fail("rel %lld: fused W1 words of rel %lld past M %lld", r, c.fuse_next, S.M);
+    }
+    // rescale tasks per step
+    if ((int32_t)S.astep.size() != steps + 1 || S.astep[0] != 0 || S.astep.back() != (int64_t)S.at.size())
+        return fail("astep: %lld entries for %lld steps, last %lld", (long long)S.astep.size(), steps,
+                    S.astep.empty() ? -1 : S.astep.back());
+    std::vector<int32_t> rel_step(n_rel, -1);
+    std::vector<std::pair<const float*, int32_t>> touch;   // (tensor, step) of every weight rescale
+    for (int32_t k = 0; k < steps; ++k) {
+        if (S.astep[k + 1] < S.astep[k]) return fail("astep not monotone at step %lld: %lld > %lld", k, S.astep[k], S.astep[k + 1]);
+        for (int64_t t = S.astep[k]; t < S.astep[k + 1]; ++t) {
+            const CleTask& tk = S.at[t];
+            if (tk.rel < 0 || tk.rel >= n_rel) return fail("rescale task %lld: relation %lld of %lld", t, tk.rel, n_rel);
+            const CleRel& c = R[tk.rel];
+            if (tk.a < 0 || tk.a >= tk.b) return fail("rescale task %lld: empty or negative span [%lld, %lld)", t, tk.a, tk.b);
+            switch (tk.kind) {
+                case kApplyW1:
+                    if (tk.b > c.c1) return fail("W1 task %lld: rows to %lld of %lld", t, tk.b, c.c1);
+                    touch.push_back({c.w1, k});
+                    break;
+                case kApplyW2Contig:
+                    if (tk.b > c.c1 || c.i2 != 1) return fail("W2 contig task %lld: channels to %lld of %lld", t, tk.b, c.c1);
+                    touch.push_back({c.w2, k});
+                    break;
+                case kApplyDwBoth:
+                    if (tk.b > c.c1 || tk.c0 < 0 || tk.c0 >= n_rel || R[tk.c0].w1 != c.w2 || R[tk.c0].dw_prev != tk.rel)
+                        return fail("depthwise pair task %lld: partner %lld, channels to %lld", t, tk.c0, tk.b);
+                    touch.push_back({c.w2, k});
+                    break;
+                case kApplyW2Tile:
+                    if (tk.b > c.o2 || tk.c0 < 0 || tk.c0 >= tk.c1 || tk.c1 > c.i2)
+                        return fail("W2 tile task %lld: rows to %lld, columns to %lld", t, tk.b, tk.c1);
+                    touch.push_back({c.w2, k});
+                    break;
+                case kApplyChannels:
+                    if (tk.b > c.c1) return fail("channel task %lld: channels to %lld of %lld", t, tk.b, c.c1);
+                    if (rel_step[tk.rel] >= 0 && rel_step[tk.rel] != k)
+                        return fail("relation %lld: channel tasks in steps %lld and %lld", tk.rel, rel_step[tk.rel], k);
+                    rel_step[tk.rel] = k;
+                    break;
+                default:
+                    return fail("rescale task %lld: kind %lld", t, tk.kind, 0);
+            }
+        }
+    }
+    for (int32_t r = 0; r < n_rel; ++r)
+        if (rel_step[r] < 0) return fail("relation %lld has no channel task", r, 0, 0);
+    // range tasks
+    const int64_t nrt = (int64_t)S.rt.size();
+    if (S.ri0 < 0 || S.ri0 > S.ri1 || S.ri1 > nrt) return fail("range slice [%lld, %lld) of %lld tasks", S.ri0, S.ri1, nrt);
+    for (int64_t t = 0; t < nrt; ++t) {
+        const CleTask& tk = S.rt[t];
+        if (tk.rel < 0 || tk.rel >= n_rel) return fail("range task %lld: relation %lld of %lld", t, tk.rel, n_rel);
+        const CleRel& c = R[tk.rel];
+        if (tk.a < 0 || tk.a >= tk.b) return fail("range task %lld: span [%lld, %lld)", t, tk.a, tk.b);
+        const bool ok = tk.kind == kRangeW2Tile ? (tk.b <= c.o2 && tk.c0 >= 0 && tk.c0 < tk.c1 && tk.c1 <= c.i2)
+                                                : (tk.kind >= kRangeW1 && tk.kind <= kRangeResetW1 && tk.b <= c.c1);
+        if (!ok) return fail("range task %lld (kind %lld): span to %lld out of the relation's shape", t, tk.kind, tk.b);
+    }
+    // metric chunks and units
+    int64_t nb1_seen = 0;
+    for (size_t ci = 0; ci < S.chunks.size(); ++ci) {
+        const CleChunk& ch = S.chunks[ci];
+        if (ch.layer < 0 || ch.layer >= n_targets) return fail("chunk %lld: layer %lld of %lld", (long long)ci, ch.layer, n_targets);
+        if (ch.c0 < 0 || ch.len <= 0 || ch.c0 + ch.len > target_n[ch.layer])
+            return fail("chunk %lld: elements [%lld, +%lld) past its layer", (long long)ci, ch.c0, ch.len);
+        const int64_t nb1 = ch.len / 32 / 256;
+        if (S.b1off[ci] != 32 * nb1_seen) return fail("chunk %lld: level-1 offset %lld, expected %lld", (long long)ci, S.b1off[ci], 32 * nb1_seen);
+        nb1_seen += nb1;
+    }
+    if (nb1_seen != S.nb1_total) return fail("level-1 slots %lld, table %lld", nb1_seen, S.nb1_total, 0);
+    for (size_t u = 0; u < S.units.size(); ++u) {
+        const CleUnit& un = S.units[u];
+        if (un.chunk < 0 || un.chunk >= (int32_t)S.chunks.size()) return fail("unit %lld: chunk %lld", (long long)u, un.chunk, 0);
+        const CleChunk& ch = S.chunks[un.chunk];
+        if (ch.len < 8 || un.tile < 0 || un.tile > ch.len / 32 / 256)
+            return fail("unit %lld: tile %lld of chunk %lld", (long long)u, un.tile, un.chunk);
+    }
+    // placement tables
+    if ((int32_t)S.uoffs.size() != 2 * NL + 1 || S.uoffs[0] != 0 || S.uoffs.back() != (int64_t)S.units.size())
+        return fail("uoffs: %lld entries for %lld launches, last %lld", (long long)S.uoffs.size(), NL, S.uoffs.back());
+    for (int32_t k = 0; k < 2 * NL; ++k)
+        if (S.uoffs[k + 1] < S.uoffs[k]) return fail("uoffs not monotone at %lld", k, 0, 0);
+    if (S.fused) {
+        if ((int32_t)S.roffs.size() != 2 * NL + 1 || S.roffs[0] != S.ri0 || S.roffs.back() != S.ri1)
+            return fail("roffs: %lld entries, [%lld, %lld)", (long long)S.roffs.size(), S.roffs.empty() ? -1 : S.roffs[0],
+                        S.roffs.empty() ? -1 : S.roffs.back());
+        for (int32_t k = 0; k < 2 * NL; ++k)
+            if (S.roffs[k + 1] < S.roffs[k]) return fail("roffs not monotone at %lld", k, 0, 0);
+    } else if ((int32_t)S.rstep.size() != steps + 1 || S.rstep.back() != nrt) {
+        return fail("unfused rstep: %lld entries, last %lld of %lld", (long long)S.rstep.size(), S.rstep.back(), nrt);
+    }
+    if (NL != (S.lagged ? steps : steps + 1)) return fail("nlaunch %lld for %lld steps (lagged %lld)", NL, steps, S.lagged);
+    // windows: a tensor's first / last rescale step
+    auto span = [&](const float* w, int32_t& first, int32_t& last) {
+        first = INT32_MAX;
+        last = -1;
+        for (const auto& x : touch)
+            if (x.first == w) {
+                first = std::min(first, x.second);
+                last = std::max(last, x.second);
+            }
+        return last >= 0;
+    };
+    auto in_window = [&](const float* w, int32_t o) {
+        int32_t f, l;
+        if (!span(w, f, l)) return o >= 0 && o <= 2 * NL - 1;
+        return o >= l + 1 && o <= std::min(2 * NL - 1, NL + f - 1);
+    };
+    int32_t umin = INT32_MAX, umax = -1;
+    for (int32_t k = 0; k < 2 * NL; ++k)
+        for (int64_t u = S.uoffs[k]; u < S.uoffs[k + 1]; ++u) {
+            const int32_t l = S.chunks[S.units[u].chunk].layer;
+            if (!S.lagged && k != steps) return fail("unit %lld of layer %lld at offset %lld outside the tiles-only launch", u, l, k);
+            if (!in_window(targets[l], k)) return fail("unit %lld of layer %lld at offset %lld outside its tensor's window", u, l, k);
+            umin = std::min(umin, k);
+            umax = std::max(umax, k);
+        }
+    if (S.fused)
+        for (int32_t k = 0; k < 2 * NL; ++k)
+            for (int64_t t = S.roffs[k]; t < S.roffs[k + 1]; ++t) {
+                const CleTask& tk = S.rt[t];
+                const CleRel& c = R[tk.rel];
+                bool ok = true;
+                switch (tk.kind) {
+                    case kRangeW1: ok = in_window(c.w1, k); break;
+                    case kRangeW2Contig:
+                    case kRangeW2Tile: ok = in_window(c.w2, k); break;
+                    case kRangeReset: {
+                        int32_t f, l;
+                        span(c.w2, f, l);
+                        ok = k >= rel_step[tk.rel] + 1 && k <= std::min(2 * NL - 1, NL + l);
+                        break;
+                    }
+                    default: ok = k >= rel_step[tk.rel] + 1 && k <= 2 * NL - 1;   // kRangeResetW1
+                }
+                if (!S.lagged && k != steps) ok = false;
+                if (!ok) return fail("range task %lld (kind %lld) at offset %lld outside its window", t, tk.kind, k);
+            }
+    if (S.lagged && S.stop_off >= 0) {
+        if (S.stop_off < steps || S.stop_off > 2 * NL - 1) return fail("stop rule at offset %lld of [%lld, %lld]", S.stop_off, steps, 2 * NL - 1);
+        if (umax >= 0 && S.stop_off <= umax) return fail("stop rule at offset %lld, not after the last tile offset %lld", S.stop_off, umax, 0);
+        if (umax >= 0 && umin + NL <= S.stop_off)
+            return fail("the next iteration's first tile (offset %lld + %lld) not after the stop rule at %lld", umin, NL, S.stop_off);
+    } else if (!S.lagged && S.stop_off != -1) {
+        return fail("unlagged plan with a stop-rule offset %lld", S.stop_off, 0, 0);
+    }
+    return DFQ_OK;
+}
+#endif

@@ -42,6 +42,18 @@ int dfq_debug_ablate(uint32_t flags);
 int dfq_probe_lds(const float* x, float* y, void* codes, float* esum, int64_t n, int32_t copy_only,
                   int32_t blocks, void* stream);
 
+/* ---- structure checks ------------------------------------------------------
+ * The CLE plan structure dfq_cle_plan_create builds for these relations and targets
+ * (host code only: no device memory is touched, addresses may be stand-ins) checked
+ * for every index its kernels derive from it -- task tables, range words, rollback
+ * saves, metric chunks / units, the lagged placement windows and the stop rule's
+ * offset (dfq_cle.hip).  info[8]: steps, nlaunch, lagged, stop_off, rescale tasks,
+ * range tasks, units, chunks.  DFQ_ERR_INVALID + msg: the first violation.  Reads
+ * the same diagnostics schedule switches as plan creation (DFQ_CLE_LAG, ...). */
+int dfq_diag_cle_check_structure(const dfq_cle_rel* rels, int32_t n_rel, float* const* targets,
+                                 const int64_t* target_n, int32_t n_targets, int32_t ref_threads, int64_t* info,
+                                 char* msg, int32_t msg_cap);
+
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }
