@@ -910,6 +910,66 @@ def pipeline_timing(dev, model="mobilenetv2"):
     return out
 
 
+def cle_roofline(dev, model="mobilenetv2", reps=4, traffic_json=None):
+    """The CLE loop (Cross_layer_equal.py:63-116, the reference's dominant cost)
+    against the HBM roofline: one blocking device run per rep on a fresh model
+    after the first BN fold (the main_dfq order), with the loop's device time from
+    one HIP event pair on its stream (Cross_layer_equal.DEVICE_TIMING).
+    ``algo_bytes_per_iteration`` (dfq_cle_plan_stats): rescales 8 B per weight
+    element and per-channel vector entry, metric tiles 12 B per target element,
+    weight-reading range tasks 4 B per element.  Per iteration =
+    device time / iteration groups launched (the iterations run + the one queued
+    no-op group).  Fastest rep.  ``traffic``: HBM bytes per iteration from the
+    committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same loop
+    (scripts/cle_pmc.sh), when present."""
+    import torch.nn as nn
+    from data_free_quantization_amd import zoo, Cross_layer_equal as cle
+    from data_free_quantization_amd.utils.layer_transform import merge_batchnorm
+    from data_free_quantization_amd.utils.relation import create_relation
+    from data_free_quantization_amd.utils.tracer import build_graph
+    import contextlib
+    import io
+    T = (nn.Conv2d, nn.Linear)
+    best = None
+    cle.DEVICE_TIMING = True
+    try:
+        for rep in range(reps + 1):   # rep 0 warms up
+            m = zoo.build(model, seed=0, relu=True).to(dev)
+            g = build_graph(m, "positional")
+            G, B = g.getGraph(), g.getBottoms()
+            with contextlib.redirect_stdout(io.StringIO()):
+                merge_batchnorm(m, G, B, T)
+                rels = create_relation(G, B, T)
+                torch.cuda.synchronize(dev)
+                cle.cross_layer_equalization(G, rels, T, Save_state=False, Treshhold=2e-7, launch=False)
+            r = dict(cle.LAST_RUN)
+            if rep > 0 and r.get("device_ms") and (best is None or r["device_ms"] < best["device_ms"]):
+                best = r
+    finally:
+        cle.DEVICE_TIMING = False
+    if best is None:
+        return None
+    groups = max(best["iterations_launched"], 1)
+    per_it_s = best["device_ms"] / 1e3 / groups
+    by = best["bytes_per_iteration"]
+    achieved = by["total"] / per_it_s / 1e9
+    out = {"model": model, "bound": "hbm", "kernel": "cle_loop_step_kernel", "iterations": best["iterations"],
+           "iteration_groups_launched": groups, "launches_per_iteration": best["launches_per_iteration"],
+           "loop_device_ms": round(best["device_ms"], 4), "device_us_per_iteration": round(per_it_s * 1e6, 3),
+           "algo_bytes_per_iteration": by, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+           "note": "latency-bound: each iteration is dependent launches of a few microseconds over ~100 MB"}
+    tj = Path(traffic_json) if traffic_json else None
+    if tj is not None and tj.exists():
+        try:
+            tr = json.loads(tj.read_text())
+            out["traffic"] = tr.get("hbm_bytes_per_iteration")
+            out["traffic_source"] = str(tj.relative_to(ROOT)) if tj.is_relative_to(ROOT) else str(tj)
+        except Exception:
+            pass
+    return out
+
+
 def pipeline_cold(model="mobilenetv2"):
     """The first run of the stage order in a FRESH process (child process,
     scripts/cold_pipeline.py: dfq_preload as main_dfq does, then a cold and a warm
@@ -1127,6 +1187,9 @@ def main(argv=None):
         # slower (profiles/r03/validate_as vs r03at: MobileNetV2 end to end 10.4 vs
         # 5.3 ms), a state a main_dfq run never starts from
         pipe = None if args.no_pipeline else {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")}
+        cle_roof = None if args.no_pipeline else {
+            m: cle_roofline(dev, m, traffic_json=ROOT / "profiles" / "r06" / f"cle_traffic_{m}.json")
+            for m in ("mobilenetv2", "resnet50")}
         second = None if args.no_secondary else secondary_configs(dev, stream)
         if second is not None:
             second.append(fold_quant_pair(dev, stream))
@@ -1233,6 +1296,7 @@ def main(argv=None):
             "single_model_latency": single,
             "sharded_single_model": sharded,
             "pipeline_ms": pipe,
+            "cle_roofline": cle_roof,
             "top1_delta": None,
             "notes": "top-1 needs ImageNet-val + the pretrained checkpoint (absent offline); weight outputs are "
                      "bit-exact with the reference CPU path (tests/test_gpu_pipeline.py)",

@@ -132,6 +132,9 @@ class _DiffPlan:
 #: caller's stream gate traps at 120 s (dfq_cle.hip, kCleGateSeconds /
 #: kCleLaunchDeadlineUs); a blocking run has no time bound.
 MAX_ITERS = int(os.environ.get("DFQ_CLE_MAX_ITERS", "100000"))
+#: measurement: blocking device runs record the loop's device time (one HIP event
+#: pair on its stream; LAST_RUN["device_ms"]); bench.py's cle_roofline sets it
+DEVICE_TIMING = False
 _TIMING = bool(os.environ.get("DFQ_CLE_TIMING"))   # host-side split of create (stderr)
 
 
@@ -268,17 +271,30 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
     return plan, ws, dev
 
 
+def _plan_stats(plan):
+    """dfq_cle_plan_stats: algorithmic HBM bytes of one iteration (rescale, metric,
+    ranges), the last run's device milliseconds (DEVICE_TIMING runs; else None) and
+    the iteration groups it enqueued."""
+    b, ms, n = (C.c_int64 * 3)(), C.c_double(-1.0), C.c_int32(0)
+    _lib.check(_lib.load().dfq_cle_plan_stats(plan, b, C.byref(ms), C.byref(n)), "dfq_cle_plan_stats")
+    return {"bytes_per_iteration": {"rescale": b[0], "metric": b[1], "ranges": b[2], "total": b[0] + b[1] + b[2]},
+            "device_ms": ms.value if ms.value >= 0 else None, "iterations_launched": n.value}
+
+
 def _run_plan(plan, dev, Treshhold, Count):
-    """dfq_cle_plan_run; returns (iterations, diffs, (chains, steps, launches per iteration))."""
+    """dfq_cle_plan_run; returns (iterations, diffs, (chains, steps, launches per iteration), stats)."""
     L = _lib.load()
     iters = C.c_int32(0)
     hist = _hist_buffer()
     stream = _lib.raw_stream(dev)
+    if DEVICE_TIMING:
+        _lib.check(L.dfq_cle_plan_set_timing(plan, 1), "dfq_cle_plan_set_timing")
     _lib.check(L.dfq_cle_plan_run(plan, float(Treshhold), int(Count), MAX_ITERS, C.byref(iters), hist, stream),
                "dfq_cle_plan_run")
     chains, steps, launches = C.c_int32(0), C.c_int32(0), C.c_int32(0)
     L.dfq_cle_plan_info(plan, C.byref(chains), C.byref(steps), C.byref(launches))
-    return iters.value, [hist[i] for i in range(iters.value)], (chains.value, steps.value, launches.value)
+    return (iters.value, [hist[i] for i in range(iters.value)], (chains.value, steps.value, launches.value),
+            _plan_stats(plan))
 
 
 def wait():
@@ -305,6 +321,7 @@ def wait():
         _lib.check(rc, "cross_layer_equalization (device loop)")
         chains, steps, launches = C.c_int32(0), C.c_int32(0), C.c_int32(0)
         L.dfq_cle_plan_info(plan, C.byref(chains), C.byref(steps), C.byref(launches))
+        stats = _plan_stats(plan)
     finally:
         L.dfq_cle_plan_destroy(plan)
         del ws
@@ -314,7 +331,7 @@ def wait():
     LAST_RUN.clear()
     LAST_RUN.update(iterations=n, diffs=[hist[i] for i in range(n)], chains=chains.value, steps=steps.value,
                     launches_per_iteration=launches.value, mode="device", launched=True,
-                    host_ms=dict(host, wait=(time.perf_counter() - t0) * 1e3))
+                    host_ms=dict(host, wait=(time.perf_counter() - t0) * 1e3), **stats)
 
 
 def _at_exit():
@@ -353,7 +370,7 @@ def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count,
             L.dfq_cle_plan_destroy(plan)
             _lib.check(rc, "dfq_cle_plan_launch")
     try:
-        iters, diffs, (chains, steps, launches) = _run_plan(plan, dev, Treshhold, Count)
+        iters, diffs, (chains, steps, launches), stats = _run_plan(plan, dev, Treshhold, Count)
     finally:
         t3 = time.perf_counter()
         _lib.load().dfq_cle_plan_destroy(plan)
@@ -363,7 +380,7 @@ def _cle_device_loop(graph, relations, Target_list, s_min_max, Treshhold, Count,
     LAST_RUN.clear()
     LAST_RUN.update(iterations=iters, diffs=diffs, chains=chains, steps=steps, launches_per_iteration=launches,
                     mode="device", launched=False, host_ms={"create": (t2 - t0) * 1e3, "run": (t3 - t2) * 1e3,
-                                            "destroy": (t4 - t3) * 1e3})
+                                            "destroy": (t4 - t3) * 1e3}, **stats)
 
 
 _HIST = None

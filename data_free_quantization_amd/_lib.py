@@ -32,12 +32,13 @@ EXPORTS = [
     "dfq_cle_ws_bytes", "dfq_cle_relation",
     "dfq_diff_plan_create", "dfq_diff_plan_snapshot", "dfq_diff_plan_execute", "dfq_diff_plan_destroy",
     "dfq_cle_plan_ws_bytes", "dfq_cle_plan_create", "dfq_cle_plan_run", "dfq_cle_plan_launch", "dfq_cle_plan_join",
-    "dfq_cle_plan_info", "dfq_cle_plan_destroy",
+    "dfq_cle_plan_info", "dfq_cle_plan_set_timing", "dfq_cle_plan_stats", "dfq_cle_plan_destroy",
     "dfq_bias_absorb", "dfq_bias_absorb_ws_bytes", "dfq_bias_absorb_batch", "dfq_bc_expect", "dfq_bc_apply", "dfq_bc_propagate", "dfq_bc_chain",
     "dfq_act_moments", "dfq_act_minmax", "dfq_act_affine",
 ]
 #: entry points only the diagnostics library exports (include/dfq_diag.h)
-DIAG_EXPORTS = ["dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline", "dfq_debug_ablate"]
+DIAG_EXPORTS = ["dfq_probe_stream", "dfq_probe_lds", "dfq_debug_timeline", "dfq_debug_ablate",
+                "dfq_diag_cle_check_structure"]
 DIAG_LIB_PATH = PKG / "libdfq_diag.so"
 
 
@@ -156,6 +157,8 @@ def load(path: Optional[os.PathLike] = None) -> C.CDLL:
         "dfq_cle_plan_join": ([P, C.POINTER(I32), C.POINTER(F64)], C.c_int),
         "dfq_cle_plan_info": ([P, C.POINTER(I32), C.POINTER(I32), C.POINTER(I32)], C.c_int),
         "dfq_cle_plan_destroy": ([P], C.c_int),
+        "dfq_cle_plan_set_timing": ([P, I32], C.c_int),
+        "dfq_cle_plan_stats": ([P, C.POINTER(I64), C.POINTER(F64), C.POINTER(I32)], C.c_int),
         "dfq_bias_absorb": ([P, P, P, P, P, I64, I64, I64, I64, F32, P], C.c_int),
         "dfq_bias_absorb_ws_bytes": ([C.POINTER(AbsorbDesc), I32], C.c_int64),
         "dfq_bias_absorb_batch": ([C.POINTER(AbsorbDesc), I32, F32, P, I64, C.POINTER(I32), P], C.c_int),

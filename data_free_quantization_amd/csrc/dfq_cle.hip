@@ -1573,6 +1573,10 @@ struct dfq_cle_plan {
     int dev = 0;
     struct CleAsync* async = nullptr;   // dfq_cle_plan_launch's worker and result
     bool abandoned = false;             // join gave up waiting for the launched loop
+    int64_t bytes[3] = {0, 0, 0};       // algorithmic bytes per iteration: rescale, metric, ranges
+    bool timed = false;                 // dfq_cle_plan_set_timing: HIP events around the loop
+    float loop_ms = -1.f;               // the last run's device time, first launch to last (timed runs)
+    int32_t launched = 0;               // iteration groups the last run enqueued
 #ifdef DFQ_DIAGNOSTICS
     std::vector<CleRel> h_rels;
     std::vector<CleTask> h_atasks;
@@ -1699,6 +1703,12 @@ struct CleStructure {
     int32_t nlaunch = 0, stop_off = -1;
     bool lagged = false;
     double t_chains = 0, t_tasks = 0, t_chunks = 0, t_place = 0;
+    // algorithmic HBM bytes of one iteration (dfq_cle_plan_stats): the rescales
+    // (8 B per weight element and per channel of each per-channel vector: read +
+    // write; a depthwise pair's filter once), the metric tiles (12 B per target
+    // element: W and the snapshot read, the snapshot written) and the range tasks
+    // that read weights (4 B per element; self ranges are free)
+    int64_t bytes_rescale = 0, bytes_metric = 0, bytes_range = 0;
 };
 
 static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, float* const* targets,
@@ -2150,6 +2160,30 @@ static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, 
     S.nlaunch = nlaunch;
     S.stop_off = stop_off;
     S.lagged = lagged;
+    for (const CleTask& tk : S.at) {
+        const CleRel& q = S.R[tk.rel];
+        const int64_t n = tk.b - tk.a;
+        switch (tk.kind) {
+            case kApplyW1: S.bytes_rescale += 8 * n * q.len1; break;
+            case kApplyW2Contig:
+            case kApplyDwBoth: S.bytes_rescale += 8 * n * q.o2g * q.khw2; break;
+            case kApplyW2Tile: S.bytes_rescale += 8 * n * (tk.c1 - tk.c0) * q.khw2; break;
+            default:
+                S.bytes_rescale += 8 * n * ((q.b1 ? 1 : 0) + (q.bnw ? 1 : 0) + (q.bnb ? 1 : 0) + (q.sacc ? 1 : 0));
+        }
+    }
+    for (int32_t l = 0; l < n_targets; ++l) S.bytes_metric += 12 * target_n[l];
+    {
+        const int64_t r0 = fused ? S.ri0 : 0, r1 = fused ? S.ri1 : (int64_t)S.rt.size();
+        for (int64_t t = r0; t < r1; ++t) {
+            const CleTask& tk = S.rt[t];
+            const CleRel& q = S.R[tk.rel];
+            const int64_t n = tk.b - tk.a;
+            if (tk.kind == kRangeW1) S.bytes_range += 4 * n * q.len1;
+            else if (tk.kind == kRangeW2Contig) S.bytes_range += 4 * n * q.o2g * q.khw2;
+            else if (tk.kind == kRangeW2Tile) S.bytes_range += 4 * n * (tk.c1 - tk.c0) * q.khw2;
+        }
+    }
     const double tp5 = now_us();
     S.t_chains = tp2 - tp1;
     S.t_tasks = tp3 - tp2;
@@ -2345,6 +2379,9 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
             if (at[t].kind == kApplyW2Tile && Rb[at[t].rel].khw2 > 1) p->step_pos[k] = 1;
     p->ri0 = ri0;
     p->ri1 = ri1;
+    p->bytes[0] = S->bytes_rescale;
+    p->bytes[1] = S->bytes_metric;
+    p->bytes[2] = S->bytes_range;
 #ifdef DFQ_DIAGNOSTICS
     if (ab_env("DFQ_CLE_TL")) {   // for the timeline report (copies cost ~0.2 ms: only when asked)
         p->h_rels = R;
@@ -2647,6 +2684,16 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     const double tc1 = now_us();
     int32_t launched = 0;
     bool deadline_hit = false;
+    // timed runs (dfq_cle_plan_set_timing, measurement only): one event pair around
+    // the loop's launches on its stream (two marker packets per run, none between
+    // iterations)
+    hipEvent_t tev[2] = {nullptr, nullptr};
+    p->loop_ms = -1.f;
+    if (p->timed) {
+        DFQ_HIP_CHECK(hipEventCreate(&tev[0]));
+        DFQ_HIP_CHECK(hipEventCreate(&tev[1]));
+        DFQ_HIP_CHECK(hipEventRecord(tev[0], s));
+    }
 #ifdef DFQ_DIAGNOSTICS
     const char* pd = ab_env("DFQ_CLE_TEST_POLL_DELAY_US");
     const int poll_delay_us = pd ? atoi(pd) : 0;
@@ -2694,8 +2741,16 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
                            p->d_atasks, p->n_at, p->d_vsave, p->d_vtag, p->d_state);
         DFQ_LAUNCH_CHECK();
     }
+    if (tev[1]) DFQ_HIP_CHECK(hipEventRecord(tev[1], s));
     if (p->d_sig) DFQ_HIP_CHECK(hipStreamWriteValue64(s, p->d_sig, p->gen, 0));
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
+    p->launched = launched;
+    if (tev[0]) {
+        float ms = -1.f;
+        if (hipEventElapsedTime(&ms, tev[0], tev[1]) == hipSuccess) p->loop_ms = ms;
+        (void)hipEventDestroy(tev[0]);
+        (void)hipEventDestroy(tev[1]);
+    }
     if (cle_timing())
         fprintf(stderr, "DFQ_CLE_TIMING run: loop %.1f us (%d iterations launched)\n", now_us() - tc1, launched);
 #ifdef DFQ_DIAGNOSTICS
@@ -3102,6 +3157,24 @@ extern "C" int dfq_cle_plan_info(const dfq_cle_plan* p, int32_t* chains, int32_t
     // per iteration: the rescale launches (+ per-step range launches when the
     // schedule is not fused), + a tiles-only launch unless the schedule is lagged
     if (launches) *launches = p->fused ? p->nlaunch : 2 * p->steps + 1;
+    return DFQ_OK;
+}
+
+extern "C" int dfq_cle_plan_set_timing(dfq_cle_plan* p, int32_t on) {
+    if (!p || p->async) return DFQ_ERR_INVALID;
+    p->timed = on != 0;
+    return DFQ_OK;
+}
+
+extern "C" int dfq_cle_plan_stats(const dfq_cle_plan* p, int64_t* bytes, double* loop_ms, int32_t* launched) {
+    if (!p) return DFQ_ERR_INVALID;
+    if (bytes) {
+        bytes[0] = p->bytes[0];
+        bytes[1] = p->bytes[1];
+        bytes[2] = p->bytes[2];
+    }
+    if (loop_ms) *loop_ms = p->loop_ms;
+    if (launched) *launched = p->launched;
     return DFQ_OK;
 }
 

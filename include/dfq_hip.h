@@ -306,6 +306,14 @@ int dfq_cle_plan_join(dfq_cle_plan* plan, int32_t* iterations, double* diffs);
  * launches = kernel launches per iteration (fused schedule: one range launch for
  * the whole iteration; DFQ_CLE_FUSED=0: one per step) */
 int dfq_cle_plan_info(const dfq_cle_plan* plan, int32_t* chains, int32_t* steps, int32_t* launches);
+/* Measurement (no reference counterpart): with timing on, the next run records one
+ * HIP event pair on the loop's stream around its launches.  stats: bytes[3] = the
+ * algorithmic HBM bytes of ONE iteration (rescales incl. the per-channel vectors,
+ * metric tiles, weight-reading range tasks), loop_ms = the last timed run's device
+ * time from its first launch to its last (-1 if not timed), launched = the
+ * iteration groups it enqueued (iterations + the queued no-op ones). */
+int dfq_cle_plan_set_timing(dfq_cle_plan* plan, int32_t on);
+int dfq_cle_plan_stats(const dfq_cle_plan* plan, int64_t* bytes, double* loop_ms, int32_t* launched);
 int dfq_cle_plan_destroy(dfq_cle_plan* plan);
 
 /* ---- high-bias absorption (bias_absorption.py:147-197) ------------------

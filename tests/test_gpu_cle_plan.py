@@ -224,7 +224,7 @@ def test_two_live_plans():
         for plan, _, _ in plans:
             cle._lib.load().dfq_cle_plan_destroy(plan)
     torch.cuda.synchronize()
-    for (m0, r0, it0, d0), (m1, _, r1), (it1, d1, _) in zip(refs, live, runs):
+    for (m0, r0, it0, d0), (m1, _, r1), (it1, d1, _, _) in zip(refs, live, runs):
         assert it0 == it1 and d0 == d1
         for (k, a), (_, b) in zip(m0.state_dict().items(), m1.state_dict().items()):
             assert torch.equal(a, b), k
@@ -384,3 +384,40 @@ def test_device_cle_many_layers(n_chains, monkeypatch):
         assert np.array_equal(g[k].bias.detach().cpu().numpy(), B[k]), k
     for i, r in enumerate(rels):
         assert np.array_equal(r.S.cpu().numpy(), S[i]), i
+
+
+def test_plan_stats_bytes_and_device_time(monkeypatch):
+    """dfq_cle_plan_stats (bench.py's cle_roofline): the metric tiles' bytes are
+    12 B per target element, the rescales' at least 8 B per element of every
+    relation's W1 and W2 (a depthwise pair's filter counted once); a timed blocking
+    run reports its loop's device time, and untimed runs report none."""
+    from data_free_quantization_amd import zoo, Cross_layer_equal as cle
+    from data_free_quantization_amd.utils.layer_transform import merge_batchnorm
+    from data_free_quantization_amd.utils.relation import create_relation
+    from data_free_quantization_amd.utils.tracer import build_graph
+    T = (nn.Conv2d, nn.Linear)
+    m = zoo.build("mobilenetv2", seed=0, relu=True).to(DEV)
+    g = build_graph(m, "positional")
+    G, B = g.getGraph(), g.getBottoms()
+    merge_batchnorm(m, G, B, T)
+    rels = create_relation(G, B, T)
+    monkeypatch.setattr(cle, "DEVICE_TIMING", True)
+    cle.cross_layer_equalization(G, rels, T, Save_state=False, Treshhold=2e-7, launch=False)
+    r = dict(cle.LAST_RUN)
+    tw = sum(G[k].weight.numel() for k in G if type(G[k]) in T)
+    by = r["bytes_per_iteration"]
+    assert by["metric"] == 12 * tw
+    w1 = sum(G[x.layer_first].weight.numel() for x in rels)
+    assert 8 * w1 <= by["rescale"] <= 8 * 2 * sum(G[x.layer_first].weight.numel() + G[x.layer_second].weight.numel()
+                                                  for x in rels)
+    assert by["total"] == by["rescale"] + by["metric"] + by["ranges"]
+    assert r["iterations"] == 44 and r["iterations_launched"] >= r["iterations"]
+    per_it_us = r["device_ms"] * 1e3 / r["iterations_launched"]
+    assert 5.0 < per_it_us < 2000.0, per_it_us
+    monkeypatch.setattr(cle, "DEVICE_TIMING", False)
+    m2 = zoo.build("mobilenetv2", seed=0, relu=True).to(DEV)
+    g2 = build_graph(m2, "positional")
+    G2, B2 = g2.getGraph(), g2.getBottoms()
+    merge_batchnorm(m2, G2, B2, T)
+    cle.cross_layer_equalization(G2, create_relation(G2, B2, T), T, Save_state=False, Treshhold=2e-7, launch=False)
+    assert cle.LAST_RUN["device_ms"] is None and cle.LAST_RUN["bytes_per_iteration"] == by
