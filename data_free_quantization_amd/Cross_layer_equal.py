@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from .utils.relation import Relation
 
 class _LastRun(MutableMapping):
     """LAST_RUN: a dict whose reads first wait for a launched (asynchronous) loop."""
@@ -229,17 +230,23 @@ def _create_plan(graph, relations, Target_list, s_min_max, signed, eps):
         bnw, bnb = _state(bn, "fake_weight"), _state(bn, "fake_bias")
         w1p, s1, n1 = _tensor_info(W1, memo)
         w2p, s2, n2 = _tensor_info(l2._parameters["weight"], memo)
-        init = rel.S is None
+        init = not rel._has_S() if isinstance(rel, Relation) else rel.S is None
         if init:
-            fresh.append((len(rows), rel, W1))
+            fresh.append((len(rows), rel, s1[0]))
         rows.append([w1p, w2p, _checked_ptr(p1["bias"]), 0 if bnw is None else _checked_ptr(bnw),
                      0 if bnb is None else _checked_ptr(bnb), 0 if init else rel.S.data_ptr(), s1[0],
                      n1 // s1[0], s2[0], s2[1], n2 // (s2[0] * s2[1]), 1 if init else 0, 0])
-    if fresh:   # one allocation for every new Relation.S (a torch.empty per relation cost ~7 us each)
-        flat = torch.empty(sum(w.size(0) for _, _, w in fresh), dtype=torch.float32, device=fresh[0][2].device)
-        for (j, rel, w), v in zip(fresh, torch.split(flat, [w.size(0) for _, _, w in fresh])):
-            rel.S = v
-            rows[j][5] = v.data_ptr()
+    if fresh:   # one allocation for every new Relation.S (a torch.empty per relation cost ~7 us each),
+        # handed out as lazy slices (Relation.S: the view is made on first read)
+        flat = torch.empty(sum(c for _, _, c in fresh), dtype=torch.float32, device=targets[0].device)
+        base, off = flat.data_ptr(), 0
+        for j, rel, c in fresh:
+            if isinstance(rel, Relation):
+                rel._set_S_lazy(flat, off, off + c)
+            else:
+                rel.S = flat[off:off + c]
+            rows[j][5] = base + 4 * off
+            off += c
     rows = [tuple(r) for r in rows]
     if tc:
         tc.append(time.perf_counter())

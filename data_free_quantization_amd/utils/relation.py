@@ -24,7 +24,32 @@ class Relation:
         self.layer_first = layer_idx_1
         self.layer_second = layer_idx_2
         self.bn_idx = bn_idx_1
-        self.S = None
+        self._S = None
+        self._S_lazy = None   # (flat, start, end): S as a slice of one allocation, made on first read
+
+    @property
+    def S(self):
+        """The accumulated scale (a tensor, or None).  The device CLE loop hands
+        every new S out as a slice of one allocation; the view object is created on
+        first access (the loop itself only needs the address), which keeps ~37 view
+        creations off MobileNetV2's CLE stage."""
+        if self._S is None and self._S_lazy is not None:
+            flat, a, b = self._S_lazy
+            self._S = flat[a:b]
+            self._S_lazy = None
+        return self._S
+
+    @S.setter
+    def S(self, value):
+        self._S = value
+        self._S_lazy = None
+
+    def _has_S(self) -> bool:
+        return self._S is not None or self._S_lazy is not None
+
+    def _set_S_lazy(self, flat, start, end):
+        self._S = None
+        self._S_lazy = (flat, start, end)
 
     def __repr__(self):
         return "({}, {})".format(self.layer_first, self.layer_second)
