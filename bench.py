@@ -884,11 +884,12 @@ def pipeline_timing(dev, model="mobilenetv2"):
         torch.cuda.synchronize(dev)
         total = time.perf_counter() - t0
         if rep > 0 and (best is None or total < best[0]):
-            best = (total, t, cle.LAST_RUN.get("iterations"))
-    total, t, iters = best
+            best = (total, t, cle.LAST_RUN.get("iterations"), cle.LAST_RUN.get("host_ms"))
+    total, t, iters, cle_host = best
     out = {k: round(v * 1e3, 3) for k, v in t.items()}
     out["total"] = round(total * 1e3, 3)
     out["cle_iterations"] = iters
+    out["cle_host_ms"] = {k: round(v, 3) for k, v in (cle_host or {}).items()}   # create / launch / join
     # the same stage order as main_dfq runs it: no device sync between the stages,
     # so the host work of absorption / fold / quantize / BC overlaps the CLE loop
     # (launched asynchronously); one sync at the end

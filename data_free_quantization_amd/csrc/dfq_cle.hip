@@ -942,10 +942,22 @@ struct CleUnit {
     int32_t tile;     // < nb1: full level-1 tile; == nb1: the chunk's tail tile
 };
 
-// snap := W for every target layer (before the first iteration): one workgroup
-// per metric tile (chunks of < 8 elements by the first workgroup)
-__global__ void cle_loop_snap_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
-                                     int64_t nchunks, const CleUnit* __restrict__ units, int64_t nunits) {
+// Before the first iteration, ONE launch instead of six fills, a state upload and
+// the snapshot kernel: both parities' range words armed (mins = 0xFF.., maxs = 0;
+// layout [parity][mins M | maxs M]), the chunk sums and arrival counters zeroed,
+// the rollback tags set to -1, the loop state from the launch argument, and
+// snap := W (one workgroup per metric tile; the chunks of < 8 elements by block 0).
+__global__ void __launch_bounds__(kThreads)
+cle_loop_init_kernel(const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks, int64_t nchunks,
+                     const CleUnit* __restrict__ units, int64_t nunits, uint32_t* __restrict__ rng, int64_t M,
+                     float* __restrict__ part, int64_t npart, uint32_t* __restrict__ cnt, int64_t ncnt,
+                     int32_t* __restrict__ vtag, int64_t nvtag, CleState* __restrict__ st, CleState init) {
+    const int64_t gt = (int64_t)blockIdx.x * kThreads + threadIdx.x, gs = (int64_t)gridDim.x * kThreads;
+    for (int64_t i = gt; i < 4 * M; i += gs) rng[i] = ((i / M) & 1) ? 0u : 0xFFFFFFFFu;
+    for (int64_t i = gt; i < npart; i += gs) part[i] = 0.f;
+    for (int64_t i = gt; i < ncnt; i += gs) cnt[i] = 0u;
+    for (int64_t i = gt; i < nvtag; i += gs) vtag[i] = -1;
+    if (gt == 0) *st = init;
     for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
         const CleUnit un = units[u];
         const CleChunk ch = chunks[un.chunk];
@@ -1612,6 +1624,8 @@ struct CleDeviceCtx {
     hipEvent_t pool_ev = nullptr;                  // behind the last upload from h_pool
     double* d_hist = nullptr;                      // histories longer than the tables' kCleHistCap
     int64_t hist_cap = 0;
+    double* h_hist = nullptr;                      // pinned: the run's history comes back here
+    int64_t h_hist_cap = 0;
     // asynchronous runs (dfq_cle_plan_launch): the signal word callers' streams
     // wait on, its last generation, the launched plan not yet joined
     void* sig = nullptr;
@@ -2583,6 +2597,14 @@ static constexpr double kCleLaunchDeadlineUs = 0.5e6 * kCleGateSeconds;
 // grown once (a launched run grows it before its caller's stream waits: hipFree
 // synchronises the whole device).
 static hipError_t cle_hist_ready(CleDeviceCtx& ctx, int32_t max_iters) {
+    if (ctx.h_hist_cap < max_iters + 1) {   // the pinned copy-back buffer
+        (void)hipHostFree(ctx.h_hist);
+        ctx.h_hist = nullptr;
+        ctx.h_hist_cap = 0;
+        const hipError_t e = hipHostMalloc(&ctx.h_hist, sizeof(double) * (max_iters + 1), hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        ctx.h_hist_cap = max_iters + 1;
+    }
     if (max_iters + 1 <= kCleHistCap || ctx.hist_cap >= max_iters + 1) return hipSuccess;
     (void)hipFree(ctx.d_hist);
     ctx.d_hist = nullptr;
@@ -2613,10 +2635,8 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     hipStream_t s = p->st;
     // the history: the tables' slots, or the context's buffer (grown once) for longer caps
     p->d_hist = p->d_hist_tables;
-    if (max_iters + 1 > kCleHistCap) {
-        DFQ_HIP_CHECK(cle_hist_ready(ctx, max_iters));
-        p->d_hist = ctx.d_hist;
-    }
+    DFQ_HIP_CHECK(cle_hist_ready(ctx, max_iters));
+    if (max_iters + 1 > kCleHistCap) p->d_hist = ctx.d_hist;
     CleState init{};
     init.diff = 1e8;
     init.thr = threshold;
@@ -2625,19 +2645,17 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     init.count = count;
     init.max_iters = max_iters;
     init.done = !((init.diff > threshold) && (0 < count)) || max_iters == 0;
-    *p->h_state = init;
-    DFQ_HIP_CHECK(hipMemcpyAsync(p->d_state, p->h_state, sizeof(CleState), hipMemcpyHostToDevice, s));
-    // both parities' ranges: mins = +inf code (0xFF..), maxs = 0
-    for (int par = 0; par < 2; ++par) {
-        DFQ_HIP_CHECK(hipMemsetAsync(p->d_rng + (int64_t)par * 2 * p->M, 0xFF, sizeof(uint32_t) * p->M, s));
-        DFQ_HIP_CHECK(hipMemsetAsync(p->d_rng + (int64_t)par * 2 * p->M + p->M, 0x00, sizeof(uint32_t) * p->M, s));
-    }
-    DFQ_HIP_CHECK(hipMemsetAsync(p->d_part, 0, sizeof(float) * p->slots * std::max(p->nl, 1), s));
-    DFQ_HIP_CHECK(hipMemsetAsync(p->d_cnt, 0, sizeof(uint32_t) * (p->nchunks + 1), s));
-    if (p->d_vtag && p->n_at > 0) DFQ_HIP_CHECK(hipMemsetAsync(p->d_vtag, 0xFF, sizeof(int32_t) * p->n_at, s));
-    if (p->nchunks > 0) {
-        hipLaunchKernelGGL(cle_loop_snap_kernel, dim3((int)std::min<int64_t>(std::max<int64_t>(p->nunits, 1), 4096)),
-                           dim3(kThreads), 0, s, p->d_layers, p->d_chunks, p->nchunks, p->d_units, p->nunits);
+    // the range words, chunk sums, counters, rollback tags, the state and the
+    // snapshots in one launch (cle_loop_init_kernel; round 5: six fills, a state
+    // upload and the snapshot kernel)
+    {
+        const int64_t npart = (int64_t)p->slots * std::max(p->nl, 1), ncnt = p->nchunks + 1;
+        const int64_t nvtag = p->d_vtag ? p->n_at : 0;
+        const int64_t words = std::max({4 * p->M, npart, ncnt, nvtag});
+        const int64_t grid = std::min<int64_t>(std::max<int64_t>({p->nunits, ceil_div(words, (int64_t)kThreads), 1}), 4096);
+        hipLaunchKernelGGL(cle_loop_init_kernel, dim3((int)grid), dim3(kThreads), 0, s, p->d_layers, p->d_chunks,
+                           p->nchunks, p->d_units, p->nunits, p->d_rng, p->M, p->d_part, npart, p->d_cnt, ncnt,
+                           p->d_vtag, nvtag, p->d_state, init);
         DFQ_LAUNCH_CHECK();
     }
     // fused schedule: the first iteration's ranges (later ones ride with the tiles)
@@ -2743,6 +2761,11 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     }
     if (tev[1]) DFQ_HIP_CHECK(hipEventRecord(tev[1], s));
     if (p->d_sig) DFQ_HIP_CHECK(hipStreamWriteValue64(s, p->d_sig, p->gen, 0));
+    // the final state and the history (at most the groups launched: iterations run
+    // <= groups) come back in the same drain -- one synchronize, not three
+    DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
+    const int32_t hn = std::min(launched, max_iters);
+    if (hist && hn > 0) DFQ_HIP_CHECK(hipMemcpyAsync(ctx.h_hist, p->d_hist, sizeof(double) * hn, hipMemcpyDeviceToHost, s));
     DFQ_HIP_CHECK(hipStreamSynchronize(s));
     p->launched = launched;
     if (tev[0]) {
@@ -2860,8 +2883,6 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     }
 #endif
     // the final state (a no-op iteration after convergence changed nothing)
-    DFQ_HIP_CHECK(hipMemcpyAsync(p->h_state, p->d_state, sizeof(CleState), hipMemcpyDeviceToHost, s));
-    DFQ_HIP_CHECK(hipStreamSynchronize(s));
     const CleState fin = *p->h_state;
     if (fin.error) {   // a range block saw the wrong parity: never expected
         set_last_hip_error(hipErrorLaunchTimeOut);
@@ -2884,8 +2905,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     if (iterations) *iterations = fin.iters;
     if (hist) {
         hist->assign((size_t)std::max(fin.iters, 0), 0.0);
-        if (fin.iters > 0)
-            DFQ_HIP_CHECK(cle_copy_back(hist->data(), p->d_hist, sizeof(double) * fin.iters, s));
+        if (fin.iters > 0) std::memcpy(hist->data(), ctx.h_hist, sizeof(double) * std::min(fin.iters, hn));
     }
     return DFQ_OK;
 }

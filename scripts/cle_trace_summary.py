@@ -30,7 +30,7 @@ def main():
                    int(k(r, "Grid_Size_X", "Grid_Size", "grid_size") or 0) //
                    max(1, int(k(r, "Workgroup_Size_X", "Workgroup_Size", "workgroup_size") or 1))))
     ev.sort()
-    snaps = [i for i, e in enumerate(ev) if "cle_loop_snap" in e[2]]
+    snaps = [i for i, e in enumerate(ev) if "cle_loop_snap" in e[2] or "cle_loop_init" in e[2]]
     if not snaps:
         print("no CLE loop in the trace")
         return
