@@ -67,8 +67,9 @@ constexpr Variant kVariants[] = {
     {2048, 64, false},    // 13: variant 6 + per-task timestamps (diagnostics: dfq_debug_timeline)
     {2048, 64, false},    // 14: variant 6 with the IEEE divide on every element (round-2 arithmetic)
     {2048, 64, false},    // 15: variant 6 with the generic quantize loop (flags tested per float4; round 3)
+    {2048, 64, false},    // 16: variant 6 with whole-row tasks in two row batches (compute_task_split)
 };
-constexpr int kNumVariants = 16;
+constexpr int kNumVariants = 17;
 // HostTask / DevTask .nrows <= kGroupTag: a row-group piece of R = kGroupTag - nrows + 1 rows
 constexpr int kGroupTag = -64;
 constexpr int kGroupMaxRows = 16;
@@ -164,6 +165,23 @@ template <bool NT = false>
 __device__ __forceinline__ void glds4(const float* g, float* lds_base) {
     __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 4, 0, NT ? 2 : 0);
 }
+// The same DMA issued through inline asm, which the compiler's wait-count pass does
+// not see as a pending LDS write: with the builtin, every LDS read after a
+// partial vmcnt wait got its own vmcnt(0) (the compiler cannot tell which DMA a
+// read depends on), which undoes the two-batch overlap (compute_task_split).
+// Every LDS read of a task's chunk is then ordered by the explicit waits alone.
+template <bool NT = false>
+__device__ __forceinline__ void glds16_asm(const float* g, float* lds_base) {
+    const uint32_t m0 = (uint32_t)(uintptr_t)(lds_void_t*)lds_base;
+    if constexpr (NT) asm volatile("global_load_lds_dwordx4 %0, off nt" ::"v"(g), "{m0}"(m0) : "memory");
+    else asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+}
+template <bool NT = false>
+__device__ __forceinline__ void glds4_asm(const float* g, float* lds_base) {
+    const uint32_t m0 = (uint32_t)(uintptr_t)(lds_void_t*)lds_base;
+    if constexpr (NT) asm volatile("global_load_lds_dword %0, off nt" ::"v"(g), "{m0}"(m0) : "memory");
+    else asm volatile("global_load_lds_dword %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+}
 // Output stores; NT: non-temporal (streamed out, never re-read by this launch).
 // Stores through address_space(1) pointers: the descriptor fields are generic
 // pointers, and a flat_store also counts on lgkmcnt, so every LDS wait would
@@ -231,7 +249,7 @@ sweep_reduce_kernel(const DevTensor* __restrict__ tensors, const DevTask* __rest
 // Main launch: one wave task.
 // ---------------------------------------------------------------------------
 // Issue the task's HBM -> LDS DMA (all loads in flight; no wait).
-template <bool NT = false>
+template <bool NT = false, bool ASM = false>
 __device__ __forceinline__ void issue_task_load(const DevTask& task, float* data, int lane) {
     const float* src = task.src;
     const int n = task.n;
@@ -239,12 +257,18 @@ __device__ __forceinline__ void issue_task_load(const DevTask& task, float* data
         const int nj = n >> 2;
         for (int m = 0; m * kWave < nj; ++m) {
             const int j = lane + m * kWave;
-            if (j < nj) glds16<NT>(src + 4 * j, data + 4 * kWave * m);
+            if (j < nj) {
+                if constexpr (ASM) glds16_asm<NT>(src + 4 * j, data + 4 * kWave * m);
+                else glds16<NT>(src + 4 * j, data + 4 * kWave * m);
+            }
         }
     } else {
         for (int m = 0; m * kWave < n; ++m) {
             const int e = lane + m * kWave;
-            if (e < n) glds4<NT>(src + e, data + kWave * m);
+            if (e < n) {
+                if constexpr (ASM) glds4_asm<NT>(src + e, data + kWave * m);
+                else glds4<NT>(src + e, data + kWave * m);
+            }
         }
     }
 }
@@ -709,6 +733,140 @@ __device__ __forceinline__ void compute_task(const DevTensor& T, const DevTask& 
     wave_lds_sync();  // LDS is reused by this wave's next task
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the count is an immediate):
+// every value 0..8, larger ones round down to 8 (waiting longer is always safe).
+__device__ __forceinline__ void vm_wait_le(int n) {
+    switch (n < 0 ? 0 : (n > 8 ? 8 : n)) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    }
+}
+
+// A whole-row task in two row batches (the single-model latency lever of DESIGN.md
+// 3.1): the wave waits only for the load instructions that cover rows [0, h),
+// reduces their ranges, builds their parameters and quantizes and STORES them
+// while the loads of rows [h, nrows) are still landing; then it waits for those
+// (vmcnt counts loads, LDS-DMA and stores together in issue order,
+// MI355X_MICROARCH.md: at most lb younger operations outstanding means every load
+// of the task has landed, for any lb <= the stores issued since) and does the
+// rest.  The same per-row arithmetic and stores as compute_task's fixed-form loop
+// (bit-identical); the KH*KW error sums run over the whole task at the end.
+// Returns false (nothing done, loads still in flight) when the task does not split:
+// the caller takes the one-wait path.
+template <int MAXROWS, bool NT, int ESPEC>
+__device__ __forceinline__ bool compute_task_split(const DevTensor& T, const DevTask& task, float* data, float* ls,
+                                                   float* lmn, int lane) {
+    const int n = task.n, nrows = task.nrows, len = (int)T.row_len;
+    const bool clip = (T.flags & DFQ_CLIP) != 0;
+    if (MAXROWS != 64 || nrows < 2 || !T.vec4 || !T.dst || (clip && !(T.clip_lo <= T.clip_hi))) return false;
+    const int nj = n >> 2;
+    const int M = (nj + kWave - 1) / kWave;   // load instructions issued (issue_task_load: 1 KiB each)
+    const int h = min(nrows - 1, ((M >> 1) * 4 * kWave) / len);   // rows inside the first half of the loads
+    if (M < 2 || h < 1) return false;
+    const int m1 = (h * len + 4 * kWave - 1) / (4 * kWave);   // load instructions covering rows [0, h)
+    const bool sym = is_sym(T.mode);
+    const int khw = T.khw;
+    const bool want_e = T.esum != nullptr;
+    const float qmin = sym ? -(float)(1 << (T.bits - 1)) : 0.f;
+    const float qmax = sym ? (float)((1 << (T.bits - 1)) - 1) : (float)((1 << T.bits) - 1);
+    const int64_t base = task_elem_start(task, T);
+    const int cb = !T.codes ? 0 : (T.code_bytes == 1 ? 1 : (T.code_bytes == 0 ? 3 : 2));
+    const int em = !want_e ? 0 : (khw == 1 ? 1 : 2);
+    const float* lrs = lmn + MAXROWS;
+    const QParams pc{};
+    auto rows = [&](int ra, int rb) {
+        // ranges and parameters of rows [ra, rb) (compute_task's whole-row reduce)
+        const int nr = rb - ra;
+        int p2 = 1;
+        while (p2 < nr && p2 < kWave) p2 <<= 1;
+        const int G = kWave / p2;
+        const int sub = lane / G, sl = lane % G;
+        for (int r0 = ra; r0 < rb; r0 += p2) {
+            const int r = r0 + sub;
+            float vmin = INFINITY, vmax = -INFINITY;
+            if (r < rb) {
+                const int q4 = len >> 2;
+                const float4* row4 = reinterpret_cast<const float4*>(data + r * len);
+                for (int i = sl; i < q4; i += 4 * G) {
+                    float4 v[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = row4[min(i + u * G, q4 - 1)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        vmin = min3_nc(min3_nc(vmin, v[u].x, v[u].y), v[u].z, v[u].w);
+                        vmax = max3_nc(max3_nc(vmax, v[u].x, v[u].y), v[u].z, v[u].w);
+                    }
+                }
+            }
+            group_minmax(vmin, vmax, G);
+            if (sl == 0 && r < rb) {
+                const QParams p = make_qparams(vmin, vmax, T.bits, sym, T.flags, T.given_min, T.given_max);
+                ls[r] = p.s;
+                lmn[r] = p.mn;
+                lmn[MAXROWS + r] = __builtin_amdgcn_rcpf(p.s);
+                const int64_t row_g = task.row0 + r;
+                if (T.scale) st<false>(T.scale + row_g, p.s);
+                if (T.zero) st<false>(T.zero + row_g, p.mn);
+            }
+        }
+        wave_lds_sync();
+        // quantize rows [ra, rb): the fixed-form loop on that element span
+        const int e0 = ra * len, ne = (rb - ra) * len;
+        if (clip) quant_vec4_c<true, NT>(cb, em, T, ne, base + e0, data + e0, ls, lmn, lrs, pc, true, e0, lane, qmin,
+                                         qmax, sym);
+        else quant_vec4_c<false, NT>(cb, em, T, ne, base + e0, data + e0, ls, lmn, lrs, pc, true, e0, lane, qmin, qmax,
+                                     sym);
+    };
+    vm_wait_le(M - m1);   // rows [0, h) have landed
+    wave_lds_sync();
+    rows(0, h);
+    // the loop above issued >= one store per iteration of ceil(h len / 4 / 128)
+    vm_wait_le(((h * len >> 2) + 2 * kWave - 1) / (2 * kWave));   // every load of the task has landed
+    wave_lds_sync();
+    rows(h, nrows);
+    if (want_e && khw > 1) {   // 4. KHW error sums over the whole task (compute_task's step 4)
+        wave_lds_sync();
+        const int np = n / khw;
+        const int64_t pbase = base / khw;
+        auto esums = [&](auto kconst) {
+            constexpr int K = decltype(kconst)::value;
+            for (int pi = lane; pi < np; pi += kWave) {
+                const float* e = data + pi * K;
+                st<false>(T.esum + pbase + pi, aten_inner_sum([&](int64_t k) { return e[k]; }, (int64_t)K));
+            }
+        };
+        auto generic = [&]() {
+            for (int pi = lane; pi < np; pi += kWave) {
+                const float* e = data + pi * khw;
+                st<false>(T.esum + pbase + pi, aten_inner_sum([&](int64_t k) { return e[k]; }, khw));
+            }
+        };
+        if constexpr (ESPEC == 2) {
+            switch (khw) {
+                case 9: esums(std::integral_constant<int, 9>{}); break;
+                case 49: esums(std::integral_constant<int, 49>{}); break;
+                case 25: esums(std::integral_constant<int, 25>{}); break;
+                case 4: esums(std::integral_constant<int, 4>{}); break;
+                default: generic();
+            }
+        } else if constexpr (ESPEC == 1) {
+            if (khw == 9) esums(std::integral_constant<int, 9>{});
+            else generic();
+        } else {
+            generic();
+        }
+    }
+    wave_lds_sync();   // LDS is reused by this wave's next task
+    return true;
+}
+
 // Diagnostics timeline (variant 13): per main-list task {start, data landed, done}
 // in s_memrealtime ticks (100 MHz) plus the executing wave's hardware ids.
 __device__ uint64_t* g_timeline = nullptr;
@@ -720,7 +878,7 @@ __device__ int64_t g_timeline_cap = 0;
 __device__ uint32_t g_ablate = 0;
 
 template <int CHUNK, int MAXROWS, bool PREFETCH, bool NT = false, int ESPEC = 2, bool TL = false, bool SCREEN = true,
-          bool FAST = true>
+          bool FAST = true, bool SPLIT = false>
 __global__ void __launch_bounds__(kBlockThreads)
 sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restrict__ tasks, int64_t ntasks,
                   const uint32_t* __restrict__ slot_min, const uint32_t* __restrict__ slot_max) {
@@ -747,10 +905,18 @@ sweep_main_kernel(const DevTensor* __restrict__ tensors, const DevTask* __restri
                 tl0 = wall_clock64();
                 abl = g_ablate;
             }
-            if (!(abl & 8)) issue_task_load<NT>(task, wl, lane);   // needs only the task record
+            if (!(abl & 8)) issue_task_load<NT, SPLIT>(task, wl, lane);   // needs only the task record
             const DevTensor T = tensors[task.tensor];
             DevTask next = task;   // next record's scalar load overlaps this task
             if (t + nwaves < ntasks) next = tasks[t + nwaves];
+            if constexpr (SPLIT && SCREEN && FAST && !TL) {
+                // whole-row tasks in two row batches, the first stored while the
+                // second's loads land (compute_task_split)
+                if (task.nrows > 0 && compute_task_split<MAXROWS, NT, ESPEC>(T, task, wl, ls, lmn, lane)) {
+                    task = next;
+                    continue;
+                }
+            }
             vm_wait_all();
             if constexpr (TL) tl1 = wall_clock64();
             wave_lds_sync();
@@ -1217,7 +1383,7 @@ static MainKernel main_kernel(int variant) {
 #define DFQ_V(i) kVariants[i].chunk, kVariants[i].max_rows, kVariants[i].prefetch
 #ifndef DFQ_DIAGNOSTICS
     (void)variant;   // the product library carries the default variant only
-    return sweep_main_kernel<DFQ_V(kDefaultVariant), true, 1>;
+    return sweep_main_kernel<DFQ_V(kDefaultVariant), true, 1, false, true, true, kDefaultVariant == 16>;
 #else
     switch (variant) {
         case 1: return sweep_main_kernel<DFQ_V(1)>;
@@ -1235,6 +1401,7 @@ static MainKernel main_kernel(int variant) {
         case 13: return sweep_main_kernel<DFQ_V(13), true, 1, true>;
         case 14: return sweep_main_kernel<DFQ_V(14), true, 1, false, false>;
         case 15: return sweep_main_kernel<DFQ_V(15), true, 1, false, true, false>;
+        case 16: return sweep_main_kernel<DFQ_V(16), true, 1, false, true, true, true>;
         default: return sweep_main_kernel<DFQ_V(0)>;
     }
 #endif
