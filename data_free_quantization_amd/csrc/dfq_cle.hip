@@ -10,6 +10,7 @@
 #include "dfq_cle_common.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -1621,6 +1622,7 @@ struct CleDeviceCtx {
     char* h_pool = nullptr;
     size_t hpool_cap = 0;
     bool pool_busy = false;
+    uint64_t pool_struct = 0;                      // CleStructure::id whose address-free tables the pool holds
     hipEvent_t pool_ev = nullptr;                  // behind the last upload from h_pool
     double* d_hist = nullptr;                      // histories longer than the tables' kCleHistCap
     int64_t hist_cap = 0;
@@ -1723,7 +1725,9 @@ struct CleStructure {
     // element: W and the snapshot read, the snapshot written) and the range tasks
     // that read weights (4 B per element; self ranges are free)
     int64_t bytes_rescale = 0, bytes_metric = 0, bytes_range = 0;
+    uint64_t id = 0;   // unique per built structure: the device pool remembers whose tables it holds
 };
+static std::atomic<uint64_t> g_struct_ids{0};
 
 static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, float* const* targets,
                                const int64_t* target_n, int32_t n_targets, int32_t ref_threads, CleStructure& S) {
@@ -2174,6 +2178,7 @@ static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, 
     S.nlaunch = nlaunch;
     S.stop_off = stop_off;
     S.lagged = lagged;
+    S.id = ++g_struct_ids;
     for (const CleTask& tk : S.at) {
         const CleRel& q = S.R[tk.rel];
         const int64_t n = tk.b - tk.a;
@@ -2441,6 +2446,7 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
                 (void)hipFree(ctx.d_pool);
                 ctx.d_pool = nullptr;
                 ctx.pool_cap = 0;
+                ctx.pool_struct = 0;
                 const size_t cap = (size_t)T.total + (size_t)T.total / 2;
                 if ((e = hipMalloc(&ctx.d_pool, cap)) == hipSuccess) ctx.pool_cap = cap;
             }
@@ -2461,21 +2467,27 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         if (e != hipSuccess) return fail(e);
     }
     std::vector<char> blob;
+    // The pool already holding this structure's address-free tables (tasks,
+    // chunks, units, level-1 offsets, layer sizes: a plan of the same structure
+    // came before, and the tables are read-only on the device): only the records
+    // that carry addresses -- relations and layers -- are written and uploaded.
+    const bool resident = p->pooled && ctx.pool_struct == S->id;
     if (!p->pooled) {
         if ((e = hipMalloc(&p->d_tables, T.total)) != hipSuccess) return fail(e);
         base = static_cast<char*>(p->d_tables);
         blob.assign(host_bytes, 0);
         hblob = blob.data();
-    } else {
+    } else if (!resident) {
         std::memset(hblob, 0, host_bytes);
     }
     const double tm1 = now_us();
     auto put = [&](int64_t off, const auto& v) {
         if (!v.empty()) std::memcpy(hblob + off, v.data(), sizeof(v[0]) * v.size());
     };
-    put(o_rels, Rb); put(o_rt, rt); put(o_at, at); put(o_layers, layers); put(o_chunks, chunks); put(o_units, units);
-    put(o_b1off, b1off);
-    {
+    put(o_rels, Rb);
+    put(o_layers, layers);
+    if (!resident) {
+        put(o_rt, rt); put(o_at, at); put(o_chunks, chunks); put(o_units, units); put(o_b1off, b1off);
         float* lm = reinterpret_cast<float*>(hblob + o_part) + (int64_t)p->slots * n_targets;
         for (int64_t l = 0; l < n_targets; ++l) {
             lm[2 * l] = (float)layers[l].n;
@@ -2483,8 +2495,18 @@ extern "C" int dfq_cle_plan_create(const dfq_cle_rel* rels, int32_t n_rel, float
         }
     }
     if (p->pooled) {   // async on the loop stream, which every launch of the plan uses
-        if ((e = hipMemcpyAsync(base, hblob, host_bytes, hipMemcpyHostToDevice, ctx.st)) != hipSuccess) return fail(e);
+        if (resident) {
+            const size_t nr = sizeof(CleRel) * Rb.size(), nly = sizeof(CleLayer) * layers.size();
+            if (nr && (e = hipMemcpyAsync(base + o_rels, hblob + o_rels, nr, hipMemcpyHostToDevice, ctx.st)) != hipSuccess)
+                return fail(e);
+            if (nly && (e = hipMemcpyAsync(base + o_layers, hblob + o_layers, nly, hipMemcpyHostToDevice, ctx.st)) !=
+                           hipSuccess)
+                return fail(e);
+        } else if ((e = hipMemcpyAsync(base, hblob, host_bytes, hipMemcpyHostToDevice, ctx.st)) != hipSuccess) {
+            return fail(e);
+        }
         if ((e = hipEventRecord(ctx.pool_ev, ctx.st)) != hipSuccess) return fail(e);
+        ctx.pool_struct = S->id;
     } else if ((e = hipMemcpy(base, hblob, host_bytes, hipMemcpyHostToDevice)) != hipSuccess) {
         return fail(e);
     }
@@ -3233,6 +3255,7 @@ hipError_t preload_cle() {   // see dfq_preload
             (void)hipFree(ctx.d_pool);
             ctx.d_pool = nullptr;
             ctx.pool_cap = 0;
+            ctx.pool_struct = 0;
             if ((e0 = hipMalloc(&ctx.d_pool, kClePreloadPool)) != hipSuccess) return e0;
             ctx.pool_cap = kClePreloadPool;
         }
