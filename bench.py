@@ -73,7 +73,7 @@ def parse(argv=None):
     p.add_argument("--prewarm-ms", type=float, default=600.0,
                    help="time-based pre-warm (ms of sweep steps) before the counted warm-up: a fresh lease starts "
                         "at idle clocks (0 = none)")
-    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r05.json"),
+    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_r06.json"),
                    help="the committed rocprofv3 summary of this bench command (scripts/profile.sh + "
                         "scripts/summarize_profile.py): PMC traffic and the kernel's rocprof average")
     p.add_argument("--no-sharded", action="store_true",
