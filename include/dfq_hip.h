@@ -295,6 +295,11 @@ int dfq_cle_plan_run(dfq_cle_plan* plan, double threshold, int32_t count, int32_
  * caller's thread goes on enqueueing the next stages meanwhile (the caller's
  * stream waits behind a one-wave gate kernel that polls the library's signal
  * word; it gives up after 120 s, and the join then reports the run failed).
+ * A launched run is time-bounded: it stops enqueueing iterations 60 s after the
+ * launch, releases the caller's stream and reports the run failed at join (the
+ * stages queued behind it then ran on partially equalized weights, so the join's
+ * error must not be ignored); a blocking run (dfq_cle_plan_run) has no time
+ * bound and stops at max_iters.
  * One launched plan per device at a time (a launch first joins the previous one).
  * DFQ_ERR_UNSUPPORTED: the device cannot make a stream wait on a value (run
  * dfq_cle_plan_run instead). */
