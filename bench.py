@@ -1266,6 +1266,10 @@ def main(argv=None):
                 "variant": st["variant"],
                 "rank": 0,
                 "launch_ms_per_rank": rank_launch_ms,
+                # the whole job: every rank's algorithmic bytes over the slowest rank's launch
+                "job_achieved": round(sum(rank_algo) / (max(rank_launch_ms) / 1e3) / 1e9, 1),
+                "job_frac_of_n_gpus": round(sum(rank_algo) / (max(rank_launch_ms) / 1e3) / 1e9
+                                            / (HBM_PEAK_GBS * world), 4),
                 "traffic_source": ("PMC FETCH_SIZE (x2, the gfx950 correction) + WRITE_SIZE per launch from "
                                    f"{prof['source']}: separate rocprofv3 --pmc passes over this bench command, "
                                    "not measured in this run") if prof else None,
