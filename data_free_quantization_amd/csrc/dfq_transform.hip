@@ -599,6 +599,85 @@ fq_given_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, i
     }
 }
 
+// ---------------------------------------------------------------------------
+// The Quant* layers' weight / bias fake quant in one call (dfq_fake_quant_tensor):
+// y = quantize(x, b, float(x.min()), float(x.max())) -- the given-range fake quant
+// of fq_given_kernel on the tensor's own range, without the fill and the separate
+// range launch of dfq_range.  words[8]: caller scratch, zero once; every call leaves
+// it armed again.
+// ---------------------------------------------------------------------------
+constexpr int64_t kFqSmall = 16384;   // one workgroup does range and fake quant
+
+// One workgroup: the range (fminf / fmaxf, as range_enc_kernel), then the fake quant.
+__global__ void __launch_bounds__(kThreads)
+fq_tensor_small_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, int bits, int sym, int flags) {
+    __shared__ float smn[kThreads / kWave], smx[kThreads / kWave];
+    float a = INFINITY, b = -INFINITY;
+    for (int64_t i = threadIdx.x; i < n; i += kThreads) {
+        const float v = x[i];
+        a = fminf(a, v);
+        b = fmaxf(b, v);
+    }
+    a = wave_min(a);
+    b = wave_max(b);
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+    if (lane == 0) {
+        smn[w] = a;
+        smx[w] = b;
+    }
+    __syncthreads();
+    for (int k = 0; k < kThreads / kWave; ++k) {   // every thread combines (same order as thread 0's)
+        a = k ? fminf(a, smn[k]) : smn[0];
+        b = k ? fmaxf(b, smx[k]) : smx[0];
+    }
+    // the range as dfq_range's encoding would give it back (the same float, read as a double)
+    const double gmin = (double)dec_ord(~(~enc_ord(a))), gmax = (double)dec_ord(enc_ord(b));
+    const QParams p = make_qparams((float)gmin, (float)gmax, bits, sym != 0, flags | DFQ_GIVEN_RANGE, gmin, gmax);
+    float q;
+    for (int64_t i = threadIdx.x; i < n; i += kThreads) y[i] = qdq_nan(x[i], p, q);
+}
+
+// Range launch of large tensors: range_enc_kernel's accumulation into words[0..1];
+// each block's atomics return before its arrival on words[2] (returning atomics:
+// the wave waits for them), and the last block to arrive takes the range with
+// atomic exchanges (re-arming words[0..1]), publishes it in words[4..5] for the
+// fake-quant launch and re-arms the counter.
+__global__ void __launch_bounds__(kThreads)
+fq_tensor_range_kernel(const float* __restrict__ x, int64_t n, uint32_t* __restrict__ words) {
+    __shared__ float smn[kThreads / kWave], smx[kThreads / kWave];
+    float a = INFINITY, b = -INFINITY;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        a = fminf(a, v);
+        b = fmaxf(b, v);
+    }
+    a = wave_min(a);
+    b = wave_max(b);
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+    if (lane == 0) {
+        smn[w] = a;
+        smx[w] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kThreads / kWave; ++k) {
+            a = fminf(a, smn[k]);
+            b = fmaxf(b, smx[k]);
+        }
+        const uint32_t o0 = __hip_atomic_fetch_max(&words[0], ~enc_ord(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t o1 = __hip_atomic_fetch_max(&words[1], enc_ord(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(o0), "v"(o1) : "memory");   // both performed before the arrival
+        const uint32_t last = gridDim.x - 1;
+        if (__hip_atomic_fetch_add(&words[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == last) {
+            const uint32_t r0 = __hip_atomic_exchange(&words[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t r1 = __hip_atomic_exchange(&words[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            words[4] = r0;
+            words[5] = r1;
+            __hip_atomic_exchange(&words[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // Whole-tensor (min, max) as order-preserving uints: {max ~enc(x), max enc(x)}, so
 // one zero memset initialises both words (exact, order-independent).
 __global__ void __launch_bounds__(kThreads)
@@ -1465,6 +1544,30 @@ extern "C" int dfq_range(const float* x, int64_t n, uint32_t* range_enc, void* s
     DFQ_HIP_CHECK(hipMemsetAsync(range_enc, 0, 2 * sizeof(uint32_t), s));
     const int grid = (int)std::min<int64_t>(ceil_div(n, (int64_t)kThreads * 8), 2048);
     hipLaunchKernelGGL(range_enc_kernel, dim3(std::max(grid, 1)), dim3(kThreads), 0, s, x, n, range_enc);
+    DFQ_LAUNCH_CHECK();
+    return DFQ_OK;
+}
+
+extern "C" int dfq_fake_quant_tensor(const float* x, float* y, int64_t n, int32_t bits, int32_t symmetric,
+                                     int32_t flags, uint32_t* words, void* stream) {
+    if (n < 1 || !x || !y || bits < 2 || bits > 16) return DFQ_ERR_INVALID;
+    if (flags & ~(DFQ_SCALE_F32)) return DFQ_ERR_INVALID;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (n <= kFqSmall) {
+        hipLaunchKernelGGL(fq_tensor_small_kernel, dim3(1), dim3(kThreads), 0, s, x, y, n, bits, symmetric, flags);
+        DFQ_LAUNCH_CHECK();
+        return DFQ_OK;
+    }
+    if (!words) return DFQ_ERR_INVALID;
+    const int grid = (int)std::min<int64_t>(ceil_div(n, (int64_t)kThreads * 8), 2048);
+    hipLaunchKernelGGL(fq_tensor_range_kernel, dim3(std::max(grid, 1)), dim3(kThreads), 0, s, x, n, words);
+    DFQ_LAUNCH_CHECK();
+    const int vec4 = (n % 4 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
+                     (reinterpret_cast<uintptr_t>(y) % 16 == 0);
+    const int64_t work = vec4 ? n / 4 : n;
+    const int g2 = (int)std::min<int64_t>(ceil_div(work, (int64_t)kThreads * 4), 16384);
+    hipLaunchKernelGGL(fq_given_kernel, dim3(std::max(g2, 1)), dim3(kThreads), 0, s, x, y, n, bits, symmetric, flags,
+                       nullptr, nullptr, static_cast<const uint32_t*>(words + 4), 0.0, 0.0, vec4);
     DFQ_LAUNCH_CHECK();
     return DFQ_OK;
 }

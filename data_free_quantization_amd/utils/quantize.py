@@ -223,6 +223,26 @@ def fake_quant_given(x: torch.Tensor, num_bits: int = 8, symmetric: bool = False
     return y
 
 
+def fake_quant_tensor(x: torch.Tensor, num_bits: int = 8, symmetric: bool = False, *, scale_f32: bool = False,
+                      words: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """quantize(x, num_bits, float(x.min()), float(x.max()), symmetric=...) -- the
+    Quant* layers' weight fake quant (utils/quantize.py:225-238; ``scale_f32`` for
+    the bias's 0-d bounds) -- as ONE library call (dfq_fake_quant_tensor): the range
+    and the fake quant without a fill or a host read.  ``words``: 8 int32 of device
+    scratch, zeroed once and reused by the caller's later calls on the same stream
+    (needed above 16,384 elements)."""
+    _lib.require_device(x, out)
+    xc = x.detach().contiguous()
+    y = torch.empty_like(xc) if out is None else out
+    if words is None and xc.numel() > 16384:
+        words = torch.zeros(8, dtype=torch.int32, device=xc.device)
+    rc = _lib.load().dfq_fake_quant_tensor(_lib.ptr(xc), _lib.ptr(y), xc.numel(), int(num_bits), int(bool(symmetric)),
+                                           _lib.DFQ_SCALE_F32 if scale_f32 else 0, _lib.ptr(words),
+                                           _lib.stream_of(xc))
+    _lib.check(rc, "dfq_fake_quant_tensor", ValueError)
+    return y
+
+
 def quantize(x, num_bits=8, min_value=None, max_value=None, inplace=False, symmetric=False, num_chunks=None):
     """utils/quantize.py:88-89."""
     return UniformQuantize.apply(x, num_bits, min_value, max_value, inplace, symmetric, num_chunks)
@@ -361,10 +381,17 @@ class _QuantWeightMixin:
                 hit = self.__dict__.get("_qw_cache")
                 if hit is not None and hit[0] == key:
                     return hit[1], hit[2]
-            qweight = fake_quant_given(weight, self.num_bits, range_enc=device_range(weight))
+            # the tensor's range and its fake quant in one library call each (the
+            # range words: this module's scratch per stream, re-armed by every call)
+            stream = _lib.stream_of(weight)
+            bufs = self.__dict__.setdefault("_fq_words", {})
+            words = bufs.get((weight.device, stream.value))
+            if words is None:
+                words = bufs[(weight.device, stream.value)] = torch.zeros(16, dtype=torch.int32, device=weight.device)
+            qweight = fake_quant_tensor(weight, self.num_bits, words=words[:8])
             qbias = None
             if bias is not None:
-                qbias = fake_quant_given(bias, self.num_bits_bias, range_enc=device_range(bias), scale_f32=True)
+                qbias = fake_quant_tensor(bias, self.num_bits_bias, scale_f32=True, words=words[8:])
             if cacheable:
                 self.__dict__["_qw_cache"] = (key, qweight, qbias)
             else:

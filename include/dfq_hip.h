@@ -156,6 +156,17 @@ int dfq_fake_quant_given(const float* x, float* y, int64_t n, int32_t bits, int3
                          const float* min_dev, const float* max_dev, const uint32_t* range_enc, double given_min,
                          double given_max, void* stream);
 
+/* quantize(x, bits, float(x.min()), float(x.max()), symmetric) -- the Quant* layers'
+ * weight / bias fake quant (utils/quantize.py:225-238) on the tensor's own range --
+ * in one async call: dfq_range + dfq_fake_quant_given without the fill.  n <= 16384:
+ * one workgroup, one launch (words may be NULL); larger: a range launch whose last
+ * block publishes the range and re-arms `words`, then the elementwise launch.
+ * words: 8 device uint32 of caller scratch, zero when allocated, left armed by every
+ * call (one set per stream: calls on two streams must not share it).  flags: 0 or
+ * DFQ_SCALE_F32, as dfq_fake_quant_given. */
+int dfq_fake_quant_tensor(const float* x, float* y, int64_t n, int32_t bits, int32_t symmetric, int32_t flags,
+                          uint32_t* words, void* stream);
+
 /* ---- grouped sweep over many tensors (replaces quantize_targ_layer,
  *      utils/layer_transform.py:288-305, fused with clip_weight.py:4-33 and the
  *      bias-correction error reduction bias_correction.py:111-144,231) ------- */

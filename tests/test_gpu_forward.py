@@ -336,3 +336,24 @@ def test_fused_observer_propagates_nan(mode):
         assert torch.isnan(y).all()
     else:                    # range finite: only the NaN input stays NaN
         assert int(torch.isnan(y).sum()) == 1
+
+
+@pytest.mark.parametrize("n", [1, 17, 1000, 16384, 16385, 40000, 1 << 20, 2_400_000])
+def test_fake_quant_tensor_equals_range_then_given(n):
+    """dfq_fake_quant_tensor (range + fake quant in one call, self-re-arming words)
+    equals dfq_range + dfq_fake_quant_given bit for bit, for one-workgroup and
+    multi-block sizes, every mode, and over repeated calls on the same words."""
+    from data_free_quantization_amd.utils.quantize import device_range, fake_quant_given, fake_quant_tensor
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(n)
+    words = torch.zeros(8, dtype=torch.int32, device=dev)
+    for rep in range(3):
+        x = torch.randn(n, device=dev, generator=g) * (1 + rep)
+        if n > 4:
+            x[n // 2] = x[0] * 0.5   # a tie-ish value in range
+        for bits, sym, f32 in ((8, False, False), (4, True, False), (16, False, True), (8, True, True)):
+            ref = fake_quant_given(x, bits, sym, range_enc=device_range(x), scale_f32=f32)
+            got = fake_quant_tensor(x, bits, sym, scale_f32=f32, words=words)
+            torch.cuda.synchronize()
+            assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), (n, rep, bits, sym, f32)
+    assert int(words[:3].abs().sum()) == 0   # re-armed (the published range stays in words[4:6])
