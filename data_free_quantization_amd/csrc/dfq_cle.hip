@@ -131,6 +131,9 @@ __device__ __forceinline__ void for_short_rows(int64_t a, int64_t b, int64_t len
     }
 }
 constexpr int64_t kCleChansPerTask = 1024;
+// rescale tasks: rows_per_task rows (one per wave) times these factors for W1 rows
+// and depthwise pairs (diagnostics switches DFQ_CLE_W1_ROWS / DFQ_CLE_DW_ROWS)
+constexpr int64_t kCleW1RowsMult = 1, kCleDwRowsMult = 1;
 
 // min / max of n floats at p, one wave, 4 loads in flight per lane
 __device__ __forceinline__ void wave_range(const float* __restrict__ p_, int64_t n, bool vec, int lane, float& vmin,
@@ -1847,13 +1850,23 @@ static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, 
                 rout->push_back({r, kRangeW1, a, std::min<int64_t>(a + k, c.c1), 0, 0});
         }
     };
+    // rows per W1 / depthwise-pair rescale task: rows_per_task (one row per wave)
+    // times a factor (diagnostics A/B: DFQ_CLE_W1_ROWS / DFQ_CLE_DW_ROWS)
+    const int64_t w1_mult = [] {
+        const char* e = ab_env("DFQ_CLE_W1_ROWS");
+        return e && *e ? std::max<int64_t>(1, atoll(e)) : kCleW1RowsMult;
+    }();
+    const int64_t dw_mult = [] {
+        const char* e = ab_env("DFQ_CLE_DW_ROWS");
+        return e && *e ? std::max<int64_t>(1, atoll(e)) : kCleDwRowsMult;
+    }();
     auto apply_tasks = [&](int32_t r, std::vector<CleTask>& out) {
         const CleRel& c = R[r];
         if (c.dw_prev < 0)   // else the predecessor's kApplyDwBoth rescales this W1
-            for (int64_t a = 0, k = rows_per_task(c.len1); a < c.c1; a += k)
+            for (int64_t a = 0, k = w1_mult * rows_per_task(c.len1); a < c.c1; a += k)
                 out.push_back({r, kApplyW1, a, std::min<int64_t>(a + k, c.c1), 0, 0});
         if (dw_next[r] >= 0) {
-            for (int64_t a = 0, k = rows_per_task(c.o2g * c.khw2); a < c.c1; a += k)
+            for (int64_t a = 0, k = dw_mult * rows_per_task(c.o2g * c.khw2); a < c.c1; a += k)
                 out.push_back({r, kApplyDwBoth, a, std::min<int64_t>(a + k, c.c1), dw_next[r], 0});
         } else if (c.i2 == 1) {
             for (int64_t a = 0, k = rows_per_task(c.o2g * c.khw2); a < c.c1; a += k)
@@ -2239,7 +2252,8 @@ static std::vector<int64_t> cle_structure_key(const std::vector<CleRel>& R, int6
     key.push_back(M);
     key.push_back(n_targets);
     key.push_back(ref_threads);
-    for (const char* sw : {"DFQ_CLE_FUSED", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_STOP"}) {   // diagnostics library only
+    for (const char* sw : {"DFQ_CLE_FUSED", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_STOP",
+                           "DFQ_CLE_W1_ROWS", "DFQ_CLE_DW_ROWS"}) {   // diagnostics library only
         const char* v = ab_env(sw);
         int64_t h = v ? 1 : 0;
         for (int k = 0; v && v[k] && k < 8; ++k) h = h * 131 + (unsigned char)v[k];

@@ -22,6 +22,7 @@ sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_STOP",
+            "DFQ_CLE_W1_ROWS", "DFQ_CLE_DW_ROWS",
             "CLE_AB_BLOCKING")
 CONFIGS = {
     "tiles_fin": {},                                # the product (lagged schedule where the plan allows it)
@@ -34,6 +35,12 @@ CONFIGS = {
     "band1": {"DFQ_CLE_BAND": "1"},                 # the tiles' band start (lagged schedule)
     "band2": {"DFQ_CLE_BAND": "2"},
     "blocking": {"CLE_AB_BLOCKING": "1"},           # run_dfq's CLE blocking (no caller gate beside the loop)
+    # round 6: rows per W1 / depthwise-pair rescale task (x one row per wave)
+    "w1x2": {"DFQ_CLE_W1_ROWS": "2"},
+    "w1x4": {"DFQ_CLE_W1_ROWS": "4"},
+    "w1x8": {"DFQ_CLE_W1_ROWS": "8"},
+    "dwx2": {"DFQ_CLE_DW_ROWS": "2"},
+    "w1x4_dwx2": {"DFQ_CLE_W1_ROWS": "4", "DFQ_CLE_DW_ROWS": "2"},
 }
 
 
