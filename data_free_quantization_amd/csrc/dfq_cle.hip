@@ -131,9 +131,13 @@ __device__ __forceinline__ void for_short_rows(int64_t a, int64_t b, int64_t len
     }
 }
 constexpr int64_t kCleChansPerTask = 1024;
-// rescale tasks: rows_per_task rows (one per wave) times these factors for W1 rows
-// and depthwise pairs (diagnostics switches DFQ_CLE_W1_ROWS / DFQ_CLE_DW_ROWS)
-constexpr int64_t kCleW1RowsMult = 1, kCleDwRowsMult = 1;
+// Rescale tasks hold rows_per_task rows (one per wave).  W1 tasks of short rows
+// (under kCleW1SmallElems elements per task: MobileNetV2's expand convs) take twice
+// that: step 0 of MobileNetV2 had 1,648 W1 tasks of ~2 us in 2,433 blocks, more than
+// are resident, so its last blocks started 8.7 us into the launch
+// (profiles/r06/cle_tl_r06h.log); A/B profiles/r06/cle_ab_rows_r06i.jsonl.
+// Diagnostics switches: DFQ_CLE_W1_ROWS (a fixed factor) / DFQ_CLE_DW_ROWS.
+constexpr int64_t kCleW1SmallElems = 1024, kCleDwRowsMult = 1;
 
 // min / max of n floats at p, one wave, 4 loads in flight per lane
 __device__ __forceinline__ void wave_range(const float* __restrict__ p_, int64_t n, bool vec, int lane, float& vmin,
@@ -1852,10 +1856,16 @@ static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, 
     };
     // rows per W1 / depthwise-pair rescale task: rows_per_task (one row per wave)
     // times a factor (diagnostics A/B: DFQ_CLE_W1_ROWS / DFQ_CLE_DW_ROWS)
+    // 0: the default rule (twice the rows for tasks of short rows, below)
     const int64_t w1_mult = [] {
         const char* e = ab_env("DFQ_CLE_W1_ROWS");
-        return e && *e ? std::max<int64_t>(1, atoll(e)) : kCleW1RowsMult;
+        return e && *e ? std::max<int64_t>(1, atoll(e)) : int64_t(0);
     }();
+    auto w1_rows = [&](int64_t len1) {
+        const int64_t k = rows_per_task(len1);
+        if (w1_mult > 0) return w1_mult * k;
+        return k * len1 < kCleW1SmallElems ? 2 * k : k;
+    };
     const int64_t dw_mult = [] {
         const char* e = ab_env("DFQ_CLE_DW_ROWS");
         return e && *e ? std::max<int64_t>(1, atoll(e)) : kCleDwRowsMult;
@@ -1863,7 +1873,7 @@ static int cle_build_structure(std::vector<CleRel> R, int64_t M, int32_t n_rel, 
     auto apply_tasks = [&](int32_t r, std::vector<CleTask>& out) {
         const CleRel& c = R[r];
         if (c.dw_prev < 0)   // else the predecessor's kApplyDwBoth rescales this W1
-            for (int64_t a = 0, k = w1_mult * rows_per_task(c.len1); a < c.c1; a += k)
+            for (int64_t a = 0, k = w1_rows(c.len1); a < c.c1; a += k)
                 out.push_back({r, kApplyW1, a, std::min<int64_t>(a + k, c.c1), 0, 0});
         if (dw_next[r] >= 0) {
             for (int64_t a = 0, k = dw_mult * rows_per_task(c.o2g * c.khw2); a < c.c1; a += k)

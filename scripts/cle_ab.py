@@ -36,6 +36,7 @@ CONFIGS = {
     "band2": {"DFQ_CLE_BAND": "2"},
     "blocking": {"CLE_AB_BLOCKING": "1"},           # run_dfq's CLE blocking (no caller gate beside the loop)
     # round 6: rows per W1 / depthwise-pair rescale task (x one row per wave)
+    "w1x1": {"DFQ_CLE_W1_ROWS": "1"},               # round 5: one row per wave in every W1 task
     "w1x2": {"DFQ_CLE_W1_ROWS": "2"},
     "w1x4": {"DFQ_CLE_W1_ROWS": "4"},
     "w1x8": {"DFQ_CLE_W1_ROWS": "8"},
