@@ -137,7 +137,7 @@ constexpr int64_t kCleChansPerTask = 1024;
 // are resident, so its last blocks started 8.7 us into the launch
 // (profiles/r06/cle_tl_r06h.log); A/B profiles/r06/cle_ab_rows_r06i.jsonl.
 // Diagnostics switches: DFQ_CLE_W1_ROWS (a fixed factor) / DFQ_CLE_DW_ROWS.
-constexpr int64_t kCleW1SmallElems = 1024, kCleDwRowsMult = 1;
+constexpr int64_t kCleW1SmallElems = 2048, kCleDwRowsMult = 1;
 
 // min / max of n floats at p, one wave, 4 loads in flight per lane
 __device__ __forceinline__ void wave_range(const float* __restrict__ p_, int64_t n, bool vec, int lane, float& vmin,
