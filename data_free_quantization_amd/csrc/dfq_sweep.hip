@@ -1373,6 +1373,11 @@ static int variant_from_env() {
 }
 
 
+// Small lists (see build_planned) run variant 10's 1,536-element tasks; one round
+// of resident sweep blocks on the 256-CU part is 4 per CU.
+constexpr int kSmallVariant = 10;
+constexpr int64_t kResidentBlocks = 4 * 256;
+
 static int lds_bytes(const Variant& V) {
     return 4 * kWavesPerBlock * ((V.prefetch ? 2 : 1) * V.chunk + 3 * V.max_rows);
 }
@@ -1382,7 +1387,8 @@ using MainKernel = void (*)(const DevTensor*, const DevTask*, int64_t, const uin
 static MainKernel main_kernel(int variant) {
 #define DFQ_V(i) kVariants[i].chunk, kVariants[i].max_rows, kVariants[i].prefetch
 #ifndef DFQ_DIAGNOSTICS
-    (void)variant;   // the product library carries the default variant only
+    // the product library carries the default variant and the small-list one
+    if (variant == kSmallVariant) return sweep_main_kernel<DFQ_V(kSmallVariant), true, 1>;
     return sweep_main_kernel<DFQ_V(kDefaultVariant), true, 1, false, true, true, kDefaultVariant == 16>;
 #else
     switch (variant) {
@@ -1466,10 +1472,34 @@ static PlanLayout plan_layout(const Built& B, int64_t n) {
 }
 }  // namespace dfq
 
+// The plan's kernel variant and task table.  A diagnostics DFQ_SWEEP_VARIANT wins.
+// Otherwise the default variant's 2,048-element tasks, unless the list is small
+// enough that 1,536-element tasks (variant 10) still fit in ONE round of resident
+// blocks (4 per CU at 97 VGPRs): a one-round grid of range-dependent tasks is
+// latency-bound, and 4/3 as many waves hide more of it (MobileNetV2 single model:
+// 560 -> 747 blocks).  Lists past one round keep 2,048 (DeepLab's single model at
+// 1,536 needs 1,123 blocks and measured 12.0 against 9.2 us; profiles/r06/chunk_rule_ab_r06o.jsonl).
+static int build_planned(const dfq_tensor_desc* descs, int32_t n, Built& B, int& variant) {
+    const char* e = ab_env("DFQ_SWEEP_VARIANT");
+    variant = variant_from_env();
+    if (int rc = build(descs, n, B, kVariants[variant])) return rc;
+    if ((e && *e) || variant != kDefaultVariant || kDefaultVariant != 6) return DFQ_OK;
+    const int64_t limit = kResidentBlocks;
+    const int64_t blocks = ceil_div((int64_t)B.main.size(), (int64_t)kWavesPerBlock);
+    if (B.main.empty() || 4 * blocks > 3 * limit) return DFQ_OK;   // 4/3 the tasks would not fit one round
+    Built S;
+    if (build(descs, n, S, kVariants[kSmallVariant]) != DFQ_OK) return DFQ_OK;
+    if (ceil_div((int64_t)S.main.size(), (int64_t)kWavesPerBlock) > limit) return DFQ_OK;
+    B = std::move(S);
+    variant = kSmallVariant;
+    return DFQ_OK;
+}
+
 extern "C" int64_t dfq_sweep_plan_ws_bytes(const dfq_tensor_desc* descs, int32_t n) {
     if ((n > 0 && !descs) || n < 0) return -1;
     Built B;
-    if (build(descs, n, B, kVariants[variant_from_env()])) return -1;
+    int variant = 0;
+    if (build_planned(descs, n, B, variant)) return -1;
     return plan_layout(B, n).total;
 }
 
@@ -1480,9 +1510,9 @@ static int sweep_plan_create_impl(const dfq_tensor_desc* descs, int32_t n, void*
                                   hipStream_t stream, dfq_sweep_plan** out) {
     if (!out || (n > 0 && !descs) || n < 0) return DFQ_ERR_INVALID;
     *out = nullptr;
-    const int variant = variant_from_env();
+    int variant = 0;
     Built B;
-    int rc = build(descs, n, B, kVariants[variant]);
+    int rc = build_planned(descs, n, B, variant);
     if (rc) return rc;
     const PlanLayout Lo = plan_layout(B, n);
     if (ws && (ws_bytes < Lo.total || reinterpret_cast<uintptr_t>(ws) % 256 != 0)) return DFQ_ERR_WORKSPACE;
