@@ -3347,6 +3347,42 @@ extern "C" int dfq_diag_cle_check_structure(const dfq_cle_rel* rels, int32_t n_r
         return rc;
     const std::vector<CleRel>& R = S.R;
     const int32_t steps = S.steps, NL = S.nlaunch;
+    if (const char* e = getenv("DFQ_CLE_PLACE_DUMP"); e && *e) {
+        // per launch offset: blocks and bytes of rescale tasks, metric tiles and range tasks
+        fprintf(stderr, "DFQ_CLE_PLACE steps %d nlaunch %d lagged %d stop_off %d\n", steps, NL, (int)S.lagged,
+                S.stop_off);
+        for (int32_t k = 0; k < 2 * NL; ++k) {
+            int64_t na = 0;
+            double ba = 0;
+            if (k < steps)
+                for (int64_t t = S.astep[k]; t < S.astep[k + 1]; ++t, ++na) {
+                    const CleTask& tk = S.at[t];
+                    const CleRel& q = R[tk.rel];
+                    const int64_t n = tk.b - tk.a;
+                    if (tk.kind == kApplyW1) ba += 8.0 * n * q.len1;
+                    else if (tk.kind == kApplyW2Tile) ba += 8.0 * n * (tk.c1 - tk.c0) * q.khw2;
+                    else if (tk.kind != kApplyChannels) ba += 8.0 * n * q.o2g * q.khw2;
+                }
+            double bu = 0;
+            for (int64_t u = S.uoffs[k]; u < S.uoffs[k + 1]; ++u) {
+                const CleChunk& ch = S.chunks[S.units[u].chunk];
+                const int64_t nb1 = ch.len / kCleTile;
+                bu += 12.0 * (S.units[u].tile < nb1 ? kCleTile : ch.len - nb1 * kCleTile);
+            }
+            double br = 0;
+            for (int64_t t = S.roffs[k]; t < S.roffs[k + 1]; ++t) {
+                const CleTask& tk = S.rt[t];
+                const CleRel& q = R[tk.rel];
+                const int64_t n = tk.b - tk.a;
+                if (tk.kind == kRangeW1) br += 4.0 * n * q.len1;
+                else if (tk.kind == kRangeW2Contig) br += 4.0 * n * q.o2g * q.khw2;
+                else if (tk.kind == kRangeW2Tile) br += 4.0 * n * (tk.c1 - tk.c0) * q.khw2;
+            }
+            fprintf(stderr, "DFQ_CLE_PLACE offset %d: rescale %lld blocks %.2f MB, tiles %lld blocks %.2f MB, ranges %lld blocks %.2f MB\n",
+                    k, (long long)na, ba / 1e6, (long long)(S.uoffs[k + 1] - S.uoffs[k]), bu / 1e6,
+                    (long long)(S.roffs[k + 1] - S.roffs[k]), br / 1e6);
+        }
+    }
     if (info) {
         const int64_t v[8] = {steps, NL, S.lagged ? 1 : 0, S.stop_off, (int64_t)S.at.size(), (int64_t)S.rt.size(),
                               (int64_t)S.units.size(), (int64_t)S.chunks.size()};
