@@ -1376,6 +1376,18 @@ union CleStepLds {
     float tiles[kCleTilesLds > kCleRangeLds ? kCleTilesLds : kCleRangeLds];
 };
 
+// Block order of a step launch: metric tiles (the launch's longest blocks: 8,192
+// elements, 12 B each), rescale tasks, the stop rule, range tasks.  MobileNetV2's
+// first launch holds 1,994 blocks, about two rounds of resident ones; with the tiles
+// last they started in the second round and set the launch's tail.  CLE 2.27-2.29
+// against 2.39-2.40 ms, ResNet-50 (tiles in a launch of their own) unchanged
+// (profiles/r06/cle_ab_tiles_first_r06t/u.jsonl; tiles then ranges first: 2.36).
+// DFQ_CLE_TILES_FIRST=0 (diagnostics): the round-6 order, tiles after the stop rule.
+constexpr bool kCleTilesFirst = true;
+#ifdef DFQ_DIAGNOSTICS
+__device__ int g_cle_tiles_first = kCleTilesFirst ? 1 : 0;
+#endif
+
 // POS = false (no position-parallel 3x3 rescale tiles): capped at 128 VGPRs,
 // 4 waves per SIMD like the rescale body alone
 // (POS capped at 3 waves per SIMD -- 168 VGPRs, 124 B of spills -- measured slower:
@@ -1394,6 +1406,16 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
     __shared__ int flag;
     if (st->done) return;
     int64_t blk = blockIdx.x;
+#ifdef DFQ_DIAGNOSTICS
+    const bool tiles_first = g_cle_tiles_first != 0;   // DFQ_CLE_TILES_FIRST (A/B)
+#else
+    constexpr bool tiles_first = kCleTilesFirst;
+#endif
+    if (tiles_first) {   // block order: metric tiles, rescale tasks, the stop rule, ranges
+        const int64_t ns = nab + (stop_it >= 0 ? 1 : 0), ntl = nto + ntp;
+        if (blk < ntl) blk += ns;
+        else if (blk < ntl + ns) blk -= ntl;
+    }
     if (blk < nab) {   // this step's rescale tasks (iteration g)
         cle_apply_body<POS>(rels, atasks, a0, a1, rng, M, g & 1, g == 0, is_signed, eps, smin, smax, blk, nab, L.apply,
                             vsave, vtag, g);
@@ -2716,6 +2738,11 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
     uint64_t* d_tl2 = nullptr;  // ... and per block of the last launch
     const int64_t n_at = p->astep.empty() ? 0 : p->astep.back();
     const size_t n_tl2 = 4 * (size_t)(kCleTl2Fin + 1);
+    {
+        const char* e = ab_env("DFQ_CLE_TILES_FIRST");
+        const int tf = e && *e ? (e[0] == '1' ? 1 : 0) : (kCleTilesFirst ? 1 : 0);
+        DFQ_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cle_tiles_first), &tf, sizeof(tf), 0, hipMemcpyHostToDevice, s));
+    }
     if (ab_env("DFQ_CLE_TL") && n_at > 0) {
         DFQ_HIP_CHECK(hipMalloc(&d_tl, sizeof(uint64_t) * 4 * n_at));
         DFQ_HIP_CHECK(hipMemsetAsync(d_tl, 0, sizeof(uint64_t) * 4 * n_at, s));

@@ -22,7 +22,7 @@ sys.path.insert(0, str(ROOT))
 os.environ["DFQ_LIB"] = "diag"
 
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_STEP_GRID", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_STOP",
-            "DFQ_CLE_W1_ROWS", "DFQ_CLE_DW_ROWS",
+            "DFQ_CLE_W1_ROWS", "DFQ_CLE_DW_ROWS", "DFQ_CLE_TILES_FIRST",
             "CLE_AB_BLOCKING")
 CONFIGS = {
     "tiles_fin": {},                                # the product (lagged schedule where the plan allows it)
@@ -42,6 +42,8 @@ CONFIGS = {
     "w1x8": {"DFQ_CLE_W1_ROWS": "8"},
     "dwx2": {"DFQ_CLE_DW_ROWS": "2"},
     "w1x4_dwx2": {"DFQ_CLE_W1_ROWS": "4", "DFQ_CLE_DW_ROWS": "2"},
+    "tiles_first": {"DFQ_CLE_TILES_FIRST": "1"},   # metric tiles before the rescale tasks (the product)
+    "tiles_last": {"DFQ_CLE_TILES_FIRST": "0"},    # round 6 before: tiles after the rescale tasks
 }
 
 

@@ -43,7 +43,7 @@ sys.path.insert(0, os.environ["DFQ_ROOT"])
 from tests.parity import pipeline_mismatches
 from data_free_quantization_amd import Cross_layer_equal as cle
 SWITCHES = ("DFQ_CLE_FUSED", "DFQ_CLE_TILE_GRID", "DFQ_CLE_LAG", "DFQ_CLE_BAND", "DFQ_CLE_STOP",
-            "DFQ_CLE_TEST_POLL_DELAY_US")
+            "DFQ_CLE_TEST_POLL_DELAY_US", "DFQ_CLE_TILES_FIRST")
 CONFIGS = {
     "product": {},                                  # the product: lagged schedule where the plan allows it
     "unfused_steps": {"DFQ_CLE_FUSED": "0"},        # per-step range launches (graphs the fused schedule rejects)
@@ -52,6 +52,7 @@ CONFIGS = {
     "band1": {"DFQ_CLE_BAND": "1"},                 # lagged, the tiles' band forced
     "band2": {"DFQ_CLE_BAND": "2"},
     "stop_arrival": {"DFQ_CLE_STOP": "arrival"},    # lagged, the stop rule at the last tile arrival
+    "tiles_last": {"DFQ_CLE_TILES_FIRST": "0"},     # a launch's blocks in the earlier order (tiles after the rescales)
     # the host thread "descheduled" 300 us after every load of the stop rule's word,
     # then querying the stream: the queued iterations drain meanwhile (ADVICE r04's
     # stale-word race ended the loop early here)
@@ -85,7 +86,7 @@ def test_cle_schedules_equal_reference_with_oversized_range_grid():
     for name in ("mobilenetv2", "resnet50", "deeplab"):   # the A/B really switched paths
         la = {x["config"]: x["launches"] for x in res if x["model"] == name}
         assert la["unfused_steps"] > la["product"] > 1, (name, la)
-        assert la["tile_grid_64"] == la["product"] == la["band1"] == la["poll_delay"], (name, la)
+        assert la["tile_grid_64"] == la["product"] == la["band1"] == la["poll_delay"] == la["tiles_last"], (name, la)
         assert la["no_lag"] >= la["product"], (name, la)
     # MobileNetV2 takes the lagged schedule: one launch fewer per iteration
     la = {x["config"]: x["launches"] for x in res if x["model"] == "mobilenetv2"}
