@@ -537,6 +537,9 @@ __device__ uint64_t* g_cle_tl = nullptr;
 // {start, end, role (1 tile, 2 range), 0}; slot kCleTl2Fin: the stop rule's {start,
 // end, chunk sums staged, layer means done}
 __device__ uint64_t* g_cle_tl2 = nullptr;
+// DFQ_CLE_TL_STEP=k: record the blocks of step k's launches instead (the launch whose
+// rescale tasks start at table index g_cle_tl2_a0; -1: every launch, the last wins)
+__device__ int64_t g_cle_tl2_a0 = -1;
 constexpr int kCleTl2Fin = 8192;
 #endif
 
@@ -1423,7 +1426,7 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
     }
     blk -= nab;
 #ifdef DFQ_DIAGNOSTICS
-    const bool tl2 = g_cle_tl2 != nullptr && blk < kCleTl2Fin;
+    const bool tl2 = g_cle_tl2 != nullptr && blk < kCleTl2Fin && (g_cle_tl2_a0 < 0 || (a0 == g_cle_tl2_a0 && nab > 0));
     const uint64_t tl2_start = tl2 ? __builtin_amdgcn_s_memrealtime() : 0;
     auto tl2_rec = [&](int role) {
         if (tl2 && threadIdx.x == 0) {
@@ -2750,6 +2753,10 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
         DFQ_HIP_CHECK(hipMalloc(&d_tl2, sizeof(uint64_t) * n_tl2));
         DFQ_HIP_CHECK(hipMemsetAsync(d_tl2, 0, sizeof(uint64_t) * n_tl2, s));
         DFQ_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cle_tl2), &d_tl2, sizeof(d_tl2), 0, hipMemcpyHostToDevice, s));
+        const char* ek = ab_env("DFQ_CLE_TL_STEP");
+        const int kk = ek && *ek ? atoi(ek) : -1;
+        const int64_t a0v = (kk >= 0 && kk < p->steps) ? p->astep[kk] : -1;
+        DFQ_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cle_tl2_a0), &a0v, sizeof(a0v), 0, hipMemcpyHostToDevice, s));
         DFQ_HIP_CHECK(hipStreamSynchronize(s));
     }
 #endif
@@ -2864,7 +2871,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             uint64_t t0 = ~0ull;
             for (int b = 0; b < kCleTl2Fin; ++b)
                 if (tl2[4 * b]) t0 = std::min(t0, tl2[4 * b]);
-            fprintf(stderr, "DFQ_CLE_TL last launch:");
+            fprintf(stderr, "DFQ_CLE_TL last launch%s:", ab_env("DFQ_CLE_TL_STEP") ? " of DFQ_CLE_TL_STEP" : "");
             for (int role = 1; role <= 2; ++role) {
                 std::vector<double> st, en, du;
                 for (int b = 0; b < kCleTl2Fin; ++b) {
