@@ -107,12 +107,23 @@ def test_full_model_sweep_vs_oracle(model, mode):
     plan.destroy()
 
 
-def test_long_rows_and_odd_sizes_vs_oracle():
+def _filler(items):
+    """A 32 MiB per-tensor item appended to a small list: past one round of
+    resident blocks, so the plan takes the 2,048-element tasks (variant 6)
+    instead of the small-list 1,536 (variant 10)."""
+    from data_free_quantization_amd.sweep import allocate
+    items.append(allocate(torch.randn(2048, 4096, device=DEV), bits=8, per_channel=False, symmetric=False))
+
+
+@pytest.mark.parametrize("small", [True, False], ids=["small_list", "large_list"])
+def test_long_rows_and_odd_sizes_vs_oracle(small):
     """rows longer than one wave task (two-launch path), odd row lengths
-    (scalar path), empty tensors, a single element."""
+    (scalar path), empty tensors, a single element -- as a small list (1,536-element
+    tasks) and with a 2M-element tensor and a filler that make the list large (2,048)."""
     from data_free_quantization_amd.sweep import allocate, SweepPlan
     rng = np.random.default_rng(7)
-    shapes = [(3, 4608), (2, 20000), (7, 27), (5, 9), (1, 1), (33, 13), (0, 9), (513, 4100)]
+    shapes = [(3, 4608), (2, 20000), (7, 27), (5, 9), (1, 1), (33, 13), (0, 9)] + ([] if small else [(513, 4100)])
+    filler = not small
     items, xs = [], []
     for shp in shapes:
         x = rng.normal(0, 1, shp).astype(np.float32)
@@ -120,7 +131,10 @@ def test_long_rows_and_odd_sizes_vs_oracle():
         for mode in range(4):
             items.append(allocate(torch.from_numpy(x).to(DEV), bits=8, per_channel=mode >= 2,
                                   symmetric=mode in (1, 3), want_esum=True))
+    if filler:
+        _filler(items)
     plan = SweepPlan(items)
+    assert plan.stats["variant"] == (6 if filler else 10), plan.stats
     plan.execute()
     torch.cuda.synchronize()
     k = 0
@@ -137,10 +151,12 @@ def test_long_rows_and_odd_sizes_vs_oracle():
     plan.destroy()
 
 
-def test_block_row_pieces_vs_oracle():
+@pytest.mark.parametrize("filler", [False, True], ids=["small_list", "with_filler"])
+def test_block_row_pieces_vs_oracle(filler):
     """Rows of 2049..4 pieces (one workgroup, single HBM pass) and just past it
     (slot path), with KH*KW error sums; small per-tensor ranges (block path) next
-    to large ones (reduce launch); odd lengths (scalar loads)."""
+    to large ones (reduce launch); odd lengths (scalar loads).  Small list and
+    behind a filler (both task sizes, _filler)."""
     from data_free_quantization_amd.sweep import allocate, SweepPlan, khw_of
     rng = np.random.default_rng(11)
     shapes = [(4, 320, 3, 3), (2, 160, 7, 7), (2, 161, 7, 7), (3, 512, 3, 3), (3, 2051), (2, 8192), (2, 8193),
@@ -153,7 +169,10 @@ def test_block_row_pieces_vs_oracle():
             t = torch.from_numpy(x).to(DEV)
             items.append(allocate(t, bits=8 if mode != 1 else 5, per_channel=mode >= 2, symmetric=mode in (1, 3),
                                   khw=khw_of(t), want_esum=True, clip=(-1.0, 1.0) if mode == 3 else None))
+    if filler:
+        _filler(items)
     plan = SweepPlan(items)
+    assert plan.stats["variant"] == (6 if filler else 10), plan.stats
     for _ in range(2):
         plan.execute()
         torch.cuda.synchronize()
