@@ -68,3 +68,31 @@ def test_small_list_variant(lib):
     for x in res:
         assert x["variant"] == EXPECTED[tuple(x["case"][:2])], x
         assert x["diff_vs_v6"] == 0 and x["oracle_mismatches"] == 0 and x["tensors"] > 0, x
+
+
+def test_small_list_falls_back_when_the_small_tasks_cannot_hold_it():
+    """A small list holding a tensor whose KH*KW (40 x 40 = 1,600) exceeds the small
+    tasks' 1,536 elements: the 1,536 table cannot be built, so the plan keeps the
+    2,048-element tasks (variant 6), and the result matches the oracle."""
+    import numpy as np
+    import torch
+    from oracle import oracle as O
+    from data_free_quantization_amd.sweep import SweepPlan, allocate, khw_of
+    rng = np.random.default_rng(3)
+    shapes = [(2, 1, 40, 40), (16, 8, 3, 3), (5, 7)]
+    items, xs = [], []
+    for shp in shapes:
+        x = rng.normal(0, 1, shp).astype(np.float32)
+        t = torch.from_numpy(x).to("cuda:0")
+        xs.append(x)
+        items.append(allocate(t, bits=8, per_channel=True, symmetric=True, khw=khw_of(t), want_esum=True))
+    plan = SweepPlan(items)
+    assert plan.stats["variant"] == 6, plan.stats
+    plan.execute()
+    torch.cuda.synchronize()
+    for x, it in zip(xs, items):
+        o = O.quantize(x, 8, 3, rows=x.shape[0], khw=it.khw, want_esum=True)
+        assert np.array_equal(it.dst.cpu().numpy(), o["dq"]), x.shape
+        assert np.array_equal(it.codes.cpu().numpy().view(o["codes"].dtype), o["codes"]), x.shape
+        assert np.array_equal(it.esum.cpu().numpy(), o["esum"]), x.shape
+    plan.destroy()
