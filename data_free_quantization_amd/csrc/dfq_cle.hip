@@ -312,7 +312,10 @@ constexpr int kTileMaxKhw = 9;   // 3x3 (and 2x2); larger kernels keep the per-c
 // Rows per position-parallel rescale tile (<= kColTileRows): their loads are in
 // flight together (16-row tiles took ~70 us a task on ResNet-50's 3x3 layers,
 // 4-row tiles ~11 us: profiles/r03/cle_tl_*.log)
-constexpr int kPosTileMaxRows = 4;
+#ifndef DFQ_CLE_POS_ROWS   // compile-time A/B (scripts/cle_lib_ab.py builds side by side)
+#define DFQ_CLE_POS_ROWS 4
+#endif
+constexpr int kPosTileMaxRows = DFQ_CLE_POS_ROWS;
 
 __device__ __forceinline__ bool tile_by_position(const CleRel& R, const CleTask& tk) {
     return R.khw2 > 1 && R.khw2 <= kTileMaxKhw && (tk.a / R.o2g) == ((tk.b - 1) / R.o2g);
@@ -1396,7 +1399,10 @@ __device__ int g_cle_tiles_first = kCleTilesFirst ? 1 : 0;
 // (POS capped at 3 waves per SIMD -- 168 VGPRs, 124 B of spills -- measured slower:
 // profiles/r04/cle_ab_r04t.jsonl)
 template <bool POS>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(POS ? 1 : 4)))
+#ifndef DFQ_CLE_POS_WAVES   // waves per SIMD asked of the POS kernel (1: no cap); A/B as above
+#define DFQ_CLE_POS_WAVES 1
+#endif
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(POS ? DFQ_CLE_POS_WAVES : 4)))
 cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict__ atasks, int64_t a0, int64_t a1,
                      int64_t nab, uint32_t* __restrict__ rng, int64_t M, int is_signed, float eps, double smin,
                      double smax, const CleLayer* __restrict__ layers, const CleChunk* __restrict__ chunks,
