@@ -13,12 +13,17 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 OUT = ROOT / "data_free_quantization_amd" / "ab"
-LIBS = {   # tag: defines
-    "rows4_w1": [],   # the product
+LIBS = {   # tag: defines (round-6 A/Bs: profiles/r06/cle_lib_ab_*.jsonl)
+    "product": [],
+    "rows2_w3": ["-DDFQ_CLE_POS_ROWS=2", "-DDFQ_CLE_POS_WAVES=3"],
+}
+ALL = {
     "rows2_w3": ["-DDFQ_CLE_POS_ROWS=2", "-DDFQ_CLE_POS_WAVES=3"],
     "rows1_w4": ["-DDFQ_CLE_POS_ROWS=1", "-DDFQ_CLE_POS_WAVES=4"],
     "rows2_w1": ["-DDFQ_CLE_POS_ROWS=2"],
 }
+if os.environ.get("CLE_LIB_AB"):   # e.g. CLE_LIB_AB=rows2_w3,rows1_w4
+    LIBS = {"product": [], **{k: ALL[k] for k in os.environ["CLE_LIB_AB"].split(",")}}
 
 CODE = r"""
 import contextlib, io, json, logging, sys, time, torch
