@@ -1046,6 +1046,20 @@ def probe_ranks(args):
         print(json.dumps({"probe_ranks": rows, "n_gpus": world, "backend": backend}), flush=True)
 
 
+def _side_leg(fn):
+    """A secondary measurement after the timed step: its exception (on this rank)
+    becomes {"error": ...} in the JSON line instead of ending the run before rank 0
+    prints the headline."""
+    try:
+        return fn()
+    except Exception as e:   # noqa: BLE001 -- reported, the headline stands
+        try:
+            torch.cuda.synchronize()
+        except Exception:   # noqa: BLE001 -- the device error itself is what gets reported
+            pass
+        return {"error": f"{type(e).__name__}: {e}"[:500]}
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
@@ -1154,14 +1168,15 @@ def main(argv=None):
     del sw, plan, run, items
     torch.cuda.empty_cache()
     gathers = weak = None
-    if world > 1:
+    if world > 1:   # the side legs after the timed step: a failure is reported in the line, not fatal
         gloo = dist.get_backend() == "gloo"   # a one-GPU rehearsal stages every transfer through the host
-        gathers = sharded_gathers(specs, dev, stream, reps=2 if gloo else 10)
-        weak = weak_scaling(specs, per_copy * copies, dev, stream, rank, world, args.steps, args.warmup)
+        gathers = _side_leg(lambda: sharded_gathers(specs, dev, stream, reps=2 if gloo else 10))
+        weak = _side_leg(lambda: weak_scaling(specs, per_copy * copies, dev, stream, rank, world, args.steps,
+                                              args.warmup))
     sharded4 = None
     if world > 1 and not args.no_sharded:
         gloo = dist.get_backend() == "gloo"   # a one-GPU rehearsal stages every transfer through the host
-        sharded4 = configs4_sharded(dev, stream, reps=2 if gloo else 10, parity=not args.no_parity)
+        sharded4 = _side_leg(lambda: configs4_sharded(dev, stream, reps=2 if gloo else 10, parity=not args.no_parity))
     traffic, prof = None, None
     tj = Path(args.traffic_json)
     if tj.exists():
