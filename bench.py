@@ -1202,33 +1202,40 @@ def main(argv=None):
         # (HIP-graph captures, many plans) the same process ran the CLE loop 2.4x
         # slower (profiles/r03/validate_as vs r03at: MobileNetV2 end to end 10.4 vs
         # 5.3 ms), a state a main_dfq run never starts from
-        pipe = None if args.no_pipeline else {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")}
-        cle_roof = None if args.no_pipeline else {
+        # every leg below is a side measurement: an exception becomes {"error": ...}
+        # in its key (_side_leg) and the headline above still prints
+        pipe = None if args.no_pipeline else _side_leg(
+            lambda: {m: pipeline_timing(dev, m) for m in ("mobilenetv2", "resnet50")})
+        cle_roof = None if args.no_pipeline else _side_leg(lambda: {
             m: cle_roofline(dev, m, traffic_json=ROOT / "profiles" / "r06" / f"cle_traffic_{m}.json")
-            for m in ("mobilenetv2", "resnet50")}
-        second = None if args.no_secondary else secondary_configs(dev, stream)
-        if second is not None:
-            second.append(fold_quant_pair(dev, stream))
-        single = None if args.no_secondary else single_model_latency(dev, stream)
+            for m in ("mobilenetv2", "resnet50")})
+        second = None if args.no_secondary else _side_leg(
+            lambda: secondary_configs(dev, stream) + [fold_quant_pair(dev, stream)])
+        single = None if args.no_secondary else _side_leg(lambda: single_model_latency(dev, stream))
         # the same-mix probe last: a ResNet-50 x22 list allocated into the blocks its
         # ~7 GB of probe buffers left ran 0.699 of peak against 0.770 before it in the
         # same process (scripts/r50_state.py; DESIGN.md 3.1 "ResNet-50 in the bench")
-        probe_stream, probe_lds = same_mix_probe(per_copy * copies, dev, stream)
+        probe = _side_leg(lambda: same_mix_probe(per_copy * copies, dev, stream))
+        probe_stream, probe_lds = probe if isinstance(probe, tuple) else (probe, probe)
         torch.cuda.empty_cache()
-        cpu = cpu_baseline(args, shapes, args.cpu_seconds) if args.cpu_seconds > 0 and world == 1 else None
-        if cpu is not None:
-            cpu["transforms"] = cpu_baseline_transforms(dev, args.cpu_seconds)
+        cpu = _side_leg(lambda: cpu_baseline(args, shapes, args.cpu_seconds)) \
+            if args.cpu_seconds > 0 and world == 1 else None
+        if isinstance(cpu, dict) and "error" not in cpu:
+            cpu["transforms"] = _side_leg(lambda: cpu_baseline_transforms(dev, args.cpu_seconds))
         parity = None
         if not args.no_parity:
-            parity = {"timed_sweep": timed_parity, "pipeline_mobilenetv2": pipeline_parity(dev)}
+            pp = _side_leg(lambda: pipeline_parity(dev))
+            parity = {"timed_sweep": timed_parity, "pipeline_mobilenetv2": pp}
             if sharded4 is not None and "parity" in sharded4:
                 parity["configs4_sharded"] = sharded4["parity"]
-            parity["mismatches"] = parity["pipeline_mobilenetv2"]["mismatches"] + \
-                (timed_parity["mismatches"] if timed_parity else 0) + \
-                (sharded4["parity"]["mismatches"] if sharded4 is not None and "parity" in sharded4 else 0)
-        if pipe is not None:   # the same run again after the other legs (see above)
-            pipe["mobilenetv2"]["end_to_end_after_other_legs"] = pipeline_timing(dev, "mobilenetv2")["end_to_end"]
-            pipe["cold_process_mobilenetv2"] = pipeline_cold("mobilenetv2")
+            parity["mismatches"] = pp.get("mismatches", "error") if "error" not in pp else "error"
+            if isinstance(parity["mismatches"], int):
+                parity["mismatches"] += (timed_parity["mismatches"] if timed_parity else 0) + \
+                    (sharded4["parity"]["mismatches"] if sharded4 is not None and "parity" in sharded4 else 0)
+        if pipe is not None and "error" not in pipe:   # the same run again after the other legs (see above)
+            pipe["mobilenetv2"]["end_to_end_after_other_legs"] = _side_leg(
+                lambda: pipeline_timing(dev, "mobilenetv2")["end_to_end"])
+            pipe["cold_process_mobilenetv2"] = _side_leg(lambda: pipeline_cold("mobilenetv2"))
         res = {
             "metric": METRIC,
             "value": round(value, 2),
