@@ -319,12 +319,25 @@ __host__ __device__ inline float aten_row_sum(Get get, int64_t size) {
 }
 
 // Sum over a contiguous dim of n elements (vectorized_inner_sum / scalar_inner_sum).
+#ifndef DFQ_INNER_SUM_FAST   // compile-time A/B (scripts/cle_lib_ab.py): 0 = the generic walk only
+#define DFQ_INNER_SUM_FAST 1
+#endif
 template <typename Get>
 __host__ __device__ inline float aten_inner_sum(Get get, int64_t n) {
     if (n < 8) return aten_row_sum(get, n);
     const int64_t vs = n / 8;
     float fa = 0.f;
     for (int64_t k = 8 * vs; k < n; ++k) fa += get(k);
+    if (DFQ_INNER_SUM_FAST && vs == 1) {
+        // n in [8, 16): one element per (vector lane, ILP) stream.  aten_row_sum of
+        // one element is ((((0 + 0) + x) + 0) + 0) + 0 with empty cascades, and
+        // 0 + x is never -0, so adding the zeros changes no bit: 0 + x.  The generic
+        // walk below made the CLE stop rule's per-layer means (8 thread slots) a
+        // 4.8 us serial chain (DFQ_CLE_TL).
+#pragma unroll
+        for (int l = 0; l < 8; ++l) fa += 0.f + get(l);
+        return fa;
+    }
     for (int l = 0; l < 8; ++l) fa += aten_row_sum([&](int64_t i) { return get(8 * i + l); }, vs);
     return fa;
 }

@@ -15,9 +15,10 @@ sys.path.insert(0, str(ROOT))
 OUT = ROOT / "data_free_quantization_amd" / "ab"
 LIBS = {   # tag: defines (round-6 A/Bs: profiles/r06/cle_lib_ab_*.jsonl)
     "product": [],
-    "rows2_w3": ["-DDFQ_CLE_POS_ROWS=2", "-DDFQ_CLE_POS_WAVES=3"],
+    "inner_sum_generic": ["-DDFQ_INNER_SUM_FAST=0"],
 }
 ALL = {
+    "inner_sum_generic": ["-DDFQ_INNER_SUM_FAST=0"],
     "rows2_w3": ["-DDFQ_CLE_POS_ROWS=2", "-DDFQ_CLE_POS_WAVES=3"],
     "rows1_w4": ["-DDFQ_CLE_POS_ROWS=1", "-DDFQ_CLE_POS_WAVES=4"],
     "rows2_w1": ["-DDFQ_CLE_POS_ROWS=2"],
