@@ -1539,7 +1539,14 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
     };
     cle_tiles_body<decltype(hook)>(layers, chunks, b1off, units + (own ? uo : up), own ? nuo : nup, b1buf, tailbuf, tb,
                                    tnb, lds, lds + kCleTile + kCleTailWords, hook);
+#ifdef DFQ_DIAGNOSTICS
+    if (tl2) {   // role 3: the block's unit was a chunk's tail tile
+        const CleUnit un0 = units[(own ? uo : up) + tb];
+        tl2_rec(un0.tile >= (chunks[un0.chunk].len / 32) / 256 ? 3 : 1);
+    }
+#else
     tl2_rec(1);
+#endif
 }
 
 // After the loop: undo a speculative iteration (the lagged schedule's iteration
@@ -2878,7 +2885,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
             for (int b = 0; b < kCleTl2Fin; ++b)
                 if (tl2[4 * b]) t0 = std::min(t0, tl2[4 * b]);
             fprintf(stderr, "DFQ_CLE_TL last launch%s:", ab_env("DFQ_CLE_TL_STEP") ? " of DFQ_CLE_TL_STEP" : "");
-            for (int role = 1; role <= 2; ++role) {
+            for (int role = 1; role <= 3; ++role) {
                 std::vector<double> st, en, du;
                 for (int b = 0; b < kCleTl2Fin; ++b) {
                     const uint64_t* r = &tl2[4 * b];
@@ -2893,7 +2900,7 @@ static int cle_run_locked(dfq_cle_plan* p, CleDeviceCtx& ctx, double threshold, 
                 double m = 0;
                 for (double x : du) m += x;
                 fprintf(stderr, " [%s: %zu blocks, start p50 %.2f max %.2f, end p50 %.2f max %.2f, dur mean %.2f]",
-                        role == 1 ? "tiles" : "ranges", st.size(), st[st.size() / 2], st.back(), en[en.size() / 2],
+                        role == 1 ? "tiles" : role == 2 ? "ranges" : "tail tiles", st.size(), st[st.size() / 2], st.back(), en[en.size() / 2],
                         en.back(), m / du.size());
             }
             const uint64_t* f = &tl2[4 * kCleTl2Fin];
@@ -3513,6 +3520,12 @@ extern "C" int dfq_diag_cle_check_structure(const dfq_cle_rel* rels, int32_t n_r
         const CleChunk& ch = S.chunks[un.chunk];
         if (ch.len < 8 || un.tile < 0 || un.tile > ch.len / 32 / 256)
             return fail("unit %lld: tile %lld of chunk %lld", (long long)u, un.tile, un.chunk);
+        // cle_tiles_body's element ranges: a full tile is 8,192 elements inside the
+        // chunk; a tail tile's [e0, len) (empty when 8,192 divides the chunk) fits the
+        // LDS staging area below the b0 sums
+        const int64_t nb1 = ch.len / 32 / 256, e0 = (int64_t)un.tile * kCleTile;
+        if (un.tile < nb1 ? e0 + kCleTile > ch.len : (ch.len - e0 < 0 || ch.len - e0 > kCleTile + kCleTailWords))
+            return fail("unit %lld: tile past chunk %lld (len %lld)", (long long)u, un.chunk, ch.len);
     }
     // placement tables
     if ((int32_t)S.uoffs.size() != 2 * NL + 1 || S.uoffs[0] != 0 || S.uoffs.back() != (int64_t)S.units.size())
