@@ -1343,6 +1343,11 @@ __device__ __forceinline__ bool handoff_arrive(uint32_t* c, uint32_t target) {
     return __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == target;
 }
 
+// Blocks of the lagged schedule's stop rule: one wave per chunk sum (host and kernel).
+__host__ __device__ inline int64_t cle_stop_blocks(int64_t nchunks) {
+    return nchunks > 0 ? (nchunks + kThreads / 64 - 1) / (kThreads / 64) : 1;
+}
+
 struct CleFin {
     uint32_t* cnt;
     float* part;
@@ -1420,8 +1425,11 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
 #else
     constexpr bool tiles_first = kCleTilesFirst;
 #endif
+    // lagged schedule: the stop rule of iteration stop_it takes cle_stop_blocks blocks
+    // (its chunk sums, then the stop rule at their last arrival)
+    const int64_t nstop = stop_it >= 0 ? cle_stop_blocks(F.nchunks) : 0;
     if (tiles_first) {   // block order: metric tiles, rescale tasks, the stop rule, ranges
-        const int64_t ns = nab + (stop_it >= 0 ? 1 : 0), ntl = nto + ntp;
+        const int64_t ns = nab + nstop, ntl = nto + ntp;
         if (blk < ntl) blk += ns;
         else if (blk < ntl + ns) blk -= ntl;
     }
@@ -1476,12 +1484,34 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         }
 #endif
     };
-    if (stop_it >= 0) {   // lagged schedule: the stop rule of iteration stop_it, a block of its own
-        if (blk == 0) {
-            finish();
+    if (stop_it >= 0) {   // lagged schedule: the stop rule of iteration stop_it
+        if (blk < nstop) {
+            // The iteration's chunk sums, one wave per chunk, from the level-1 sums and
+            // tail words its tiles wrote in earlier launches (no tile of any iteration
+            // runs in this launch: the stop rule's offset follows its iteration's
+            // band and precedes the next iteration's; host structure checker); the
+            // last block to arrive runs the stop rule.  The tiles themselves no longer
+            // arrive anywhere (their chunk's last arrival summed the chunk: a store
+            // drain, an arrival and a staged sum on the launch's longest blocks).
+            // (Staging each wave's level-1 sums through LDS first measured the same:
+            // profiles/r06/cle_lib_ab_stop_chunk_sums_staged_r06z.jsonl.)
+            const int64_t c = blk * (kThreads / 64) + (threadIdx.x >> 6);
+            if (c < F.nchunks) {
+                const CleChunk ch = chunks[c];
+                if (ch.len >= 8) {   // (tiny chunks: finish, thread 0)
+                    const float fa = cle_chunk_sum(ch, b1buf + b1off[c], tailbuf + c * kCleTailWords, threadIdx.x & 63);
+                    if ((threadIdx.x & 63) == 0) st_coh(F.part + (int64_t)ch.layer * F.S + ch.t, 0.f + fa);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0)
+                flag = handoff_arrive(F.cnt + F.nchunks, ((uint32_t)stop_it + 1u) * (uint32_t)nstop - 1u);
+            __syncthreads();
+            if (flag) finish();
             return;
         }
-        blk -= 1;
+        blk -= nstop;
     }
     const int64_t ntiles = nto + ntp;
     if (blk >= ntiles) {   // next-iteration ranges of tensors final by now
@@ -1537,8 +1567,12 @@ cle_loop_step_kernel(const CleRel* __restrict__ rels, const CleTask* __restrict_
         }
         if (F.stop_arrival && arrive(F.cnt + F.nchunks, fin_members)) finish();   // the iteration's last arrival
     };
-    cle_tiles_body<decltype(hook)>(layers, chunks, b1off, units + (own ? uo : up), own ? nuo : nup, b1buf, tailbuf, tb,
-                                   tnb, lds, lds + kCleTile + kCleTailWords, hook);
+    if (F.stop_arrival)   // round-4 schedule: chunk sums and the stop rule at the tiles' arrivals
+        cle_tiles_body<decltype(hook)>(layers, chunks, b1off, units + (own ? uo : up), own ? nuo : nup, b1buf, tailbuf,
+                                       tb, tnb, lds, lds + kCleTile + kCleTailWords, hook);
+    else   // lagged schedule: the stop rule's launch sums the chunks (above)
+        cle_tiles_body(layers, chunks, b1off, units + (own ? uo : up), own ? nuo : nup, b1buf, tailbuf, tb, tnb, lds,
+                       lds + kCleTile + kCleTailWords);
 #ifdef DFQ_DIAGNOSTICS
     if (tl2) {   // role 3: the block's unit was a chunk's tail tile
         const CleUnit un0 = units[(own ? uo : up) + tb];
@@ -2646,7 +2680,7 @@ static int cle_enqueue_iteration(dfq_cle_plan* p, hipStream_t s, int32_t g, int3
         int32_t stop_it = -1;
         if (p->stop_off == k && run_g) stop_it = g;
         else if (p->stop_off == NL + k && prev) stop_it = g - 1;
-        const int64_t nblk = nab + (stop_it >= 0 ? 1 : 0) + nto + ntp + nro + nrp;
+        const int64_t nblk = nab + (stop_it >= 0 ? cle_stop_blocks(p->nchunks) : 0) + nto + ntp + nro + nrp;
         if (nblk == 0) continue;
         auto kern = (step && p->step_pos[k]) ? cle_loop_step_kernel<true> : cle_loop_step_kernel<false>;
         hipLaunchKernelGGL(kern, dim3((int)nblk), dim3(kThreads), 0, s, p->d_rels, p->d_atasks, a0, a1, nab, p->d_rng,
